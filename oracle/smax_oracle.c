@@ -1,0 +1,549 @@
+/*
+ * oracle/smax_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker; never part
+ * of the product path, which fails loudly without its HIP library).
+ *
+ * Three independent CPU derivations of the supermaximal-repeat intervals of
+ * an enhanced suffix array, plus a restatement of GenomeTools' maximal-pair
+ * enumerator used to pin the ESA against the reference's golden
+ * testdata/repfind-8-Atinsert.txt:
+ *
+ *  1. orc_linsmax        -- linear plateau scan over (.lcp/.llv, .bwt): the
+ *                           A10 predicate of SURVEY.md §8(a).  This is also the
+ *                           single-core CPU baseline ("port") timed by bench.py.
+ *  2. orc_bottomup_smax  -- the stack-based bottom-up lcp-interval traversal of
+ *                           src/match/esa-bottomup.c:116-273 driving a smax
+ *                           visitor (leaf-only interval + pairwise distinct left
+ *                           characters, ISLEFTDIVERSE semantics of
+ *                           src/match/esa-maxpairs.c:24-31).
+ *  3. orc_brute_smax     -- text-level definition, no ESA at all: a string w
+ *                           (>= minlen, no special symbol) occurring >= 2 times
+ *                           is supermaximal iff every one-symbol right extension
+ *                           wc and every left extension cw occurs at most once
+ *                           (specials and text ends are unique).  Small texts.
+ *
+ *  orc_maxpairs          -- restates gt_esa_bottomup_maxpairs
+ *                           (src/match/esa-bottomup-maxpairs.inc:136-264) with
+ *                           processleafedge/processbranchingedge
+ *                           (src/match/esa-maxpairs.c:181-360), including the
+ *                           stack-slot reuse that hands a popped child's lists
+ *                           to its new father, so the pair ORDER matches
+ *                           `gt repfind`.
+ *  orc_format_pair       -- gt_simpleexactselfmatchoutput + gt_querymatch_output
+ *                           (src/tools/gt_repfind.c:49-84,
+ *                           src/match/querymatch.c:130-190).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { uint64_t position, value; } OrcLlv;
+
+/* ----------------------------------------------------------- LCP decoding */
+
+/* Sequential decode as SSAR_NEXTSEQUENTIALLCPTABVALUE does
+ * (src/match/esa-seqread.h:104-157): byte 255 consumes the next .llv entry. */
+int orc_decode_lcp(const uint8_t *lcpbytes, uint64_t count, const OrcLlv *llv,
+                   uint64_t numllv, uint64_t *out)
+{
+  uint64_t k, li = 0;
+  for (k = 0; k < count; k++) {
+    if (lcpbytes[k] < 255) {
+      out[k] = lcpbytes[k];
+    } else {
+      if (li >= numllv || llv[li].position != k) return -1;
+      out[k] = llv[li++].value;
+    }
+  }
+  return 0;
+}
+
+/* ----------------------------------------------------- diversity helper */
+
+typedef struct { uint64_t w[4]; } Seen;
+
+/* returns 1 if c (<254) was already seen; B >= 254 counts as unique */
+static int seen_add(Seen *s, uint8_t c)
+{
+  uint64_t bit;
+  if (c >= 254) return 0;
+  bit = (uint64_t) 1 << (c & 63);
+  if (s->w[c >> 6] & bit) return 1;
+  s->w[c >> 6] |= bit;
+  return 0;
+}
+
+static int leftdiverse(const uint8_t *bwt, uint64_t lb, uint64_t rb)
+{
+  Seen s;
+  uint64_t k;
+  memset(&s, 0, sizeof s);
+  for (k = lb; k <= rb; k++)
+    if (seen_add(&s, bwt[k])) return 0;
+  return 1;
+}
+
+/* --------------------------------------------------------- 1. linsmax */
+
+/* L[k] = lcp(S[k-1],S[k]) for 1<=k<=N-1, L[0]=L[N]=0.
+ * out: triples (lcp, lb, rb) in ascending lb, at most cap of them; returns the
+ * total number found (may exceed cap). */
+uint64_t orc_linsmax(const uint8_t *lcpbytes, const OrcLlv *llv,
+                     uint64_t numllv, const uint8_t *bwt, uint64_t nonspecials,
+                     uint64_t minlen, uint64_t *out, uint64_t cap)
+{
+  uint64_t N = nonspecials, k, li = 0, found = 0, prev = 0;
+#define ORC_L(IDX, VAR)                                                       \
+  do {                                                                        \
+    uint64_t ix_ = (IDX);                                                     \
+    if (ix_ == 0 || ix_ >= N) { VAR = 0; }                                    \
+    else if (lcpbytes[ix_] < 255) { VAR = lcpbytes[ix_]; }                    \
+    else { while (li < numllv && llv[li].position < ix_) li++;                \
+           VAR = llv[li].value; }                                             \
+  } while (0)
+  if (N < 2) return 0;
+  k = 1;
+  while (k <= N - 1) {
+    uint64_t l, j, next;
+    ORC_L(k, l);
+    if (l > prev && l >= minlen) {
+      j = k;
+      for (;;) {
+        if (j + 1 > N - 1) { next = 0; break; }
+        ORC_L(j + 1, next);
+        if (next != l) break;
+        j++;
+      }
+      if (next < l && leftdiverse(bwt, k - 1, j)) {
+        if (found < cap) {
+          out[3 * found] = l;
+          out[3 * found + 1] = k - 1;
+          out[3 * found + 2] = j;
+        }
+        found++;
+      }
+      /* position j+1 starts a new comparison against L[j] == l */
+      prev = l;
+      k = j + 1;
+      continue;
+    }
+    prev = l;
+    k++;
+  }
+#undef ORC_L
+  return found;
+}
+
+/* --------------------------------------------- 2. bottom-up smax visitor */
+
+typedef struct {
+  uint64_t lcp, lb, rb;
+  int has_branch;   /* a branching edge ends here: not a local maximum */
+  int dup;          /* two leaves with the same left character < 254 */
+  Seen seen;
+} BUItv;
+
+typedef struct {
+  BUItv *space;
+  uint64_t next, alloc;
+} BUStack;
+
+static void bu_push(BUStack *st, uint64_t lcp, uint64_t lb)
+{
+  if (st->next >= st->alloc) {
+    uint64_t na = st->alloc + 32;
+    st->space = realloc(st->space, sizeof (BUItv) * na);
+    memset(st->space + st->alloc, 0, sizeof (BUItv) * 32);
+    st->alloc = na;
+  }
+  st->space[st->next].lcp = lcp;
+  st->space[st->next].lb = lb;
+  st->space[st->next].rb = UINT64_MAX;
+  st->next++;
+}
+
+#define BU_TOP(st) ((st)->space[(st)->next - 1])
+
+static uint8_t leftchar_of(const uint8_t *text, uint64_t pos)
+{
+  return pos == 0 ? (uint8_t) 254 : text[pos - 1];
+}
+
+static void smax_leaf(BUItv *f, int firstsucc, uint8_t lc)
+{
+  if (firstsucc) {
+    f->has_branch = 0; f->dup = 0; memset(&f->seen, 0, sizeof f->seen);
+  }
+  if (seen_add(&f->seen, lc)) f->dup = 1;
+}
+
+static void smax_branch(BUItv *f, int firstsucc)
+{
+  /* any interval child disqualifies the father as a local maximum; with
+   * firstsucc the father reuses the child's slot, so reset it. */
+  if (firstsucc) {
+    f->dup = 0; memset(&f->seen, 0, sizeof f->seen);
+  }
+  f->has_branch = 1;
+}
+
+/* Traversal as in gt_esa_bottomup (src/match/esa-bottomup.c:116-273).
+ * lcp: decoded, lcp[idx+1] read at step idx; suftab full; text encoded. */
+uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
+                           const uint8_t *text, uint64_t nonspecials,
+                           uint64_t minlen, uint64_t *out, uint64_t cap)
+{
+  BUStack st = {NULL, 0, 0};
+  BUItv *last = NULL;
+  BUItv lastcopy;
+  uint64_t idx, found = 0;
+  int firstedgefromroot = 1;
+#define EMIT(I)                                                              \
+  do {                                                                       \
+    if ((I)->lcp >= minlen && !(I)->has_branch && !(I)->dup) {               \
+      if (found < cap) { out[3*found] = (I)->lcp; out[3*found+1] = (I)->lb;  \
+                         out[3*found+2] = (I)->rb; }                         \
+      found++;                                                               \
+    }                                                                        \
+  } while (0)
+  bu_push(&st, 0, 0);
+  for (idx = 0; idx < nonspecials; idx++) {
+    uint64_t lcpvalue = lcp[idx + 1];
+    uint64_t prevsuffix = suftab[idx];
+    int firstedge;
+    if (lcpvalue <= BU_TOP(&st).lcp) {
+      if (BU_TOP(&st).lcp > 0 || !firstedgefromroot) firstedge = 0;
+      else { firstedge = 1; firstedgefromroot = 0; }
+      smax_leaf(&BU_TOP(&st), firstedge, leftchar_of(text, prevsuffix));
+    }
+    last = NULL;
+    while (lcpvalue < BU_TOP(&st).lcp) {
+      st.next--;
+      lastcopy = st.space[st.next];
+      last = &lastcopy;
+      last->rb = idx;
+      EMIT(last);
+      if (lcpvalue <= BU_TOP(&st).lcp) {
+        if (BU_TOP(&st).lcp > 0 || !firstedgefromroot) firstedge = 0;
+        else { firstedge = 1; firstedgefromroot = 0; }
+        smax_branch(&BU_TOP(&st), firstedge);
+        last = NULL;
+      }
+    }
+    if (lcpvalue > BU_TOP(&st).lcp) {
+      if (last != NULL) {
+        bu_push(&st, lcpvalue, last->lb);
+        smax_branch(&BU_TOP(&st), 1);
+        last = NULL;
+      } else {
+        bu_push(&st, lcpvalue, idx);
+        smax_leaf(&BU_TOP(&st), 1, leftchar_of(text, prevsuffix));
+      }
+    }
+  }
+  if (BU_TOP(&st).lcp > 0) {
+    /* never reached on file-based indexes: LCP[N] == 0 */
+    BU_TOP(&st).rb = idx;
+    EMIT(&BU_TOP(&st));
+  }
+  free(st.space);
+#undef EMIT
+  return found;
+}
+
+/* --------------------------------------------------------- 3. brute force */
+
+static int is_spec(const uint8_t *t, uint64_t n, int64_t p)
+{
+  return p < 0 || (uint64_t) p >= n || t[p] >= 254;
+}
+
+/* All supermaximal repeats of text[0..n) with length >= minlen.
+ * out: (length, first occurrence, number of occurrences) triples sorted by
+ * (first occ); occs receives all occurrence positions, ascending per repeat.
+ * O(n^3); meant for n <= ~400. */
+uint64_t orc_brute_smax(const uint8_t *t, uint64_t n, uint64_t minlen,
+                        uint64_t *out, uint64_t cap, uint64_t *occs,
+                        uint64_t occcap)
+{
+  uint64_t found = 0, nocc = 0, i, len;
+  uint64_t *pos = malloc(sizeof (uint64_t) * (n + 1));
+  for (len = minlen > 0 ? minlen : 1; len <= n; len++) {
+    for (i = 0; i + len <= n; i++) {
+      uint64_t j, cnt = 0, q;
+      int ok = 1, firstocc = 1;
+      for (q = 0; q < len; q++) if (t[i + q] >= 254) { ok = 0; break; }
+      if (!ok) continue;
+      /* i must be the first occurrence */
+      for (j = 0; j < i && firstocc; j++)
+        if (memcmp(t + j, t + i, len) == 0) firstocc = 0;
+      if (!firstocc) continue;
+      for (j = i; j + len <= n; j++)
+        if (memcmp(t + j, t + i, len) == 0) pos[cnt++] = j;
+      if (cnt < 2) continue;
+      /* right extensions: pairwise distinct or special */
+      {
+        uint64_t a, b;
+        for (a = 0; a < cnt && ok; a++)
+          for (b = a + 1; b < cnt && ok; b++) {
+            int64_t ra = (int64_t) (pos[a] + len), rb = (int64_t) (pos[b] + len);
+            int64_t la = (int64_t) pos[a] - 1, lb = (int64_t) pos[b] - 1;
+            if (!is_spec(t, n, ra) && !is_spec(t, n, rb) && t[ra] == t[rb])
+              ok = 0;
+            if (!is_spec(t, n, la) && !is_spec(t, n, lb) && t[la] == t[lb])
+              ok = 0;
+          }
+      }
+      if (!ok) continue;
+      if (found < cap) {
+        out[3 * found] = len; out[3 * found + 1] = i; out[3 * found + 2] = cnt;
+      }
+      for (j = 0; j < cnt; j++) { if (nocc < occcap) occs[nocc] = pos[j]; nocc++; }
+      found++;
+    }
+  }
+  free(pos);
+  return found;
+}
+
+/* ------------------------------------------------------------- maxpairs */
+
+typedef struct { uint64_t start, length; } MPList;
+
+typedef struct {
+  uint8_t commonchar;
+  uint64_t ucstart, uclen;
+  MPList npl[4];
+} MPInfo;
+
+typedef struct {
+  uint64_t lcp, lb, rb;
+  MPInfo info;
+} MPItv;
+
+typedef struct { uint64_t *space, next, alloc; } U64Arr;
+
+static void arr_add(U64Arr *a, uint64_t v)
+{
+  if (a->next >= a->alloc) {
+    a->alloc = a->alloc * 2 + 64;
+    a->space = realloc(a->space, sizeof (uint64_t) * a->alloc);
+  }
+  a->space[a->next++] = v;
+}
+
+typedef struct {
+  unsigned sigma, searchlength;
+  int initialized;
+  U64Arr uniquechar, poslist[4];
+  const uint8_t *text;
+  U64Arr pairs; /* len, pos1, pos2 triples in emission order */
+} MPState;
+
+#define ISLD(s) ((uint8_t) (s)->sigma)
+#define INITC(s) ((uint8_t) ((s)->sigma + 1))
+
+static void mp_emit(MPState *s, uint64_t len, uint64_t p1, uint64_t p2)
+{
+  arr_add(&s->pairs, len); arr_add(&s->pairs, p1); arr_add(&s->pairs, p2);
+}
+
+static void mp_add2poslist(MPState *s, MPInfo *ni, unsigned base, uint64_t leaf)
+{
+  if (base >= s->sigma) { ni->uclen++; arr_add(&s->uniquechar, leaf); }
+  else { arr_add(&s->poslist[base], leaf); ni->npl[base].length++; }
+}
+
+static void mp_cart1(MPState *s, uint64_t depth, const MPInfo *ni,
+                     unsigned base, uint64_t leaf)
+{
+  uint64_t k;
+  const MPList *pl = &ni->npl[base];
+  for (k = 0; k < pl->length; k++)
+    mp_emit(s, depth, leaf, s->poslist[base].space[pl->start + k]);
+}
+
+static void mp_cart2(MPState *s, uint64_t depth, const MPInfo *n1,
+                     unsigned b1, const MPInfo *n2, unsigned b2)
+{
+  uint64_t a, b;
+  const MPList *p1 = &n1->npl[b1], *p2 = &n2->npl[b2];
+  for (a = 0; a < p1->length; a++)
+    for (b = 0; b < p2->length; b++)
+      mp_emit(s, depth, s->poslist[b1].space[p1->start + a],
+              s->poslist[b2].space[p2->start + b]);
+}
+
+static void mp_setpostabto0(MPState *s)
+{
+  unsigned b;
+  if (!s->initialized) {
+    for (b = 0; b < s->sigma; b++) s->poslist[b].next = 0;
+    s->uniquechar.next = 0;
+    s->initialized = 1;
+  }
+}
+
+static void mp_leaf(MPState *s, int firstsucc, uint64_t depth, MPInfo *f,
+                    uint64_t leaf)
+{
+  unsigned base;
+  uint8_t lc;
+  if (depth < s->searchlength) { mp_setpostabto0(s); return; }
+  lc = leaf == 0 ? INITC(s) : s->text[leaf - 1];
+  s->initialized = 0;
+  if (firstsucc) {
+    f->commonchar = lc; f->uclen = 0; f->ucstart = s->uniquechar.next;
+    for (base = 0; base < s->sigma; base++) {
+      f->npl[base].start = s->poslist[base].next;
+      f->npl[base].length = 0;
+    }
+    mp_add2poslist(s, f, lc, leaf);
+    return;
+  }
+  if (f->commonchar != ISLD(s)) {
+    if (f->commonchar != lc || lc >= ISLD(s)) f->commonchar = ISLD(s);
+  }
+  if (f->commonchar == ISLD(s)) {
+    uint64_t k;
+    for (base = 0; base < s->sigma; base++)
+      if (lc != (uint8_t) base) mp_cart1(s, depth, f, base, leaf);
+    for (k = 0; k < f->uclen; k++)
+      mp_emit(s, depth, leaf, s->uniquechar.space[f->ucstart + k]);
+  }
+  mp_add2poslist(s, f, lc, leaf);
+}
+
+static void mp_branch(MPState *s, int firstsucc, uint64_t depth, MPInfo *f,
+                      MPInfo *son)
+{
+  unsigned cf, cs, base;
+  uint64_t k, m;
+  if (depth < s->searchlength) { mp_setpostabto0(s); return; }
+  s->initialized = 0;
+  if (firstsucc) return;
+  if (f->commonchar != ISLD(s)) {
+    if (son->commonchar != ISLD(s)) {
+      if (f->commonchar != son->commonchar || son->commonchar >= ISLD(s))
+        f->commonchar = ISLD(s);
+    } else {
+      f->commonchar = ISLD(s);
+    }
+  }
+  if (f->commonchar == ISLD(s)) {
+    for (cf = 0; cf < s->sigma; cf++) {
+      for (cs = 0; cs < s->sigma; cs++)
+        if (cs != cf) mp_cart2(s, depth, f, cf, son, cs);
+      for (k = 0; k < son->uclen; k++)
+        mp_cart1(s, depth, f, cf, s->uniquechar.space[son->ucstart + k]);
+    }
+    for (m = 0; m < f->uclen; m++) {
+      uint64_t fp = s->uniquechar.space[f->ucstart + m];
+      for (cs = 0; cs < s->sigma; cs++) mp_cart1(s, depth, son, cs, fp);
+      for (k = 0; k < son->uclen; k++)
+        mp_emit(s, depth, fp, s->uniquechar.space[son->ucstart + k]);
+    }
+  }
+  for (base = 0; base < s->sigma; base++)
+    f->npl[base].length += son->npl[base].length;
+  f->uclen += son->uclen;
+}
+
+/* Returns number of pairs; *pairs_out (malloc'd) holds (len,pos1,pos2). */
+uint64_t orc_maxpairs(const uint64_t *lcp, const uint64_t *suftab,
+                      const uint8_t *text, uint64_t nonspecials,
+                      unsigned minlen, uint64_t **pairs_out)
+{
+  MPState s;
+  MPItv *stk = NULL;
+  uint64_t next = 0, alloc = 0, idx;
+  MPItv *last = NULL;
+  int firstedgefromroot = 1;
+  memset(&s, 0, sizeof s);
+  s.sigma = 4; s.searchlength = minlen; s.text = text;
+#define MP_TOP (stk[next - 1])
+#define MP_PUSH(L, B)                                                        \
+  do {                                                                       \
+    if (next >= alloc) {                                                     \
+      stk = realloc(stk, sizeof (MPItv) * (alloc + 32));                     \
+      memset(stk + alloc, 0, sizeof (MPItv) * 32);                           \
+      alloc += 32;                                                           \
+    }                                                                        \
+    stk[next].lcp = (L); stk[next].lb = (B); stk[next].rb = UINT64_MAX;      \
+    next++;                                                                  \
+  } while (0)
+  MP_PUSH(0, 0);
+  for (idx = 0; idx < nonspecials; idx++) {
+    uint64_t lcpvalue = lcp[idx + 1], prevsuffix = suftab[idx];
+    int firstedge;
+    if (lcpvalue <= MP_TOP.lcp) {
+      if (MP_TOP.lcp > 0 || !firstedgefromroot) firstedge = 0;
+      else { firstedge = 1; firstedgefromroot = 0; }
+      mp_leaf(&s, firstedge, MP_TOP.lcp, &MP_TOP.info, prevsuffix);
+    }
+    last = NULL;
+    while (lcpvalue < MP_TOP.lcp) {
+      last = &stk[--next];     /* slot stays valid: reused by a later PUSH */
+      last->rb = idx;
+      if (lcpvalue <= MP_TOP.lcp) {
+        if (MP_TOP.lcp > 0 || !firstedgefromroot) firstedge = 0;
+        else { firstedge = 1; firstedgefromroot = 0; }
+        mp_branch(&s, firstedge, MP_TOP.lcp, &MP_TOP.info, &last->info);
+        last = NULL;
+      }
+    }
+    if (lcpvalue > MP_TOP.lcp) {
+      if (last != NULL) {
+        uint64_t llb = last->lb;
+        /* PUSH writes into the popped child's slot: father inherits info */
+        MP_PUSH(lcpvalue, llb);
+        mp_branch(&s, 1, MP_TOP.lcp, &MP_TOP.info, NULL);
+        last = NULL;
+      } else {
+        MP_PUSH(lcpvalue, idx);
+        mp_leaf(&s, 1, MP_TOP.lcp, &MP_TOP.info, prevsuffix);
+      }
+    }
+  }
+  free(stk);
+  free(s.uniquechar.space);
+  {
+    unsigned b;
+    for (b = 0; b < 4; b++) free(s.poslist[b].space);
+  }
+  *pairs_out = s.pairs.space;
+#undef MP_TOP
+#undef MP_PUSH
+  return s.pairs.next / 3;
+}
+
+/* ------------------------------------------------------- pair formatting */
+
+/* seqnum of absolute position p given sorted separator positions */
+static uint64_t seqnum_of(const uint64_t *sep, uint64_t nsep, uint64_t p)
+{
+  uint64_t lo = 0, hi = nsep;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    if (sep[mid] < p) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+/* Formats one repfind line "len seq1 rel1 F len seq2 rel2\n" into buf.
+ * Returns number of chars, or 0 if filtered. */
+int orc_format_pair(uint64_t len, uint64_t pos1, uint64_t pos2,
+                    const uint64_t *sep, uint64_t nsep, char *buf, int bufsz)
+{
+  uint64_t s1, s2, st1, st2;
+  if (pos1 > pos2) { uint64_t t = pos1; pos1 = pos2; pos2 = t; }
+  s1 = seqnum_of(sep, nsep, pos1);
+  s2 = seqnum_of(sep, nsep, pos2);
+  st1 = s1 == 0 ? 0 : sep[s1 - 1] + 1;
+  st2 = s2 == 0 ? 0 : sep[s2 - 1] + 1;
+  if (s1 == s2 && pos1 - st1 > pos2 - st2) return 0;
+  return snprintf(buf, (size_t) bufsz, "%lu %lu %lu F %lu %lu %lu\n",
+                  (unsigned long) len, (unsigned long) s1,
+                  (unsigned long) (pos1 - st1), (unsigned long) len,
+                  (unsigned long) s2, (unsigned long) (pos2 - st2));
+}

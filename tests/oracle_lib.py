@@ -1,0 +1,172 @@
+"""ctypes view of the CPU oracle (oracle/*.c) -- test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this
+module; the product package never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "liborc.so")
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(LIB)
+        L.orc_encode_fasta.argtypes = [ctypes.c_char_p, ctypes.c_uint64, _u8p, _u64p, _u64p]
+        L.orc_build_esa.argtypes = [_u8p, ctypes.c_uint64] + [ctypes.c_void_p] * 4 + [_u64p, ctypes.c_void_p]
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_index_fasta.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.orc_decode_lcp.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, _u64p]
+        L.orc_linsmax.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint64, _u8p, ctypes.c_uint64,
+                                  ctypes.c_uint64, _u64p, ctypes.c_uint64]
+        L.orc_linsmax.restype = ctypes.c_uint64
+        L.orc_bottomup_smax.argtypes = [_u64p, _u64p, _u8p, ctypes.c_uint64, ctypes.c_uint64,
+                                        _u64p, ctypes.c_uint64]
+        L.orc_bottomup_smax.restype = ctypes.c_uint64
+        L.orc_brute_smax.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64, _u64p, ctypes.c_uint64,
+                                     _u64p, ctypes.c_uint64]
+        L.orc_brute_smax.restype = ctypes.c_uint64
+        L.orc_maxpairs.argtypes = [_u64p, _u64p, _u8p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p]
+        L.orc_maxpairs.restype = ctypes.c_uint64
+        L.orc_format_pair.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _u64p,
+                                      ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def encode_fasta(path):
+    with open(path, "rb") as fh:
+        buf = fh.read()
+    out = np.empty(len(buf) + 1, dtype=np.uint8)
+    n = ctypes.c_uint64()
+    ns = ctypes.c_uint64()
+    rc = lib().orc_encode_fasta(buf, len(buf), _p(out, _u8p), ctypes.byref(n), ctypes.byref(ns))
+    if rc != 0:
+        raise ValueError("illegal symbol in %s" % path)
+    return out[: n.value].copy(), ns.value
+
+
+class Esa:
+    """In-memory enhanced suffix array built by the oracle (gt layout)."""
+
+    def __init__(self, text):
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        n = len(text)
+        ptrs = [ctypes.c_void_p() for _ in range(4)]
+        numllv = ctypes.c_uint64()
+        bwtp = ctypes.c_void_p()
+        rc = lib().orc_build_esa(_p(text, _u8p), n, *[ctypes.byref(p) for p in ptrs],
+                                 ctypes.byref(numllv), ctypes.byref(bwtp))
+        assert rc == 0
+        sufp, lcpp, lcpbp, llvp = ptrs
+
+        def grab(ptr, count, dtype):
+            size = count * np.dtype(dtype).itemsize
+            buf = (ctypes.c_uint8 * max(size, 1)).from_address(ptr.value)
+            arr = np.frombuffer(buf, dtype=np.uint8, count=size).view(dtype).copy()
+            lib().orc_free(ptr)
+            return arr
+
+        self.text = text
+        self.n = n
+        self.suftab = grab(sufp, n + 1, np.uint64)
+        self.lcp = grab(lcpp, n + 1, np.uint64)
+        self.lcpbytes = grab(lcpbp, n + 1, np.uint8)
+        self.llv = grab(llvp, max(numllv.value, 0) * 2, np.uint64).reshape(-1, 2)
+        self.bwt = grab(bwtp, n + 1, np.uint8)
+        self.nonspecials = int(n - np.count_nonzero(text >= 254))
+        self.separators = np.sort(np.flatnonzero(text == 255)).astype(np.uint64)
+
+
+def index_fasta(fasta, indexname, suftab_bytes=8):
+    rc = lib().orc_index_fasta(fasta.encode(), indexname.encode(), suftab_bytes)
+    if rc != 0:
+        raise RuntimeError("orc_index_fasta failed: %d" % rc)
+
+
+def _triples(out, found):
+    return out[: 3 * found].reshape(-1, 3).copy()
+
+
+def linsmax(lcpbytes, llv, bwt, nonspecials, minlen):
+    llv = np.ascontiguousarray(llv, dtype=np.uint64).reshape(-1, 2)
+    cap = max(16, nonspecials // 2 + 1)
+    out = np.empty(3 * cap, dtype=np.uint64)
+    found = lib().orc_linsmax(_p(lcpbytes, _u8p), llv.ctypes.data_as(ctypes.c_void_p), len(llv),
+                              _p(bwt, _u8p), nonspecials, minlen, _p(out, _u64p), cap)
+    assert found <= cap
+    return _triples(out, found)
+
+
+def bottomup_smax(esa, minlen):
+    cap = max(16, esa.nonspecials // 2 + 1)
+    out = np.empty(3 * cap, dtype=np.uint64)
+    found = lib().orc_bottomup_smax(_p(esa.lcp, _u64p), _p(esa.suftab, _u64p), _p(esa.text, _u8p),
+                                    esa.nonspecials, minlen, _p(out, _u64p), cap)
+    assert found <= cap
+    return _triples(out, found)
+
+
+def brute_smax(text, minlen):
+    text = np.ascontiguousarray(text, dtype=np.uint8)
+    n = len(text)
+    cap = n * n + 16
+    out = np.empty(3 * cap, dtype=np.uint64)
+    occ = np.empty(cap, dtype=np.uint64)
+    found = lib().orc_brute_smax(_p(text, _u8p), n, minlen, _p(out, _u64p), cap, _p(occ, _u64p), cap)
+    trip = _triples(out, found)
+    res = []
+    o = 0
+    for length, first, cnt in trip:
+        res.append((int(length), tuple(int(x) for x in occ[o: o + int(cnt)])))
+        o += int(cnt)
+    return res
+
+
+def maxpairs(esa, minlen):
+    pp = ctypes.c_void_p()
+    cnt = lib().orc_maxpairs(_p(esa.lcp, _u64p), _p(esa.suftab, _u64p), _p(esa.text, _u8p),
+                             esa.nonspecials, minlen, ctypes.byref(pp))
+    if cnt == 0:
+        return np.zeros((0, 3), dtype=np.uint64)
+    buf = (ctypes.c_uint64 * (3 * cnt)).from_address(pp.value)
+    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).copy()
+    lib().orc_free(pp)
+    return arr
+
+
+def format_pairs(pairs, separators):
+    sep = np.ascontiguousarray(separators, dtype=np.uint64)
+    buf = ctypes.create_string_buffer(256)
+    lines = []
+    for length, p1, p2 in pairs:
+        k = lib().orc_format_pair(int(length), int(p1), int(p2), _p(sep, _u64p), len(sep), buf, 256)
+        if k > 0:
+            lines.append(buf.value.decode())
+    return lines
+
+
+def smax_pairs(intervals, suftab):
+    """All occurrence pairs of each smax interval, as (len, pos1, pos2)."""
+    out = []
+    for length, lb, rb in intervals:
+        occ = [int(suftab[k]) for k in range(int(lb), int(rb) + 1)]
+        for a in range(len(occ)):
+            for b in range(a + 1, len(occ)):
+                out.append((int(length), occ[a], occ[b]))
+    return out
