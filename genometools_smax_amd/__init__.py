@@ -1,0 +1,417 @@
+"""genometools_smax_amd -- MI355X supermaximal-repeat finder behind
+GenomeTools' ESA interfaces.
+
+Host-side mirror (Python) of the pieces of the reference the smax path sits
+behind.  The compute path is the HIP library lib/libgtsmax_hip.so
+(csrc/smax_kernels.hip, C-ABI in include/gt_smax_hip.h); there is no CPU
+fallback: every entry point raises if the library or a HIP device is missing.
+
+  EsaIndex            mmap of a `gt suffixerator -suf -lcp -bwt` index,
+                      restating Suffixarray / gt_mapsuffixarray
+                      (src/match/sarr-def.h:101-126, src/match/esa-map.c:296-515)
+  enumerate_smax      gt_smax_hip_enumerate_to_buffer -> (lcp, lb, rb) rows in
+                      ascending lb, the order gt_esa_bottomup pops them
+  SmaxPlan            device-resident plan over tables already in HBM
+  repfind_smax_lines  `gt repfind -smax` output: one line per occurrence pair,
+                      format of gt_simpleexactselfmatchoutput
+                      (src/tools/gt_repfind.c:49-84, src/match/querymatch.c:130-190)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgtsmax_hip.so")
+BIN_DIR = os.path.join(_HERE, "bin")
+
+PAD_FRONT = 256
+PAD_BACK = 32768
+
+
+class SmaxError(RuntimeError):
+    """Error reported through the C-ABI's errbuf (GtError analogue)."""
+
+
+class GtSmaxLlv(ctypes.Structure):
+    _fields_ = [("position", ctypes.c_uint64), ("value", ctypes.c_uint64)]
+
+
+class GtSmaxInput(ctypes.Structure):
+    _fields_ = [
+        ("lcptab", ctypes.c_void_p),
+        ("llvtab", ctypes.c_void_p),
+        ("numllv", ctypes.c_uint64),
+        ("bwttab", ctypes.c_void_p),
+        ("suftab", ctypes.c_void_p),
+        ("suftab_bytes", ctypes.c_int),
+        ("totallength", ctypes.c_uint64),
+        ("nonspecials", ctypes.c_uint64),
+    ]
+
+
+class GtSmaxDevShard(ctypes.Structure):
+    _fields_ = [
+        ("lcp_dev", ctypes.c_void_p),
+        ("bwt_dev", ctypes.c_void_p),
+        ("llv_dev", ctypes.c_void_p),
+        ("numllv", ctypes.c_uint64),
+        ("base", ctypes.c_uint64),
+        ("local_len", ctypes.c_uint64),
+        ("begin", ctypes.c_uint64),
+        ("end", ctypes.c_uint64),
+        ("nonspecials", ctypes.c_uint64),
+        ("device", ctypes.c_int),
+    ]
+
+
+class GtSmaxDiv(ctypes.Structure):
+    _fields_ = [("seen", ctypes.c_uint64 * 4), ("dup", ctypes.c_uint64)]
+
+
+class GtSmaxBoundary(ctypes.Structure):
+    _fields_ = [
+        ("pend_valid", ctypes.c_uint64),
+        ("pend_c", ctypes.c_uint64),
+        ("pend_lcp", ctypes.c_uint64),
+        ("pend_div", GtSmaxDiv),
+        ("head_v", ctypes.c_uint64),
+        ("head_f", ctypes.c_uint64),
+        ("head_next", ctypes.c_uint64),
+        ("head_div", GtSmaxDiv),
+        ("shard_begin", ctypes.c_uint64),
+        ("shard_end", ctypes.c_uint64),
+    ]
+
+
+class GtSmaxRecord(ctypes.Structure):
+    _fields_ = [("lb", ctypes.c_uint64), ("lcp", ctypes.c_uint32), ("width", ctypes.c_uint32)]
+
+
+BOUNDARY_BYTES = ctypes.sizeof(GtSmaxBoundary)
+RECORD_DTYPE = np.dtype([("lb", "<u8"), ("lcp", "<u4"), ("width", "<u4")])
+
+_lib = None
+
+
+def lib():
+    """The HIP library; raises (never falls back) when it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SmaxError("HIP library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, u32, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int
+        cs, sz = ctypes.c_char_p, ctypes.c_size_t
+        L.gt_smax_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput), u32, ci,
+                                                      ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
+        L.gt_smax_free.argtypes = [vp]
+        L.gt_smax_device_count.restype = ci
+        L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
+        L.gt_smax_dev_free_table.argtypes = [ci, vp]
+        L.gt_smax_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtSmaxDevShard), u32, u64,
+                                          cs, sz]
+        L.gt_smax_plan_delete.argtypes = [vp]
+        L.gt_smax_plan_run.argtypes = [vp, vp]
+        L.gt_smax_plan_records.argtypes = [vp]
+        L.gt_smax_plan_records.restype = vp
+        L.gt_smax_plan_count_dev.argtypes = [vp]
+        L.gt_smax_plan_count_dev.restype = vp
+        L.gt_smax_plan_boundary_dev.argtypes = [vp]
+        L.gt_smax_plan_boundary_dev.restype = vp
+        L.gt_smax_plan_capacity.argtypes = [vp]
+        L.gt_smax_plan_capacity.restype = u64
+        L.gt_smax_plan_num_tiles.argtypes = [vp]
+        L.gt_smax_plan_num_tiles.restype = u64
+        L.gt_smax_plan_stitch.argtypes = [vp, vp, ci, ci, vp]
+        L.gt_smax_stitch_host.argtypes = [ctypes.POINTER(GtSmaxBoundary), ci, ci, u32,
+                                          ctypes.POINTER(GtSmaxRecord)]
+        L.gt_smax_plan_fetch_count.argtypes = [vp, ctypes.POINTER(u64)]
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    """Every function include/gt_smax_hip.h declares (checked by tests)."""
+    import re
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "gt_smax_hip.h")
+    with open(hdr) as fh:
+        text = fh.read()
+    return sorted(set(re.findall(r"\b(gt_smax_\w+)\s*\(", text)))
+
+
+def _errbuf():
+    return ctypes.create_string_buffer(1024)
+
+
+def _check(rc, eb):
+    if rc != 0:
+        raise SmaxError(eb.value.decode(errors="replace") or "gt_smax error")
+
+
+# --------------------------------------------------------------- ESA index
+
+class EsaIndex:
+    """Memory-mapped gt ESA (.prj .lcp .llv .bwt [.suf]).
+
+    Restates inputsuffixarray/gt_mapsuffixarray (src/match/esa-map.c:296-515):
+    .prj keys checked as scanprjfileuintkeysviafileptr does (:55-214), table
+    sizes checked against totallength+1, nonspecials = totallength -
+    specialcharacters (src/match/esa-seqread.c:56-57).  The .suf width is
+    inferred from its size (8 B GtUword, or 4 B from -suftabuint).
+    """
+
+    def __init__(self, indexname, need_suftab=True):
+        self.indexname = indexname
+        self.prj = self._read_prj(indexname + ".prj")
+        p = self.prj
+        for key in ("totallength", "specialcharacters", "integersize", "littleendian",
+                    "readmode", "mirrored"):
+            if key not in p:
+                raise SmaxError("%s.prj: missing key %s" % (indexname, key))
+        if p["integersize"] not in (32, 64):
+            raise SmaxError("%s.prj contains illegal line defining the integer size" % indexname)
+        if p["littleendian"] != 1:
+            raise SmaxError("index was built on a big endian computer")
+        if p["readmode"] > 3:
+            raise SmaxError("illegal readmode %d" % p["readmode"])
+        if p["mirrored"] > 1:
+            raise SmaxError("illegal mirroring flag %d" % p["mirrored"])
+        if p["readmode"] != 0 or p["mirrored"] != 0:
+            raise SmaxError("smax supports forward, non-mirrored indexes only "
+                            "(readmode=%d mirrored=%d)" % (p["readmode"], p["mirrored"]))
+        self.totallength = n = p["totallength"]
+        self.nonspecials = n - p["specialcharacters"]
+        self.lcptab = self._map(".lcp", np.uint8, n + 1)
+        self.bwttab = self._map(".bwt", np.uint8, n + 1)
+        llvpath = indexname + ".llv"
+        size = os.path.getsize(llvpath) if os.path.exists(llvpath) else 0
+        if size % 16:
+            raise SmaxError("%s: size %d not a multiple of 16" % (llvpath, size))
+        if size:
+            self.llvtab = np.memmap(llvpath, dtype=np.uint64, mode="r").reshape(-1, 2)
+        else:
+            self.llvtab = np.zeros((0, 2), dtype=np.uint64)
+        if "largelcpvalues" in p and p["largelcpvalues"] != len(self.llvtab):
+            raise SmaxError("%s.llv holds %d entries, .prj says %d"
+                            % (indexname, len(self.llvtab), p["largelcpvalues"]))
+        self.suftab = None
+        if need_suftab and os.path.exists(indexname + ".suf"):
+            ssize = os.path.getsize(indexname + ".suf")
+            if ssize == 8 * (n + 1):
+                self.suftab = np.memmap(indexname + ".suf", dtype=np.uint64, mode="r")
+            elif ssize == 4 * (n + 1):
+                self.suftab = np.memmap(indexname + ".suf", dtype=np.uint32, mode="r")
+            else:
+                raise SmaxError("%s.suf: number of mapped units does not match %d"
+                                % (indexname, n + 1))
+
+    def _map(self, suffix, dtype, count):
+        path = self.indexname + suffix
+        if not os.path.exists(path):
+            raise SmaxError("cannot open file \"%s\"" % path)
+        size = os.path.getsize(path)
+        if size != count * np.dtype(dtype).itemsize:
+            raise SmaxError("%s: number of mapped units (of size %d) = %d != %d"
+                            % (path, np.dtype(dtype).itemsize, size // np.dtype(dtype).itemsize,
+                               count))
+        return np.memmap(path, dtype=dtype, mode="r")
+
+    @staticmethod
+    def _read_prj(path):
+        if not os.path.exists(path):
+            raise SmaxError("cannot open file \"%s\"" % path)
+        out = {}
+        with open(path) as fh:
+            for line in fh:
+                line = line.strip()
+                if not line or line.startswith("dbfile="):
+                    continue
+                key, _, val = line.partition("=")
+                try:
+                    out[key] = float(val) if "." in val else int(val)
+                except ValueError:
+                    out[key] = val
+        return out
+
+    def separators(self):
+        """Separator positions = sort({suftab[k]-1 : bwt[k] == 255})
+        (equals the .ssp contents)."""
+        if self.suftab is None:
+            raise SmaxError("suftab required for sequence numbers")
+        k = np.flatnonzero(np.asarray(self.bwttab) == 255)
+        return np.sort(np.asarray(self.suftab)[k].astype(np.uint64) - 1)
+
+
+# ------------------------------------------------------------- host-buffer API
+
+def enumerate_smax(lcptab, llvtab, bwttab, totallength, nonspecials, minlen, num_gpus=1):
+    """All smax intervals as an (k,3) uint64 array of (lcp, lb, rb), lb ascending.
+
+    Thin wrapper over gt_smax_hip_enumerate_to_buffer."""
+    lcptab = np.ascontiguousarray(lcptab, dtype=np.uint8)
+    bwttab = np.ascontiguousarray(bwttab, dtype=np.uint8)
+    llvtab = np.ascontiguousarray(llvtab, dtype=np.uint64).reshape(-1, 2)
+    inp = GtSmaxInput()
+    inp.lcptab = lcptab.ctypes.data
+    inp.llvtab = llvtab.ctypes.data if len(llvtab) else None
+    inp.numllv = len(llvtab)
+    inp.bwttab = bwttab.ctypes.data
+    inp.suftab = None
+    inp.suftab_bytes = 0
+    inp.totallength = int(totallength)
+    inp.nonspecials = int(nonspecials)
+    out = ctypes.c_void_p()
+    cnt = ctypes.c_uint64()
+    eb = _errbuf()
+    rc = lib().gt_smax_hip_enumerate_to_buffer(ctypes.byref(inp), int(minlen), int(num_gpus),
+                                               ctypes.byref(out), ctypes.byref(cnt), eb, len(eb))
+    _check(rc, eb)
+    n = cnt.value
+    if n == 0:
+        if out.value:
+            lib().gt_smax_free(out)
+        return np.zeros((0, 3), dtype=np.uint64)
+    buf = (ctypes.c_uint64 * (3 * n)).from_address(out.value)
+    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).copy()
+    lib().gt_smax_free(out)
+    return arr
+
+
+def enumerate_index(index, minlen, num_gpus=1):
+    return enumerate_smax(index.lcptab, index.llvtab, index.bwttab, index.totallength,
+                          index.nonspecials, minlen, num_gpus)
+
+
+# ------------------------------------------------------------------ output
+
+def _seqnum(sep, p):
+    return np.searchsorted(sep, p, side="left")
+
+
+def repfind_smax_lines(intervals, suftab, separators):
+    """`gt repfind`-format lines for every occurrence pair of each interval.
+
+    Pairs are emitted per interval in occurrence order; each line orders
+    pos1 < pos2 and maps both to (seqnum, relpos) as
+    gt_simpleexactselfmatchoutput does (src/tools/gt_repfind.c:49-84)."""
+    sep = np.asarray(separators, dtype=np.uint64)
+    starts = np.concatenate([[0], sep + 1]).astype(np.uint64)
+    lines = []
+    for length, lb, rb in np.asarray(intervals, dtype=np.uint64):
+        occ = [int(suftab[k]) for k in range(int(lb), int(rb) + 1)]
+        for a in range(len(occ)):
+            for b in range(a + 1, len(occ)):
+                p1, p2 = min(occ[a], occ[b]), max(occ[a], occ[b])
+                s1, s2 = int(_seqnum(sep, p1)), int(_seqnum(sep, p2))
+                r1, r2 = p1 - int(starts[s1]), p2 - int(starts[s2])
+                if s1 == s2 and r1 > r2:
+                    continue
+                lines.append("%d %d %d F %d %d %d" % (length, s1, r1, length, s2, r2))
+    return lines
+
+
+# ------------------------------------------------------- device-resident API
+
+class DeviceTable:
+    """Padded device byte table (gt_smax_dev_alloc_table)."""
+
+    def __init__(self, device, length):
+        self.device = device
+        self.length = int(length)
+        p = ctypes.c_void_p()
+        eb = _errbuf()
+        _check(lib().gt_smax_dev_alloc_table(device, self.length, ctypes.byref(p), eb, len(eb)), eb)
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            lib().gt_smax_dev_free_table(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class SmaxPlan:
+    """One shard's smax pass over device-resident tables (gt_smax_plan_*).
+
+    lcp_ptr/bwt_ptr are device pointers laid out as GtSmaxDevShard requires
+    (DeviceTable, or torch tensors with PAD_FRONT/PAD_BACK slack)."""
+
+    def __init__(self, lcp_ptr, bwt_ptr, llv_ptr, numllv, base, local_len, begin, end,
+                 nonspecials, minlen, device=0, capacity=0):
+        sh = GtSmaxDevShard()
+        sh.lcp_dev, sh.bwt_dev, sh.llv_dev = lcp_ptr, bwt_ptr, llv_ptr
+        sh.numllv, sh.base, sh.local_len = int(numllv), int(base), int(local_len)
+        sh.begin, sh.end, sh.nonspecials, sh.device = int(begin), int(end), int(nonspecials), device
+        self.shard = sh
+        self.minlen = int(minlen)
+        p = ctypes.c_void_p()
+        eb = _errbuf()
+        _check(lib().gt_smax_plan_create(ctypes.byref(p), ctypes.byref(sh), self.minlen,
+                                         int(capacity), eb, len(eb)), eb)
+        self.plan = p.value
+
+    def run(self, stream=0):
+        if lib().gt_smax_plan_run(self.plan, stream or None) != 0:
+            raise SmaxError("gt_smax_plan_run failed")
+
+    def stitch(self, all_boundaries_ptr, nshards, shard_index, stream=0):
+        if lib().gt_smax_plan_stitch(self.plan, all_boundaries_ptr, nshards, shard_index,
+                                     stream or None) != 0:
+            raise SmaxError("gt_smax_plan_stitch failed")
+
+    @property
+    def records_ptr(self):
+        return lib().gt_smax_plan_records(self.plan)
+
+    @property
+    def count_ptr(self):
+        return lib().gt_smax_plan_count_dev(self.plan)
+
+    @property
+    def boundary_ptr(self):
+        return lib().gt_smax_plan_boundary_dev(self.plan)
+
+    @property
+    def capacity(self):
+        return lib().gt_smax_plan_capacity(self.plan)
+
+    @property
+    def num_tiles(self):
+        return lib().gt_smax_plan_num_tiles(self.plan)
+
+    def fetch_count(self):
+        c = ctypes.c_uint64()
+        if lib().gt_smax_plan_fetch_count(self.plan, ctypes.byref(c)) != 0:
+            raise SmaxError("gt_smax_plan_fetch_count failed")
+        return c.value
+
+    def close(self):
+        if self.plan:
+            lib().gt_smax_plan_delete(self.plan)
+            self.plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def stitch_host(boundaries, shard_index, minlen):
+    """Host form of the boundary stitch (pure function of the records)."""
+    arr = (GtSmaxBoundary * len(boundaries))(*boundaries)
+    rec = GtSmaxRecord()
+    ok = lib().gt_smax_stitch_host(arr, len(boundaries), shard_index, int(minlen), ctypes.byref(rec))
+    if ok:
+        return (int(rec.lcp), int(rec.lb), int(rec.lb) + int(rec.width) - 1)
+    return None
+
+
+def device_count():
+    return lib().gt_smax_device_count()

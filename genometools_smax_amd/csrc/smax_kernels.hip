@@ -1,0 +1,998 @@
+// smax_kernels.hip -- CDNA4 (gfx950) kernels for the supermaximal-repeat
+// hot path, plus the C-ABI declared in include/gt_smax_hip.h.
+//
+// Replaces the serial stack walk of gt_esa_bottomup
+// (src/match/esa-bottomup.c:116-273, specialised at
+// src/match/esa-bottomup-maxpairs.inc:136-264) by a data-parallel plateau
+// segmentation of the LCP array.  An smax interval [lb..rb] of lcp-value l
+//  is a maximal run LCP[lb+1..rb] == l with
+// LCP[lb] < l and LCP[rb+1] < l (a leaf-only lcp-interval: the interval the
+// reference pops without a branching edge), l >= minlen, whose BWT symbols
+// BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
+// src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
+//
+// Kernel K1 (smax_scan_kernel), one 256-thread workgroup per 16384-row tile:
+//   phase 0  coalesced 16 B/lane loads of the tile's LCP bytes into
+//            registers + LDS (plus a 16-byte left and 64-byte right halo);
+//   phase 1  per 16-byte segment a SWAR pre-filter (any byte >= minlen);
+//            surviving rows test "plateau start" LCP[c] > LCP[c-1] and scan
+//            the plateau to its end in LDS (255 bytes resolved through an
+//            LDS copy of the tile's .llv window);
+//   phase 2  only if the tile has a local-maximum candidate, the tile's BWT
+//            bytes are loaded (coalesced) into LDS -- uniform DNA at
+//            minlen 20 never touches .bwt;
+//   phase 3  left-diversity: 256-bit seen-set over BWT[lb..rb];
+//   phase 4  block scan of per-thread counts, decoupled look-back across
+//            tiles (tile order from an atomic ticket, status words with
+//            epoch tags read/written with agent-scope relaxed atomics),
+//            ordered write of 16-byte records -> output is ascending lb,
+//            exactly the order the reference's traversal pops intervals.
+// No MFMA: integer/byte work bounded by HBM bandwidth.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gt_smax_hip.h"
+
+#define SMAX_THREADS 256
+#define SMAX_SEGS 4                                   // uint4 per thread
+#define SMAX_WAVE_BYTES (SMAX_SEGS * 64 * 16)         // 4096 rows per wave
+#define SMAX_TILE (SMAX_THREADS * SMAX_SEGS * 16)     // 16384 rows per tile
+#define SMAX_LH 16                                    // left halo (bytes)
+#define SMAX_RH 64                                    // right halo (bytes)
+#define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)
+#define SMAX_LLV_CAP 512
+
+#define ST_FLAG_AGG 1ull
+#define ST_FLAG_PFX 2ull
+#define ST_EPOCH_BITS 22
+#define ST_VALUE_BITS 40
+#define ST_VALUE_MASK ((1ull << ST_VALUE_BITS) - 1)
+#define ST_EPOCH_MASK ((1ull << ST_EPOCH_BITS) - 1)
+
+static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
+              "back padding must cover a whole tile plus halo");
+static_assert(GT_SMAX_PAD_FRONT >= SMAX_LH, "front padding covers the halo");
+
+struct SmaxScanArgs {
+  const uint8_t *lcp;        // local tables: index i <-> global base+i
+  const uint8_t *bwt;
+  const GtSmaxLlv *llv;      // shard's llv entries (global positions)
+  uint64_t numllv;
+  const uint32_t *llv_lo;    // per tile: first llv index >= tile_g0 - LH
+  const uint32_t *llv_hi;    // per tile: first llv index >= tile_g1 + RH
+  uint64_t base, begin, end, N;
+  uint32_t minlen;
+  uint32_t num_tiles;
+  GtSmaxRecord *out;
+  uint64_t capacity;
+  uint64_t *status;
+  unsigned long long *ticket;
+  uint64_t ticket_base;
+  uint64_t epoch;
+  uint64_t *count;
+  GtSmaxBoundary *bnd;
+};
+
+// ------------------------------------------------------------ helpers
+
+__device__ __forceinline__ uint64_t ld_status(uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exact LCP value from the global .llv (binary search in [lo, hi))
+__device__ static uint32_t llv_search_global(const GtSmaxLlv *llv, uint64_t lo,
+                                             uint64_t hi, uint64_t g) {
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    uint64_t p = llv[mid].position;
+    if (p < g) lo = mid + 1; else hi = mid;
+  }
+  return (uint32_t) llv[lo].value;   // present by construction of .llv
+}
+
+struct TileCtx {
+  const uint8_t *glcp;        // global (local-indexed) tables
+  const uint8_t *gbwt;
+  const GtSmaxLlv *llv;
+  uint64_t numllv, base, N, end;
+  const uint8_t *L;           // LDS L window, index = g - w0
+  const uint8_t *B;           // LDS B window
+  const uint32_t *lpos;       // LDS llv positions (g - w0)
+  const uint32_t *lval;
+  int nllv;                   // -1: not in LDS, search global [glo, ghi)
+  uint64_t glo, ghi;
+  uint64_t w0, w1;            // global window [w0, w1) held in LDS
+};
+
+// exact LCP[g] (g global), L[0] = L[N] = 0
+__device__ static uint32_t lcp_at(const TileCtx &t, uint64_t g) {
+  if (g == 0 || g >= t.N) return 0;
+  uint32_t b;
+  bool inwin = (g >= t.w0 && g < t.w1);
+  if (inwin) b = t.L[g - t.w0];
+  else b = t.glcp[g - t.base];
+  if (b < 255) return b;
+  if (inwin && t.nllv >= 0) {
+    uint32_t key = (uint32_t) (g - t.w0);
+    int lo = 0, hi = t.nllv;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (t.lpos[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return t.lval[lo];
+  }
+  if (inwin) return llv_search_global(t.llv, t.glo, t.ghi, g);
+  return llv_search_global(t.llv, 0, t.numllv, g);
+}
+
+__device__ __forceinline__ uint32_t bwt_at(const TileCtx &t, uint64_t g) {
+  if (g >= t.w0 && g < t.w1) return t.B[g - t.w0];
+  return t.gbwt[g - t.base];
+}
+
+// Any byte of w >= m (m <= 128); superset filter for larger m.
+// (both return a mask whose high bits mark the qualifying bytes)
+__device__ __forceinline__ uint32_t any_byte_ge(uint32_t w, uint32_t m) {
+  uint32_t add = (128u - m) * 0x01010101u;
+  return (w | ((w & 0x7f7f7f7fu) + add)) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t any_byte_ff(uint32_t w) {
+  uint32_t x = ~w;
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
+// Plateau scan from start c (LCP[c] == l): returns j (last row of the run)
+// and sets *next to LCP[j+1]; *pending when the run reaches the shard end.
+__device__ static uint64_t plateau_end(const TileCtx &t, uint64_t c, uint32_t l,
+                                       uint32_t *next, bool *pending) {
+  uint64_t j = c;
+  *pending = false;
+  for (;;) {
+    uint64_t g = j + 1;
+    uint32_t nx = lcp_at(t, g);
+    if (nx != l) { *next = nx; return j; }
+    if (g >= t.end) { *pending = true; *next = nx; return j; }  // g == end < N
+    j = g;
+  }
+}
+
+__device__ __forceinline__ void ctx_init(TileCtx &t, const SmaxScanArgs &a) {
+  t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
+  t.base = a.base; t.N = a.N; t.end = a.end;
+}
+
+struct Seen {
+  uint64_t w0, w1, w2, w3;
+};
+__device__ __forceinline__ bool seen_add(Seen &s, uint32_t c) {
+  if (c >= 254) return false;
+  const uint64_t bit = 1ull << (c & 63);
+  const uint32_t wi = c >> 6;
+  const uint64_t cur = wi == 0 ? s.w0 : wi == 1 ? s.w1 : wi == 2 ? s.w2 : s.w3;
+  s.w0 |= wi == 0 ? bit : 0;
+  s.w1 |= wi == 1 ? bit : 0;
+  s.w2 |= wi == 2 ? bit : 0;
+  s.w3 |= wi == 3 ? bit : 0;
+  return (cur & bit) != 0;
+}
+
+// ------------------------------------------------------------ K0: head run
+
+// One wave: the boundary record's head (run of LCP == LCP[begin]) and reset
+// of the pending slot.  Runs before K1 on the same stream.
+__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
+  if (threadIdx.x != 0) return;
+  TileCtx t;
+  ctx_init(t, a);
+  t.L = nullptr; t.B = nullptr; t.lpos = nullptr; t.lval = nullptr;
+  t.nllv = -1; t.glo = 0; t.ghi = a.numllv; t.w0 = 0; t.w1 = 0;
+  GtSmaxBoundary *b = a.bnd;
+  b->pend_valid = 0;
+  b->shard_begin = a.begin;
+  b->shard_end = a.end;
+  uint32_t v = lcp_at(t, a.begin);
+  b->head_v = v;
+  Seen s = {0, 0, 0, 0};
+  uint64_t dup = 0;
+  uint64_t f = UINT64_MAX, nxt = 0;
+  if (v >= a.minlen && a.begin < a.end) {
+    uint64_t g = a.begin;
+    for (;;) {
+      if (seen_add(s, a.bwt[g - a.base])) { dup = 1; break; }
+      uint64_t h = g + 1;
+      uint32_t nx = lcp_at(t, h);
+      if (nx != v) { f = h; nxt = nx; break; }
+      if (h >= a.end) break;   // run covers the whole shard: passthrough
+      g = h;
+    }
+  } else {
+    f = a.begin;   // irrelevant head: no pending plateau can continue here
+    nxt = v;
+  }
+  b->head_f = f;
+  b->head_next = nxt;
+  b->head_div.seen[0] = s.w0; b->head_div.seen[1] = s.w1;
+  b->head_div.seen[2] = s.w2; b->head_div.seen[3] = s.w3;
+  b->head_div.dup = dup;
+}
+
+// ------------------------------------------------------------ K1: scan
+
+__global__ void __launch_bounds__(SMAX_THREADS)
+smax_scan_kernel(SmaxScanArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sL[SMAX_LDSB];
+  __shared__ __attribute__((aligned(16))) uint8_t sB[SMAX_LDSB];
+  __shared__ uint32_t sLpos[SMAX_LLV_CAP];
+  __shared__ uint32_t sLval[SMAX_LLV_CAP];
+  __shared__ uint32_t sWaveSum[SMAX_THREADS / 64];
+  __shared__ uint64_t sTile, sExcl;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  if (tid == 0) {
+    unsigned long long old = atomicAdd(a.ticket, 1ull);
+    sTile = old - a.ticket_base;
+  }
+  __syncthreads();
+  const uint64_t tile = sTile;
+  const uint64_t l0 = tile * (uint64_t) SMAX_TILE;       // local index
+  const uint64_t g0 = a.base + l0;                         // global index
+  const uint64_t w0 = g0 - SMAX_LH;                        // LDS window start
+
+  // ---- phase 0: coalesced L loads (registers + LDS)
+  uint4 seg[SMAX_SEGS];
+  const uint8_t *lsrc = a.lcp + l0;
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    uint32_t off = wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+    seg[r] = *reinterpret_cast<const uint4 *>(lsrc + off);
+    *reinterpret_cast<uint4 *>(&sL[SMAX_LH + off]) = seg[r];
+  }
+  if (tid < 5) {   // halo: 16 bytes left, 64 bytes right
+    int64_t off = (tid == 0) ? -SMAX_LH : (int64_t) SMAX_TILE + (tid - 1) * 16;
+    *reinterpret_cast<uint4 *>(&sL[SMAX_LH + off]) =
+        *reinterpret_cast<const uint4 *>(lsrc + off);
+  }
+  uint32_t has_ff = 0;
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++)
+    has_ff |= any_byte_ff(seg[r].x) | any_byte_ff(seg[r].y) |
+              any_byte_ff(seg[r].z) | any_byte_ff(seg[r].w);
+  __syncthreads();
+  if (tid < 5) {
+    const uint8_t *h = &sL[tid == 0 ? 0 : SMAX_LH + SMAX_TILE + (tid - 1) * 16];
+    uint4 hv = *reinterpret_cast<const uint4 *>(h);
+    has_ff |= any_byte_ff(hv.x) | any_byte_ff(hv.y) | any_byte_ff(hv.z) |
+              any_byte_ff(hv.w);
+  }
+  const bool tile_ff = __syncthreads_or(has_ff != 0);
+
+  TileCtx t;
+  ctx_init(t, a);
+  t.L = sL; t.B = sB; t.lpos = sLpos; t.lval = sLval;
+  t.w0 = w0; t.w1 = w0 + SMAX_LDSB;
+  t.nllv = 0; t.glo = 0; t.ghi = 0;
+  if (tile_ff) {
+    uint64_t lo = a.llv_lo[tile], hi = a.llv_hi[tile];
+    t.glo = lo; t.ghi = hi;
+    if (hi - lo <= SMAX_LLV_CAP) {
+      for (uint64_t i = lo + tid; i < hi; i += SMAX_THREADS) {
+        sLpos[i - lo] = (uint32_t) (a.llv[i].position - w0);
+        sLval[i - lo] = (uint32_t) a.llv[i].value;
+      }
+      t.nllv = (int) (hi - lo);
+    } else {
+      t.nllv = -1;
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 1: plateau starts that are local maxima (L only)
+  const uint32_t m = a.minlen;
+  const uint32_t mf = m < 128 ? m : 128;
+  uint64_t cand = 0;          // bit r*16+q: row is a local-maximum start
+  bool pend_here = false;
+  uint64_t pend_c = 0;
+  uint32_t pend_l = 0;
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    const uint4 v = seg[r];
+    if ((any_byte_ge(v.x, mf) | any_byte_ge(v.y, mf) | any_byte_ge(v.z, mf) |
+         any_byte_ge(v.w, mf)) == 0)
+      continue;
+    const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+    const uint64_t lo8 = (uint64_t) v.x | ((uint64_t) v.y << 32);
+    const uint64_t hi8 = (uint64_t) v.z | ((uint64_t) v.w << 32);
+    for (int q = 0; q < 16; q++) {
+      uint32_t byte = (uint32_t) (((q < 8) ? (lo8 >> (8 * q)) : (hi8 >> (8 * (q - 8)))) & 0xffu);
+      if (byte < 255 && byte < m) continue;
+      const uint64_t c = sg + q;
+      if (c < a.begin || c >= a.end) continue;
+      uint32_t cur = lcp_at(t, c);
+      if (cur < m) continue;
+      uint32_t prev = lcp_at(t, c - 1);
+      if (cur <= prev) continue;
+      uint32_t nx;
+      bool pend;
+      uint64_t j = plateau_end(t, c, cur, &nx, &pend);
+      (void) j;
+      if (pend) {
+        pend_here = true; pend_c = c; pend_l = cur;
+      } else if (nx < cur) {
+        cand |= 1ull << (r * 16 + q);
+      }
+    }
+  }
+
+  // ---- phase 2: BWT tile only when some row needs it
+  const bool need_b = __syncthreads_or(cand != 0 || pend_here);
+  if (need_b) {
+    const uint8_t *bsrc = a.bwt + l0;
+#pragma unroll
+    for (int r = 0; r < SMAX_SEGS; r++) {
+      uint32_t off = wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+      *reinterpret_cast<uint4 *>(&sB[SMAX_LH + off]) =
+          *reinterpret_cast<const uint4 *>(bsrc + off);
+    }
+    if (tid < 5) {
+      int64_t off = (tid == 0) ? -SMAX_LH : (int64_t) SMAX_TILE + (tid - 1) * 16;
+      *reinterpret_cast<uint4 *>(&sB[SMAX_LH + off]) =
+          *reinterpret_cast<const uint4 *>(bsrc + off);
+    }
+    __syncthreads();
+  }
+
+  // ---- phase 3: left-diversity
+  uint64_t tmp = cand;
+  while (tmp) {
+    int bit = __builtin_ctzll(tmp);
+    tmp &= tmp - 1;
+    int r = bit >> 4, q = bit & 15;
+    uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
+    uint32_t cur = lcp_at(t, c), nx;
+    bool pend;
+    uint64_t j = plateau_end(t, c, cur, &nx, &pend);
+    Seen s = {0, 0, 0, 0};
+    bool dup = false;
+    for (uint64_t g = c - 1; g <= j && !dup; g++) dup = seen_add(s, bwt_at(t, g));
+    if (dup) cand &= ~(1ull << bit);
+  }
+  if (pend_here) {
+    Seen s = {0, 0, 0, 0};
+    bool dup = false;
+    for (uint64_t g = pend_c - 1; g < a.end && !dup; g++)
+      dup = seen_add(s, bwt_at(t, g));
+    if (!dup) {
+      GtSmaxBoundary *b = a.bnd;
+      b->pend_c = pend_c;
+      b->pend_lcp = pend_l;
+      b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
+      b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
+      b->pend_div.dup = 0;
+      b->pend_valid = 1;
+    }
+  }
+
+  // ---- phase 4: block scan of counts
+  uint32_t mycount = (uint32_t) __popcll(cand);
+  uint32_t incl = mycount;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) sWaveSum[wave] = incl;
+  __syncthreads();
+  uint32_t wave_off = 0, tile_count = 0;
+#pragma unroll
+  for (int w = 0; w < SMAX_THREADS / 64; w++) {
+    uint32_t ws = sWaveSum[w];
+    if (w < wave) wave_off += ws;
+    tile_count += ws;
+  }
+  const uint32_t my_off = wave_off + incl - mycount;
+
+  // ---- phase 5: decoupled look-back (wave 0)
+  const uint64_t ep = (a.epoch & ST_EPOCH_MASK) << ST_VALUE_BITS;
+  if (wave == 0) {
+    uint64_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0)
+        st_status(&a.status[0], (ST_FLAG_PFX << 62) | ep | (uint64_t) tile_count);
+    } else {
+      if (lane == 0)
+        st_status(&a.status[tile], (ST_FLAG_AGG << 62) | ep | (uint64_t) tile_count);
+      int64_t pos = (int64_t) tile - 1;
+      for (;;) {
+        int64_t idx = pos - lane;
+        uint64_t sv;
+        if (idx >= 0) sv = ld_status(&a.status[idx]);
+        else sv = (ST_FLAG_PFX << 62) | ep;    // virtual prefix 0 before tile 0
+        uint64_t flag = sv >> 62;
+        bool valid = flag != 0 && ((sv >> ST_VALUE_BITS) & ST_EPOCH_MASK) ==
+                                      (a.epoch & ST_EPOCH_MASK);
+        bool ispfx = valid && flag == ST_FLAG_PFX;
+        uint64_t pfx_mask = __ballot(ispfx);
+        uint64_t inv_mask = __ballot(!valid);
+        // lanes up to and including the first prefix must all be valid
+        uint64_t upto = pfx_mask ? ((pfx_mask & (~pfx_mask + 1)) << 1) - 1 : ~0ull;
+        if (pfx_mask == (1ull << 63)) upto = ~0ull;
+        if (inv_mask & upto) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint64_t val = (lane < 64 && ((upto >> lane) & 1)) ? (sv & ST_VALUE_MASK) : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
+        excl += val;
+        if (pfx_mask) break;
+        pos -= 64;
+      }
+      if (lane == 0)
+        st_status(&a.status[tile],
+                  (ST_FLAG_PFX << 62) | ep | ((excl + tile_count) & ST_VALUE_MASK));
+    }
+    if (lane == 0) {
+      sExcl = excl;
+      if (tile == a.num_tiles - 1) *a.count = excl + tile_count;
+    }
+  }
+  __syncthreads();
+  const uint64_t base_out = sExcl + my_off;
+
+  // ---- phase 6: ordered record writes
+  tmp = cand;
+  uint64_t k = 0;
+  while (tmp) {
+    int bit = __builtin_ctzll(tmp);
+    tmp &= tmp - 1;
+    int r = bit >> 4, q = bit & 15;
+    uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
+    uint32_t cur = lcp_at(t, c), nx;
+    bool pend;
+    uint64_t j = plateau_end(t, c, cur, &nx, &pend);
+    uint64_t o = base_out + k++;
+    if (o < a.capacity) {
+      GtSmaxRecord rec;
+      rec.lb = c - 1;
+      rec.lcp = cur;
+      rec.width = (uint32_t) (j - c + 2);
+      a.out[o] = rec;
+    }
+  }
+}
+
+// ------------------------------------------------------------ llv index
+
+__global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
+                                      uint64_t base, uint32_t num_tiles,
+                                      uint32_t *lo_out, uint32_t *hi_out,
+                                      uint32_t *err) {
+  uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (t < numllv) {
+    if (llv[t].value > 0xffffffffull) atomicOr(err, 1u);
+    if (t > 0 && llv[t].position <= llv[t - 1].position) atomicOr(err, 2u);
+  }
+  if (t >= num_tiles) return;
+  uint64_t g0 = base + t * (uint64_t) SMAX_TILE;
+  uint64_t keys[2] = {g0 >= SMAX_LH ? g0 - SMAX_LH : 0, g0 + SMAX_TILE + SMAX_RH};
+  for (int s = 0; s < 2; s++) {
+    uint64_t lo = 0, hi = numllv;
+    while (lo < hi) {
+      uint64_t mid = (lo + hi) >> 1;
+      if (llv[mid].position < keys[s]) lo = mid + 1; else hi = mid;
+    }
+    if (s == 0) lo_out[t] = (uint32_t) lo; else hi_out[t] = (uint32_t) lo;
+  }
+}
+
+// ------------------------------------------------------------ stitch
+
+__host__ __device__ static int stitch_resolve(const GtSmaxBoundary *all,
+                                              int nshards, int idx,
+                                              unsigned int minlen,
+                                              GtSmaxRecord *rec) {
+  const GtSmaxBoundary *me = &all[idx];
+  if (!me->pend_valid) return 0;
+  uint64_t l = me->pend_lcp;
+  uint64_t seen[4] = {me->pend_div.seen[0], me->pend_div.seen[1],
+                      me->pend_div.seen[2], me->pend_div.seen[3]};
+  (void) minlen;
+  for (int r = idx + 1; r < nshards; r++) {
+    const GtSmaxBoundary *h = &all[r];
+    if (h->head_v != l) return 0;          // cannot happen: LCP[end] == l
+    if (h->head_div.dup) return 0;
+    for (int w = 0; w < 4; w++) {
+      if (seen[w] & h->head_div.seen[w]) return 0;
+      seen[w] |= h->head_div.seen[w];
+    }
+    if (h->head_f != UINT64_MAX) {
+      if (h->head_next >= l) return 0;     // not a local maximum
+      uint64_t lb = me->pend_c - 1, rb = h->head_f - 1;
+      rec->lb = lb;
+      rec->lcp = (uint32_t) l;
+      rec->width = (uint32_t) (rb - lb + 1);
+      return 1;
+    }
+  }
+  return 0;   // last shard always ends the run (LCP[N] == 0)
+}
+
+__global__ void smax_stitch_kernel(const GtSmaxBoundary *all, int nshards,
+                                   int idx, unsigned int minlen,
+                                   GtSmaxRecord *out, uint64_t capacity,
+                                   uint64_t *count) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  GtSmaxRecord rec;
+  if (stitch_resolve(all, nshards, idx, minlen, &rec)) {
+    uint64_t c = *count;
+    if (c < capacity) out[c] = rec;
+    *count = c + 1;
+  }
+}
+
+// ============================================================ host side
+
+static void seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
+  if (errbuf == NULL || errlen == 0) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(errbuf, errlen, fmt, ap);
+  va_end(ap);
+}
+
+#define HIPCHK(call)                                                         \
+  do {                                                                       \
+    hipError_t e_ = (call);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      seterr(errbuf, errlen, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
+             __FILE__, __LINE__);                                            \
+      goto fail;                                                             \
+    }                                                                        \
+  } while (0)
+
+struct GtSmaxPlan {
+  GtSmaxDevShard shard;
+  unsigned int minlen;
+  uint64_t capacity;
+  uint32_t num_tiles;
+  GtSmaxRecord *out;
+  uint64_t *status;
+  unsigned long long *ticket;
+  uint64_t ticket_base;
+  uint64_t epoch;
+  uint64_t *count;
+  GtSmaxBoundary *bnd;
+  uint32_t *llv_lo, *llv_hi;
+};
+
+extern "C" int gt_smax_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" void gt_smax_free(void *ptr) { free(ptr); }
+
+extern "C" int gt_smax_dev_alloc_table(int device, uint64_t len,
+                                       uint8_t **table, char *errbuf,
+                                       size_t errlen) {
+  uint8_t *p = NULL;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(&p, len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
+  HIPCHK(hipMemset(p, 0, GT_SMAX_PAD_FRONT));
+  HIPCHK(hipMemset(p + GT_SMAX_PAD_FRONT + len, 0, GT_SMAX_PAD_BACK));
+  *table = p + GT_SMAX_PAD_FRONT;
+  return 0;
+fail:
+  if (p) (void) hipFree(p);
+  return -1;
+}
+
+extern "C" int gt_smax_dev_free_table(int device, uint8_t *table) {
+  if (table == NULL) return 0;
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  return hipFree(table - GT_SMAX_PAD_FRONT) == hipSuccess ? 0 : -1;
+}
+
+static uint32_t plan_tiles(const GtSmaxDevShard *s) {
+  uint64_t rows = s->end > s->base ? s->end - s->base : 1;
+  return (uint32_t) ((rows + SMAX_TILE - 1) / SMAX_TILE);
+}
+
+extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
+                                   const GtSmaxDevShard *shard,
+                                   unsigned int minlen, uint64_t capacity,
+                                   char *errbuf, size_t errlen) {
+  GtSmaxPlan *p = (GtSmaxPlan *) calloc(1, sizeof *p);
+  uint32_t *derr = NULL;
+  uint32_t herr = 0;
+  *planp = NULL;
+  if (p == NULL) { seterr(errbuf, errlen, "out of memory"); return -1; }
+  if (minlen == 0) { seterr(errbuf, errlen, "minlen must be >= 1"); free(p); return -1; }
+  if (shard->begin < 1 || shard->begin > shard->end ||
+      shard->end > shard->nonspecials || shard->base + 1 > shard->begin ||
+      shard->base + shard->local_len <= shard->end) {
+    seterr(errbuf, errlen,
+           "bad shard: base=%lu len=%lu begin=%lu end=%lu N=%lu",
+           (unsigned long) shard->base, (unsigned long) shard->local_len,
+           (unsigned long) shard->begin, (unsigned long) shard->end,
+           (unsigned long) shard->nonspecials);
+    free(p);
+    return -1;
+  }
+  if (((uintptr_t) shard->lcp_dev & 15) || ((uintptr_t) shard->bwt_dev & 15)) {
+    seterr(errbuf, errlen, "device tables must be 16-byte aligned");
+    free(p);
+    return -1;
+  }
+  p->shard = *shard;
+  p->minlen = minlen;
+  p->num_tiles = plan_tiles(shard);
+  if (capacity == 0) {
+    uint64_t rows = shard->end - shard->begin;
+    capacity = rows / 64 + 4096;
+  }
+  p->capacity = capacity;
+  p->epoch = 1;
+  HIPCHK(hipSetDevice(shard->device));
+  HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
+  HIPCHK(hipMalloc(&p->status, sizeof (uint64_t) * p->num_tiles));
+  HIPCHK(hipMemset(p->status, 0, sizeof (uint64_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&p->ticket, sizeof (unsigned long long)));
+  HIPCHK(hipMemset(p->ticket, 0, sizeof (unsigned long long)));
+  HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
+  HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
+  HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
+  HIPCHK(hipMemset(p->bnd, 0, sizeof (GtSmaxBoundary)));
+  HIPCHK(hipMalloc(&p->llv_lo, sizeof (uint32_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&p->llv_hi, sizeof (uint32_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&derr, sizeof (uint32_t)));
+  HIPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
+  if (shard->numllv > 0xffffffffull) {
+    seterr(errbuf, errlen, "more than 2^32 .llv entries in one shard");
+    goto fail;
+  }
+  {
+    uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
+    unsigned blocks = (unsigned) ((work + 255) / 256);
+    hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
+                       shard->llv_dev, shard->numllv, shard->base,
+                       p->num_tiles, p->llv_lo, p->llv_hi, derr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
+  }
+  if (herr & 1u) { seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
+  if (herr & 2u) { seterr(errbuf, errlen, ".llv positions not strictly increasing"); goto fail; }
+  (void) hipFree(derr);
+  *planp = p;
+  return 0;
+fail:
+  if (derr) (void) hipFree(derr);
+  gt_smax_plan_delete(p);
+  return -1;
+}
+
+extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
+  if (p == NULL) return;
+  (void) hipSetDevice(p->shard.device);
+  if (p->out) (void) hipFree(p->out);
+  if (p->status) (void) hipFree(p->status);
+  if (p->ticket) (void) hipFree(p->ticket);
+  if (p->count) (void) hipFree(p->count);
+  if (p->bnd) (void) hipFree(p->bnd);
+  if (p->llv_lo) (void) hipFree(p->llv_lo);
+  if (p->llv_hi) (void) hipFree(p->llv_hi);
+  free(p);
+}
+
+static SmaxScanArgs plan_args(GtSmaxPlan *p) {
+  SmaxScanArgs a;
+  a.lcp = p->shard.lcp_dev;
+  a.bwt = p->shard.bwt_dev;
+  a.llv = p->shard.llv_dev;
+  a.numllv = p->shard.numllv;
+  a.llv_lo = p->llv_lo;
+  a.llv_hi = p->llv_hi;
+  a.base = p->shard.base;
+  a.begin = p->shard.begin;
+  a.end = p->shard.end;
+  a.N = p->shard.nonspecials;
+  a.minlen = p->minlen;
+  a.num_tiles = p->num_tiles;
+  a.out = p->out;
+  a.capacity = p->capacity;
+  a.status = p->status;
+  a.ticket = p->ticket;
+  a.ticket_base = p->ticket_base;
+  a.epoch = p->epoch;
+  a.count = p->count;
+  a.bnd = p->bnd;
+  return a;
+}
+
+extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  hipStream_t s = (hipStream_t) stream;
+  HIPCHK(hipSetDevice(p->shard.device));
+  if (p->epoch >= ST_EPOCH_MASK) {   // wrap: clear stale status words
+    HIPCHK(hipMemsetAsync(p->status, 0, sizeof (uint64_t) * p->num_tiles, s));
+    p->epoch = 1;
+  }
+  {
+    SmaxScanArgs a = plan_args(p);
+    if (p->shard.begin >= p->shard.end) {
+      HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
+      hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
+    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(smax_scan_kernel, dim3(p->num_tiles), dim3(SMAX_THREADS),
+                       0, s, a);
+    HIPCHK(hipGetLastError());
+  }
+  p->ticket_base += p->num_tiles;
+  p->epoch += 1;
+  return 0;
+fail:
+  return -1;
+}
+
+extern "C" GtSmaxRecord *gt_smax_plan_records(GtSmaxPlan *p) { return p->out; }
+extern "C" uint64_t *gt_smax_plan_count_dev(GtSmaxPlan *p) { return p->count; }
+extern "C" GtSmaxBoundary *gt_smax_plan_boundary_dev(GtSmaxPlan *p) { return p->bnd; }
+extern "C" uint64_t gt_smax_plan_capacity(GtSmaxPlan *p) { return p->capacity; }
+extern "C" uint64_t gt_smax_plan_num_tiles(GtSmaxPlan *p) { return p->num_tiles; }
+
+extern "C" int gt_smax_plan_stitch(GtSmaxPlan *p, const GtSmaxBoundary *all_dev,
+                                   int nshards, int shard_index, void *stream) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  HIPCHK(hipSetDevice(p->shard.device));
+  hipLaunchKernelGGL(smax_stitch_kernel, dim3(1), dim3(64), 0,
+                     (hipStream_t) stream, all_dev, nshards, shard_index,
+                     p->minlen, p->out, p->capacity, p->count);
+  HIPCHK(hipGetLastError());
+  return 0;
+fail:
+  return -1;
+}
+
+extern "C" int gt_smax_stitch_host(const GtSmaxBoundary *all, int nshards,
+                                   int shard_index, unsigned int minlen,
+                                   GtSmaxRecord *rec) {
+  return stitch_resolve(all, nshards, shard_index, minlen, rec);
+}
+
+extern "C" int gt_smax_plan_fetch_count(GtSmaxPlan *p, uint64_t *count) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  HIPCHK(hipSetDevice(p->shard.device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(count, p->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
+  return 0;
+fail:
+  return -1;
+}
+
+// ---------------------------------------------------- host-buffer API
+
+struct ShardRun {
+  GtSmaxDevShard sh;
+  uint8_t *lcp, *bwt;
+  GtSmaxLlv *llv;
+  GtSmaxPlan *plan;
+  hipStream_t stream;
+};
+
+static int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
+  if (in == NULL || in->lcptab == NULL || in->bwttab == NULL) {
+    seterr(errbuf, errlen, "missing lcptab or bwttab");
+    return -1;
+  }
+  if (in->numllv > 0 && in->llvtab == NULL) {
+    seterr(errbuf, errlen, "missing llvtab");
+    return -1;
+  }
+  if (in->nonspecials > in->totallength) {
+    seterr(errbuf, errlen, "nonspecials (%lu) exceeds totallength (%lu)",
+           (unsigned long) in->nonspecials, (unsigned long) in->totallength);
+    return -1;
+  }
+  for (uint64_t i = 0; i < in->numllv; i++) {
+    if (in->llvtab[i].position > in->totallength ||
+        (i > 0 && in->llvtab[i].position <= in->llvtab[i - 1].position) ||
+        in->lcptab[in->llvtab[i].position] != 255) {
+      seterr(errbuf, errlen, "inconsistent .llv entry %lu", (unsigned long) i);
+      return -1;
+    }
+  }
+  return 0;
+}
+
+static uint64_t llv_lower(const GtSmaxInput *in, uint64_t g) {
+  uint64_t lo = 0, hi = in->numllv;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (in->llvtab[mid].position < g) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
+                      uint64_t **trip_out, uint64_t *count_out, char *errbuf,
+                      size_t errlen) {
+  const uint64_t N = in->nonspecials;
+  int ndev = gt_smax_device_count();
+  ShardRun *runs = NULL;
+  GtSmaxBoundary *bnds = NULL;
+  uint64_t *counts = NULL, total = 0, *trip = NULL;
+  int rc = -1;
+  *trip_out = NULL;
+  *count_out = 0;
+  if (ndev <= 0) {
+    seterr(errbuf, errlen, "no HIP device available");
+    return -1;
+  }
+  if (N < 2) {
+    *trip_out = (uint64_t *) malloc(sizeof (uint64_t));
+    return 0;
+  }
+  if (nshards < 1) nshards = 1;
+  if ((uint64_t) nshards > N - 1) nshards = (int) (N - 1);
+  runs = (ShardRun *) calloc((size_t) nshards, sizeof *runs);
+  bnds = (GtSmaxBoundary *) calloc((size_t) nshards, sizeof *bnds);
+  counts = (uint64_t *) calloc((size_t) nshards, sizeof *counts);
+  if (!runs || !bnds || !counts) {
+    seterr(errbuf, errlen, "out of memory");
+    goto fail;
+  }
+  for (int s = 0; s < nshards; s++) {
+    ShardRun *r = &runs[s];
+    uint64_t begin = 1 + (N - 1) * (uint64_t) s / (uint64_t) nshards;
+    uint64_t end = 1 + (N - 1) * (uint64_t) (s + 1) / (uint64_t) nshards;
+    uint64_t base = begin - 1;
+    uint64_t len = end - base + 1;           // LCP[base .. end]
+    uint64_t lo = llv_lower(in, base), hi = llv_lower(in, base + len);
+    r->sh.device = s % ndev;
+    HIPCHK(hipSetDevice(r->sh.device));
+    HIPCHK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    if (gt_smax_dev_alloc_table(r->sh.device, len, &r->lcp, errbuf, errlen)) goto fail;
+    if (gt_smax_dev_alloc_table(r->sh.device, len, &r->bwt, errbuf, errlen)) goto fail;
+    HIPCHK(hipMemcpyAsync(r->lcp, in->lcptab + base, len, hipMemcpyHostToDevice, r->stream));
+    {
+      uint64_t blen = len <= in->totallength + 1 - base ? len : in->totallength + 1 - base;
+      HIPCHK(hipMemcpyAsync(r->bwt, in->bwttab + base, blen, hipMemcpyHostToDevice, r->stream));
+    }
+    HIPCHK(hipMalloc(&r->llv, sizeof (GtSmaxLlv) * (hi - lo + 1)));
+    if (hi > lo)
+      HIPCHK(hipMemcpyAsync(r->llv, in->llvtab + lo, sizeof (GtSmaxLlv) * (hi - lo),
+                            hipMemcpyHostToDevice, r->stream));
+    HIPCHK(hipStreamSynchronize(r->stream));
+    r->sh.lcp_dev = r->lcp;
+    r->sh.bwt_dev = r->bwt;
+    r->sh.llv_dev = r->llv;
+    r->sh.numllv = hi - lo;
+    r->sh.base = base;
+    r->sh.local_len = len;
+    r->sh.begin = begin;
+    r->sh.end = end;
+    r->sh.nonspecials = N;
+    if (gt_smax_plan_create(&r->plan, &r->sh, minlen, 0, errbuf, errlen)) goto fail;
+    if (gt_smax_plan_run(r->plan, r->stream)) goto fail;
+  }
+  for (int s = 0; s < nshards; s++) {
+    ShardRun *r = &runs[s];
+    HIPCHK(hipSetDevice(r->sh.device));
+    HIPCHK(hipStreamSynchronize(r->stream));
+    HIPCHK(hipMemcpy(&counts[s], r->plan->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&bnds[s], r->plan->bnd, sizeof (GtSmaxBoundary), hipMemcpyDeviceToHost));
+    if (counts[s] > r->plan->capacity) {   // re-run with exact capacity
+      uint64_t need = counts[s] + 1;
+      gt_smax_plan_delete(r->plan);
+      r->plan = NULL;
+      if (gt_smax_plan_create(&r->plan, &r->sh, minlen, need, errbuf, errlen)) goto fail;
+      if (gt_smax_plan_run(r->plan, r->stream)) goto fail;
+      HIPCHK(hipStreamSynchronize(r->stream));
+      HIPCHK(hipMemcpy(&counts[s], r->plan->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
+    }
+    total += counts[s] + 1;   // +1 slot for a stitched interval
+  }
+  trip = (uint64_t *) malloc(sizeof (uint64_t) * 3 * (total + 1));
+  if (trip == NULL) {
+    seterr(errbuf, errlen, "out of memory for %lu intervals", (unsigned long) total);
+    goto fail;
+  }
+  total = 0;
+  for (int s = 0; s < nshards; s++) {
+    ShardRun *r = &runs[s];
+    GtSmaxRecord *h = (GtSmaxRecord *) malloc(sizeof (GtSmaxRecord) * (counts[s] + 1));
+    if (h == NULL) { seterr(errbuf, errlen, "out of memory"); goto fail; }
+    HIPCHK(hipSetDevice(r->sh.device));
+    if (counts[s] > 0)
+      HIPCHK(hipMemcpy(h, r->plan->out, sizeof (GtSmaxRecord) * counts[s],
+                       hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < counts[s]; i++) {
+      trip[3 * total] = h[i].lcp;
+      trip[3 * total + 1] = h[i].lb;
+      trip[3 * total + 2] = h[i].lb + h[i].width - 1;
+      total++;
+    }
+    free(h);
+    GtSmaxRecord rec;
+    if (stitch_resolve(bnds, nshards, s, minlen, &rec)) {
+      trip[3 * total] = rec.lcp;
+      trip[3 * total + 1] = rec.lb;
+      trip[3 * total + 2] = rec.lb + rec.width - 1;
+      total++;
+    }
+  }
+  *trip_out = trip;
+  *count_out = total;
+  trip = NULL;
+  rc = 0;
+fail:
+  free(trip);
+  if (runs) {
+    for (int s = 0; s < nshards; s++) {
+      ShardRun *r = &runs[s];
+      if (r->plan) gt_smax_plan_delete(r->plan);
+      gt_smax_dev_free_table(r->sh.device, r->lcp);
+      gt_smax_dev_free_table(r->sh.device, r->bwt);
+      if (r->llv) { (void) hipSetDevice(r->sh.device); (void) hipFree(r->llv); }
+      if (r->stream) (void) hipStreamDestroy(r->stream);
+    }
+  }
+  free(runs);
+  free(bnds);
+  free(counts);
+  return rc;
+}
+
+extern "C" int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in,
+                                               unsigned int minlen,
+                                               int num_gpus,
+                                               uint64_t **lcp_lb_rb,
+                                               uint64_t *count, char *errbuf,
+                                               size_t errlen) {
+  if (validate_input(in, errbuf, errlen)) return -1;
+  if (minlen == 0) {
+    seterr(errbuf, errlen, "minlen must be >= 1");
+    return -1;
+  }
+  return run_shards(in, minlen, num_gpus, lcp_lb_rb, count, errbuf, errlen);
+}
+
+extern "C" int gt_smax_hip_enumerate(const GtSmaxInput *in, unsigned int minlen,
+                                     int num_gpus, GtSmaxIntervalFunc cb,
+                                     void *data, char *errbuf, size_t errlen) {
+  uint64_t *trip = NULL, count = 0;
+  if (cb == NULL) {
+    seterr(errbuf, errlen, "no interval callback");
+    return -1;
+  }
+  if (gt_smax_hip_enumerate_to_buffer(in, minlen, num_gpus, &trip, &count,
+                                      errbuf, errlen))
+    return -1;
+  for (uint64_t i = 0; i < count; i++) {
+    if (cb(data, trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]) != 0) {
+      seterr(errbuf, errlen, "interval callback failed at interval %lu",
+             (unsigned long) i);
+      free(trip);
+      return -1;
+    }
+  }
+  free(trip);
+  return 0;
+}

@@ -1,0 +1,190 @@
+/*
+ * gt_smax_hip.h -- C-ABI of the MI355X supermaximal-repeat (smax) layer.
+ *
+ * Drop-in boundary for the smax hot path of GenomeTools.
+ * Plain C types only: a C host (the gt repfind runner, esa_linsmax.c, the
+ * repo's own CLI) links libgtsmax_hip.so and never sees HIP or torch types.
+ *
+ * Each entry point names the reference interface it replaces:
+ *
+ *  gt_smax_hip_enumerate          replaces the bottom-up traversal driving a
+ *                                 GtESAVisitor lcp-interval callback:
+ *                                 gt_esa_bottomup(ssar, visitor, err)
+ *                                   src/match/esa-bottomup.h:31-33,
+ *                                   src/match/esa-bottomup.c:116-273
+ *                                 visit_lcp_interval(lcp, lb, rb)
+ *                                   src/match/esa_visitor_rep.h:46-51
+ *                                 and the maxpairs driver pattern
+ *                                 gt_callenummaxpairs
+ *                                   src/match/esa-maxpairs.c:476-520
+ *                                 Intervals arrive in ascending lb, the order
+ *                                 in which the bottom-up traversal pops
+ *                                 leaf-only intervals.
+ *  gt_smax_hip_enumerate_to_buffer  same, returning a malloc'd array.
+ *  GtSmaxInput                    the mapped tables of Suffixarray
+ *                                   src/match/sarr-def.h:101-126
+ *                                 as exposed by
+ *                                   gt_suffixarraySequentialsuffixarrayreader
+ *                                   src/match/esa-seqread.h:238-239
+ *  GtSmaxLlv                      Largelcpvalue {position,value} on LP64
+ *                                   src/match/lcpoverflow.h:23-30
+ *
+ * The gt_smax_dev_* functions are the device-resident form used when the
+ * tables already live in HBM (one process per GPU under torch.distributed):
+ * they enqueue work on a caller-provided HIP stream and never synchronise
+ * except where documented.
+ *
+ * Conventions follow GenomeTools: 0 = success, -1 = error with a message in
+ * errbuf (the gt shim copies it into GtError via gt_error_set, as
+ * src/match/esa-maxpairs.c:443 returns haserr ? -1 : 0).  A non-zero return
+ * from the interval callback stops the enumeration and is propagated as -1
+ * (src/match/esa-bottomup.c:147-157).  Input pointers are borrowed for the
+ * duration of the call only; every device and pinned buffer is owned and
+ * freed by this layer.
+ */
+#ifndef GT_SMAX_HIP_H
+#define GT_SMAX_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  uint64_t position, value;
+} GtSmaxLlv;
+
+typedef struct {
+  const uint8_t *lcptab;     /* .lcp, totallength+1 bytes, 255 = overflow  */
+  const GtSmaxLlv *llvtab;   /* .llv, sorted by position                   */
+  uint64_t numllv;
+  const uint8_t *bwttab;     /* .bwt, totallength+1 bytes                  */
+  const void *suftab;        /* .suf (optional for enumeration)            */
+  int suftab_bytes;          /* 4, 8, or 0 when suftab is NULL             */
+  uint64_t totallength;      /* n  (.prj totallength)                      */
+  uint64_t nonspecials;      /* N = n - specialcharacters                  */
+} GtSmaxInput;
+
+/* visit_lcp_interval analogue: one supermaximal-repeat interval
+ * [lb..rb] of lcp-value lcp (occurrences are suftab[lb..rb]). */
+typedef int (*GtSmaxIntervalFunc)(void *data, uint64_t lcp, uint64_t lb,
+                                  uint64_t rb);
+
+/* Device output record: interval [lb .. lb+width-1] with lcp-value lcp. */
+typedef struct {
+  uint64_t lb;
+  uint32_t lcp;
+  uint32_t width;
+} GtSmaxRecord;
+
+int gt_smax_hip_enumerate(const GtSmaxInput *in, unsigned int minlen,
+                          int num_gpus, GtSmaxIntervalFunc cb, void *data,
+                          char *errbuf, size_t errlen);
+
+/* *lcp_lb_rb receives 3*count uint64 (lcp,lb,rb triples, ascending lb),
+ * allocated with malloc; free with gt_smax_free. */
+int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in,
+                                    unsigned int minlen, int num_gpus,
+                                    uint64_t **lcp_lb_rb, uint64_t *count,
+                                    char *errbuf, size_t errlen);
+
+void gt_smax_free(void *ptr);
+
+/* Number of HIP devices visible (0 if the runtime has none). */
+int gt_smax_device_count(void);
+
+/* -------------------------------------------------- device-resident API */
+
+/*
+ * A shard owns the suffix-array rows whose plateau starts c = lb+1 lie in
+ * [begin, end) of [1, nonspecials).  Its device tables cover global indices
+ * [base, base+local_len): lcp_dev[i] is LCP[base+i], bwt_dev[i] is
+ * BWT[base+i], with base <= begin-1 and base+local_len > end (the shard needs
+ * LCP[begin-1 .. end] and BWT[begin-1 .. end-1]).  Both device buffers must
+ * be readable GT_SMAX_PAD_FRONT bytes before and GT_SMAX_PAD_BACK bytes after
+ * their local_len bytes (use gt_smax_dev_alloc_table).  llv_dev holds the
+ * .llv entries with base <= position < base+local_len (global positions).
+ */
+#define GT_SMAX_PAD_FRONT 256
+#define GT_SMAX_PAD_BACK 32768
+
+typedef struct {
+  const uint8_t *lcp_dev;
+  const uint8_t *bwt_dev;
+  const GtSmaxLlv *llv_dev;
+  uint64_t numllv;
+  uint64_t base, local_len;
+  uint64_t begin, end;
+  uint64_t nonspecials;      /* global N: LCP[0] = LCP[N] = 0 */
+  int device;                /* HIP device ordinal */
+} GtSmaxDevShard;
+
+/* Diversity of a run of BWT rows: set of symbols < 254 seen, dup flag. */
+typedef struct {
+  uint64_t seen[4];
+  uint64_t dup;
+} GtSmaxDiv;
+
+/* Fixed-size boundary record exchanged by the all-gather. */
+typedef struct {
+  /* tail: plateau owned by this shard that runs into the next shard */
+  uint64_t pend_valid, pend_c, pend_lcp;
+  GtSmaxDiv pend_div;
+  /* head: the run of LCP == LCP[begin] at the start of this shard */
+  uint64_t head_v;           /* exact LCP[begin]                         */
+  uint64_t head_f;           /* first t>begin... with LCP[t] != head_v,   */
+                             /* or UINT64_MAX if the run covers the shard */
+  uint64_t head_next;        /* exact LCP[head_f]                         */
+  GtSmaxDiv head_div;        /* diversity of BWT[begin .. head_f-1]       */
+  uint64_t shard_begin, shard_end;
+} GtSmaxBoundary;
+
+typedef struct GtSmaxPlan GtSmaxPlan;
+
+/* Allocate a device table of len bytes with the required padding; returns
+ * the usable pointer (free with gt_smax_dev_free_table). */
+int gt_smax_dev_alloc_table(int device, uint64_t len, uint8_t **table,
+                            char *errbuf, size_t errlen);
+int gt_smax_dev_free_table(int device, uint8_t *table);
+
+/* Creates a plan for one shard: output capacity (records), look-back state
+ * and the per-tile .llv index.  capacity==0 picks a default. */
+int gt_smax_plan_create(GtSmaxPlan **plan, const GtSmaxDevShard *shard,
+                        unsigned int minlen, uint64_t capacity,
+                        char *errbuf, size_t errlen);
+void gt_smax_plan_delete(GtSmaxPlan *plan);
+
+/* Enqueue one smax pass (scan + ordered compaction + boundary record) on
+ * stream (a hipStream_t, NULL = default stream).  Asynchronous. */
+int gt_smax_plan_run(GtSmaxPlan *plan, void *stream);
+
+/* Device pointers owned by the plan. */
+GtSmaxRecord *gt_smax_plan_records(GtSmaxPlan *plan);
+uint64_t *gt_smax_plan_count_dev(GtSmaxPlan *plan);   /* 1 x uint64 */
+GtSmaxBoundary *gt_smax_plan_boundary_dev(GtSmaxPlan *plan);
+uint64_t gt_smax_plan_capacity(GtSmaxPlan *plan);
+uint64_t gt_smax_plan_num_tiles(GtSmaxPlan *plan);
+
+/* After all shards' boundary records are gathered (in rank order) into
+ * all_dev (nshards records, device memory), append this shard's stitched
+ * interval, if any, to its records.  Asynchronous on stream. */
+int gt_smax_plan_stitch(GtSmaxPlan *plan, const GtSmaxBoundary *all_dev,
+                        int nshards, int shard_index, void *stream);
+
+/* Pure host form of the stitch: resolves the pending plateau of shard
+ * shard_index against the following heads.  Returns 1 and fills *rec if an
+ * interval results, 0 otherwise. */
+int gt_smax_stitch_host(const GtSmaxBoundary *all, int nshards,
+                        int shard_index, unsigned int minlen,
+                        GtSmaxRecord *rec);
+
+/* Synchronises the plan's device and copies the record count to the host. */
+int gt_smax_plan_fetch_count(GtSmaxPlan *plan, uint64_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,181 @@
+"""Pins the CPU oracle to the reference's own fixtures (no GPU needed).
+
+Parity anchors (the reference is unbuildable here -- see DESIGN.md):
+  * testdata/repfind-8-Atinsert.txt: `gt repfind -l 8` on Atinsert, compared
+    in gt_idxsearch_include.rb:144-154 with diff -w.  The oracle's ESA +
+    maxpairs restatement must reproduce it line for line, in order.
+  * testdata/prj-files/*.prj: .prj statistics of gt suffixerator runs.
+  * SURVEY.md §8(c) verified counts from the reference build (Atinsert l=8:
+    114 smax / 263 occurrences / 205 pairs; at1MB l=20: n=772,376,
+    N=753,453, 2,317 llv entries, max lcp 517, 38,153 local maxima,
+    884 / 1,771 / 890, 4,507 repfind lines).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from conftest import GOLDEN, oracle_esa
+
+
+def _norm(lines):
+    return [" ".join(l.split()) for l in lines if l.strip() and not l.startswith("#")]
+
+
+def test_maxpairs_reproduces_repfind_golden():
+    e = oracle_esa("Atinsert.fna")
+    lines = O.format_pairs(O.maxpairs(e, 8), e.separators)
+    with open(os.path.join(GOLDEN, "repfind-8-Atinsert.txt")) as fh:
+        gold = _norm(fh)
+    assert _norm(lines) == gold
+    assert len(gold) == 452
+
+
+def test_atinsert_smax_known_answer():
+    e = oracle_esa("Atinsert.fna")
+    assert (e.n, e.nonspecials) == (11817, 8867)
+    a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8)
+    assert len(a) == 114
+    assert int((a[:, 2] - a[:, 1] + 1).sum()) == 263
+    pairs = O.format_pairs(O.smax_pairs(a, e.suftab), e.separators)
+    assert len(pairs) == 205
+    with open(os.path.join(GOLDEN, "repfind-8-Atinsert.txt")) as fh:
+        gold = set(_norm(fh))
+    assert set(_norm(pairs)) <= gold
+
+
+def _local_maxima(lcp, N, minlen):
+    L = lcp[: N + 1].astype(np.int64).copy()
+    L[0] = 0
+    L[N] = 0
+    cnt = 0
+    k = 1
+    while k <= N - 1:
+        if L[k] > L[k - 1] and L[k] >= minlen:
+            j = k
+            while j + 1 <= N - 1 and L[j + 1] == L[k]:
+                j += 1
+            nxt = L[j + 1] if j + 1 <= N - 1 else 0
+            if nxt < L[k]:
+                cnt += 1
+            k = j + 1
+        else:
+            k += 1
+    return cnt
+
+
+def test_at1mb_known_answer():
+    e = oracle_esa("at1MB")
+    assert (e.n, e.nonspecials) == (772376, 753453)
+    assert len(e.llv) == 2317
+    assert int(e.lcp.max()) == 517
+    assert _local_maxima(e.lcp, e.nonspecials, 20) == 38153
+    a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 20)
+    assert len(a) == 884
+    assert int((a[:, 2] - a[:, 1] + 1).sum()) == 1771
+    mp = O.format_pairs(O.maxpairs(e, 20), e.separators)
+    assert len(mp) == 4507
+    sp = O.format_pairs(O.smax_pairs(a, e.suftab), e.separators)
+    assert len(sp) == 890
+    assert set(_norm(sp)) <= set(_norm(mp))
+
+
+@pytest.mark.parametrize("minlen", [1, 4, 8, 12, 20])
+def test_linsmax_equals_bottomup_atinsert(minlen):
+    e = oracle_esa("Atinsert.fna")
+    a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+    b = O.bottomup_smax(e, minlen)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("minlen", [10, 50, 255, 300])
+def test_linsmax_equals_bottomup_at1mb(minlen):
+    e = oracle_esa("at1MB")
+    a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+    b = O.bottomup_smax(e, minlen)
+    assert np.array_equal(a, b)
+
+
+def _random_text(rng, n, sigma=4, pspecial=0.02):
+    t = rng.integers(0, sigma, n, dtype=np.uint8)
+    sp = rng.random(n) < pspecial
+    t[sp] = rng.choice(np.array([254, 255], dtype=np.uint8), sp.sum())
+    return t
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_three_derivations_agree_random(seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 220))
+    sigma = int(rng.integers(1, 5))
+    t = _random_text(rng, n, sigma, pspecial=float(rng.choice([0.0, 0.03, 0.2])))
+    if seed % 3 == 0:   # tandem repeats give long plateaus / nested intervals
+        unit = rng.integers(0, sigma, int(rng.integers(1, 6)), dtype=np.uint8)
+        t = np.tile(unit, n // len(unit) + 1)[:n].copy()
+    e = O.Esa(t)
+    for minlen in (1, 2, 3, 5):
+        a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        b = O.bottomup_smax(e, minlen)
+        assert np.array_equal(a, b)
+        brute = O.brute_smax(t, minlen)
+        esa_sets = sorted((int(l), tuple(sorted(int(e.suftab[k]) for k in range(lb, rb + 1))))
+                          for l, lb, rb in a)
+        assert esa_sets == sorted(brute)
+
+
+def test_special_example_from_survey():
+    # >t ACACNACAC  >u ACAC : smax ACAC with 3 occurrences
+    t = np.array([0, 1, 0, 1, 254, 0, 1, 0, 1, 255, 0, 1, 0, 1], dtype=np.uint8)
+    e = O.Esa(t)
+    assert (e.n, e.nonspecials) == (14, 12)
+    assert list(e.suftab[:3]) == [0, 5, 10]
+    assert list(e.bwt[:3]) == [254, 254, 255]
+    a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 4)
+    assert a.tolist() == [[4, 0, 2]]
+
+
+def _prj(path):
+    out = {}
+    with open(path) as fh:
+        for line in fh:
+            if "=" in line and not line.startswith("dbfile"):
+                k, v = line.strip().split("=")
+                out[k] = v
+    return out
+
+
+@pytest.mark.parametrize("fasta,prj", [
+    (["Random-Small.fna"], "Random-Small.prj"),
+    (["Random.fna"], "Random.prj"),
+    (["TTT-small.fna"], "TTT-small.prj"),
+    (["Atinsert.fna", "Random.fna"], "Atinsert+Random.prj"),
+])
+def test_prj_statistics_match_reference(tmp_path, fasta, prj):
+    cat = tmp_path / "in.fna"
+    with open(cat, "wb") as out:
+        for f in fasta:
+            with open(os.path.join(GOLDEN, f), "rb") as fh:
+                data = fh.read()
+            out.write(data if data.endswith(b"\n") else data + b"\n")
+    idx = str(tmp_path / "idx")
+    O.index_fasta(str(cat), idx)
+    mine, ref = _prj(idx + ".prj"), _prj(os.path.join(GOLDEN, "prj", prj))
+    for key in ("totallength", "specialcharacters", "specialranges", "realspecialranges",
+                "lengthofspecialprefix", "lengthofspecialsuffix", "numofsequences",
+                "largelcpvalues", "readmode"):
+        assert mine[key] == ref[key], key
+
+
+def test_index_files_layout(tmp_path):
+    idx = str(tmp_path / "at")
+    O.index_fasta(os.path.join(GOLDEN, "Atinsert.fna"), idx)
+    e = oracle_esa("Atinsert.fna")
+    n = e.n
+    assert os.path.getsize(idx + ".suf") == 8 * (n + 1)
+    assert os.path.getsize(idx + ".lcp") == n + 1
+    assert os.path.getsize(idx + ".bwt") == n + 1
+    assert os.path.getsize(idx + ".llv") == 0
+    assert np.array_equal(np.fromfile(idx + ".suf", dtype=np.uint64), e.suftab)
+    O.index_fasta(os.path.join(GOLDEN, "Atinsert.fna"), idx + "4", suftab_bytes=4)
+    assert np.array_equal(np.fromfile(idx + "4.suf", dtype=np.uint32).astype(np.uint64), e.suftab)

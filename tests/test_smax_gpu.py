@@ -1,0 +1,126 @@
+"""GPU parity: the HIP smax path (through the C-ABI) against the CPU oracle.
+
+Bit-exact comparison of the (lcp, lb, rb) interval lists, ascending lb, on
+the reference's fixtures (Atinsert, at1MB), on seeded random/repetitive
+texts (specials, long plateaus, .llv overflow values) and across shard
+counts (the boundary stitch), at sizes the oracle finishes in seconds.
+"""
+import numpy as np
+import pytest
+
+import genometools_smax_amd as G
+import oracle_lib as O
+from conftest import oracle_esa
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu(e, minlen, shards=1):
+    return G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, minlen, shards)
+
+
+def _cpu(e, minlen):
+    return O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+
+
+def test_device_present():
+    assert G.device_count() >= 1
+
+
+@pytest.mark.parametrize("minlen", [1, 2, 4, 8, 12, 20, 40])
+def test_atinsert(minlen):
+    e = oracle_esa("Atinsert.fna")
+    got, want = _gpu(e, minlen), _cpu(e, minlen)
+    assert np.array_equal(got, want), (len(got), len(want))
+
+
+def test_atinsert_known_answer():
+    e = oracle_esa("Atinsert.fna")
+    got = _gpu(e, 8)
+    assert len(got) == 114 and int((got[:, 2] - got[:, 1] + 1).sum()) == 263
+
+
+@pytest.mark.parametrize("minlen", [1, 5, 10, 20, 50, 200, 255, 256, 300, 517, 518])
+def test_at1mb(minlen):
+    e = oracle_esa("at1MB")
+    got, want = _gpu(e, minlen), _cpu(e, minlen)
+    assert np.array_equal(got, want), (len(got), len(want))
+
+
+@pytest.mark.parametrize("shards", [2, 3, 5, 8, 17])
+def test_at1mb_sharded(shards):
+    e = oracle_esa("at1MB")
+    want = _cpu(e, 20)
+    got = _gpu(e, 20, shards)
+    assert np.array_equal(got, want)
+
+
+def _repetitive_text(rng, n, pspecial):
+    # random genome with inserted copies of a few families (long lcps -> .llv)
+    t = rng.integers(0, 4, n, dtype=np.uint8)
+    fams = [rng.integers(0, 4, int(rng.integers(50, 800)), dtype=np.uint8) for _ in range(6)]
+    pos = 0
+    while pos < n:
+        f = fams[int(rng.integers(0, len(fams)))]
+        at = int(rng.integers(0, n))
+        L = min(len(f), n - at)
+        cp = f[:L].copy()
+        mut = rng.random(L) < 0.01
+        cp[mut] = rng.integers(0, 4, int(mut.sum()), dtype=np.uint8)
+        t[at:at + L] = cp
+        pos += L * 3
+    sp = rng.random(n) < pspecial
+    t[sp] = rng.choice(np.array([254, 255], dtype=np.uint8), int(sp.sum()))
+    return t
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_repetitive(seed):
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(20000, 200000))
+    t = _repetitive_text(rng, n, [0.0, 0.001, 0.02][seed % 3])
+    e = O.Esa(t)
+    for minlen in (3, 10, 20, 100, 300):
+        want = _cpu(e, minlen)
+        assert np.array_equal(_gpu(e, minlen), want), minlen
+        assert np.array_equal(_gpu(e, minlen, 1 + seed), want), (minlen, seed)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_small_edge_texts(seed):
+    rng = np.random.default_rng(seed)
+    for _ in range(20):
+        n = int(rng.integers(1, 300))
+        sigma = int(rng.integers(1, 5))
+        t = rng.integers(0, sigma, n, dtype=np.uint8)
+        if rng.random() < 0.5:
+            sp = rng.random(n) < 0.1
+            t[sp] = 254
+        e = O.Esa(t)
+        for minlen in (1, 2, 3):
+            want = _cpu(e, minlen)
+            for shards in (1, 2, 4):
+                assert np.array_equal(_gpu(e, minlen, shards), want)
+
+
+def test_tandem_runs_cross_tiles():
+    # homopolymer / short-period tandem repeats: plateaus and lcp ramps that
+    # straddle 16384-row tiles and shard boundaries
+    rng = np.random.default_rng(7)
+    parts = [rng.integers(0, 4, 16000, dtype=np.uint8), np.zeros(3000, dtype=np.uint8),
+             np.array([255], dtype=np.uint8), np.tile(np.array([0, 1], dtype=np.uint8), 2500),
+             np.array([254], dtype=np.uint8), rng.integers(0, 4, 50000, dtype=np.uint8)]
+    t = np.concatenate(parts)
+    e = O.Esa(t)
+    for minlen in (1, 5, 255, 1000):
+        want = _cpu(e, minlen)
+        for shards in (1, 3, 7):
+            assert np.array_equal(_gpu(e, minlen, shards), want), (minlen, shards)
+
+
+def test_errors_are_reported():
+    e = oracle_esa("Atinsert.fna")
+    with pytest.raises(G.SmaxError):
+        G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.n + 5, 8)
+    with pytest.raises(G.SmaxError):
+        G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 0)
