@@ -381,15 +381,23 @@ smax_scan_kernel(SmaxScanArgs a) {
     }
   }
 
-  // ---- phase 4: block scan of counts
-  uint32_t mycount = (uint32_t) __popcll(cand);
-  uint32_t incl = mycount;
+  // ---- phase 4: block scan of counts in row order.  A wave's rows are
+  // ordered segment-major (r), then lane, so scan each segment slice.
+  uint32_t seg_off[SMAX_SEGS];
+  uint32_t wave_total = 0;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    const uint32_t c = (uint32_t) __popcll((cand >> (16 * r)) & 0xffffull);
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    seg_off[r] = wave_total + incl - c;
+    wave_total += __shfl(incl, 63, 64);
   }
-  if (lane == 63) sWaveSum[wave] = incl;
+  if (lane == 0) sWaveSum[wave] = wave_total;
   __syncthreads();
   uint32_t wave_off = 0, tile_count = 0;
 #pragma unroll
@@ -398,7 +406,6 @@ smax_scan_kernel(SmaxScanArgs a) {
     if (w < wave) wave_off += ws;
     tile_count += ws;
   }
-  const uint32_t my_off = wave_off + incl - mycount;
 
   // ---- phase 5: decoupled look-back (wave 0)
   const uint64_t ep = (a.epoch & ST_EPOCH_MASK) << ST_VALUE_BITS;
@@ -446,11 +453,10 @@ smax_scan_kernel(SmaxScanArgs a) {
     }
   }
   __syncthreads();
-  const uint64_t base_out = sExcl + my_off;
+  const uint64_t base_out = sExcl + wave_off;
 
   // ---- phase 6: ordered record writes
   tmp = cand;
-  uint64_t k = 0;
   while (tmp) {
     int bit = __builtin_ctzll(tmp);
     tmp &= tmp - 1;
@@ -459,7 +465,10 @@ smax_scan_kernel(SmaxScanArgs a) {
     uint32_t cur = lcp_at(t, c), nx;
     bool pend;
     uint64_t j = plateau_end(t, c, cur, &nx, &pend);
-    uint64_t o = base_out + k++;
+    // rank of this row among the thread's rows of segment r
+    uint32_t before = (uint32_t) __popcll(cand & ((1ull << bit) - 1) & (0xffffull << (16 * r)));
+    uint32_t so = r == 0 ? seg_off[0] : r == 1 ? seg_off[1] : r == 2 ? seg_off[2] : seg_off[3];
+    uint64_t o = base_out + so + before;
     if (o < a.capacity) {
       GtSmaxRecord rec;
       rec.lb = c - 1;

@@ -1,0 +1,64 @@
+"""The C host CLI (`gt repfind -smax`) end to end on the GPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import genometools_smax_amd as G
+import oracle_lib as O
+from conftest import GOLDEN, oracle_esa
+
+CLI = os.path.join(G.BIN_DIR, "gt-repfind")
+
+
+def _norm(lines):
+    return [" ".join(l.split()) for l in lines if l.strip() and not l.startswith("#")]
+
+
+def _index(tmp_path, fasta, suftab_bytes=8):
+    idx = str(tmp_path / os.path.basename(fasta))
+    O.index_fasta(os.path.join(GOLDEN, fasta), idx, suftab_bytes)
+    return idx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scan,width", [(False, 8), (True, 8), (True, 4)])
+def test_cli_atinsert_pairs(tmp_path, scan, width):
+    idx = _index(tmp_path, "Atinsert.fna", width)
+    cmd = [CLI, "-smax", "-l", "8", "-ii", idx] + (["-scan"] if scan else [])
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+    mine = _norm(out.splitlines())
+    e = oracle_esa("Atinsert.fna")
+    want = _norm(O.format_pairs(O.smax_pairs(O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8),
+                                             e.suftab), e.separators))
+    assert mine == want
+    assert len(mine) == 205
+    with open(os.path.join(GOLDEN, "repfind-8-Atinsert.txt")) as fh:
+        assert set(mine) <= set(_norm(fh))
+
+
+@pytest.mark.gpu
+def test_cli_at1mb_intervals_and_gpus(tmp_path):
+    idx = _index(tmp_path, "at1MB")
+    e = oracle_esa("at1MB")
+    want = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 20)
+    for gpus in ("1", "4"):
+        out = subprocess.run([CLI, "-smax", "-l", "20", "-ii", idx, "-intervals", "-gpus", gpus],
+                             check=True, capture_output=True, text=True).stdout
+        got = np.array([[int(x) for x in l.split()] for l in out.splitlines()], dtype=np.uint64)
+        assert np.array_equal(got, want)
+
+
+def test_cli_errors(tmp_path):
+    r = subprocess.run([CLI, "-l", "8", "-ii", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "gt repfind: error:" in r.stderr
+    r = subprocess.run([CLI, "-smax", "-r", "-ii", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "exclude each other" in r.stderr
+    r = subprocess.run([CLI, "-smax", "-l", "0", "-ii", "x"], capture_output=True, text=True)
+    assert r.returncode == 1
+    r = subprocess.run([CLI, "-smax", "-ii", str(tmp_path / "missing")], capture_output=True, text=True)
+    assert r.returncode == 1 and "cannot open" in r.stderr
+    idx = _index(tmp_path, "Atinsert.fna", 4)
+    r = subprocess.run([CLI, "-smax", "-ii", idx], capture_output=True, text=True)
+    assert r.returncode == 1 and "number of mapped units" in r.stderr
