@@ -415,3 +415,97 @@ def stitch_host(boundaries, shard_index, minlen):
 
 def device_count():
     return lib().gt_smax_device_count()
+
+
+# ------------------------------------------------------- ESA construction (F1)
+
+class GtSmaxEsaDev(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("totallength", ctypes.c_uint64),
+        ("nonspecials", ctypes.c_uint64),
+        ("numllv", ctypes.c_uint64),
+        ("maxbranchdepth", ctypes.c_uint64),
+        ("averagelcp", ctypes.c_double),
+        ("sort_rounds", ctypes.c_int),
+        ("lcptab_dev", ctypes.c_void_p),
+        ("bwttab_dev", ctypes.c_void_p),
+        ("llvtab_dev", ctypes.c_void_p),
+        ("suftab_dev", ctypes.c_void_p),
+    ]
+
+
+def _esa_lib():
+    L = lib()
+    if not getattr(L, "_esa_ready", False):
+        vp, u64, ci, cs, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t
+        L.gt_smax_esa_build.argtypes = [ci, vp, u64, ci, ctypes.POINTER(GtSmaxEsaDev), cs, sz]
+        L.gt_smax_esa_download.argtypes = [ctypes.POINTER(GtSmaxEsaDev), vp, vp, vp, vp, cs, sz]
+        L.gt_smax_esa_release.argtypes = [ctypes.POINTER(GtSmaxEsaDev)]
+        L.gt_smax_synth_total_length.argtypes = [ci, u64, ctypes.POINTER(u64)]
+        L.gt_smax_synth_generate.argtypes = [ci, u64, u64, vp, u64, ctypes.POINTER(u64), ci]
+        L._esa_ready = True
+    return L
+
+
+class DeviceEsa:
+    """Enhanced suffix array built in HBM by gt_smax_esa_build (the
+    `gt suffixerator -suf -lcp -bwt` replacement for the smax inputs)."""
+
+    def __init__(self, text, device=0, keep_suftab=False):
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        self.esa = GtSmaxEsaDev()
+        eb = _errbuf()
+        _check(_esa_lib().gt_smax_esa_build(device, text.ctypes.data, len(text), int(keep_suftab),
+                                            ctypes.byref(self.esa), eb, len(eb)), eb)
+        self.device = device
+        self.totallength = self.esa.totallength
+        self.nonspecials = self.esa.nonspecials
+        self.numllv = self.esa.numllv
+
+    def download(self, suftab=False):
+        m = self.totallength + 1
+        lcp = np.empty(m, dtype=np.uint8)
+        bwt = np.empty(m, dtype=np.uint8)
+        llv = np.empty((max(self.numllv, 1), 2), dtype=np.uint64)
+        suf = np.empty(m, dtype=np.uint64) if suftab else None
+        eb = _errbuf()
+        _check(_esa_lib().gt_smax_esa_download(ctypes.byref(self.esa), lcp.ctypes.data, bwt.ctypes.data,
+                                               llv.ctypes.data, suf.ctypes.data if suftab else None,
+                                               eb, len(eb)), eb)
+        return {"lcptab": lcp, "bwttab": bwt, "llvtab": llv[: self.numllv], "suftab": suf}
+
+    def plan(self, minlen, begin=None, end=None, capacity=0):
+        """Single-shard (or sub-range) smax plan over the device tables."""
+        N = self.nonspecials
+        begin = 1 if begin is None else begin
+        end = N if end is None else end
+        return SmaxPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
+                        0, self.totallength + 1, begin, end, N, minlen, self.device, capacity)
+
+    def release(self):
+        if self.esa.lcptab_dev:
+            _esa_lib().gt_smax_esa_release(ctypes.byref(self.esa))
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+SYNTH_KINDS = {"uniform": 0, "human": 1, "plant": 2}
+
+
+def synth_genome(kind, bases, seed, threads=None):
+    """Deterministic synthetic genome (encoded symbols) -- gt_smax_synth_generate."""
+    k = SYNTH_KINDS[kind] if isinstance(kind, str) else int(kind)
+    n = ctypes.c_uint64()
+    if _esa_lib().gt_smax_synth_total_length(k, int(bases), ctypes.byref(n)) != 0:
+        raise SmaxError("bad synthetic genome request")
+    out = np.empty(n.value, dtype=np.uint8)
+    threads = threads or min(16, os.cpu_count() or 1)
+    if _esa_lib().gt_smax_synth_generate(k, int(bases), int(seed), out.ctypes.data, n.value,
+                                         ctypes.byref(n), int(threads)) != 0:
+        raise SmaxError("synthetic genome generation failed")
+    return out

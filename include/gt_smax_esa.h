@@ -1,0 +1,50 @@
+/*
+ * gt_smax_esa.h -- GPU construction of the smax inputs:
+ * the `gt suffixerator -dna -suf -lcp -bwt` tables, built in HBM.
+ *
+ * Replaces, for the smax path, suffixeratorwithoutput
+ * (src/match/sfx-run.c:213-300): bwttab2file (:174-212), outlcpvalues
+ * (src/match/sfx-lcpvalues.c:371-470) and the suffix sort.  Output tables are
+ * byte-identical to suffixerator's (.suf values, .lcp bytes, .llv entries,
+ * .bwt bytes).  Limited to n+1 < 2^32 suffixes (32-bit suffix array).
+ */
+#ifndef GT_SMAX_ESA_H
+#define GT_SMAX_ESA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gt_smax_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int device;
+  uint64_t totallength, nonspecials, numllv, maxbranchdepth;
+  double averagelcp;
+  int sort_rounds;            /* prefix-doubling rounds after the 21-mer sort */
+  uint8_t *lcptab_dev;        /* totallength+1 bytes, GT_SMAX_PAD layout     */
+  uint8_t *bwttab_dev;        /* totallength+1 bytes, GT_SMAX_PAD layout     */
+  GtSmaxLlv *llvtab_dev;      /* numllv entries                              */
+  uint32_t *suftab_dev;       /* totallength+1 entries, or NULL              */
+} GtSmaxEsaDev;
+
+/* text: n encoded symbols on the host (0..3, 254 wildcard, 255 separator). */
+int gt_smax_esa_build(int device, const uint8_t *text, uint64_t n,
+                      int keep_suftab, GtSmaxEsaDev *out, char *errbuf,
+                      size_t errlen);
+
+/* Copies tables to host buffers (any may be NULL); suftab widened to 8 B. */
+int gt_smax_esa_download(const GtSmaxEsaDev *esa, uint8_t *lcptab,
+                         uint8_t *bwttab, GtSmaxLlv *llvtab, uint64_t *suftab,
+                         char *errbuf, size_t errlen);
+
+void gt_smax_esa_release(GtSmaxEsaDev *esa);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
