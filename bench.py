@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py -- throughput of the smax hot path on MI355X (BASELINE.json metric).
+
+One "step" = one smax pass over the whole suffix array of the workload:
+the fused plateau-scan / left-diversity / ordered-compaction kernel K1
+(plus the one-wave head kernel) on every rank's suffix-array range and, with
+N > 1, the RCCL all-gather of the fixed-size boundary records and the stitch
+kernel.  The LCP/BWT/.llv tables are resident in HBM before timing starts
+(built on each GPU by the repo's GPU suffixerator replacement from a
+deterministic synthetic genome; ESA construction is reported as setup).
+
+Workload (default, configs[2] of BASELINE.json, where the ≥10x / ≥50 % HBM
+target is quoted): 3 Gbp synthetic human-like DNA (40 % interspersed repeats,
+STRs, segmental duplications, N gaps, 24 sequences), minlen 20.  --config c2
+runs configs[1] (100 Mbp uniform ACGT).  N GPUs shard the same suffix array
+by range (strong scaling): value = nonspecials / max-over-ranks step time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+"roofline" for K1 (algorithmic bytes = 2 B per suffix row + 16 B per .llv
+entry, SURVEY.md §8(d), over the average K1 duration from HIP events recorded
+on K1's stream during the timed region) and, at N = 1, "cpu_baseline": the
+oracle's single-core linear scan (oracle/smax_oracle.c orc_linsmax, the
+repo's CPU esa_linsmax restatement) timed on this host over the same tables.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("suffix-positions/s (and supermax repeats/s) at minlen=20; % HBM roofline; "
+          "1/2/4/8 GPU")
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    "c3": dict(kind="human", bases=3_000_000_000, seed=1, minlen=20,
+               workload="3 Gbp synthetic human-like DNA (40% repeats), minlen=20"),
+    "c2": dict(kind="uniform", bases=100_000_000, seed=42, minlen=20,
+               workload="100 Mbp synthetic uniform ACGT, minlen=20"),
+}
+
+
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--bases", type=int, default=None, help="override genome size")
+    ap.add_argument("--minlen", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=3_200_000_000,
+                    help="max suffix rows timed on the CPU")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import genometools_smax_amd as G
+
+    cfg = dict(CONFIGS[args.config])
+    if args.bases:
+        cfg["bases"] = args.bases
+        cfg["workload"] = cfg["workload"].replace(
+            "3 Gbp" if args.config == "c3" else "100 Mbp", "%.3g bp" % args.bases)
+    if args.minlen:
+        cfg["minlen"] = args.minlen
+    minlen = cfg["minlen"]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # ---- setup (untimed): synthetic genome -> GPU ESA
+    t0 = time.time()
+    text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
+    t_gen = time.time() - t0
+    log("rank %d: generated %d symbols in %.1fs" % (rank, len(text), t_gen))
+    t0 = time.time()
+    esa = G.DeviceEsa(text, device=local, keep_suftab=False)
+    t_esa = time.time() - t0
+    n, N = esa.totallength, esa.nonspecials
+    log("rank %d: GPU ESA n=%d N=%d llv=%d rounds=%d in %.1fs"
+        % (rank, n, N, esa.numllv, esa.esa.sort_rounds, t_esa))
+
+    # ---- this rank's suffix-array range
+    begin = 1 + (N - 1) * rank // world
+    end = 1 + (N - 1) * (rank + 1) // world
+    plan = esa.plan(minlen, begin, end)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    send = recv = None
+    if world > 1:
+        send = torch.zeros(G.BOUNDARY_BYTES, dtype=torch.uint8, device="cuda")
+        recv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8, device="cuda")
+
+    def step():
+        plan.run(sptr)
+        if world > 1:
+            plan.copy_boundary(send.data_ptr(), sptr)
+            dist.all_gather_into_tensor(recv, send)
+            plan.stitch(recv.data_ptr(), world, rank, sptr)
+
+    # first pass sizes the output exactly (re-plan on overflow)
+    step()
+    torch.cuda.synchronize()
+    cnt = plan.fetch_count()
+    if cnt > plan.capacity:
+        log("rank %d: %d intervals > capacity %d, re-planning" % (rank, cnt, plan.capacity))
+        plan.close()
+        plan = esa.plan(minlen, begin, end, capacity=cnt + 16)
+
+    for _ in range(args.warmup):
+        step()
+    plan.enable_timing(args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    k1_ms, k1_n = plan.kernel_ms()
+    count = plan.fetch_count()
+
+    # llv entries in this rank's rows (algorithmic bytes)
+    host = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        host = esa.download()
+        llv_pos = host["llvtab"][:, 0] if len(host["llvtab"]) else np.zeros(0, np.uint64)
+    else:
+        llv_pos = esa.download()["llvtab"][:, 0] if esa.numllv else np.zeros(0, np.uint64)
+    llv_here = int(np.count_nonzero((llv_pos >= begin - 1) & (llv_pos <= end)))
+    rows = end - begin + 1
+    alg_bytes = 2 * rows + 16 * llv_here
+
+    stats = torch.tensor([elapsed, float(count), k1_ms / max(k1_n, 1)], dtype=torch.float64,
+                         device="cuda")
+    if dist:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot = stats.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, k1_avg_ms = float(mx[0]), float(mx[2])
+        count = int(tot[1])
+    else:
+        k1_avg_ms = float(stats[2])
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = N / (elapsed / args.steps)
+    achieved = alg_bytes / (k1_avg_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
+    if os.path.exists(pmc_path) and not args.bases:
+        with open(pmc_path) as fh:
+            pmc = json.load(fh)
+        traffic = pmc.get("hbm_bytes_per_launch")
+
+    cpu = None
+    if host is not None:
+        import oracle_lib  # noqa: E402  (tests/: the checker, CPU baseline leg only)
+        sample = min(N, args.cpu_sample)
+        log("cpu baseline: oracle linsmax over %d rows (1 core)" % sample)
+        t0 = time.perf_counter()
+        res = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample, minlen)
+        t_cpu = time.perf_counter() - t0
+        if sample == N and len(res) != count:
+            log("WARNING: GPU %d intervals != CPU oracle %d" % (count, len(res)))
+        elif sample == N:
+            log("GPU interval count matches the CPU oracle (%d)" % count)
+        cpu = {"value": sample / t_cpu, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
+               "sample": "oracle orc_linsmax (single core, -O3) over suffix rows [0,%d) of the same "
+                         "tables: %.2fs" % (sample, t_cpu)}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "suffix-positions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": cfg["workload"], "minlen": minlen, "totallength": n,
+                       "nonspecials": N, "llv_entries": esa.numllv, "global_batch": N,
+                       "parallelism": "sa-range-shard x%d + RCCL all-gather stitch" % world
+                       if world > 1 else "single GPU"},
+            "smax_intervals": count,
+            "supermax_repeats_per_s": count / (elapsed / args.steps),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "smax_scan_kernel", "kernel_avg_ms": k1_avg_ms,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2)},
+        }
+        print(json.dumps(out), flush=True)
+    plan.close()
+    esa.release()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    main()

@@ -127,6 +127,9 @@ def lib():
         L.gt_smax_stitch_host.argtypes = [ctypes.POINTER(GtSmaxBoundary), ci, ci, u32,
                                           ctypes.POINTER(GtSmaxRecord)]
         L.gt_smax_plan_fetch_count.argtypes = [vp, ctypes.POINTER(u64)]
+        L.gt_smax_plan_timing.argtypes = [vp, ci]
+        L.gt_smax_plan_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci)]
+        L.gt_smax_plan_copy_boundary.argtypes = [vp, vp, vp]
         _lib = L
     return _lib
 
@@ -384,6 +387,23 @@ class SmaxPlan:
     @property
     def num_tiles(self):
         return lib().gt_smax_plan_num_tiles(self.plan)
+
+    def enable_timing(self, nslots):
+        """Record hipEvents around the scan kernel of the next runs."""
+        if lib().gt_smax_plan_timing(self.plan, int(nslots)) != 0:
+            raise SmaxError("gt_smax_plan_timing failed")
+
+    def kernel_ms(self):
+        """(sum of scan-kernel milliseconds, launches timed)."""
+        ms = ctypes.c_double()
+        n = ctypes.c_int()
+        if lib().gt_smax_plan_timing_read(self.plan, ctypes.byref(ms), ctypes.byref(n)) != 0:
+            raise SmaxError("gt_smax_plan_timing_read failed")
+        return ms.value, n.value
+
+    def copy_boundary(self, dst_ptr, stream=0):
+        if lib().gt_smax_plan_copy_boundary(self.plan, dst_ptr, stream or None) != 0:
+            raise SmaxError("gt_smax_plan_copy_boundary failed")
 
     def fetch_count(self):
         c = ctypes.c_uint64()

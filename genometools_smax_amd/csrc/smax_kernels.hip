@@ -581,6 +581,10 @@ struct GtSmaxPlan {
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint32_t *llv_lo, *llv_hi;
+  // optional K1 timing: event pairs recorded around the scan kernel
+  hipEvent_t *ev;
+  int nslots;
+  uint64_t runs;
 };
 
 extern "C" int gt_smax_device_count(void) {
@@ -700,6 +704,8 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p->bnd) (void) hipFree(p->bnd);
   if (p->llv_lo) (void) hipFree(p->llv_lo);
   if (p->llv_hi) (void) hipFree(p->llv_hi);
+  for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
+  free(p->ev);
   free(p);
 }
 
@@ -747,10 +753,14 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
     HIPCHK(hipGetLastError());
+    const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
+    if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
     hipLaunchKernelGGL(smax_scan_kernel, dim3(p->num_tiles), dim3(SMAX_THREADS),
                        0, s, a);
     HIPCHK(hipGetLastError());
+    if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
   }
+  p->runs++;
   p->ticket_base += p->num_tiles;
   p->epoch += 1;
   return 0;
@@ -782,6 +792,58 @@ extern "C" int gt_smax_stitch_host(const GtSmaxBoundary *all, int nshards,
                                    int shard_index, unsigned int minlen,
                                    GtSmaxRecord *rec) {
   return stitch_resolve(all, nshards, shard_index, minlen, rec);
+}
+
+extern "C" int gt_smax_plan_timing(GtSmaxPlan *p, int nslots) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  HIPCHK(hipSetDevice(p->shard.device));
+  for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
+  free(p->ev);
+  p->ev = NULL;
+  p->nslots = 0;
+  p->runs = 0;
+  if (nslots <= 0) return 0;
+  p->ev = (hipEvent_t *) calloc((size_t) (2 * nslots), sizeof (hipEvent_t));
+  if (p->ev == NULL) return -1;
+  for (int i = 0; i < 2 * nslots; i++) {
+    HIPCHK(hipEventCreate(&p->ev[i]));
+    p->nslots = (i + 2) / 2;
+  }
+  p->nslots = nslots;
+  return 0;
+fail:
+  return -1;
+}
+
+extern "C" int gt_smax_plan_timing_read(GtSmaxPlan *p, double *sum_ms, int *nread) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  double acc = 0.0;
+  int n = (int) (p->runs < (uint64_t) p->nslots ? p->runs : (uint64_t) p->nslots);
+  HIPCHK(hipSetDevice(p->shard.device));
+  for (int i = 0; i < n; i++) {
+    float ms = 0.0f;
+    HIPCHK(hipEventSynchronize(p->ev[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]));
+    acc += ms;
+  }
+  *sum_ms = acc;
+  *nread = n;
+  return 0;
+fail:
+  return -1;
+}
+
+extern "C" int gt_smax_plan_copy_boundary(GtSmaxPlan *p, void *dst_dev, void *stream) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  HIPCHK(hipSetDevice(p->shard.device));
+  HIPCHK(hipMemcpyAsync(dst_dev, p->bnd, sizeof (GtSmaxBoundary),
+                        hipMemcpyDeviceToDevice, (hipStream_t) stream));
+  return 0;
+fail:
+  return -1;
 }
 
 extern "C" int gt_smax_plan_fetch_count(GtSmaxPlan *p, uint64_t *count) {

@@ -180,6 +180,16 @@ int gt_smax_stitch_host(const GtSmaxBoundary *all, int nshards,
                         int shard_index, unsigned int minlen,
                         GtSmaxRecord *rec);
 
+/* K1 timing: record hipEvents around the scan kernel of the next runs into
+ * nslots ring slots (0 disables); read sums the elapsed time of the slots
+ * filled so far (synchronising on them). */
+int gt_smax_plan_timing(GtSmaxPlan *plan, int nslots);
+int gt_smax_plan_timing_read(GtSmaxPlan *plan, double *sum_ms, int *nread);
+
+/* Copies this shard's boundary record to dst_dev (device memory) on stream,
+ * e.g. into the send buffer of an all-gather. */
+int gt_smax_plan_copy_boundary(GtSmaxPlan *plan, void *dst_dev, void *stream);
+
 /* Synchronises the plan's device and copies the record count to the host. */
 int gt_smax_plan_fetch_count(GtSmaxPlan *plan, uint64_t *count);
 
