@@ -11,22 +11,26 @@
 // BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
-// Kernel K1 (smax_scan_kernel), one 256-thread workgroup per 16384-row tile:
-//   phase 0  coalesced 16 B/lane loads of the tile's LCP bytes into
-//            registers + LDS (plus a 16-byte left and 64-byte right halo);
-//   phase 1  per 16-byte segment a SWAR pre-filter (any byte >= minlen);
-//            surviving rows test "plateau start" LCP[c] > LCP[c-1] and scan
-//            the plateau to its end in LDS (255 bytes resolved through an
-//            LDS copy of the tile's .llv window);
-//   phase 2  only if the tile has a local-maximum candidate, the tile's BWT
-//            bytes are loaded (coalesced) into LDS -- uniform DNA at
-//            minlen 20 never touches .bwt;
+// Kernel K1 (smax_scan_kernel) is persistent: each 256-thread workgroup
+// claims 16384-row tiles from an atomic ticket (tile order = claim order) and
+// software-pipelines them -- the next tile's LCP bytes (16 B/lane, coalesced)
+// are in flight while the current tile is processed:
+//   stage    current tile's LCP bytes + 16 B left / 64 B right halo -> LDS;
+//   filter   SWAR "any byte >= minlen" per 16-byte segment; if any row of
+//            the tile can start a candidate, the tile's BWT bytes are loaded
+//            (coalesced) while phase 1 runs -- uniform DNA tiles whose LCP
+//            stays below minlen never touch .bwt;
+//   .llv     a 255 byte is resolved in O(1): its rank among the window's 255
+//            bytes (per-16-byte-chunk prefix counts in LDS + a SWAR count)
+//            indexes the .llv entries, which are in position order;
+//   phase 1  plateau starts LCP[c] > LCP[c-1] scanned to their end in LDS;
+//            local maxima become candidates (exact values only when two
+//            compared bytes are both 255);
 //   phase 3  left-diversity: 256-bit seen-set over BWT[lb..rb];
-//   phase 4  block scan of per-thread counts, decoupled look-back across
-//            tiles (tile order from an atomic ticket, status words with
-//            epoch tags read/written with agent-scope relaxed atomics),
-//            ordered write of 16-byte records -> output is ascending lb,
-//            exactly the order the reference's traversal pops intervals.
+//   phase 4  block scan of per-row counts (row order), decoupled look-back
+//            across tiles (status words with epoch tags, agent-scope relaxed
+//            atomics), ordered 16-byte record writes -> output is ascending
+//            lb, the order the reference's traversal pops intervals.
 // No MFMA: integer/byte work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -42,8 +46,8 @@
 #define SMAX_TILE (SMAX_THREADS * SMAX_SEGS * 16)     // 16384 rows per tile
 #define SMAX_LH 16                                    // left halo (bytes)
 #define SMAX_RH 64                                    // right halo (bytes)
-#define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)
-#define SMAX_LLV_CAP 512
+#define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
+#define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
 
 #define ST_FLAG_AGG 1ull
 #define ST_FLAG_PFX 2ull
@@ -55,6 +59,7 @@
 static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
 static_assert(GT_SMAX_PAD_FRONT >= SMAX_LH, "front padding covers the halo");
+static_assert(SMAX_LDSB % 16 == 0, "window is whole 16-byte chunks");
 
 struct SmaxScanArgs {
   const uint8_t *lcp;        // local tables: index i <-> global base+i
@@ -64,6 +69,7 @@ struct SmaxScanArgs {
   const uint32_t *llv_lo;    // per tile: first llv index >= tile_g0 - LH
   const uint32_t *llv_hi;    // per tile: first llv index >= tile_g1 + RH
   uint64_t base, begin, end, N;
+  uint64_t tile_first;       // first local tile holding an owned row
   uint32_t minlen;
   uint32_t num_tiles;
   GtSmaxRecord *out;
@@ -96,75 +102,97 @@ __device__ static uint32_t llv_search_global(const GtSmaxLlv *llv, uint64_t lo,
   return (uint32_t) llv[lo].value;   // present by construction of .llv
 }
 
-struct TileCtx {
+// high bit of each byte of w that is >= m (m <= 128); exact
+__device__ __forceinline__ uint32_t bytes_ge(uint32_t w, uint32_t m) {
+  uint32_t add = (128u - m) * 0x01010101u;
+  return (w | ((w & 0x7f7f7f7fu) + add)) & 0x80808080u;
+}
+// high bit of each byte of w that equals 0xff; exact
+__device__ __forceinline__ uint32_t bytes_ff(uint32_t w) {
+  uint32_t x = ~w;
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu) & 0x80808080u;
+}
+
+struct Win {
   const uint8_t *glcp;        // global (local-indexed) tables
   const uint8_t *gbwt;
   const GtSmaxLlv *llv;
   uint64_t numllv, base, N, end;
-  const uint8_t *L;           // LDS L window, index = g - w0
-  const uint8_t *B;           // LDS B window
-  const uint32_t *lpos;       // LDS llv positions (g - w0)
-  const uint32_t *lval;
-  int nllv;                   // -1: not in LDS, search global [glo, ghi)
-  uint64_t glo, ghi;
-  uint64_t w0, w1;            // global window [w0, w1) held in LDS
+  const uint8_t *L;           // LDS window: index o = g - g0 + LH
+  const uint8_t *B;
+  const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
+  uint64_t g0;                // global row of the tile start
+  uint64_t llv_base;          // first llv entry of the window
 };
 
-// exact LCP[g] (g global), L[0] = L[N] = 0
-__device__ static uint32_t lcp_at(const TileCtx &t, uint64_t g) {
-  if (g == 0 || g >= t.N) return 0;
-  uint32_t b;
-  bool inwin = (g >= t.w0 && g < t.w1);
-  if (inwin) b = t.L[g - t.w0];
-  else b = t.glcp[g - t.base];
-  if (b < 255) return b;
-  if (inwin && t.nllv >= 0) {
-    uint32_t key = (uint32_t) (g - t.w0);
-    int lo = 0, hi = t.nllv;
-    while (lo < hi) {
-      int mid = (lo + hi) >> 1;
-      if (t.lpos[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    return t.lval[lo];
+__device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
+  t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
+  t.base = a.base; t.N = a.N; t.end = a.end;
+  t.L = nullptr; t.B = nullptr; t.rank = nullptr; t.g0 = 0; t.llv_base = 0;
+}
+
+__device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
+  return (int64_t) (g - t.g0) + SMAX_LH;
+}
+
+// exact LCP of a row whose byte is 255
+__device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
+  int64_t o = win_off(t, g);
+  if (t.rank != nullptr && o >= 0 && o < SMAX_LDSB) {
+    int chunk = (int) (o >> 4), within = (int) (o & 15);
+    uint4 v = *reinterpret_cast<const uint4 *>(&t.L[chunk * 16]);
+    uint32_t f0 = bytes_ff(v.x), f1 = bytes_ff(v.y), f2 = bytes_ff(v.z),
+             f3 = bytes_ff(v.w);
+    // bytes below `within` only
+    uint64_t lo = (uint64_t) f0 | ((uint64_t) f1 << 32);
+    uint64_t hi = (uint64_t) f2 | ((uint64_t) f3 << 32);
+    int cnt;
+    if (within < 8) cnt = __popcll(lo & ((1ull << (8 * within)) - 1));
+    else cnt = __popcll(lo) + __popcll(hi & ((1ull << (8 * (within - 8))) - 1));
+    uint64_t idx = t.llv_base + t.rank[chunk] + (uint64_t) cnt;
+    return (uint32_t) t.llv[idx].value;
   }
-  if (inwin) return llv_search_global(t.llv, t.glo, t.ghi, g);
   return llv_search_global(t.llv, 0, t.numllv, g);
 }
 
-__device__ __forceinline__ uint32_t bwt_at(const TileCtx &t, uint64_t g) {
-  if (g >= t.w0 && g < t.w1) return t.B[g - t.w0];
+// byte of LCP[g] (LCP[0] = LCP[N] = 0 are returned as 0)
+__device__ __forceinline__ uint32_t lcp_byte(const Win &t, uint64_t g) {
+  if (g == 0 || g >= t.N) return 0;
+  int64_t o = win_off(t, g);
+  if (t.L != nullptr && o >= 0 && o < SMAX_LDSB) return t.L[o];
+  return t.glcp[g - t.base];
+}
+
+__device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
+  uint32_t b = lcp_byte(t, g);
+  return b < 255 ? b : lcp_big(t, g);
+}
+
+__device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
+  int64_t o = win_off(t, g);
+  if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
   return t.gbwt[g - t.base];
 }
 
-// Any byte of w >= m (m <= 128); superset filter for larger m.
-// (both return a mask whose high bits mark the qualifying bytes)
-__device__ __forceinline__ uint32_t any_byte_ge(uint32_t w, uint32_t m) {
-  uint32_t add = (128u - m) * 0x01010101u;
-  return (w | ((w & 0x7f7f7f7fu) + add)) & 0x80808080u;
-}
-__device__ __forceinline__ uint32_t any_byte_ff(uint32_t w) {
-  uint32_t x = ~w;
-  return (x - 0x01010101u) & ~x & 0x80808080u;
-}
-
-// Plateau scan from start c (LCP[c] == l): returns j (last row of the run)
-// and sets *next to LCP[j+1]; *pending when the run reaches the shard end.
-__device__ static uint64_t plateau_end(const TileCtx &t, uint64_t c, uint32_t l,
-                                       uint32_t *next, bool *pending) {
+// Plateau scan from start c with exact value l (byte lb = min(l,255)):
+// returns j (last row of the run) and sets *next = LCP[j+1] relative to l:
+// -1 smaller, +1 larger; *pending when the run reaches the shard end.
+__device__ static uint64_t plateau_end(const Win &t, uint64_t c, uint32_t l,
+                                       int *rel, bool *pending) {
+  const uint32_t lb = l < 255 ? l : 255;
   uint64_t j = c;
   *pending = false;
   for (;;) {
-    uint64_t g = j + 1;
-    uint32_t nx = lcp_at(t, g);
-    if (nx != l) { *next = nx; return j; }
-    if (g >= t.end) { *pending = true; *next = nx; return j; }  // g == end < N
+    const uint64_t g = j + 1;
+    uint32_t nb = lcp_byte(t, g);
+    if (nb != lb) { *rel = nb < lb ? -1 : 1; return j; }
+    if (lb == 255) {
+      uint32_t nx = lcp_big(t, g);
+      if (nx != l) { *rel = nx < l ? -1 : 1; return j; }
+    }
+    if (g >= t.end) { *pending = true; *rel = 0; return j; }   // g == end < N
     j = g;
   }
-}
-
-__device__ __forceinline__ void ctx_init(TileCtx &t, const SmaxScanArgs &a) {
-  t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
-  t.base = a.base; t.N = a.N; t.end = a.end;
 }
 
 struct Seen {
@@ -182,21 +210,54 @@ __device__ __forceinline__ bool seen_add(Seen &s, uint32_t c) {
   return (cur & bit) != 0;
 }
 
+// exclusive prefix of per-(segment, lane) counts in row order within the
+// block: returns per-segment offsets inside the wave and the wave's offset
+// inside the block; *total = block total.  Uses sWave[4]; two barriers.
+__device__ __forceinline__ void block_scan_rows(const uint32_t cnt[SMAX_SEGS],
+                                                uint32_t seg_off[SMAX_SEGS],
+                                                uint32_t *wave_off,
+                                                uint32_t *total,
+                                                uint32_t *sWave) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t wt = 0;
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    uint32_t incl = cnt[r];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    seg_off[r] = wt + incl - cnt[r];
+    wt += __shfl(incl, 63, 64);
+  }
+  __syncthreads();                 // sWave free (previous users done)
+  if (lane == 0) sWave[wave] = wt;
+  __syncthreads();
+  uint32_t wo = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < SMAX_THREADS / 64; w++) {
+    uint32_t ws = sWave[w];
+    if (w < wave) wo += ws;
+    tot += ws;
+  }
+  *wave_off = wo;
+  *total = tot;
+}
+
 // ------------------------------------------------------------ K0: head run
 
-// One wave: the boundary record's head (run of LCP == LCP[begin]) and reset
+// One lane: the boundary record's head (run of LCP == LCP[begin]) and reset
 // of the pending slot.  Runs before K1 on the same stream.
 __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (threadIdx.x != 0) return;
-  TileCtx t;
-  ctx_init(t, a);
-  t.L = nullptr; t.B = nullptr; t.lpos = nullptr; t.lval = nullptr;
-  t.nllv = -1; t.glo = 0; t.ghi = a.numllv; t.w0 = 0; t.w1 = 0;
+  Win t;
+  win_init(t, a);
   GtSmaxBoundary *b = a.bnd;
   b->pend_valid = 0;
   b->shard_begin = a.begin;
   b->shard_end = a.end;
-  uint32_t v = lcp_at(t, a.begin);
+  uint32_t v = lcp_exact(t, a.begin);
   b->head_v = v;
   Seen s = {0, 0, 0, 0};
   uint64_t dup = 0;
@@ -206,7 +267,7 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
     for (;;) {
       if (seen_add(s, a.bwt[g - a.base])) { dup = 1; break; }
       uint64_t h = g + 1;
-      uint32_t nx = lcp_at(t, h);
+      uint32_t nx = lcp_exact(t, h);
       if (nx != v) { f = h; nxt = nx; break; }
       if (h >= a.end) break;   // run covers the whole shard: passthrough
       g = h;
@@ -224,265 +285,321 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
 
 // ------------------------------------------------------------ K1: scan
 
+// Tile loads: 4 x 16 B per lane of LCP and of BWT (coalesced, 1 KiB per
+// wave instruction); halo chunks go to threads 0..4 (LCP: 16 B left, 64 B
+// right) and 5..9 (BWT, same chunks), one uint4 each.  Named fields, no
+// arrays: keeps the prefetch in VGPRs (arrays written under a condition were
+// demoted to scratch by hipcc).
+struct TileRegs {
+  uint4 l0, l1, l2, l3, b0, b1, b2, b3, h;
+};
+
+__device__ __forceinline__ void load_tile(const uint8_t *lcp, const uint8_t *bwt,
+                                          uint64_t l0, TileRegs &R) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint8_t *ls = lcp + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
+  const uint8_t *bs = bwt + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
+  R.l0 = *reinterpret_cast<const uint4 *>(ls);
+  R.l1 = *reinterpret_cast<const uint4 *>(ls + 1024);
+  R.l2 = *reinterpret_cast<const uint4 *>(ls + 2048);
+  R.l3 = *reinterpret_cast<const uint4 *>(ls + 3072);
+  R.b0 = *reinterpret_cast<const uint4 *>(bs);
+  R.b1 = *reinterpret_cast<const uint4 *>(bs + 1024);
+  R.b2 = *reinterpret_cast<const uint4 *>(bs + 2048);
+  R.b3 = *reinterpret_cast<const uint4 *>(bs + 3072);
+  if (tid < 10) {
+    const int h = tid < 5 ? tid : tid - 5;
+    const int64_t off = (h == 0) ? -SMAX_LH : (int64_t) SMAX_TILE + (h - 1) * 16;
+    R.h = *reinterpret_cast<const uint4 *>((tid < 5 ? lcp : bwt) + l0 + off);
+  }
+}
+
+__device__ __forceinline__ void store_tile(uint8_t *sL, uint8_t *sB, const TileRegs &R) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t o = SMAX_LH + wave * SMAX_WAVE_BYTES + lane * 16;
+  *reinterpret_cast<uint4 *>(&sL[o]) = R.l0;
+  *reinterpret_cast<uint4 *>(&sL[o + 1024]) = R.l1;
+  *reinterpret_cast<uint4 *>(&sL[o + 2048]) = R.l2;
+  *reinterpret_cast<uint4 *>(&sL[o + 3072]) = R.l3;
+  *reinterpret_cast<uint4 *>(&sB[o]) = R.b0;
+  *reinterpret_cast<uint4 *>(&sB[o + 1024]) = R.b1;
+  *reinterpret_cast<uint4 *>(&sB[o + 2048]) = R.b2;
+  *reinterpret_cast<uint4 *>(&sB[o + 3072]) = R.b3;
+  if (tid < 10) {
+    const int h = tid < 5 ? tid : tid - 5;
+    const int off = (h == 0) ? 0 : SMAX_LH + SMAX_TILE + (h - 1) * 16;
+    *reinterpret_cast<uint4 *>(&(tid < 5 ? sL : sB)[off]) = R.h;
+  }
+}
+
+__device__ __forceinline__ uint32_t seg_ge(const uint4 v, uint32_t mf) {
+  return bytes_ge(v.x, mf) | bytes_ge(v.y, mf) | bytes_ge(v.z, mf) | bytes_ge(v.w, mf);
+}
+__device__ __forceinline__ uint32_t seg_ffcount(const uint4 v) {
+  return __popc(bytes_ff(v.x)) + __popc(bytes_ff(v.y)) + __popc(bytes_ff(v.z)) +
+         __popc(bytes_ff(v.w));
+}
+
 __global__ void __launch_bounds__(SMAX_THREADS)
 smax_scan_kernel(SmaxScanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sL[SMAX_LDSB];
   __shared__ __attribute__((aligned(16))) uint8_t sB[SMAX_LDSB];
-  __shared__ uint32_t sLpos[SMAX_LLV_CAP];
-  __shared__ uint32_t sLval[SMAX_LLV_CAP];
-  __shared__ uint32_t sWaveSum[SMAX_THREADS / 64];
-  __shared__ uint64_t sTile, sExcl;
+  __shared__ uint16_t sRank[SMAX_NCHUNK];
+  __shared__ uint32_t sWave[SMAX_THREADS / 64];
+  __shared__ uint64_t sNext, sExcl;
+  __shared__ uint32_t sFlags;
+  __shared__ uint32_t sHalo[5];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-
-  if (tid == 0) {
-    unsigned long long old = atomicAdd(a.ticket, 1ull);
-    sTile = old - a.ticket_base;
-  }
-  __syncthreads();
-  const uint64_t tile = sTile;
-  const uint64_t l0 = tile * (uint64_t) SMAX_TILE;       // local index
-  const uint64_t g0 = a.base + l0;                         // global index
-  const uint64_t w0 = g0 - SMAX_LH;                        // LDS window start
-
-  // ---- phase 0: coalesced L loads (registers + LDS)
-  uint4 seg[SMAX_SEGS];
-  const uint8_t *lsrc = a.lcp + l0;
-#pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++) {
-    uint32_t off = wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-    seg[r] = *reinterpret_cast<const uint4 *>(lsrc + off);
-    *reinterpret_cast<uint4 *>(&sL[SMAX_LH + off]) = seg[r];
-  }
-  if (tid < 5) {   // halo: 16 bytes left, 64 bytes right
-    int64_t off = (tid == 0) ? -SMAX_LH : (int64_t) SMAX_TILE + (tid - 1) * 16;
-    *reinterpret_cast<uint4 *>(&sL[SMAX_LH + off]) =
-        *reinterpret_cast<const uint4 *>(lsrc + off);
-  }
-  uint32_t has_ff = 0;
-#pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++)
-    has_ff |= any_byte_ff(seg[r].x) | any_byte_ff(seg[r].y) |
-              any_byte_ff(seg[r].z) | any_byte_ff(seg[r].w);
-  __syncthreads();
-  if (tid < 5) {
-    const uint8_t *h = &sL[tid == 0 ? 0 : SMAX_LH + SMAX_TILE + (tid - 1) * 16];
-    uint4 hv = *reinterpret_cast<const uint4 *>(h);
-    has_ff |= any_byte_ff(hv.x) | any_byte_ff(hv.y) | any_byte_ff(hv.z) |
-              any_byte_ff(hv.w);
-  }
-  const bool tile_ff = __syncthreads_or(has_ff != 0);
-
-  TileCtx t;
-  ctx_init(t, a);
-  t.L = sL; t.B = sB; t.lpos = sLpos; t.lval = sLval;
-  t.w0 = w0; t.w1 = w0 + SMAX_LDSB;
-  t.nllv = 0; t.glo = 0; t.ghi = 0;
-  if (tile_ff) {
-    uint64_t lo = a.llv_lo[tile], hi = a.llv_hi[tile];
-    t.glo = lo; t.ghi = hi;
-    if (hi - lo <= SMAX_LLV_CAP) {
-      for (uint64_t i = lo + tid; i < hi; i += SMAX_THREADS) {
-        sLpos[i - lo] = (uint32_t) (a.llv[i].position - w0);
-        sLval[i - lo] = (uint32_t) a.llv[i].value;
-      }
-      t.nllv = (int) (hi - lo);
-    } else {
-      t.nllv = -1;
-    }
-    __syncthreads();
-  }
-
-  // ---- phase 1: plateau starts that are local maxima (L only)
   const uint32_t m = a.minlen;
   const uint32_t mf = m < 128 ? m : 128;
-  uint64_t cand = 0;          // bit r*16+q: row is a local-maximum start
-  bool pend_here = false;
-  uint64_t pend_c = 0;
-  uint32_t pend_l = 0;
-#pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++) {
-    const uint4 v = seg[r];
-    if ((any_byte_ge(v.x, mf) | any_byte_ge(v.y, mf) | any_byte_ge(v.z, mf) |
-         any_byte_ge(v.w, mf)) == 0)
-      continue;
-    const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-    const uint64_t lo8 = (uint64_t) v.x | ((uint64_t) v.y << 32);
-    const uint64_t hi8 = (uint64_t) v.z | ((uint64_t) v.w << 32);
-    for (int q = 0; q < 16; q++) {
-      uint32_t byte = (uint32_t) (((q < 8) ? (lo8 >> (8 * q)) : (hi8 >> (8 * (q - 8)))) & 0xffu);
-      if (byte < 255 && byte < m) continue;
-      const uint64_t c = sg + q;
-      if (c < a.begin || c >= a.end) continue;
-      uint32_t cur = lcp_at(t, c);
-      if (cur < m) continue;
-      uint32_t prev = lcp_at(t, c - 1);
-      if (cur <= prev) continue;
-      uint32_t nx;
-      bool pend;
-      uint64_t j = plateau_end(t, c, cur, &nx, &pend);
-      (void) j;
-      if (pend) {
-        pend_here = true; pend_c = c; pend_l = cur;
-      } else if (nx < cur) {
-        cand |= 1ull << (r * 16 + q);
-      }
-    }
-  }
+  const uint64_t ep = (a.epoch & ST_EPOCH_MASK) << ST_VALUE_BITS;
 
-  // ---- phase 2: BWT tile only when some row needs it
-  const bool need_b = __syncthreads_or(cand != 0 || pend_here);
-  if (need_b) {
-    const uint8_t *bsrc = a.bwt + l0;
+  if (tid == 0) {
+    sNext = atomicAdd(a.ticket, 1ull) - a.ticket_base;
+    sFlags = 0;
+  }
+  __syncthreads();
+  uint64_t tile = sNext;
+  if (tile >= a.num_tiles) return;
+
+  Win t;
+  win_init(t, a);
+  t.L = sL;
+  t.B = sB;
+
+  TileRegs R;
+  R.h = make_uint4(0, 0, 0, 0);
+  load_tile(a.lcp, a.bwt, (a.tile_first + tile) * (uint64_t) SMAX_TILE, R);
+
+  for (;;) {
+    const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
+    const uint64_t g0 = a.base + l0;                                      // global row
+    t.g0 = g0;
+
+    // ---- stage the prefetched tile, claim the next one, filter
+    store_tile(sL, sB, R);
+    if (tid == 0) sNext = atomicAdd(a.ticket, 1ull) - a.ticket_base;
+    uint32_t cntff[SMAX_SEGS];
+    const uint32_t p0 = seg_ge(R.l0, mf), p1 = seg_ge(R.l1, mf), p2 = seg_ge(R.l2, mf),
+                   p3 = seg_ge(R.l3, mf);
+    const uint32_t pre = p0 | p1 | p2 | p3;
+    const uint32_t segpre = (p0 ? 1u : 0u) | (p1 ? 2u : 0u) | (p2 ? 4u : 0u) | (p3 ? 8u : 0u);
+    cntff[0] = seg_ffcount(R.l0);
+    cntff[1] = seg_ffcount(R.l1);
+    cntff[2] = seg_ffcount(R.l2);
+    cntff[3] = seg_ffcount(R.l3);
+    const uint32_t ff = cntff[0] | cntff[1] | cntff[2] | cntff[3];
+    const uint32_t hff = tid < 5 ? seg_ffcount(R.h) : 0u;
+    const uint32_t fl = (pre ? 1u : 0u) | ((ff | hff) ? 2u : 0u);
+    if (fl) atomicOr(&sFlags, fl);
+    __syncthreads();
+    const uint32_t flags = sFlags;
+    const uint64_t next = sNext;
+    const bool need_b = (flags & 1u) != 0;
+    const bool has_ff = (flags & 2u) != 0;
+
+    // ---- prefetch the next tile (LCP + BWT) while this one is processed
+    if (next < a.num_tiles)
+      load_tile(a.lcp, a.bwt, (a.tile_first + next) * (uint64_t) SMAX_TILE, R);
+
+    // ---- .llv ranks of the window's 255 bytes
+    if (has_ff) {
+      uint32_t so[SMAX_SEGS], wo, tot;
+      block_scan_rows(cntff, so, &wo, &tot, sWave);
+      // chunk 0 = left halo, 1..1024 = tile rows, 1025..1028 = right halo
+      if (tid < 5) sHalo[tid] = hff;
+      __syncthreads();
+      const uint32_t h0 = sHalo[0];
 #pragma unroll
-    for (int r = 0; r < SMAX_SEGS; r++) {
-      uint32_t off = wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-      *reinterpret_cast<uint4 *>(&sB[SMAX_LH + off]) =
-          *reinterpret_cast<const uint4 *>(bsrc + off);
-    }
-    if (tid < 5) {
-      int64_t off = (tid == 0) ? -SMAX_LH : (int64_t) SMAX_TILE + (tid - 1) * 16;
-      *reinterpret_cast<uint4 *>(&sB[SMAX_LH + off]) =
-          *reinterpret_cast<const uint4 *>(bsrc + off);
+      for (int r = 0; r < SMAX_SEGS; r++)
+        sRank[1 + wave * 256 + r * 64 + lane] = (uint16_t) (h0 + wo + so[r]);
+      if (tid == 0) {
+        sRank[0] = 0;
+        uint32_t acc = h0 + tot;
+        for (int k = 0; k < 4; k++) {
+          sRank[1 + SMAX_TILE / 16 + k] = (uint16_t) acc;
+          acc += sHalo[1 + k];
+        }
+      }
+      t.rank = sRank;
+      t.llv_base = a.llv_lo[tile];
+    } else {
+      t.rank = nullptr;
     }
     __syncthreads();
-  }
 
-  // ---- phase 3: left-diversity
-  uint64_t tmp = cand;
-  while (tmp) {
-    int bit = __builtin_ctzll(tmp);
-    tmp &= tmp - 1;
-    int r = bit >> 4, q = bit & 15;
-    uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
-    uint32_t cur = lcp_at(t, c), nx;
-    bool pend;
-    uint64_t j = plateau_end(t, c, cur, &nx, &pend);
-    Seen s = {0, 0, 0, 0};
-    bool dup = false;
-    for (uint64_t g = c - 1; g <= j && !dup; g++) dup = seen_add(s, bwt_at(t, g));
-    if (dup) cand &= ~(1ull << bit);
-  }
-  if (pend_here) {
-    Seen s = {0, 0, 0, 0};
-    bool dup = false;
-    for (uint64_t g = pend_c - 1; g < a.end && !dup; g++)
-      dup = seen_add(s, bwt_at(t, g));
-    if (!dup) {
-      GtSmaxBoundary *b = a.bnd;
-      b->pend_c = pend_c;
-      b->pend_lcp = pend_l;
-      b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
-      b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
-      b->pend_div.dup = 0;
-      b->pend_valid = 1;
-    }
-  }
-
-  // ---- phase 4: block scan of counts in row order.  A wave's rows are
-  // ordered segment-major (r), then lane, so scan each segment slice.
-  uint32_t seg_off[SMAX_SEGS];
-  uint32_t wave_total = 0;
+    // ---- phase 1: plateau starts that are local maxima (L only)
+    uint64_t cand = 0;          // bit r*16+q: row is a local-maximum start
+    bool pend_here = false;
+    uint64_t pend_c = 0;
+    uint32_t pend_l = 0;
+    if (need_b) {
 #pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++) {
-    const uint32_t c = (uint32_t) __popcll((cand >> (16 * r)) & 0xffffull);
-    uint32_t incl = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
-    }
-    seg_off[r] = wave_total + incl - c;
-    wave_total += __shfl(incl, 63, 64);
-  }
-  if (lane == 0) sWaveSum[wave] = wave_total;
-  __syncthreads();
-  uint32_t wave_off = 0, tile_count = 0;
-#pragma unroll
-  for (int w = 0; w < SMAX_THREADS / 64; w++) {
-    uint32_t ws = sWaveSum[w];
-    if (w < wave) wave_off += ws;
-    tile_count += ws;
-  }
-
-  // ---- phase 5: decoupled look-back (wave 0)
-  const uint64_t ep = (a.epoch & ST_EPOCH_MASK) << ST_VALUE_BITS;
-  if (wave == 0) {
-    uint64_t excl = 0;
-    if (tile == 0) {
-      if (lane == 0)
-        st_status(&a.status[0], (ST_FLAG_PFX << 62) | ep | (uint64_t) tile_count);
-    } else {
-      if (lane == 0)
-        st_status(&a.status[tile], (ST_FLAG_AGG << 62) | ep | (uint64_t) tile_count);
-      int64_t pos = (int64_t) tile - 1;
-      for (;;) {
-        int64_t idx = pos - lane;
-        uint64_t sv;
-        if (idx >= 0) sv = ld_status(&a.status[idx]);
-        else sv = (ST_FLAG_PFX << 62) | ep;    // virtual prefix 0 before tile 0
-        uint64_t flag = sv >> 62;
-        bool valid = flag != 0 && ((sv >> ST_VALUE_BITS) & ST_EPOCH_MASK) ==
-                                      (a.epoch & ST_EPOCH_MASK);
-        bool ispfx = valid && flag == ST_FLAG_PFX;
-        uint64_t pfx_mask = __ballot(ispfx);
-        uint64_t inv_mask = __ballot(!valid);
-        // lanes up to and including the first prefix must all be valid
-        uint64_t upto = pfx_mask ? ((pfx_mask & (~pfx_mask + 1)) << 1) - 1 : ~0ull;
-        if (pfx_mask == (1ull << 63)) upto = ~0ull;
-        if (inv_mask & upto) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+      for (int r = 0; r < SMAX_SEGS; r++) {
+        if (!((segpre >> r) & 1)) continue;
+        const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+        const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
+        const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+        const uint64_t lo8 = (uint64_t) v.x | ((uint64_t) v.y << 32);
+        const uint64_t hi8 = (uint64_t) v.z | ((uint64_t) v.w << 32);
+        uint32_t prevb = lcp_byte(t, sg - 1);
+        for (int q = 0; q < 16; q++) {
+          const uint64_t c = sg + q;
+          uint32_t cb = (uint32_t) (((q < 8) ? (lo8 >> (8 * q)) : (hi8 >> (8 * (q - 8)))) & 0xffu);
+          if (c >= a.N || c == 0) cb = 0;
+          const uint32_t pb = prevb;
+          prevb = cb;
+          if (cb < m && cb != 255) continue;
+          if (c < a.begin || c >= a.end) continue;
+          uint32_t cur;
+          if (cb != 255) {
+            if (cb <= pb) continue;                  // pb < 255 here
+            cur = cb;
+          } else {
+            cur = lcp_big(t, c);
+            if (cur < m) continue;
+            if (pb == 255 && lcp_big(t, c - 1) >= cur) continue;
+          }
+          int rel;
+          bool pend;
+          (void) plateau_end(t, c, cur, &rel, &pend);
+          if (pend) {
+            pend_here = true; pend_c = c; pend_l = cur;
+          } else if (rel < 0) {
+            cand |= 1ull << (r * 16 + q);
+          }
         }
-        uint64_t val = (lane < 64 && ((upto >> lane) & 1)) ? (sv & ST_VALUE_MASK) : 0;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-        excl += val;
-        if (pfx_mask) break;
-        pos -= 64;
       }
-      if (lane == 0)
-        st_status(&a.status[tile],
-                  (ST_FLAG_PFX << 62) | ep | ((excl + tile_count) & ST_VALUE_MASK));
     }
-    if (lane == 0) {
-      sExcl = excl;
-      if (tile == a.num_tiles - 1) *a.count = excl + tile_count;
-    }
-  }
-  __syncthreads();
-  const uint64_t base_out = sExcl + wave_off;
 
-  // ---- phase 6: ordered record writes
-  tmp = cand;
-  while (tmp) {
-    int bit = __builtin_ctzll(tmp);
-    tmp &= tmp - 1;
-    int r = bit >> 4, q = bit & 15;
-    uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
-    uint32_t cur = lcp_at(t, c), nx;
-    bool pend;
-    uint64_t j = plateau_end(t, c, cur, &nx, &pend);
-    // rank of this row among the thread's rows of segment r
-    uint32_t before = (uint32_t) __popcll(cand & ((1ull << bit) - 1) & (0xffffull << (16 * r)));
-    uint32_t so = r == 0 ? seg_off[0] : r == 1 ? seg_off[1] : r == 2 ? seg_off[2] : seg_off[3];
-    uint64_t o = base_out + so + before;
-    if (o < a.capacity) {
-      GtSmaxRecord rec;
-      rec.lb = c - 1;
-      rec.lcp = cur;
-      rec.width = (uint32_t) (j - c + 2);
-      a.out[o] = rec;
+    // ---- phase 3: left-diversity
+    uint64_t tmp = cand;
+    while (tmp) {
+      const int bit = __builtin_ctzll(tmp);
+      tmp &= tmp - 1;
+      const int r = bit >> 4, q = bit & 15;
+      const uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
+      const uint32_t cur = lcp_exact(t, c);
+      int rel;
+      bool pend;
+      const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
+      Seen s = {0, 0, 0, 0};
+      bool dup = false;
+      for (uint64_t g = c - 1; g <= j && !dup; g++) dup = seen_add(s, bwt_at(t, g));
+      if (dup) cand &= ~(1ull << bit);
     }
+    if (pend_here) {
+      Seen s = {0, 0, 0, 0};
+      bool dup = false;
+      for (uint64_t g = pend_c - 1; g < a.end && !dup; g++)
+        dup = seen_add(s, bwt_at(t, g));
+      if (!dup) {
+        GtSmaxBoundary *b = a.bnd;
+        b->pend_c = pend_c;
+        b->pend_lcp = pend_l;
+        b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
+        b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
+        b->pend_div.dup = 0;
+        b->pend_valid = 1;
+      }
+    }
+
+    // ---- phase 4: block scan of counts in row order
+    uint32_t cnt[SMAX_SEGS], seg_off[SMAX_SEGS], wave_off, tile_count;
+#pragma unroll
+    for (int r = 0; r < SMAX_SEGS; r++)
+      cnt[r] = (uint32_t) __popcll((cand >> (16 * r)) & 0xffffull);
+    block_scan_rows(cnt, seg_off, &wave_off, &tile_count, sWave);
+
+    // ---- phase 5: decoupled look-back (wave 0)
+    if (wave == 0) {
+      uint64_t excl = 0;
+      if (tile == 0) {
+        if (lane == 0)
+          st_status(&a.status[0], (ST_FLAG_PFX << 62) | ep | (uint64_t) tile_count);
+      } else {
+        if (lane == 0)
+          st_status(&a.status[tile], (ST_FLAG_AGG << 62) | ep | (uint64_t) tile_count);
+        int64_t pos = (int64_t) tile - 1;
+        for (;;) {
+          const int64_t idx = pos - lane;
+          uint64_t sv;
+          if (idx >= 0) sv = ld_status(&a.status[idx]);
+          else sv = (ST_FLAG_PFX << 62) | ep;    // virtual prefix 0 before tile 0
+          const uint64_t flag = sv >> 62;
+          const bool valid = flag != 0 &&
+              ((sv >> ST_VALUE_BITS) & ST_EPOCH_MASK) == (a.epoch & ST_EPOCH_MASK);
+          const bool ispfx = valid && flag == ST_FLAG_PFX;
+          const uint64_t pfx_mask = __ballot(ispfx);
+          const uint64_t inv_mask = __ballot(!valid);
+          // lanes up to and including the first prefix must all be valid
+          const uint64_t upto = pfx_mask ? ((pfx_mask & (~pfx_mask + 1)) - 1) |
+                                               (pfx_mask & (~pfx_mask + 1))
+                                         : ~0ull;
+          if (inv_mask & upto) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          uint64_t val = ((upto >> lane) & 1) ? (sv & ST_VALUE_MASK) : 0;
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
+          excl += val;
+          if (pfx_mask) break;
+          pos -= 64;
+        }
+        if (lane == 0)
+          st_status(&a.status[tile],
+                    (ST_FLAG_PFX << 62) | ep | ((excl + tile_count) & ST_VALUE_MASK));
+      }
+      if (lane == 0) {
+        sExcl = excl;
+        if (tile == a.num_tiles - 1) *a.count = excl + tile_count;
+      }
+    }
+    __syncthreads();
+    const uint64_t base_out = sExcl + wave_off;
+
+    // ---- phase 6: ordered record writes
+    tmp = cand;
+    while (tmp) {
+      const int bit = __builtin_ctzll(tmp);
+      tmp &= tmp - 1;
+      const int r = bit >> 4, q = bit & 15;
+      const uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
+      const uint32_t cur = lcp_exact(t, c);
+      int rel;
+      bool pend;
+      const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
+      const uint32_t before = (uint32_t) __popcll(cand & ((1ull << bit) - 1) &
+                                                  (0xffffull << (16 * r)));
+      const uint32_t so = r == 0 ? seg_off[0] : r == 1 ? seg_off[1]
+                        : r == 2 ? seg_off[2] : seg_off[3];
+      const uint64_t o = base_out + so + before;
+      if (o < a.capacity) {
+        GtSmaxRecord rec;
+        rec.lb = c - 1;
+        rec.lcp = cur;
+        rec.width = (uint32_t) (j - c + 2);
+        a.out[o] = rec;
+      }
+    }
+
+    // ---- next tile
+    if (tid == 0) sFlags = 0;
+    __syncthreads();               // LDS (L, B, ranks, flags) free again
+    tile = next;
+    if (tile >= a.num_tiles) break;
   }
 }
 
 // ------------------------------------------------------------ llv index
 
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
-                                      uint64_t base, uint32_t num_tiles,
+                                      uint64_t base, uint64_t tile_first,
+                                      uint32_t num_tiles,
                                       uint32_t *lo_out, uint32_t *hi_out,
                                       uint32_t *err) {
   uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
@@ -491,7 +608,7 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
     if (t > 0 && llv[t].position <= llv[t - 1].position) atomicOr(err, 2u);
   }
   if (t >= num_tiles) return;
-  uint64_t g0 = base + t * (uint64_t) SMAX_TILE;
+  uint64_t g0 = base + (tile_first + t) * (uint64_t) SMAX_TILE;
   uint64_t keys[2] = {g0 >= SMAX_LH ? g0 - SMAX_LH : 0, g0 + SMAX_TILE + SMAX_RH};
   for (int s = 0; s < 2; s++) {
     uint64_t lo = 0, hi = numllv;
@@ -573,6 +690,8 @@ struct GtSmaxPlan {
   unsigned int minlen;
   uint64_t capacity;
   uint32_t num_tiles;
+  uint64_t tile_first;
+  uint32_t grid;
   GtSmaxRecord *out;
   uint64_t *status;
   unsigned long long *ticket;
@@ -616,9 +735,12 @@ extern "C" int gt_smax_dev_free_table(int device, uint8_t *table) {
   return hipFree(table - GT_SMAX_PAD_FRONT) == hipSuccess ? 0 : -1;
 }
 
-static uint32_t plan_tiles(const GtSmaxDevShard *s) {
-  uint64_t rows = s->end > s->base ? s->end - s->base : 1;
-  return (uint32_t) ((rows + SMAX_TILE - 1) / SMAX_TILE);
+// tiles of the local grid [first, last] that hold owned rows [begin, end)
+static uint32_t plan_tiles(const GtSmaxDevShard *s, uint64_t *first) {
+  uint64_t lo = (s->begin - s->base) / SMAX_TILE;
+  uint64_t hi = s->end > s->begin ? (s->end - 1 - s->base) / SMAX_TILE : lo;
+  *first = lo;
+  return (uint32_t) (hi - lo + 1);
 }
 
 extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
@@ -649,7 +771,18 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   }
   p->shard = *shard;
   p->minlen = minlen;
-  p->num_tiles = plan_tiles(shard);
+  p->num_tiles = plan_tiles(shard, &p->tile_first);
+  {
+    int dev_cus = 0, per_cu = 0;
+    HIPCHK(hipSetDevice(shard->device));
+    HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
+                                 shard->device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smax_scan_kernel,
+                                                        SMAX_THREADS, 0));
+    if (per_cu < 1) per_cu = 1;
+    uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
+    p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
+  }
   if (capacity == 0) {
     uint64_t rows = shard->end - shard->begin;
     capacity = rows / 64 + 4096;
@@ -679,7 +812,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     unsigned blocks = (unsigned) ((work + 255) / 256);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
                        shard->llv_dev, shard->numllv, shard->base,
-                       p->num_tiles, p->llv_lo, p->llv_hi, derr);
+                       p->tile_first, p->num_tiles, p->llv_lo, p->llv_hi, derr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   }
@@ -721,6 +854,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.begin = p->shard.begin;
   a.end = p->shard.end;
   a.N = p->shard.nonspecials;
+  a.tile_first = p->tile_first;
   a.minlen = p->minlen;
   a.num_tiles = p->num_tiles;
   a.out = p->out;
@@ -755,13 +889,13 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     HIPCHK(hipGetLastError());
     const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
-    hipLaunchKernelGGL(smax_scan_kernel, dim3(p->num_tiles), dim3(SMAX_THREADS),
+    hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS),
                        0, s, a);
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
   }
   p->runs++;
-  p->ticket_base += p->num_tiles;
+  p->ticket_base += (uint64_t) p->num_tiles + p->grid;   // one failed claim per block
   p->epoch += 1;
   return 0;
 fail:
