@@ -379,9 +379,8 @@ smax_scan_kernel(SmaxScanArgs a) {
     const uint64_t g0 = a.base + l0;                                      // global row
     t.g0 = g0;
 
-    // ---- stage the prefetched tile, claim the next one, filter
+    // ---- stage the prefetched tile, filter
     store_tile(sL, sB, R);
-    if (tid == 0) sNext = atomicAdd(a.ticket, 1ull) - a.ticket_base;
     uint32_t cntff[SMAX_SEGS];
     const uint32_t p0 = seg_ge(R.l0, mf), p1 = seg_ge(R.l1, mf), p2 = seg_ge(R.l2, mf),
                    p3 = seg_ge(R.l3, mf);
@@ -397,13 +396,9 @@ smax_scan_kernel(SmaxScanArgs a) {
     if (fl) atomicOr(&sFlags, fl);
     __syncthreads();
     const uint32_t flags = sFlags;
-    const uint64_t next = sNext;
     const bool need_b = (flags & 1u) != 0;
     const bool has_ff = (flags & 2u) != 0;
 
-    // ---- prefetch the next tile (LCP + BWT) while this one is processed
-    if (next < a.num_tiles)
-      load_tile(a.lcp, a.bwt, (a.tile_first + next) * (uint64_t) SMAX_TILE, R);
 
     // ---- .llv ranks of the window's 255 bytes
     if (has_ff) {
@@ -514,15 +509,27 @@ smax_scan_kernel(SmaxScanArgs a) {
       cnt[r] = (uint32_t) __popcll((cand >> (16 * r)) & 0xffffull);
     block_scan_rows(cnt, seg_off, &wave_off, &tile_count, sWave);
 
-    // ---- phase 5: decoupled look-back (wave 0)
+    // ---- phase 5a: publish this tile's aggregate, then claim the next tile.
+    // Claiming only after publishing keeps every claimed tile's aggregate at
+    // most one tile-processing time away, so look-backs never chain behind a
+    // claimed-but-unstarted tile.
+    if (tid == 0) {
+      if (tile == 0)
+        st_status(&a.status[0], (ST_FLAG_PFX << 62) | ep | (uint64_t) tile_count);
+      else
+        st_status(&a.status[tile], (ST_FLAG_AGG << 62) | ep | (uint64_t) tile_count);
+      sNext = atomicAdd(a.ticket, 1ull) - a.ticket_base;
+    }
+    __syncthreads();
+    const uint64_t next = sNext;
+    // prefetch the next tile (LCP + BWT) across the look-back and the writes
+    if (next < a.num_tiles)
+      load_tile(a.lcp, a.bwt, (a.tile_first + next) * (uint64_t) SMAX_TILE, R);
+
+    // ---- phase 5b: decoupled look-back (wave 0)
     if (wave == 0) {
       uint64_t excl = 0;
-      if (tile == 0) {
-        if (lane == 0)
-          st_status(&a.status[0], (ST_FLAG_PFX << 62) | ep | (uint64_t) tile_count);
-      } else {
-        if (lane == 0)
-          st_status(&a.status[tile], (ST_FLAG_AGG << 62) | ep | (uint64_t) tile_count);
+      if (tile != 0) {
         int64_t pos = (int64_t) tile - 1;
         for (;;) {
           const int64_t idx = pos - lane;
