@@ -80,6 +80,7 @@ struct SmaxScanArgs {
   uint64_t epoch;
   uint64_t *count;
   GtSmaxBoundary *bnd;
+  uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
 
 // ------------------------------------------------------------ helpers
@@ -397,7 +398,7 @@ smax_scan_kernel(SmaxScanArgs a) {
     __syncthreads();
     const uint32_t flags = sFlags;
     const bool need_b = (flags & 1u) != 0;
-    const bool has_ff = (flags & 2u) != 0;
+    const bool has_ff = (flags & 2u) != 0 && !(a.dbg & 16u);
 
 
     // ---- .llv ranks of the window's 255 bytes
@@ -431,7 +432,7 @@ smax_scan_kernel(SmaxScanArgs a) {
     bool pend_here = false;
     uint64_t pend_c = 0;
     uint32_t pend_l = 0;
-    if (need_b) {
+    if (need_b && !(a.dbg & 2u)) {
 #pragma unroll
       for (int r = 0; r < SMAX_SEGS; r++) {
         if (!((segpre >> r) & 1)) continue;
@@ -471,7 +472,7 @@ smax_scan_kernel(SmaxScanArgs a) {
     }
 
     // ---- phase 3: left-diversity
-    uint64_t tmp = cand;
+    uint64_t tmp = (a.dbg & 4u) ? 0 : cand;
     while (tmp) {
       const int bit = __builtin_ctzll(tmp);
       tmp &= tmp - 1;
@@ -529,7 +530,7 @@ smax_scan_kernel(SmaxScanArgs a) {
     // ---- phase 5b: decoupled look-back (wave 0)
     if (wave == 0) {
       uint64_t excl = 0;
-      if (tile != 0) {
+      if (tile != 0 && !(a.dbg & 1u)) {
         int64_t pos = (int64_t) tile - 1;
         for (;;) {
           const int64_t idx = pos - lane;
@@ -570,7 +571,7 @@ smax_scan_kernel(SmaxScanArgs a) {
     const uint64_t base_out = sExcl + wave_off;
 
     // ---- phase 6: ordered record writes
-    tmp = cand;
+    tmp = (a.dbg & 8u) ? 0 : cand;
     while (tmp) {
       const int bit = __builtin_ctzll(tmp);
       tmp &= tmp - 1;
@@ -872,6 +873,10 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.epoch = p->epoch;
   a.count = p->count;
   a.bnd = p->bnd;
+  {
+    const char *d = getenv("GT_SMAX_DEBUG");
+    a.dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
+  }
   return a;
 }
 
