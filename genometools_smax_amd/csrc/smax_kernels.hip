@@ -11,28 +11,31 @@
 // BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
-// Kernel K1 (smax_scan_kernel) is persistent: each 256-thread workgroup
-// claims 16384-row tiles from an atomic ticket (tile order = claim order) and
-// software-pipelines them -- the next tile's LCP bytes (16 B/lane, coalesced)
-// are in flight while the current tile is processed:
-//   stage    current tile's LCP bytes + 16 B left / 64 B right halo -> LDS;
-//   filter   SWAR "any byte >= minlen" per 16-byte segment; if any row of
-//            the tile can start a candidate, the tile's BWT bytes are loaded
-//            (coalesced) while phase 1 runs -- uniform DNA tiles whose LCP
-//            stays below minlen never touch .bwt;
+// One pass = four launches on one stream, no host synchronisation:
+//   K0 smax_head_kernel   one lane: the shard's boundary head record
+//   K1 smax_scan_kernel   the streaming kernel (HBM bound, see below)
+//   K2 rocPRIM exclusive scan of the per-tile interval counts
+//   K3 smax_compact_kernel ordered copy of the tiles' records -> ascending lb
+//
+// K1: persistent 256-thread workgroups, static tile schedule (tile =
+// blockIdx.x + k*gridDim.x, 16384 suffix rows per tile) and no
+// inter-workgroup waits.  Per tile:
+//   stage    the prefetched LCP and BWT bytes (16 B/lane, coalesced, 1 KiB
+//            per wave instruction) -> LDS, plus a 16 B left / 64 B right halo;
+//            the NEXT tile's loads are issued right after, so they are in
+//            flight for the whole processing of this tile;
 //   .llv     a 255 byte is resolved in O(1): its rank among the window's 255
-//            bytes (per-16-byte-chunk prefix counts in LDS + a SWAR count)
-//            indexes the .llv entries, which are in position order;
-//   phase 1  plateau starts LCP[c] > LCP[c-1] scanned to their end in LDS;
-//            local maxima become candidates (exact values only when two
-//            compared bytes are both 255);
-//   phase 3  left-diversity: 256-bit seen-set over BWT[lb..rb];
-//   phase 4  block scan of per-row counts (row order), decoupled look-back
-//            across tiles (status words with epoch tags, agent-scope relaxed
-//            atomics), ordered 16-byte record writes -> output is ascending
-//            lb, the order the reference's traversal pops intervals.
+//            bytes (per-16-byte-chunk prefix counts + a SWAR count) indexes
+//            the tile's .llv values, staged in LDS with one coalesced load;
+//   phase 1  SWAR filter "any byte >= minlen" per 16-byte segment, then per
+//            row the plateau-start test LCP[c] > LCP[c-1] and a scan to the
+//            plateau end in LDS; local maxima become candidates;
+//   phase 3  left-diversity: 256-bit seen-set over BWT[lb..rb] in LDS;
+//   output   block scan of per-row counts in row order, records written to
+//            the tile's slot (or the overflow area) -- K2/K3 place them.
 // No MFMA: integer/byte work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,13 +51,8 @@
 #define SMAX_RH 64                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
-
-#define ST_FLAG_AGG 1ull
-#define ST_FLAG_PFX 2ull
-#define ST_EPOCH_BITS 22
-#define ST_VALUE_BITS 40
-#define ST_VALUE_MASK ((1ull << ST_VALUE_BITS) - 1)
-#define ST_EPOCH_MASK ((1ull << ST_EPOCH_BITS) - 1)
+#define SMAX_LLV_CAP 1024                             // .llv values in LDS
+#define SMAX_SLOT 256                                 // records per tile slot
 
 static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
@@ -67,30 +65,21 @@ struct SmaxScanArgs {
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
   uint64_t numllv;
   const uint32_t *llv_lo;    // per tile: first llv index >= tile_g0 - LH
-  const uint32_t *llv_hi;    // per tile: first llv index >= tile_g1 + RH
   uint64_t base, begin, end, N;
   uint64_t tile_first;       // first local tile holding an owned row
   uint32_t minlen;
   uint32_t num_tiles;
-  GtSmaxRecord *out;
-  uint64_t capacity;
-  uint64_t *status;
-  unsigned long long *ticket;
-  uint64_t ticket_base;
-  uint64_t epoch;
-  uint64_t *count;
+  GtSmaxRecord *slots;       // num_tiles * SMAX_SLOT records
+  uint32_t *tile_count;      // per tile
+  uint64_t *tile_ovf;        // per tile: overflow offset (count > SMAX_SLOT)
+  GtSmaxRecord *ovf;
+  uint64_t ovf_cap;
+  unsigned long long *ovf_cursor;
   GtSmaxBoundary *bnd;
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
 
 // ------------------------------------------------------------ helpers
-
-__device__ __forceinline__ uint64_t ld_status(uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // exact LCP value from the global .llv (binary search in [lo, hi))
 __device__ static uint32_t llv_search_global(const GtSmaxLlv *llv, uint64_t lo,
@@ -103,7 +92,7 @@ __device__ static uint32_t llv_search_global(const GtSmaxLlv *llv, uint64_t lo,
   return (uint32_t) llv[lo].value;   // present by construction of .llv
 }
 
-// high bit of each byte of w that is >= m (m <= 128); exact
+// high bit of each byte of w that is >= m (1 <= m <= 128); exact
 __device__ __forceinline__ uint32_t bytes_ge(uint32_t w, uint32_t m) {
   uint32_t add = (128u - m) * 0x01010101u;
   return (w | ((w & 0x7f7f7f7fu) + add)) & 0x80808080u;
@@ -122,6 +111,8 @@ struct Win {
   const uint8_t *L;           // LDS window: index o = g - g0 + LH
   const uint8_t *B;
   const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
+  const uint32_t *val;        // LDS .llv values in rank order (nval of them)
+  int nval;                   // -1: values not staged (read global by rank)
   uint64_t g0;                // global row of the tile start
   uint64_t llv_base;          // first llv entry of the window
 };
@@ -129,7 +120,8 @@ struct Win {
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end;
-  t.L = nullptr; t.B = nullptr; t.rank = nullptr; t.g0 = 0; t.llv_base = 0;
+  t.L = nullptr; t.B = nullptr; t.rank = nullptr; t.val = nullptr; t.nval = -1;
+  t.g0 = 0; t.llv_base = 0;
 }
 
 __device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
@@ -138,20 +130,18 @@ __device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
 
 // exact LCP of a row whose byte is 255
 __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
-  int64_t o = win_off(t, g);
+  const int64_t o = win_off(t, g);
   if (t.rank != nullptr && o >= 0 && o < SMAX_LDSB) {
-    int chunk = (int) (o >> 4), within = (int) (o & 15);
-    uint4 v = *reinterpret_cast<const uint4 *>(&t.L[chunk * 16]);
-    uint32_t f0 = bytes_ff(v.x), f1 = bytes_ff(v.y), f2 = bytes_ff(v.z),
-             f3 = bytes_ff(v.w);
-    // bytes below `within` only
-    uint64_t lo = (uint64_t) f0 | ((uint64_t) f1 << 32);
-    uint64_t hi = (uint64_t) f2 | ((uint64_t) f3 << 32);
+    const int chunk = (int) (o >> 4), within = (int) (o & 15);
+    const uint4 v = *reinterpret_cast<const uint4 *>(&t.L[chunk * 16]);
+    const uint64_t lo = (uint64_t) bytes_ff(v.x) | ((uint64_t) bytes_ff(v.y) << 32);
+    const uint64_t hi = (uint64_t) bytes_ff(v.z) | ((uint64_t) bytes_ff(v.w) << 32);
     int cnt;
     if (within < 8) cnt = __popcll(lo & ((1ull << (8 * within)) - 1));
     else cnt = __popcll(lo) + __popcll(hi & ((1ull << (8 * (within - 8))) - 1));
-    uint64_t idx = t.llv_base + t.rank[chunk] + (uint64_t) cnt;
-    return (uint32_t) t.llv[idx].value;
+    const uint32_t r = t.rank[chunk] + (uint32_t) cnt;
+    if ((int) r < t.nval) return t.val[r];
+    return (uint32_t) t.llv[t.llv_base + r].value;
   }
   return llv_search_global(t.llv, 0, t.numllv, g);
 }
@@ -159,25 +149,25 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
 // byte of LCP[g] (LCP[0] = LCP[N] = 0 are returned as 0)
 __device__ __forceinline__ uint32_t lcp_byte(const Win &t, uint64_t g) {
   if (g == 0 || g >= t.N) return 0;
-  int64_t o = win_off(t, g);
+  const int64_t o = win_off(t, g);
   if (t.L != nullptr && o >= 0 && o < SMAX_LDSB) return t.L[o];
   return t.glcp[g - t.base];
 }
 
 __device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
-  uint32_t b = lcp_byte(t, g);
+  const uint32_t b = lcp_byte(t, g);
   return b < 255 ? b : lcp_big(t, g);
 }
 
 __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
-  int64_t o = win_off(t, g);
+  const int64_t o = win_off(t, g);
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
   return t.gbwt[g - t.base];
 }
 
-// Plateau scan from start c with exact value l (byte lb = min(l,255)):
-// returns j (last row of the run) and sets *next = LCP[j+1] relative to l:
-// -1 smaller, +1 larger; *pending when the run reaches the shard end.
+// Plateau scan from start c with exact value l: returns j (last row of the
+// run); *rel = sign of LCP[j+1] - l (-1 / +1); *pending when the run reaches
+// the shard end (LCP[end] == l with end < N).
 __device__ static uint64_t plateau_end(const Win &t, uint64_t c, uint32_t l,
                                        int *rel, bool *pending) {
   const uint32_t lb = l < 255 ? l : 255;
@@ -185,13 +175,13 @@ __device__ static uint64_t plateau_end(const Win &t, uint64_t c, uint32_t l,
   *pending = false;
   for (;;) {
     const uint64_t g = j + 1;
-    uint32_t nb = lcp_byte(t, g);
+    const uint32_t nb = lcp_byte(t, g);
     if (nb != lb) { *rel = nb < lb ? -1 : 1; return j; }
     if (lb == 255) {
-      uint32_t nx = lcp_big(t, g);
+      const uint32_t nx = lcp_big(t, g);
       if (nx != l) { *rel = nx < l ? -1 : 1; return j; }
     }
-    if (g >= t.end) { *pending = true; *rel = 0; return j; }   // g == end < N
+    if (g >= t.end) { *pending = true; *rel = 0; return j; }
     j = g;
   }
 }
@@ -211,34 +201,38 @@ __device__ __forceinline__ bool seen_add(Seen &s, uint32_t c) {
   return (cur & bit) != 0;
 }
 
-// exclusive prefix of per-(segment, lane) counts in row order within the
-// block: returns per-segment offsets inside the wave and the wave's offset
-// inside the block; *total = block total.  Uses sWave[4]; two barriers.
-__device__ __forceinline__ void block_scan_rows(const uint32_t cnt[SMAX_SEGS],
-                                                uint32_t seg_off[SMAX_SEGS],
-                                                uint32_t *wave_off,
-                                                uint32_t *total,
+// Exclusive prefix of per-(segment, lane) counts in row order within the
+// block (a wave's rows are segment-major, then lane): per-segment offsets
+// inside the wave, the wave's offset inside the block, the block total.
+__device__ __forceinline__ void block_scan_rows(const uint32_t c0, const uint32_t c1,
+                                                const uint32_t c2, const uint32_t c3,
+                                                uint32_t *o0, uint32_t *o1,
+                                                uint32_t *o2, uint32_t *o3,
+                                                uint32_t *wave_off, uint32_t *total,
                                                 uint32_t *sWave) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t wt = 0;
+  const uint32_t cs[4] = {c0, c1, c2, c3};
+  uint32_t os[4];
 #pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++) {
-    uint32_t incl = cnt[r];
+  for (int r = 0; r < 4; r++) {
+    uint32_t incl = cs[r];
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      uint32_t o = __shfl_up(incl, d, 64);
+      const uint32_t o = __shfl_up(incl, d, 64);
       if (lane >= d) incl += o;
     }
-    seg_off[r] = wt + incl - cnt[r];
+    os[r] = wt + incl - cs[r];
     wt += __shfl(incl, 63, 64);
   }
+  *o0 = os[0]; *o1 = os[1]; *o2 = os[2]; *o3 = os[3];
   __syncthreads();                 // sWave free (previous users done)
   if (lane == 0) sWave[wave] = wt;
   __syncthreads();
   uint32_t wo = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < SMAX_THREADS / 64; w++) {
-    uint32_t ws = sWave[w];
+    const uint32_t ws = sWave[w];
     if (w < wave) wo += ws;
     tot += ws;
   }
@@ -248,17 +242,18 @@ __device__ __forceinline__ void block_scan_rows(const uint32_t cnt[SMAX_SEGS],
 
 // ------------------------------------------------------------ K0: head run
 
-// One lane: the boundary record's head (run of LCP == LCP[begin]) and reset
-// of the pending slot.  Runs before K1 on the same stream.
+// One lane: the boundary record's head (run of LCP == LCP[begin]), reset of
+// the pending slot and of the overflow cursor.  Runs before K1.
 __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (threadIdx.x != 0) return;
   Win t;
   win_init(t, a);
+  *a.ovf_cursor = 0;
   GtSmaxBoundary *b = a.bnd;
   b->pend_valid = 0;
   b->shard_begin = a.begin;
   b->shard_end = a.end;
-  uint32_t v = lcp_exact(t, a.begin);
+  const uint32_t v = lcp_exact(t, a.begin);
   b->head_v = v;
   Seen s = {0, 0, 0, 0};
   uint64_t dup = 0;
@@ -267,8 +262,8 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
     uint64_t g = a.begin;
     for (;;) {
       if (seen_add(s, a.bwt[g - a.base])) { dup = 1; break; }
-      uint64_t h = g + 1;
-      uint32_t nx = lcp_exact(t, h);
+      const uint64_t h = g + 1;
+      const uint32_t nx = lcp_exact(t, h);
       if (nx != v) { f = h; nxt = nx; break; }
       if (h >= a.end) break;   // run covers the whole shard: passthrough
       g = h;
@@ -286,11 +281,10 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
 
 // ------------------------------------------------------------ K1: scan
 
-// Tile loads: 4 x 16 B per lane of LCP and of BWT (coalesced, 1 KiB per
-// wave instruction); halo chunks go to threads 0..4 (LCP: 16 B left, 64 B
-// right) and 5..9 (BWT, same chunks), one uint4 each.  Named fields, no
-// arrays: keeps the prefetch in VGPRs (arrays written under a condition were
-// demoted to scratch by hipcc).
+// Tile registers: 4 x 16 B per lane of LCP and of BWT; halo chunks go to
+// threads 0..4 (LCP: 16 B left, 64 B right) and 5..9 (BWT).  Named fields,
+// no arrays: keeps the prefetch in VGPRs (arrays written under a condition
+// were demoted to scratch by hipcc).
 struct TileRegs {
   uint4 l0, l1, l2, l3, b0, b1, b2, b3, h;
 };
@@ -341,134 +335,161 @@ __device__ __forceinline__ uint32_t seg_ffcount(const uint4 v) {
          __popc(bytes_ff(v.w));
 }
 
+// Candidate detection for one 16-row segment read from LDS (rows sg..sg+15).
+__device__ __forceinline__ void segment_candidates(const Win &t, const SmaxScanArgs &a,
+                                                   uint64_t sg, const uint4 v, int r,
+                                                   uint64_t &cand, bool &pend_here,
+                                                   uint64_t &pend_c, uint32_t &pend_l) {
+  const uint32_t m = a.minlen;
+  const uint64_t lo8 = (uint64_t) v.x | ((uint64_t) v.y << 32);
+  const uint64_t hi8 = (uint64_t) v.z | ((uint64_t) v.w << 32);
+  uint32_t prevb = lcp_byte(t, sg - 1);
+  for (int q = 0; q < 16; q++) {
+    const uint64_t c = sg + q;
+    uint32_t cb = (uint32_t) (((q < 8) ? (lo8 >> (8 * q)) : (hi8 >> (8 * (q - 8)))) & 0xffu);
+    if (c >= a.N || c == 0) cb = 0;
+    const uint32_t pb = prevb;
+    prevb = cb;
+    if (cb < m && cb != 255) continue;
+    if (c < a.begin || c >= a.end) continue;
+    uint32_t cur;
+    if (cb != 255) {
+      if (cb <= pb) continue;                  // pb < 255 here
+      cur = cb;
+    } else {
+      cur = lcp_big(t, c);
+      if (cur < m) continue;
+      if (pb == 255 && lcp_big(t, c - 1) >= cur) continue;
+    }
+    int rel;
+    bool pend;
+    (void) plateau_end(t, c, cur, &rel, &pend);
+    if (pend) {
+      pend_here = true; pend_c = c; pend_l = cur;
+    } else if (rel < 0) {
+      cand |= 1ull << (r * 16 + q);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(SMAX_THREADS)
 smax_scan_kernel(SmaxScanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sL[SMAX_LDSB];
   __shared__ __attribute__((aligned(16))) uint8_t sB[SMAX_LDSB];
   __shared__ uint16_t sRank[SMAX_NCHUNK];
+  __shared__ uint32_t sVal[SMAX_LLV_CAP];
   __shared__ uint32_t sWave[SMAX_THREADS / 64];
-  __shared__ uint64_t sNext, sExcl;
-  __shared__ uint32_t sFlags;
   __shared__ uint32_t sHalo[5];
+  __shared__ uint32_t sFlags;
+  __shared__ uint32_t sLlvBase;
+  __shared__ uint64_t sOvf;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const uint32_t m = a.minlen;
-  const uint32_t mf = m < 128 ? m : 128;
-  const uint64_t ep = (a.epoch & ST_EPOCH_MASK) << ST_VALUE_BITS;
+  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
+  const uint64_t stride = gridDim.x;
 
-  if (tid == 0) {
-    sNext = atomicAdd(a.ticket, 1ull) - a.ticket_base;
-    sFlags = 0;
-  }
-  __syncthreads();
-  uint64_t tile = sNext;
+  uint64_t tile = blockIdx.x;
   if (tile >= a.num_tiles) return;
+  if (tid == 0) sFlags = 0;
 
   Win t;
   win_init(t, a);
   t.L = sL;
   t.B = sB;
+  t.val = sVal;
 
   TileRegs R;
   R.h = make_uint4(0, 0, 0, 0);
   load_tile(a.lcp, a.bwt, (a.tile_first + tile) * (uint64_t) SMAX_TILE, R);
+  uint32_t llv_lo_next = tid == 0 ? a.llv_lo[tile] : 0;
 
   for (;;) {
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
+    const uint64_t next = tile + stride;
     t.g0 = g0;
 
     // ---- stage the prefetched tile, filter
+    __syncthreads();               // LDS free (previous tile done), sFlags reset
     store_tile(sL, sB, R);
-    uint32_t cntff[SMAX_SEGS];
     const uint32_t p0 = seg_ge(R.l0, mf), p1 = seg_ge(R.l1, mf), p2 = seg_ge(R.l2, mf),
                    p3 = seg_ge(R.l3, mf);
-    const uint32_t pre = p0 | p1 | p2 | p3;
     const uint32_t segpre = (p0 ? 1u : 0u) | (p1 ? 2u : 0u) | (p2 ? 4u : 0u) | (p3 ? 8u : 0u);
-    cntff[0] = seg_ffcount(R.l0);
-    cntff[1] = seg_ffcount(R.l1);
-    cntff[2] = seg_ffcount(R.l2);
-    cntff[3] = seg_ffcount(R.l3);
-    const uint32_t ff = cntff[0] | cntff[1] | cntff[2] | cntff[3];
+    const uint32_t f0 = seg_ffcount(R.l0), f1 = seg_ffcount(R.l1), f2 = seg_ffcount(R.l2),
+                   f3 = seg_ffcount(R.l3);
     const uint32_t hff = tid < 5 ? seg_ffcount(R.h) : 0u;
-    const uint32_t fl = (pre ? 1u : 0u) | ((ff | hff) ? 2u : 0u);
+    const uint32_t fl = (segpre ? 1u : 0u) | ((f0 | f1 | f2 | f3 | hff) ? 2u : 0u);
     if (fl) atomicOr(&sFlags, fl);
+    if (tid < 5) sHalo[tid] = hff;
+    if (tid == 0) sLlvBase = llv_lo_next;
     __syncthreads();
     const uint32_t flags = sFlags;
-    const bool need_b = (flags & 1u) != 0;
+    const bool any_pre = (flags & 1u) != 0 && !(a.dbg & 2u);
     const bool has_ff = (flags & 2u) != 0 && !(a.dbg & 16u);
 
+    // ---- prefetch the next tile: in flight during all of this tile's work
+    if (next < a.num_tiles) {
+      load_tile(a.lcp, a.bwt, (a.tile_first + next) * (uint64_t) SMAX_TILE, R);
+      if (tid == 0) llv_lo_next = a.llv_lo[next];
+    }
 
-    // ---- .llv ranks of the window's 255 bytes
+    // ---- .llv ranks of the window's 255 bytes and their values in LDS
+    t.rank = nullptr;
+    t.nval = -1;
     if (has_ff) {
-      uint32_t so[SMAX_SEGS], wo, tot;
-      block_scan_rows(cntff, so, &wo, &tot, sWave);
+      uint32_t o0, o1, o2, o3, wo, tot;
+      block_scan_rows(f0, f1, f2, f3, &o0, &o1, &o2, &o3, &wo, &tot, sWave);
       // chunk 0 = left halo, 1..1024 = tile rows, 1025..1028 = right halo
-      if (tid < 5) sHalo[tid] = hff;
-      __syncthreads();
       const uint32_t h0 = sHalo[0];
-#pragma unroll
-      for (int r = 0; r < SMAX_SEGS; r++)
-        sRank[1 + wave * 256 + r * 64 + lane] = (uint16_t) (h0 + wo + so[r]);
+      const uint32_t cb = 1 + wave * 256 + lane;
+      sRank[cb] = (uint16_t) (h0 + wo + o0);
+      sRank[cb + 64] = (uint16_t) (h0 + wo + o1);
+      sRank[cb + 128] = (uint16_t) (h0 + wo + o2);
+      sRank[cb + 192] = (uint16_t) (h0 + wo + o3);
+      uint32_t nff = h0 + tot;
       if (tid == 0) {
         sRank[0] = 0;
-        uint32_t acc = h0 + tot;
+        uint32_t acc = nff;
         for (int k = 0; k < 4; k++) {
           sRank[1 + SMAX_TILE / 16 + k] = (uint16_t) acc;
           acc += sHalo[1 + k];
         }
+        sFlags = acc;              // total 255 bytes in the window (reuse)
+      }
+      __syncthreads();
+      nff = sFlags;
+      t.llv_base = sLlvBase;
+      if (nff <= SMAX_LLV_CAP) {
+        for (uint32_t i = tid; i < nff; i += SMAX_THREADS)
+          sVal[i] = (uint32_t) a.llv[t.llv_base + i].value;
+        t.nval = (int) nff;
       }
       t.rank = sRank;
-      t.llv_base = a.llv_lo[tile];
-    } else {
-      t.rank = nullptr;
+      __syncthreads();
     }
-    __syncthreads();
 
     // ---- phase 1: plateau starts that are local maxima (L only)
     uint64_t cand = 0;          // bit r*16+q: row is a local-maximum start
     bool pend_here = false;
     uint64_t pend_c = 0;
     uint32_t pend_l = 0;
-    if (need_b && !(a.dbg & 2u)) {
-#pragma unroll
-      for (int r = 0; r < SMAX_SEGS; r++) {
-        if (!((segpre >> r) & 1)) continue;
-        const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-        const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
-        const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-        const uint64_t lo8 = (uint64_t) v.x | ((uint64_t) v.y << 32);
-        const uint64_t hi8 = (uint64_t) v.z | ((uint64_t) v.w << 32);
-        uint32_t prevb = lcp_byte(t, sg - 1);
-        for (int q = 0; q < 16; q++) {
-          const uint64_t c = sg + q;
-          uint32_t cb = (uint32_t) (((q < 8) ? (lo8 >> (8 * q)) : (hi8 >> (8 * (q - 8)))) & 0xffu);
-          if (c >= a.N || c == 0) cb = 0;
-          const uint32_t pb = prevb;
-          prevb = cb;
-          if (cb < m && cb != 255) continue;
-          if (c < a.begin || c >= a.end) continue;
-          uint32_t cur;
-          if (cb != 255) {
-            if (cb <= pb) continue;                  // pb < 255 here
-            cur = cb;
-          } else {
-            cur = lcp_big(t, c);
-            if (cur < m) continue;
-            if (pb == 255 && lcp_big(t, c - 1) >= cur) continue;
-          }
-          int rel;
-          bool pend;
-          (void) plateau_end(t, c, cur, &rel, &pend);
-          if (pend) {
-            pend_here = true; pend_c = c; pend_l = cur;
-          } else if (rel < 0) {
-            cand |= 1ull << (r * 16 + q);
-          }
-        }
-      }
+    if (any_pre) {
+      const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + lane * 16;
+      const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + lane * 16;
+      if (segpre & 1u)
+        segment_candidates(t, a, sg, *reinterpret_cast<const uint4 *>(&sL[so]), 0,
+                           cand, pend_here, pend_c, pend_l);
+      if (segpre & 2u)
+        segment_candidates(t, a, sg + 1024, *reinterpret_cast<const uint4 *>(&sL[so + 1024]), 1,
+                           cand, pend_here, pend_c, pend_l);
+      if (segpre & 4u)
+        segment_candidates(t, a, sg + 2048, *reinterpret_cast<const uint4 *>(&sL[so + 2048]), 2,
+                           cand, pend_here, pend_c, pend_l);
+      if (segpre & 8u)
+        segment_candidates(t, a, sg + 3072, *reinterpret_cast<const uint4 *>(&sL[so + 3072]), 3,
+                           cand, pend_here, pend_c, pend_l);
     }
 
     // ---- phase 3: left-diversity
@@ -503,74 +524,24 @@ smax_scan_kernel(SmaxScanArgs a) {
       }
     }
 
-    // ---- phase 4: block scan of counts in row order
-    uint32_t cnt[SMAX_SEGS], seg_off[SMAX_SEGS], wave_off, tile_count;
-#pragma unroll
-    for (int r = 0; r < SMAX_SEGS; r++)
-      cnt[r] = (uint32_t) __popcll((cand >> (16 * r)) & 0xffffull);
-    block_scan_rows(cnt, seg_off, &wave_off, &tile_count, sWave);
-
-    // ---- phase 5a: publish this tile's aggregate, then claim the next tile.
-    // Claiming only after publishing keeps every claimed tile's aggregate at
-    // most one tile-processing time away, so look-backs never chain behind a
-    // claimed-but-unstarted tile.
-    if (tid == 0) {
-      if (tile == 0)
-        st_status(&a.status[0], (ST_FLAG_PFX << 62) | ep | (uint64_t) tile_count);
-      else
-        st_status(&a.status[tile], (ST_FLAG_AGG << 62) | ep | (uint64_t) tile_count);
-      sNext = atomicAdd(a.ticket, 1ull) - a.ticket_base;
+    // ---- output: row-order offsets, records into the tile slot / overflow
+    uint32_t so0, so1, so2, so3, wave_off, tile_count;
+    block_scan_rows((uint32_t) __popcll(cand & 0xffffull),
+                    (uint32_t) __popcll((cand >> 16) & 0xffffull),
+                    (uint32_t) __popcll((cand >> 32) & 0xffffull),
+                    (uint32_t) __popcll((cand >> 48) & 0xffffull),
+                    &so0, &so1, &so2, &so3, &wave_off, &tile_count, sWave);
+    GtSmaxRecord *dst = a.slots + tile * (uint64_t) SMAX_SLOT;
+    uint64_t dcap = SMAX_SLOT;
+    if (tile_count > SMAX_SLOT) {            // block-uniform
+      if (tid == 0) sOvf = atomicAdd(a.ovf_cursor, (unsigned long long) tile_count);
+      __syncthreads();
+      const uint64_t off = sOvf;
+      if (tid == 0) a.tile_ovf[tile] = off;
+      dst = a.ovf + off;
+      dcap = off < a.ovf_cap ? a.ovf_cap - off : 0;
     }
-    __syncthreads();
-    const uint64_t next = sNext;
-    // prefetch the next tile (LCP + BWT) across the look-back and the writes
-    if (next < a.num_tiles)
-      load_tile(a.lcp, a.bwt, (a.tile_first + next) * (uint64_t) SMAX_TILE, R);
-
-    // ---- phase 5b: decoupled look-back (wave 0)
-    if (wave == 0) {
-      uint64_t excl = 0;
-      if (tile != 0 && !(a.dbg & 1u)) {
-        int64_t pos = (int64_t) tile - 1;
-        for (;;) {
-          const int64_t idx = pos - lane;
-          uint64_t sv;
-          if (idx >= 0) sv = ld_status(&a.status[idx]);
-          else sv = (ST_FLAG_PFX << 62) | ep;    // virtual prefix 0 before tile 0
-          const uint64_t flag = sv >> 62;
-          const bool valid = flag != 0 &&
-              ((sv >> ST_VALUE_BITS) & ST_EPOCH_MASK) == (a.epoch & ST_EPOCH_MASK);
-          const bool ispfx = valid && flag == ST_FLAG_PFX;
-          const uint64_t pfx_mask = __ballot(ispfx);
-          const uint64_t inv_mask = __ballot(!valid);
-          // lanes up to and including the first prefix must all be valid
-          const uint64_t upto = pfx_mask ? ((pfx_mask & (~pfx_mask + 1)) - 1) |
-                                               (pfx_mask & (~pfx_mask + 1))
-                                         : ~0ull;
-          if (inv_mask & upto) {
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-          }
-          uint64_t val = ((upto >> lane) & 1) ? (sv & ST_VALUE_MASK) : 0;
-#pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-          excl += val;
-          if (pfx_mask) break;
-          pos -= 64;
-        }
-        if (lane == 0)
-          st_status(&a.status[tile],
-                    (ST_FLAG_PFX << 62) | ep | ((excl + tile_count) & ST_VALUE_MASK));
-      }
-      if (lane == 0) {
-        sExcl = excl;
-        if (tile == a.num_tiles - 1) *a.count = excl + tile_count;
-      }
-    }
-    __syncthreads();
-    const uint64_t base_out = sExcl + wave_off;
-
-    // ---- phase 6: ordered record writes
+    if (tid == 0) a.tile_count[tile] = tile_count;
     tmp = (a.dbg & 8u) ? 0 : cand;
     while (tmp) {
       const int bit = __builtin_ctzll(tmp);
@@ -583,23 +554,53 @@ smax_scan_kernel(SmaxScanArgs a) {
       const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
       const uint32_t before = (uint32_t) __popcll(cand & ((1ull << bit) - 1) &
                                                   (0xffffull << (16 * r)));
-      const uint32_t so = r == 0 ? seg_off[0] : r == 1 ? seg_off[1]
-                        : r == 2 ? seg_off[2] : seg_off[3];
-      const uint64_t o = base_out + so + before;
-      if (o < a.capacity) {
+      const uint32_t so = r == 0 ? so0 : r == 1 ? so1 : r == 2 ? so2 : so3;
+      const uint64_t o = wave_off + so + before;
+      if (o < dcap) {
         GtSmaxRecord rec;
         rec.lb = c - 1;
         rec.lcp = cur;
         rec.width = (uint32_t) (j - c + 2);
-        a.out[o] = rec;
+        dst[o] = rec;
       }
     }
 
-    // ---- next tile
     if (tid == 0) sFlags = 0;
-    __syncthreads();               // LDS (L, B, ranks, flags) free again
     tile = next;
     if (tile >= a.num_tiles) break;
+  }
+}
+
+// ------------------------------------------------------------ K3: compact
+
+// One wave per tile (grid-stride): copy the tile's records to their final
+// position (exclusive scan of tile counts) -> ascending lb overall.
+__global__ void __launch_bounds__(256)
+smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *tile_count,
+                    const uint64_t *tile_ovf, const GtSmaxRecord *ovf,
+                    uint64_t ovf_cap, const uint64_t *tile_off, uint32_t num_tiles,
+                    GtSmaxRecord *out, uint64_t capacity, uint64_t *count) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (blockIdx.x * (uint64_t) blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t) gridDim.x * blockDim.x) >> 6;
+  for (uint64_t tl = wave; tl < num_tiles; tl += nwaves) {
+    const uint32_t cnt = tile_count[tl];
+    const uint64_t off = tile_off[tl];
+    if (tl == num_tiles - 1 && lane == 0) *count = off + cnt;
+    if (cnt == 0) continue;
+    const GtSmaxRecord *src;
+    uint64_t scap;
+    if (cnt > SMAX_SLOT) {
+      const uint64_t o = tile_ovf[tl];
+      src = ovf + o;
+      scap = o < ovf_cap ? ovf_cap - o : 0;
+    } else {
+      src = slots + tl * (uint64_t) SMAX_SLOT;
+      scap = SMAX_SLOT;
+    }
+    for (uint32_t i = lane; i < cnt; i += 64) {
+      if (off + i < capacity && i < scap) out[off + i] = src[i];
+    }
   }
 }
 
@@ -607,25 +608,22 @@ smax_scan_kernel(SmaxScanArgs a) {
 
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
                                       uint64_t base, uint64_t tile_first,
-                                      uint32_t num_tiles,
-                                      uint32_t *lo_out, uint32_t *hi_out,
+                                      uint32_t num_tiles, uint32_t *lo_out,
                                       uint32_t *err) {
-  uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (t < numllv) {
     if (llv[t].value > 0xffffffffull) atomicOr(err, 1u);
     if (t > 0 && llv[t].position <= llv[t - 1].position) atomicOr(err, 2u);
   }
   if (t >= num_tiles) return;
-  uint64_t g0 = base + (tile_first + t) * (uint64_t) SMAX_TILE;
-  uint64_t keys[2] = {g0 >= SMAX_LH ? g0 - SMAX_LH : 0, g0 + SMAX_TILE + SMAX_RH};
-  for (int s = 0; s < 2; s++) {
-    uint64_t lo = 0, hi = numllv;
-    while (lo < hi) {
-      uint64_t mid = (lo + hi) >> 1;
-      if (llv[mid].position < keys[s]) lo = mid + 1; else hi = mid;
-    }
-    if (s == 0) lo_out[t] = (uint32_t) lo; else hi_out[t] = (uint32_t) lo;
+  const uint64_t g0 = base + (tile_first + t) * (uint64_t) SMAX_TILE;
+  const uint64_t key = g0 >= SMAX_LH ? g0 - SMAX_LH : 0;
+  uint64_t lo = 0, hi = numllv;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (llv[mid].position < key) lo = mid + 1; else hi = mid;
   }
+  lo_out[t] = (uint32_t) lo;
 }
 
 // ------------------------------------------------------------ stitch
@@ -636,7 +634,7 @@ __host__ __device__ static int stitch_resolve(const GtSmaxBoundary *all,
                                               GtSmaxRecord *rec) {
   const GtSmaxBoundary *me = &all[idx];
   if (!me->pend_valid) return 0;
-  uint64_t l = me->pend_lcp;
+  const uint64_t l = me->pend_lcp;
   uint64_t seen[4] = {me->pend_div.seen[0], me->pend_div.seen[1],
                       me->pend_div.seen[2], me->pend_div.seen[3]};
   (void) minlen;
@@ -650,7 +648,7 @@ __host__ __device__ static int stitch_resolve(const GtSmaxBoundary *all,
     }
     if (h->head_f != UINT64_MAX) {
       if (h->head_next >= l) return 0;     // not a local maximum
-      uint64_t lb = me->pend_c - 1, rb = h->head_f - 1;
+      const uint64_t lb = me->pend_c - 1, rb = h->head_f - 1;
       rec->lb = lb;
       rec->lcp = (uint32_t) l;
       rec->width = (uint32_t) (rb - lb + 1);
@@ -667,7 +665,7 @@ __global__ void smax_stitch_kernel(const GtSmaxBoundary *all, int nshards,
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   GtSmaxRecord rec;
   if (stitch_resolve(all, nshards, idx, minlen, &rec)) {
-    uint64_t c = *count;
+    const uint64_t c = *count;
     if (c < capacity) out[c] = rec;
     *count = c + 1;
   }
@@ -699,15 +697,19 @@ struct GtSmaxPlan {
   uint64_t capacity;
   uint32_t num_tiles;
   uint64_t tile_first;
-  uint32_t grid;
-  GtSmaxRecord *out;
-  uint64_t *status;
-  unsigned long long *ticket;
-  uint64_t ticket_base;
-  uint64_t epoch;
+  uint32_t grid, compact_grid;
+  GtSmaxRecord *out;         // capacity records, ascending lb
+  GtSmaxRecord *slots;       // num_tiles * SMAX_SLOT
+  GtSmaxRecord *ovf;         // capacity records
+  uint32_t *tile_count;
+  uint64_t *tile_ovf, *tile_off;
+  unsigned long long *ovf_cursor;
   uint64_t *count;
   GtSmaxBoundary *bnd;
-  uint32_t *llv_lo, *llv_hi;
+  uint32_t *llv_lo;
+  void *scan_tmp;
+  size_t scan_tmp_bytes;
+  uint32_t dbg;
   // optional K1 timing: event pairs recorded around the scan kernel
   hipEvent_t *ev;
   int nslots;
@@ -745,8 +747,8 @@ extern "C" int gt_smax_dev_free_table(int device, uint8_t *table) {
 
 // tiles of the local grid [first, last] that hold owned rows [begin, end)
 static uint32_t plan_tiles(const GtSmaxDevShard *s, uint64_t *first) {
-  uint64_t lo = (s->begin - s->base) / SMAX_TILE;
-  uint64_t hi = s->end > s->begin ? (s->end - 1 - s->base) / SMAX_TILE : lo;
+  const uint64_t lo = (s->begin - s->base) / SMAX_TILE;
+  const uint64_t hi = s->end > s->begin ? (s->end - 1 - s->base) / SMAX_TILE : lo;
   *first = lo;
   return (uint32_t) (hi - lo + 1);
 }
@@ -780,35 +782,41 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   p->shard = *shard;
   p->minlen = minlen;
   p->num_tiles = plan_tiles(shard, &p->tile_first);
+  if (capacity == 0) capacity = (shard->end - shard->begin) / 64 + 4096;
+  p->capacity = capacity;
+  {
+    const char *d = getenv("GT_SMAX_DEBUG");
+    p->dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
+  }
+  HIPCHK(hipSetDevice(shard->device));
   {
     int dev_cus = 0, per_cu = 0;
-    HIPCHK(hipSetDevice(shard->device));
     HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
                                  shard->device));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smax_scan_kernel,
                                                         SMAX_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
-    uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
+    const uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
     p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
+    const uint64_t cg = ((uint64_t) p->num_tiles + 3) / 4;   // 4 waves per block
+    p->compact_grid = (uint32_t) (cg < 4096 ? (cg ? cg : 1) : 4096);
   }
-  if (capacity == 0) {
-    uint64_t rows = shard->end - shard->begin;
-    capacity = rows / 64 + 4096;
-  }
-  p->capacity = capacity;
-  p->epoch = 1;
-  HIPCHK(hipSetDevice(shard->device));
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
-  HIPCHK(hipMalloc(&p->status, sizeof (uint64_t) * p->num_tiles));
-  HIPCHK(hipMemset(p->status, 0, sizeof (uint64_t) * p->num_tiles));
-  HIPCHK(hipMalloc(&p->ticket, sizeof (unsigned long long)));
-  HIPCHK(hipMemset(p->ticket, 0, sizeof (unsigned long long)));
+  HIPCHK(hipMalloc(&p->ovf, sizeof (GtSmaxRecord) * capacity));
+  HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_SLOT * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_ovf, sizeof (uint64_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&p->ovf_cursor, sizeof (unsigned long long)));
   HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
   HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMemset(p->bnd, 0, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMalloc(&p->llv_lo, sizeof (uint32_t) * p->num_tiles));
-  HIPCHK(hipMalloc(&p->llv_hi, sizeof (uint32_t) * p->num_tiles));
+  HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
+                                 (uint64_t) 0, (size_t) p->num_tiles,
+                                 rocprim::plus<uint64_t>(), (hipStream_t) 0));
+  HIPCHK(hipMalloc(&p->scan_tmp, p->scan_tmp_bytes ? p->scan_tmp_bytes : 16));
   HIPCHK(hipMalloc(&derr, sizeof (uint32_t)));
   HIPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
   if (shard->numllv > 0xffffffffull) {
@@ -816,11 +824,11 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     goto fail;
   }
   {
-    uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
-    unsigned blocks = (unsigned) ((work + 255) / 256);
+    const uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
+    const unsigned blocks = (unsigned) ((work + 255) / 256);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
-                       shard->llv_dev, shard->numllv, shard->base,
-                       p->tile_first, p->num_tiles, p->llv_lo, p->llv_hi, derr);
+                       shard->llv_dev, shard->numllv, shard->base, p->tile_first,
+                       p->num_tiles, p->llv_lo, derr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   }
@@ -838,13 +846,10 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  if (p->out) (void) hipFree(p->out);
-  if (p->status) (void) hipFree(p->status);
-  if (p->ticket) (void) hipFree(p->ticket);
-  if (p->count) (void) hipFree(p->count);
-  if (p->bnd) (void) hipFree(p->bnd);
-  if (p->llv_lo) (void) hipFree(p->llv_lo);
-  if (p->llv_hi) (void) hipFree(p->llv_hi);
+  void *bufs[] = {p->out, p->ovf, p->slots, p->tile_count, p->tile_ovf, p->tile_off,
+                  p->ovf_cursor, p->count, p->bnd, p->llv_lo, p->scan_tmp};
+  for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
+    if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
   free(p->ev);
   free(p);
@@ -857,7 +862,6 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;
   a.llv_lo = p->llv_lo;
-  a.llv_hi = p->llv_hi;
   a.base = p->shard.base;
   a.begin = p->shard.begin;
   a.end = p->shard.end;
@@ -865,18 +869,14 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.tile_first = p->tile_first;
   a.minlen = p->minlen;
   a.num_tiles = p->num_tiles;
-  a.out = p->out;
-  a.capacity = p->capacity;
-  a.status = p->status;
-  a.ticket = p->ticket;
-  a.ticket_base = p->ticket_base;
-  a.epoch = p->epoch;
-  a.count = p->count;
+  a.slots = p->slots;
+  a.tile_count = p->tile_count;
+  a.tile_ovf = p->tile_ovf;
+  a.ovf = p->ovf;
+  a.ovf_cap = p->capacity;
+  a.ovf_cursor = p->ovf_cursor;
   a.bnd = p->bnd;
-  {
-    const char *d = getenv("GT_SMAX_DEBUG");
-    a.dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
-  }
+  a.dbg = p->dbg;
   return a;
 }
 
@@ -885,30 +885,29 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
   size_t errlen = 0;
   hipStream_t s = (hipStream_t) stream;
   HIPCHK(hipSetDevice(p->shard.device));
-  if (p->epoch >= ST_EPOCH_MASK) {   // wrap: clear stale status words
-    HIPCHK(hipMemsetAsync(p->status, 0, sizeof (uint64_t) * p->num_tiles, s));
-    p->epoch = 1;
-  }
   {
     SmaxScanArgs a = plan_args(p);
-    if (p->shard.begin >= p->shard.end) {
-      HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
-      hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
-      HIPCHK(hipGetLastError());
-      return 0;
-    }
     hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
     HIPCHK(hipGetLastError());
+    if (p->shard.begin >= p->shard.end) {
+      HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
+      return 0;
+    }
     const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
-    hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS),
-                       0, s, a);
+    hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
+    size_t bytes = p->scan_tmp_bytes;
+    HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->tile_count, p->tile_off,
+                                   (uint64_t) 0, (size_t) p->num_tiles,
+                                   rocprim::plus<uint64_t>(), s));
+    hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
+                       p->slots, p->tile_count, p->tile_ovf, p->ovf, p->capacity,
+                       p->tile_off, p->num_tiles, p->out, p->capacity, p->count);
+    HIPCHK(hipGetLastError());
   }
   p->runs++;
-  p->ticket_base += (uint64_t) p->num_tiles + p->grid;   // one failed claim per block
-  p->epoch += 1;
   return 0;
 fail:
   return -1;
@@ -952,11 +951,8 @@ extern "C" int gt_smax_plan_timing(GtSmaxPlan *p, int nslots) {
   if (nslots <= 0) return 0;
   p->ev = (hipEvent_t *) calloc((size_t) (2 * nslots), sizeof (hipEvent_t));
   if (p->ev == NULL) return -1;
-  for (int i = 0; i < 2 * nslots; i++) {
-    HIPCHK(hipEventCreate(&p->ev[i]));
-    p->nslots = (i + 2) / 2;
-  }
   p->nslots = nslots;
+  for (int i = 0; i < 2 * nslots; i++) HIPCHK(hipEventCreate(&p->ev[i]));
   return 0;
 fail:
   return -1;
@@ -966,7 +962,7 @@ extern "C" int gt_smax_plan_timing_read(GtSmaxPlan *p, double *sum_ms, int *nrea
   char *errbuf = NULL;
   size_t errlen = 0;
   double acc = 0.0;
-  int n = (int) (p->runs < (uint64_t) p->nslots ? p->runs : (uint64_t) p->nslots);
+  const int n = (int) (p->runs < (uint64_t) p->nslots ? p->runs : (uint64_t) p->nslots);
   HIPCHK(hipSetDevice(p->shard.device));
   for (int i = 0; i < n; i++) {
     float ms = 0.0f;
