@@ -372,8 +372,60 @@ __device__ __forceinline__ void segment_candidates(const Win &t, const SmaxScanA
   }
 }
 
-__global__ void __launch_bounds__(SMAX_THREADS)
-smax_scan_kernel(SmaxScanArgs a) {
+// SWAR byte compares: high bit of each byte where the relation holds.
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t y) {
+  const uint32_t z = x ^ y;
+  return ~(((z & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z | 0x7f7f7f7fu) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t bytes_lt(uint32_t x, uint32_t y) {   // x < y
+  const uint32_t H = 0x80808080u;
+  const uint32_t d = (x | H) - (y & ~H);      // per byte 128 + xl - yl, no borrow
+  return (~x & y & H) | (~(x ^ y) & H & ~d);
+}
+// 4 byte-flags (bits 7,15,23,31) -> 4 consecutive bits
+__device__ __forceinline__ uint32_t pack4(uint32_t m) {
+  return (((m >> 7) * 0x00204081u) >> 21) & 0xfu;
+}
+
+// Fast candidate detection for one 16-row segment, entirely in registers:
+// bytes of rows sg..sg+31 (w[0..7]) and of row sg-1 (prevb).  Valid when no
+// byte is 255, all 32 rows are owned (< end <= N) and sg >= 1.  Returns the
+// 16-bit candidate mask; *slow gets the rows whose plateau reaches row 31
+// (their end lies beyond the 32-byte window: resolved by plateau_end).
+__device__ __forceinline__ uint32_t segment_fast(const uint32_t w[8], uint32_t prevb,
+                                                 uint32_t m, uint32_t mf,
+                                                 uint32_t *slow) {
+  uint32_t GE = 0, UP = 0, EQN = 0, LTN = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t cur = w[k];
+    const uint32_t prv = k == 0 ? ((cur << 8) | prevb) : __builtin_amdgcn_alignbyte(cur, w[k - 1], 3);
+    const uint32_t nxt = k == 7 ? (cur >> 8) : __builtin_amdgcn_alignbyte(w[k + 1], cur, 1);
+    GE |= pack4(bytes_ge(cur, mf)) << (4 * k);
+    UP |= pack4(bytes_lt(prv, cur)) << (4 * k);
+    EQN |= pack4(bytes_eq(nxt, cur)) << (4 * k);
+    LTN |= pack4(bytes_lt(nxt, cur)) << (4 * k);
+  }
+  EQN &= 0x7fffffffu;                 // row 31's successor is unknown
+  uint32_t starts = GE & UP & 0xffffu;
+  uint32_t cand = 0, sl = 0;
+  while (starts) {
+    const int q = __builtin_ctz(starts);
+    starts &= starts - 1;
+    if (m > 128) {                    // the SWAR filter is a superset here
+      const uint32_t b = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
+      if (b < m) continue;
+    }
+    const uint32_t e = ~EQN >> q;
+    const int j = q + __builtin_ctz(e);
+    if (j >= 31) { sl |= 1u << q; continue; }
+    if ((LTN >> j) & 1u) cand |= 1u << q;
+  }
+  *slow = sl;
+  return cand;
+}
+
+__device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ __attribute__((aligned(16))) uint8_t sL[SMAX_LDSB];
   __shared__ __attribute__((aligned(16))) uint8_t sB[SMAX_LDSB];
   __shared__ uint16_t sRank[SMAX_NCHUNK];
@@ -476,20 +528,38 @@ smax_scan_kernel(SmaxScanArgs a) {
     uint64_t pend_c = 0;
     uint32_t pend_l = 0;
     if (any_pre) {
-      const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + lane * 16;
-      const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + lane * 16;
-      if (segpre & 1u)
-        segment_candidates(t, a, sg, *reinterpret_cast<const uint4 *>(&sL[so]), 0,
-                           cand, pend_here, pend_c, pend_l);
-      if (segpre & 2u)
-        segment_candidates(t, a, sg + 1024, *reinterpret_cast<const uint4 *>(&sL[so + 1024]), 1,
-                           cand, pend_here, pend_c, pend_l);
-      if (segpre & 4u)
-        segment_candidates(t, a, sg + 2048, *reinterpret_cast<const uint4 *>(&sL[so + 2048]), 2,
-                           cand, pend_here, pend_c, pend_l);
-      if (segpre & 8u)
-        segment_candidates(t, a, sg + 3072, *reinterpret_cast<const uint4 *>(&sL[so + 3072]), 3,
-                           cand, pend_here, pend_c, pend_l);
+#pragma unroll
+      for (int r = 0; r < SMAX_SEGS; r++) {
+        if (!((segpre >> r) & 1u)) continue;
+        const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+        const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+        const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
+        const uint4 n = *reinterpret_cast<const uint4 *>(&sL[so + 16]);
+        const uint32_t prevb = sL[so - 1];
+        const uint32_t w[8] = {v.x, v.y, v.z, v.w, n.x, n.y, n.z, n.w};
+        uint32_t any255 = prevb == 255u ? 1u : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; k++) any255 |= bytes_ff(w[k]);
+        const bool fast_ok = any255 == 0 && sg >= a.begin && sg + 32 <= a.end && sg >= 1;
+        if (fast_ok) {
+          uint32_t slow;
+          const uint32_t c16 = segment_fast(w, prevb, a.minlen, mf, &slow);
+          cand |= (uint64_t) c16 << (16 * r);
+          while (slow) {               // plateau runs past the 32-row window
+            const int q = __builtin_ctz(slow);
+            slow &= slow - 1;
+            const uint64_t c = sg + q;
+            const uint32_t cur = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
+            int rel;
+            bool pend;
+            (void) plateau_end(t, c, cur, &rel, &pend);
+            if (pend) { pend_here = true; pend_c = c; pend_l = cur; }
+            else if (rel < 0) cand |= 1ull << (r * 16 + q);
+          }
+        } else {
+          segment_candidates(t, a, sg, v, r, cand, pend_here, pend_c, pend_l);
+        }
+      }
     }
 
     // ---- phase 3: left-diversity
@@ -569,6 +639,15 @@ smax_scan_kernel(SmaxScanArgs a) {
     tile = next;
     if (tile >= a.num_tiles) break;
   }
+}
+
+// K1 instantiations: 4 waves/SIMD (<= 128 VGPRs, 4 workgroups/CU, what the
+// LDS budget allows) is the default; the unconstrained build is kept for A/B.
+__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel(SmaxScanArgs a) {
+  smax_scan_body(a);
+}
+__global__ void __launch_bounds__(SMAX_THREADS) smax_scan_kernel_w3(SmaxScanArgs a) {
+  smax_scan_body(a);
 }
 
 // ------------------------------------------------------------ K3: compact
@@ -793,8 +872,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     int dev_cus = 0, per_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
                                  shard->device));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smax_scan_kernel,
-                                                        SMAX_THREADS, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, (p->dbg & 256u) ? smax_scan_kernel_w3 : smax_scan_kernel, SMAX_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
     const uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
     p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
@@ -895,7 +974,10 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
-    hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
+    if (p->dbg & 256u)
+      hipLaunchKernelGGL(smax_scan_kernel_w3, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
+    else
+      hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
     size_t bytes = p->scan_tmp_bytes;
