@@ -540,11 +540,14 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
         uint32_t any255 = prevb == 255u ? 1u : 0u;
 #pragma unroll
         for (int k = 0; k < 8; k++) any255 |= bytes_ff(w[k]);
-        const bool fast_ok = any255 == 0 && sg >= a.begin && sg + 32 <= a.end && sg >= 1;
+        const bool fast_ok = any255 == 0 && sg >= a.begin && sg + 32 <= a.end && sg >= 1 &&
+                             !(a.dbg & 64u);
+        if (!fast_ok && (a.dbg & 128u)) continue;
         if (fast_ok) {
           uint32_t slow;
           const uint32_t c16 = segment_fast(w, prevb, a.minlen, mf, &slow);
           cand |= (uint64_t) c16 << (16 * r);
+          if (a.dbg & 512u) slow = 0;
           while (slow) {               // plateau runs past the 32-row window
             const int q = __builtin_ctz(slow);
             slow &= slow - 1;
