@@ -52,7 +52,7 @@
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
 #define SMAX_LLV_CAP 1024                             // .llv values in LDS
-#define SMAX_SLOT 256                                 // records per tile slot
+#define SMAX_WSLOT 2048                               // records per (tile, wave) slot
 
 static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
@@ -69,12 +69,8 @@ struct SmaxScanArgs {
   uint64_t tile_first;       // first local tile holding an owned row
   uint32_t minlen;
   uint32_t num_tiles;
-  GtSmaxRecord *slots;       // num_tiles * SMAX_SLOT records
-  uint32_t *tile_count;      // per tile
-  uint64_t *tile_ovf;        // per tile: overflow offset (count > SMAX_SLOT)
-  GtSmaxRecord *ovf;
-  uint64_t ovf_cap;
-  unsigned long long *ovf_cursor;
+  GtSmaxRecord *slots;       // [tile][wave][SMAX_WSLOT] records, row order
+  uint32_t *tile_count;      // [tile][wave] record counts
   GtSmaxBoundary *bnd;
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
@@ -248,7 +244,6 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (threadIdx.x != 0) return;
   Win t;
   win_init(t, a);
-  *a.ovf_cursor = 0;
   GtSmaxBoundary *b = a.bnd;
   b->pend_valid = 0;
   b->shard_begin = a.begin;
@@ -425,6 +420,223 @@ __device__ __forceinline__ uint32_t segment_fast(const uint32_t w[8], uint32_t p
   return cand;
 }
 
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  return (1ull << (threadIdx.x & 63)) - 1;
+}
+
+__device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
+  if ((int) r < t.nval) return t.val[r];
+  return (uint32_t) t.llv[t.llv_base + r].value;
+}
+
+// diversity of BWT rows [lo, hi] (pairwise distinct symbols < 254)
+__device__ __forceinline__ bool diverse_rows(const Win &t, uint64_t lo, uint64_t hi) {
+  Seen s = {0, 0, 0, 0};
+  for (uint64_t g = lo; g <= hi; g++)
+    if (seen_add(s, bwt_at(t, g))) return false;
+  return true;
+}
+
+// Record a plateau that ran past the wave's rows (lane 0 only): resolve its
+// end, left-diversity and pending state exactly.
+__device__ static void finish_open(const Win &t, const SmaxScanArgs &a, uint64_t c, uint32_t l,
+                                   GtSmaxRecord *wdst, uint32_t *wcount) {
+  int rel;
+  bool pend;
+  const uint64_t j = plateau_end(t, c, l, &rel, &pend);
+  if (pend) {
+    Seen s = {0, 0, 0, 0};
+    bool dup = false;
+    for (uint64_t g = c - 1; g < a.end && !dup; g++) dup = seen_add(s, bwt_at(t, g));
+    if (!dup) {
+      GtSmaxBoundary *b = a.bnd;
+      b->pend_c = c;
+      b->pend_lcp = l;
+      b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
+      b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
+      b->pend_div.dup = 0;
+      b->pend_valid = 1;
+    }
+    return;
+  }
+  if (rel < 0 && diverse_rows(t, c - 1, j)) {
+    GtSmaxRecord rec;
+    rec.lb = c - 1;
+    rec.lcp = l;
+    rec.width = (uint32_t) (j - c + 2);
+    wdst[*wcount] = rec;
+    *wcount += 1;
+  }
+}
+
+// Wave-row-parallel smax detection over the wave's 4096 rows of an interior
+// tile (all rows owned or before begin, none >= end or >= N): 64-row chunks,
+// one row per lane; exact LCP values via ballot-counted .llv ranks; plateau
+// ends from the ballot of change points; records in row order to wdst.
+__device__ static uint32_t wave_rows(const Win &t, const SmaxScanArgs &a, uint32_t wave_rank0,
+                                     uint64_t gw, uint32_t wrow0, const uint8_t *sL,
+                                     GtSmaxRecord *wdst) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t m = a.minlen;
+  uint32_t wcount = 0;
+  uint32_t r255 = wave_rank0;
+  uint32_t carry;
+  {
+    const uint32_t b = sL[wrow0 - 1];
+    carry = b < 255 ? b : llv_by_rank(t, r255 - 1);
+  }
+  bool open = false;
+  uint64_t open_c = 0;
+  uint32_t open_v = 0;
+  for (int j = 0; j < SMAX_WAVE_BYTES / 64; j++) {
+    const uint32_t b = sL[wrow0 + j * 64 + lane];
+    const uint64_t hot = __ballot(b >= m || b == 255);
+    if (!hot && !open) {               // no byte reaches minlen, nothing open
+      carry = __shfl(b, 63, 64);
+      continue;
+    }
+    const bool is255 = b == 255;
+    const uint64_t m255 = __ballot(is255);
+    uint32_t v = b;
+    if (m255) {
+      if (is255) v = llv_by_rank(t, r255 + (uint32_t) __popcll(m255 & lanemask_lt()));
+      r255 += (uint32_t) __popcll(m255);
+    }
+    uint32_t vprev = __shfl_up(v, 1, 64);
+    if (lane == 0) vprev = carry;
+    carry = __shfl(v, 63, 64);
+    const uint64_t chg = __ballot(v != vprev);
+    const uint64_t g = gw + (uint64_t) j * 64 + lane;
+    // a plateau opened in an earlier chunk ends at this chunk's first change
+    if (open && chg) {
+      const int e = __builtin_ctzll(chg);
+      const uint32_t ve = __shfl(v, e, 64);
+      int ok = 0;
+      if (lane == 0 && ve < open_v) {
+        const uint64_t rb = gw + (uint64_t) j * 64 + e - 1;
+        if (diverse_rows(t, open_c - 1, rb)) {
+          GtSmaxRecord rec;
+          rec.lb = open_c - 1;
+          rec.lcp = open_v;
+          rec.width = (uint32_t) (rb - open_c + 2);
+          wdst[wcount] = rec;
+          ok = 1;
+        }
+      }
+      wcount += (uint32_t) __shfl(ok, 0, 64);
+      open = false;
+    }
+    const bool up = v > vprev && v >= m && g >= a.begin;
+    if (__ballot(up) == 0) continue;
+    const uint64_t above = chg & ~((2ull << lane) - 1);   // change points after this row
+    const int e = above ? __builtin_ctzll(above) : 0;
+    const uint32_t ve = __shfl(v, e, 64);
+    const bool lmax = up && above != 0 && ve < v;
+    const uint64_t to_open = __ballot(up && above == 0);  // at most the last up row
+    if (to_open) {
+      const int ol = 63 - __builtin_clzll(to_open);
+      open = true;
+      open_c = gw + (uint64_t) j * 64 + ol;
+      open_v = __shfl(v, ol, 64);
+    }
+    bool acc = false;
+    if (lmax) acc = diverse_rows(t, g - 1, g + (uint64_t) (e - lane) - 1);
+    const uint64_t accm = __ballot(acc);
+    if (acc) {
+      GtSmaxRecord rec;
+      rec.lb = g - 1;
+      rec.lcp = v;
+      rec.width = (uint32_t) (e - lane + 1);
+      wdst[wcount + (uint32_t) __popcll(accm & lanemask_lt())] = rec;
+    }
+    wcount += (uint32_t) __popcll(accm);
+  }
+  if (open) {
+    uint32_t wc = wcount;
+    if (lane == 0) finish_open(t, a, open_c, open_v, wdst, &wc);
+    wcount = __shfl(wc, 0, 64);
+  }
+  return wcount;
+}
+
+// Per-lane path for the shard's edge tiles (rows >= end or N, row 0, the
+// pending plateau): the lane's 4 segments of 16 rows, exact per-row logic.
+__device__ static uint32_t edge_rows(const Win &t, const SmaxScanArgs &a, uint64_t g0,
+                                     const uint8_t *sL, GtSmaxRecord *wdst) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t cand = 0;
+  bool pend_here = false;
+  uint64_t pend_c = 0;
+  uint32_t pend_l = 0;
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+    const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+    segment_candidates(t, a, sg, *reinterpret_cast<const uint4 *>(&sL[so]), r, cand,
+                       pend_here, pend_c, pend_l);
+  }
+  uint64_t tmp = cand;
+  while (tmp) {
+    const int bit = __builtin_ctzll(tmp);
+    tmp &= tmp - 1;
+    const int r = bit >> 4, q = bit & 15;
+    const uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
+    const uint32_t cur = lcp_exact(t, c);
+    int rel;
+    bool pend;
+    const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
+    if (!diverse_rows(t, c - 1, j)) cand &= ~(1ull << bit);
+  }
+  if (pend_here) {
+    Seen s = {0, 0, 0, 0};
+    bool dup = false;
+    for (uint64_t g = pend_c - 1; g < a.end && !dup; g++) dup = seen_add(s, bwt_at(t, g));
+    if (!dup) {
+      GtSmaxBoundary *b = a.bnd;
+      b->pend_c = pend_c;
+      b->pend_lcp = pend_l;
+      b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
+      b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
+      b->pend_div.dup = 0;
+      b->pend_valid = 1;
+    }
+  }
+  // wave-level offsets in row order (segment-major, then lane)
+  uint32_t wt = 0, so_r[SMAX_SEGS];
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    const uint32_t c = (uint32_t) __popcll((cand >> (16 * r)) & 0xffffull);
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    so_r[r] = wt + incl - c;
+    wt += __shfl(incl, 63, 64);
+  }
+  tmp = cand;
+  while (tmp) {
+    const int bit = __builtin_ctzll(tmp);
+    tmp &= tmp - 1;
+    const int r = bit >> 4, q = bit & 15;
+    const uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
+    const uint32_t cur = lcp_exact(t, c);
+    int rel;
+    bool pend;
+    const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
+    const uint32_t before = (uint32_t) __popcll(cand & ((1ull << bit) - 1) &
+                                                (0xffffull << (16 * r)));
+    const uint32_t so = r == 0 ? so_r[0] : r == 1 ? so_r[1] : r == 2 ? so_r[2] : so_r[3];
+    GtSmaxRecord rec;
+    rec.lb = c - 1;
+    rec.lcp = cur;
+    rec.width = (uint32_t) (j - c + 2);
+    wdst[so + before] = rec;
+  }
+  return wt;
+}
+
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ __attribute__((aligned(16))) uint8_t sL[SMAX_LDSB];
   __shared__ __attribute__((aligned(16))) uint8_t sB[SMAX_LDSB];
@@ -434,7 +646,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ uint32_t sHalo[5];
   __shared__ uint32_t sFlags;
   __shared__ uint32_t sLlvBase;
-  __shared__ uint64_t sOvf;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -466,20 +677,17 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     // ---- stage the prefetched tile, filter
     __syncthreads();               // LDS free (previous tile done), sFlags reset
     store_tile(sL, sB, R);
-    const uint32_t p0 = seg_ge(R.l0, mf), p1 = seg_ge(R.l1, mf), p2 = seg_ge(R.l2, mf),
-                   p3 = seg_ge(R.l3, mf);
-    const uint32_t segpre = (p0 ? 1u : 0u) | (p1 ? 2u : 0u) | (p2 ? 4u : 0u) | (p3 ? 8u : 0u);
+    const uint32_t segpre = seg_ge(R.l0, mf) | seg_ge(R.l1, mf) | seg_ge(R.l2, mf) |
+                            seg_ge(R.l3, mf);
     const uint32_t f0 = seg_ffcount(R.l0), f1 = seg_ffcount(R.l1), f2 = seg_ffcount(R.l2),
                    f3 = seg_ffcount(R.l3);
     const uint32_t hff = tid < 5 ? seg_ffcount(R.h) : 0u;
-    const uint32_t fl = (segpre ? 1u : 0u) | ((f0 | f1 | f2 | f3 | hff) ? 2u : 0u);
-    if (fl) atomicOr(&sFlags, fl);
+    if ((f0 | f1 | f2 | f3 | hff) != 0) atomicOr(&sFlags, 2u);
     if (tid < 5) sHalo[tid] = hff;
     if (tid == 0) sLlvBase = llv_lo_next;
     __syncthreads();
-    const uint32_t flags = sFlags;
-    const bool any_pre = (flags & 1u) != 0 && !(a.dbg & 2u);
-    const bool has_ff = (flags & 2u) != 0 && !(a.dbg & 16u);
+    const bool has_ff = (sFlags & 2u) != 0 && !(a.dbg & 16u);
+    const bool wave_pre = __ballot(segpre != 0) != 0 && !(a.dbg & 2u);
 
     // ---- prefetch the next tile: in flight during all of this tile's work
     if (next < a.num_tiles) {
@@ -500,10 +708,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
       sRank[cb + 64] = (uint16_t) (h0 + wo + o1);
       sRank[cb + 128] = (uint16_t) (h0 + wo + o2);
       sRank[cb + 192] = (uint16_t) (h0 + wo + o3);
-      uint32_t nff = h0 + tot;
       if (tid == 0) {
         sRank[0] = 0;
-        uint32_t acc = nff;
+        uint32_t acc = h0 + tot;
         for (int k = 0; k < 4; k++) {
           sRank[1 + SMAX_TILE / 16 + k] = (uint16_t) acc;
           acc += sHalo[1 + k];
@@ -511,7 +718,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
         sFlags = acc;              // total 255 bytes in the window (reuse)
       }
       __syncthreads();
-      nff = sFlags;
+      const uint32_t nff = sFlags;
       t.llv_base = sLlvBase;
       if (nff <= SMAX_LLV_CAP) {
         for (uint32_t i = tid; i < nff; i += SMAX_THREADS)
@@ -522,121 +729,20 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
       __syncthreads();
     }
 
-    // ---- phase 1: plateau starts that are local maxima (L only)
-    uint64_t cand = 0;          // bit r*16+q: row is a local-maximum start
-    bool pend_here = false;
-    uint64_t pend_c = 0;
-    uint32_t pend_l = 0;
-    if (any_pre) {
-#pragma unroll
-      for (int r = 0; r < SMAX_SEGS; r++) {
-        if (!((segpre >> r) & 1u)) continue;
-        const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-        const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-        const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
-        const uint4 n = *reinterpret_cast<const uint4 *>(&sL[so + 16]);
-        const uint32_t prevb = sL[so - 1];
-        const uint32_t w[8] = {v.x, v.y, v.z, v.w, n.x, n.y, n.z, n.w};
-        uint32_t any255 = prevb == 255u ? 1u : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; k++) any255 |= bytes_ff(w[k]);
-        const bool fast_ok = any255 == 0 && sg >= a.begin && sg + 32 <= a.end && sg >= 1 &&
-                             !(a.dbg & 64u);
-        if (!fast_ok && (a.dbg & 128u)) continue;
-        if (fast_ok) {
-          uint32_t slow;
-          const uint32_t c16 = segment_fast(w, prevb, a.minlen, mf, &slow);
-          cand |= (uint64_t) c16 << (16 * r);
-          if (a.dbg & 512u) slow = 0;
-          while (slow) {               // plateau runs past the 32-row window
-            const int q = __builtin_ctz(slow);
-            slow &= slow - 1;
-            const uint64_t c = sg + q;
-            const uint32_t cur = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
-            int rel;
-            bool pend;
-            (void) plateau_end(t, c, cur, &rel, &pend);
-            if (pend) { pend_here = true; pend_c = c; pend_l = cur; }
-            else if (rel < 0) cand |= 1ull << (r * 16 + q);
-          }
-        } else {
-          segment_candidates(t, a, sg, v, r, cand, pend_here, pend_c, pend_l);
-        }
+    // ---- detection, diversity, records (per wave, row order)
+    GtSmaxRecord *wdst = a.slots + (tile * 4 + wave) * (uint64_t) SMAX_WSLOT;
+    uint32_t wcount = 0;
+    if (wave_pre) {
+      const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
+      if (!edge) {
+        const uint32_t wrow0 = SMAX_LH + wave * SMAX_WAVE_BYTES;
+        const uint32_t rank0 = t.rank ? t.rank[1 + wave * 256] : 0u;
+        wcount = wave_rows(t, a, rank0, g0 + wave * SMAX_WAVE_BYTES, wrow0, sL, wdst);
+      } else {
+        wcount = edge_rows(t, a, g0, sL, wdst);
       }
     }
-
-    // ---- phase 3: left-diversity
-    uint64_t tmp = (a.dbg & 4u) ? 0 : cand;
-    while (tmp) {
-      const int bit = __builtin_ctzll(tmp);
-      tmp &= tmp - 1;
-      const int r = bit >> 4, q = bit & 15;
-      const uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
-      const uint32_t cur = lcp_exact(t, c);
-      int rel;
-      bool pend;
-      const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
-      Seen s = {0, 0, 0, 0};
-      bool dup = false;
-      for (uint64_t g = c - 1; g <= j && !dup; g++) dup = seen_add(s, bwt_at(t, g));
-      if (dup) cand &= ~(1ull << bit);
-    }
-    if (pend_here) {
-      Seen s = {0, 0, 0, 0};
-      bool dup = false;
-      for (uint64_t g = pend_c - 1; g < a.end && !dup; g++)
-        dup = seen_add(s, bwt_at(t, g));
-      if (!dup) {
-        GtSmaxBoundary *b = a.bnd;
-        b->pend_c = pend_c;
-        b->pend_lcp = pend_l;
-        b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
-        b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
-        b->pend_div.dup = 0;
-        b->pend_valid = 1;
-      }
-    }
-
-    // ---- output: row-order offsets, records into the tile slot / overflow
-    uint32_t so0, so1, so2, so3, wave_off, tile_count;
-    block_scan_rows((uint32_t) __popcll(cand & 0xffffull),
-                    (uint32_t) __popcll((cand >> 16) & 0xffffull),
-                    (uint32_t) __popcll((cand >> 32) & 0xffffull),
-                    (uint32_t) __popcll((cand >> 48) & 0xffffull),
-                    &so0, &so1, &so2, &so3, &wave_off, &tile_count, sWave);
-    GtSmaxRecord *dst = a.slots + tile * (uint64_t) SMAX_SLOT;
-    uint64_t dcap = SMAX_SLOT;
-    if (tile_count > SMAX_SLOT) {            // block-uniform
-      if (tid == 0) sOvf = atomicAdd(a.ovf_cursor, (unsigned long long) tile_count);
-      __syncthreads();
-      const uint64_t off = sOvf;
-      if (tid == 0) a.tile_ovf[tile] = off;
-      dst = a.ovf + off;
-      dcap = off < a.ovf_cap ? a.ovf_cap - off : 0;
-    }
-    if (tid == 0) a.tile_count[tile] = tile_count;
-    tmp = (a.dbg & 8u) ? 0 : cand;
-    while (tmp) {
-      const int bit = __builtin_ctzll(tmp);
-      tmp &= tmp - 1;
-      const int r = bit >> 4, q = bit & 15;
-      const uint64_t c = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16 + q;
-      const uint32_t cur = lcp_exact(t, c);
-      int rel;
-      bool pend;
-      const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
-      const uint32_t before = (uint32_t) __popcll(cand & ((1ull << bit) - 1) &
-                                                  (0xffffull << (16 * r)));
-      const uint32_t so = r == 0 ? so0 : r == 1 ? so1 : r == 2 ? so2 : so3;
-      const uint64_t o = wave_off + so + before;
-      if (o < dcap) {
-        GtSmaxRecord rec;
-        rec.lb = c - 1;
-        rec.lcp = cur;
-        rec.width = (uint32_t) (j - c + 2);
-        dst[o] = rec;
-      }
-    }
+    if (lane == 0) a.tile_count[tile * 4 + wave] = wcount;
 
     if (tid == 0) sFlags = 0;
     tile = next;
@@ -655,34 +761,23 @@ __global__ void __launch_bounds__(SMAX_THREADS) smax_scan_kernel_w3(SmaxScanArgs
 
 // ------------------------------------------------------------ K3: compact
 
-// One wave per tile (grid-stride): copy the tile's records to their final
-// position (exclusive scan of tile counts) -> ascending lb overall.
+// One wave per (tile, wave) slot, grid-stride: copy the slot's records to
+// their final position (exclusive scan of the slot counts, which are in row
+// order) -> ascending lb overall.  Also publishes the total.
 __global__ void __launch_bounds__(256)
-smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *tile_count,
-                    const uint64_t *tile_ovf, const GtSmaxRecord *ovf,
-                    uint64_t ovf_cap, const uint64_t *tile_off, uint32_t num_tiles,
-                    GtSmaxRecord *out, uint64_t capacity, uint64_t *count) {
+smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
+                    const uint64_t *slot_off, uint64_t nslots, GtSmaxRecord *out,
+                    uint64_t capacity, uint64_t *count) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (blockIdx.x * (uint64_t) blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t) gridDim.x * blockDim.x) >> 6;
-  for (uint64_t tl = wave; tl < num_tiles; tl += nwaves) {
-    const uint32_t cnt = tile_count[tl];
-    const uint64_t off = tile_off[tl];
-    if (tl == num_tiles - 1 && lane == 0) *count = off + cnt;
-    if (cnt == 0) continue;
-    const GtSmaxRecord *src;
-    uint64_t scap;
-    if (cnt > SMAX_SLOT) {
-      const uint64_t o = tile_ovf[tl];
-      src = ovf + o;
-      scap = o < ovf_cap ? ovf_cap - o : 0;
-    } else {
-      src = slots + tl * (uint64_t) SMAX_SLOT;
-      scap = SMAX_SLOT;
-    }
-    for (uint32_t i = lane; i < cnt; i += 64) {
-      if (off + i < capacity && i < scap) out[off + i] = src[i];
-    }
+  for (uint64_t sl = wave; sl < nslots; sl += nwaves) {
+    const uint32_t cnt = slot_count[sl];
+    const uint64_t off = slot_off[sl];
+    if (sl == nslots - 1 && lane == 0) *count = off + cnt;
+    const GtSmaxRecord *src = slots + sl * (uint64_t) SMAX_WSLOT;
+    for (uint32_t i = lane; i < cnt; i += 64)
+      if (off + i < capacity) out[off + i] = src[i];
   }
 }
 
@@ -781,11 +876,9 @@ struct GtSmaxPlan {
   uint64_t tile_first;
   uint32_t grid, compact_grid;
   GtSmaxRecord *out;         // capacity records, ascending lb
-  GtSmaxRecord *slots;       // num_tiles * SMAX_SLOT
-  GtSmaxRecord *ovf;         // capacity records
-  uint32_t *tile_count;
-  uint64_t *tile_ovf, *tile_off;
-  unsigned long long *ovf_cursor;
+  GtSmaxRecord *slots;       // num_tiles * 4 * SMAX_WSLOT
+  uint32_t *tile_count;      // num_tiles * 4
+  uint64_t *tile_off;        // num_tiles * 4
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint32_t *llv_lo;
@@ -880,23 +973,20 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     if (per_cu < 1) per_cu = 1;
     const uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
     p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
-    const uint64_t cg = ((uint64_t) p->num_tiles + 3) / 4;   // 4 waves per block
+    const uint64_t cg = (uint64_t) p->num_tiles;              // 4 slots per block
     p->compact_grid = (uint32_t) (cg < 4096 ? (cg ? cg : 1) : 4096);
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
-  HIPCHK(hipMalloc(&p->ovf, sizeof (GtSmaxRecord) * capacity));
-  HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_SLOT * (uint64_t) p->num_tiles));
-  HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * p->num_tiles));
-  HIPCHK(hipMalloc(&p->tile_ovf, sizeof (uint64_t) * p->num_tiles));
-  HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * p->num_tiles));
-  HIPCHK(hipMalloc(&p->ovf_cursor, sizeof (unsigned long long)));
+  HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * 4 * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * 4 * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * 4 * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
   HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMemset(p->bnd, 0, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMalloc(&p->llv_lo, sizeof (uint32_t) * p->num_tiles));
   HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
-                                 (uint64_t) 0, (size_t) p->num_tiles,
+                                 (uint64_t) 0, (size_t) p->num_tiles * 4,
                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
   HIPCHK(hipMalloc(&p->scan_tmp, p->scan_tmp_bytes ? p->scan_tmp_bytes : 16));
   HIPCHK(hipMalloc(&derr, sizeof (uint32_t)));
@@ -928,8 +1018,8 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->ovf, p->slots, p->tile_count, p->tile_ovf, p->tile_off,
-                  p->ovf_cursor, p->count, p->bnd, p->llv_lo, p->scan_tmp};
+  void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
+                  p->llv_lo, p->scan_tmp};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -953,10 +1043,6 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.num_tiles = p->num_tiles;
   a.slots = p->slots;
   a.tile_count = p->tile_count;
-  a.tile_ovf = p->tile_ovf;
-  a.ovf = p->ovf;
-  a.ovf_cap = p->capacity;
-  a.ovf_cursor = p->ovf_cursor;
   a.bnd = p->bnd;
   a.dbg = p->dbg;
   return a;
@@ -985,11 +1071,11 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
     size_t bytes = p->scan_tmp_bytes;
     HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->tile_count, p->tile_off,
-                                   (uint64_t) 0, (size_t) p->num_tiles,
+                                   (uint64_t) 0, (size_t) p->num_tiles * 4,
                                    rocprim::plus<uint64_t>(), s));
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->slots, p->tile_count, p->tile_ovf, p->ovf, p->capacity,
-                       p->tile_off, p->num_tiles, p->out, p->capacity, p->count);
+                       p->slots, p->tile_count, p->tile_off, (uint64_t) p->num_tiles * 4,
+                       p->out, p->capacity, p->count);
     HIPCHK(hipGetLastError());
   }
   p->runs++;
