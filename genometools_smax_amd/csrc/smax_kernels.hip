@@ -971,7 +971,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, (p->dbg & 256u) ? smax_scan_kernel_w3 : smax_scan_kernel, SMAX_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
-    const uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
+    uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
+    const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
+    if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
     p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
     const uint64_t cg = (uint64_t) p->num_tiles;              // 4 slots per block
     p->compact_grid = (uint32_t) (cg < 4096 ? (cg ? cg : 1) : 4096);
