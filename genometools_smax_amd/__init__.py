@@ -130,6 +130,8 @@ def lib():
         L.gt_smax_plan_timing.argtypes = [vp, ci]
         L.gt_smax_plan_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci)]
         L.gt_smax_plan_copy_boundary.argtypes = [vp, vp, vp]
+        L.gt_smax_plan_error_bits.argtypes = [vp]
+        L.gt_smax_plan_error_bits.restype = ctypes.c_uint32
         _lib = L
     return _lib
 
@@ -404,6 +406,9 @@ class SmaxPlan:
     def copy_boundary(self, dst_ptr, stream=0):
         if lib().gt_smax_plan_copy_boundary(self.plan, dst_ptr, stream or None) != 0:
             raise SmaxError("gt_smax_plan_copy_boundary failed")
+
+    def error_bits(self):
+        return lib().gt_smax_plan_error_bits(self.plan)
 
     def fetch_count(self):
         c = ctypes.c_uint64()

@@ -66,6 +66,8 @@ struct SmaxScanArgs {
   uint64_t numllv;
   const uint32_t *llv_lo;    // per tile: first llv index >= tile_g0 - LH
   uint64_t base, begin, end, N;
+  uint64_t local_len;        // readable: [-PAD_FRONT, local_len + PAD_BACK)
+  uint32_t *err;             // sticky error bits (bounds), read by the host
   uint64_t tile_first;       // first local tile holding an owned row
   uint32_t minlen;
   uint32_t num_tiles;
@@ -77,15 +79,23 @@ struct SmaxScanArgs {
 
 // ------------------------------------------------------------ helpers
 
+#define SMAX_ERR_LLV 1u        // a 255 byte without its .llv entry
+#define SMAX_ERR_RANGE 2u      // a table read outside the shard's rows
+
 // exact LCP value from the global .llv (binary search in [lo, hi))
 __device__ static uint32_t llv_search_global(const GtSmaxLlv *llv, uint64_t lo,
-                                             uint64_t hi, uint64_t g) {
+                                             uint64_t hi, uint64_t g, uint32_t *err) {
+  const uint64_t stop = hi;
   while (lo < hi) {
     uint64_t mid = (lo + hi) >> 1;
     uint64_t p = llv[mid].position;
     if (p < g) lo = mid + 1; else hi = mid;
   }
-  return (uint32_t) llv[lo].value;   // present by construction of .llv
+  if (lo >= stop || llv[lo].position != g) {   // never for a consistent index
+    atomicOr(err, SMAX_ERR_LLV);
+    return 255;
+  }
+  return (uint32_t) llv[lo].value;
 }
 
 // high bit of each byte of w that is >= m (1 <= m <= 128); exact
@@ -103,7 +113,8 @@ struct Win {
   const uint8_t *glcp;        // global (local-indexed) tables
   const uint8_t *gbwt;
   const GtSmaxLlv *llv;
-  uint64_t numllv, base, N, end;
+  uint64_t numllv, base, N, end, local_len;
+  uint32_t *err;
   const uint8_t *L;           // LDS window: index o = g - g0 + LH
   const uint8_t *B;
   const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
@@ -115,7 +126,7 @@ struct Win {
 
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
-  t.base = a.base; t.N = a.N; t.end = a.end;
+  t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
   t.L = nullptr; t.B = nullptr; t.rank = nullptr; t.val = nullptr; t.nval = -1;
   t.g0 = 0; t.llv_base = 0;
 }
@@ -137,9 +148,10 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
     else cnt = __popcll(lo) + __popcll(hi & ((1ull << (8 * (within - 8))) - 1));
     const uint32_t r = t.rank[chunk] + (uint32_t) cnt;
     if ((int) r < t.nval) return t.val[r];
+    if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
     return (uint32_t) t.llv[t.llv_base + r].value;
   }
-  return llv_search_global(t.llv, 0, t.numllv, g);
+  return llv_search_global(t.llv, 0, t.numllv, g, t.err);
 }
 
 // byte of LCP[g] (LCP[0] = LCP[N] = 0 are returned as 0)
@@ -147,6 +159,7 @@ __device__ __forceinline__ uint32_t lcp_byte(const Win &t, uint64_t g) {
   if (g == 0 || g >= t.N) return 0;
   const int64_t o = win_off(t, g);
   if (t.L != nullptr && o >= 0 && o < SMAX_LDSB) return t.L[o];
+  if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 0; }
   return t.glcp[g - t.base];
 }
 
@@ -158,6 +171,7 @@ __device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
 __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
+  if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
   return t.gbwt[g - t.base];
 }
 
@@ -256,7 +270,7 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (v >= a.minlen && a.begin < a.end) {
     uint64_t g = a.begin;
     for (;;) {
-      if (seen_add(s, a.bwt[g - a.base])) { dup = 1; break; }
+      if (seen_add(s, bwt_at(t, g))) { dup = 1; break; }
       const uint64_t h = g + 1;
       const uint32_t nx = lcp_exact(t, h);
       if (nx != v) { f = h; nxt = nx; break; }
@@ -426,6 +440,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 
 __device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
   if ((int) r < t.nval) return t.val[r];
+  if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
   return (uint32_t) t.llv[t.llv_base + r].value;
 }
 
@@ -882,6 +897,7 @@ struct GtSmaxPlan {
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint32_t *llv_lo;
+  uint32_t *err;
   void *scan_tmp;
   size_t scan_tmp_bytes;
   uint32_t dbg;
@@ -987,6 +1003,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMemset(p->bnd, 0, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMalloc(&p->llv_lo, sizeof (uint32_t) * p->num_tiles));
+  HIPCHK(hipMalloc(&p->err, sizeof (uint32_t)));
+  HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
   HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
                                  (uint64_t) 0, (size_t) p->num_tiles * 4,
                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
@@ -1021,7 +1039,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
-                  p->llv_lo, p->scan_tmp};
+                  p->llv_lo, p->err, p->scan_tmp};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -1040,6 +1058,8 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.begin = p->shard.begin;
   a.end = p->shard.end;
   a.N = p->shard.nonspecials;
+  a.local_len = p->shard.local_len;
+  a.err = p->err;
   a.tile_first = p->tile_first;
   a.minlen = p->minlen;
   a.num_tiles = p->num_tiles;
@@ -1164,12 +1184,25 @@ fail:
 extern "C" int gt_smax_plan_fetch_count(GtSmaxPlan *p, uint64_t *count) {
   char *errbuf = NULL;
   size_t errlen = 0;
+  uint32_t e = 0;
   HIPCHK(hipSetDevice(p->shard.device));
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(count, p->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&e, p->err, sizeof e, hipMemcpyDeviceToHost));
+  if (e != 0) {
+    fprintf(stderr, "gt_smax: inconsistent index (device error bits 0x%x)\n", e);
+    return -1;
+  }
   return 0;
 fail:
   return -1;
+}
+
+extern "C" uint32_t gt_smax_plan_error_bits(GtSmaxPlan *p) {
+  uint32_t e = 0;
+  if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;
+  if (hipMemcpy(&e, p->err, sizeof e, hipMemcpyDeviceToHost) != hipSuccess) return 0xffffffffu;
+  return e;
 }
 
 // ---------------------------------------------------- host-buffer API
@@ -1284,6 +1317,16 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
     HIPCHK(hipStreamSynchronize(r->stream));
     HIPCHK(hipMemcpy(&counts[s], r->plan->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&bnds[s], r->plan->bnd, sizeof (GtSmaxBoundary), hipMemcpyDeviceToHost));
+    {
+      uint32_t e = 0;
+      HIPCHK(hipMemcpy(&e, r->plan->err, sizeof e, hipMemcpyDeviceToHost));
+      if (e != 0) {
+        seterr(errbuf, errlen, "inconsistent index: %s%s",
+               (e & 1u) ? "a .lcp byte 255 without its .llv entry " : "",
+               (e & 2u) ? "a table read outside the shard" : "");
+        goto fail;
+      }
+    }
     if (counts[s] > r->plan->capacity) {   // re-run with exact capacity
       uint64_t need = counts[s] + 1;
       gt_smax_plan_delete(r->plan);

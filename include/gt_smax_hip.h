@@ -190,8 +190,13 @@ int gt_smax_plan_timing_read(GtSmaxPlan *plan, double *sum_ms, int *nread);
  * e.g. into the send buffer of an all-gather. */
 int gt_smax_plan_copy_boundary(GtSmaxPlan *plan, void *dst_dev, void *stream);
 
-/* Synchronises the plan's device and copies the record count to the host. */
+/* Synchronises the plan's device and copies the record count to the host;
+ * -1 if the kernels flagged an inconsistent index (see error bits). */
 int gt_smax_plan_fetch_count(GtSmaxPlan *plan, uint64_t *count);
+
+/* Sticky device error bits: 1 = an .lcp byte 255 without its .llv entry,
+ * 2 = a table read outside the shard's rows. */
+uint32_t gt_smax_plan_error_bits(GtSmaxPlan *plan);
 
 #ifdef __cplusplus
 }

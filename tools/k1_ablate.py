@@ -22,6 +22,8 @@ for rnd in range(3):
         os.environ["GT_SMAX_DEBUG"] = str(v)
         p = esa.plan(20)
         p.run(); torch.cuda.synchronize()
+        if p.error_bits():
+            print("dbg=%d: device error bits 0x%x" % (v, p.error_bits()), flush=True)
         p.enable_timing(10)
         for _ in range(10):
             p.run()
