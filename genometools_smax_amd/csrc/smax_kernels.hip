@@ -396,39 +396,66 @@ __device__ __forceinline__ uint32_t pack4(uint32_t m) {
   return (((m >> 7) * 0x00204081u) >> 21) & 0xfu;
 }
 
-// Fast candidate detection for one 16-row segment, entirely in registers:
-// bytes of rows sg..sg+31 (w[0..7]) and of row sg-1 (prevb).  Valid when no
-// byte is 255, all 32 rows are owned (< end <= N) and sg >= 1.  Returns the
-// 16-bit candidate mask; *slow gets the rows whose plateau reaches row 31
-// (their end lies beyond the 32-byte window: resolved by plateau_end).
-__device__ __forceinline__ uint32_t segment_fast(const uint32_t w[8], uint32_t prevb,
-                                                 uint32_t m, uint32_t mf,
+// Fast candidate detection for one 16-row segment of an interior tile,
+// SWAR over the rows' LCP bytes in registers: rows sg..sg+19 (16 own rows +
+// 4 look-ahead rows) and row sg-1.  Masks (bit q = row sg+q):
+//   GE  byte >= min(minlen,128)       UP  LCP[q] > LCP[q-1]
+//   EQN LCP[q+1] == LCP[q]            LTN LCP[q+1] < LCP[q]
+// Byte compares are exact except between two 255 bytes; those (rare) pairs
+// are fixed up with exact .llv values.  A start q ends its plateau at the
+// first row e >= q with EQN clear; it is a local maximum iff LTN bit e.
+// Plateaus reaching row 19 are resolved by plateau_end (returned in *slow).
+__device__ __forceinline__ uint32_t segment_fast(const Win &t, const SmaxScanArgs &a,
+                                                 uint64_t sg, uint32_t so, const uint8_t *sL,
+                                                 uint32_t ownmask, uint32_t mf,
                                                  uint32_t *slow) {
-  uint32_t GE = 0, UP = 0, EQN = 0, LTN = 0;
+  const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
+  const uint32_t x = *reinterpret_cast<const uint32_t *>(&sL[so + 16]);
+  const uint32_t prevb = sL[so - 1];
+  const uint32_t w[5] = {v.x, v.y, v.z, v.w, x};
+  uint32_t GE = 0, UP = 0, EQN = 0, LTN = 0, FF = 0;
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
+  for (int k = 0; k < 5; k++) {
     const uint32_t cur = w[k];
     const uint32_t prv = k == 0 ? ((cur << 8) | prevb) : __builtin_amdgcn_alignbyte(cur, w[k - 1], 3);
-    const uint32_t nxt = k == 7 ? (cur >> 8) : __builtin_amdgcn_alignbyte(w[k + 1], cur, 1);
+    const uint32_t nxt = k == 4 ? (cur >> 8) : __builtin_amdgcn_alignbyte(w[k + 1], cur, 1);
     GE |= pack4(bytes_ge(cur, mf)) << (4 * k);
     UP |= pack4(bytes_lt(prv, cur)) << (4 * k);
     EQN |= pack4(bytes_eq(nxt, cur)) << (4 * k);
     LTN |= pack4(bytes_lt(nxt, cur)) << (4 * k);
+    FF |= pack4(bytes_ff(cur)) << (4 * k);
   }
-  EQN &= 0x7fffffffu;                 // row 31's successor is unknown
-  uint32_t starts = GE & UP & 0xffffu;
+  EQN &= 0x7ffffu;                       // row 19's successor is unknown
+  if (FF | (prevb == 255u)) {
+    // exact compares where both bytes are 255
+    uint32_t fu = FF & ((FF << 1) | (prevb == 255u ? 1u : 0u)) & 0xffffu;
+    uint32_t fn = FF & (FF >> 1) & 0x7ffffu;
+    while (fu) {
+      const int q = __builtin_ctz(fu);
+      fu &= fu - 1;
+      const uint32_t c = lcp_big(t, sg + q), p = lcp_big(t, sg + q - 1);
+      UP = (UP & ~(1u << q)) | ((c > p ? 1u : 0u) << q);
+    }
+    while (fn) {
+      const int q = __builtin_ctz(fn);
+      fn &= fn - 1;
+      const uint32_t c = lcp_big(t, sg + q), n = lcp_big(t, sg + q + 1);
+      EQN = (EQN & ~(1u << q)) | ((c == n ? 1u : 0u) << q);
+      LTN = (LTN & ~(1u << q)) | ((n < c ? 1u : 0u) << q);
+    }
+  }
+  uint32_t starts = GE & UP & ownmask;
   uint32_t cand = 0, sl = 0;
   while (starts) {
     const int q = __builtin_ctz(starts);
     starts &= starts - 1;
-    if (m > 128) {                    // the SWAR filter is a superset here
-      const uint32_t b = (w[q >> 2] >> (8 * (q & 3))) & 0xffu;
-      if (b < m) continue;
+    if (a.minlen > 128) {                // the SWAR filter is a superset here
+      const uint32_t b = sL[so + q];
+      if ((b < 255 ? b : lcp_big(t, sg + q)) < a.minlen) continue;
     }
-    const uint32_t e = ~EQN >> q;
-    const int j = q + __builtin_ctz(e);
-    if (j >= 31) { sl |= 1u << q; continue; }
-    if ((LTN >> j) & 1u) cand |= 1u << q;
+    const int e = q + __builtin_ctz(~EQN >> q);
+    if (e >= 19) { sl |= 1u << q; continue; }
+    if ((LTN >> e) & 1u) cand |= 1u << q;
   }
   *slow = sl;
   return cand;
@@ -484,111 +511,45 @@ __device__ static void finish_open(const Win &t, const SmaxScanArgs &a, uint64_t
   }
 }
 
-// Wave-row-parallel smax detection over the wave's 4096 rows of an interior
-// tile (all rows owned or before begin, none >= end or >= N): 64-row chunks,
-// one row per lane; exact LCP values via ballot-counted .llv ranks; plateau
-// ends from the ballot of change points; records in row order to wdst.
-__device__ static uint32_t wave_rows(const Win &t, const SmaxScanArgs &a, uint32_t wave_rank0,
-                                     uint64_t gw, uint32_t wrow0, const uint8_t *sL,
-                                     GtSmaxRecord *wdst) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t m = a.minlen;
-  uint32_t wcount = 0;
-  uint32_t r255 = wave_rank0;
-  uint32_t carry;
-  {
-    const uint32_t b = sL[wrow0 - 1];
-    carry = b < 255 ? b : llv_by_rank(t, r255 - 1);
-  }
-  bool open = false;
-  uint64_t open_c = 0;
-  uint32_t open_v = 0;
-  for (int j = 0; j < SMAX_WAVE_BYTES / 64; j++) {
-    const uint32_t b = sL[wrow0 + j * 64 + lane];
-    const uint64_t hot = __ballot(b >= m || b == 255);
-    if (!hot && !open) {               // no byte reaches minlen, nothing open
-      carry = __shfl(b, 63, 64);
-      continue;
-    }
-    const bool is255 = b == 255;
-    const uint64_t m255 = __ballot(is255);
-    uint32_t v = b;
-    if (m255) {
-      if (is255) v = llv_by_rank(t, r255 + (uint32_t) __popcll(m255 & lanemask_lt()));
-      r255 += (uint32_t) __popcll(m255);
-    }
-    uint32_t vprev = __shfl_up(v, 1, 64);
-    if (lane == 0) vprev = carry;
-    carry = __shfl(v, 63, 64);
-    const uint64_t chg = __ballot(v != vprev);
-    const uint64_t g = gw + (uint64_t) j * 64 + lane;
-    // a plateau opened in an earlier chunk ends at this chunk's first change
-    if (open && chg) {
-      const int e = __builtin_ctzll(chg);
-      const uint32_t ve = __shfl(v, e, 64);
-      int ok = 0;
-      if (lane == 0 && ve < open_v) {
-        const uint64_t rb = gw + (uint64_t) j * 64 + e - 1;
-        if (diverse_rows(t, open_c - 1, rb)) {
-          GtSmaxRecord rec;
-          rec.lb = open_c - 1;
-          rec.lcp = open_v;
-          rec.width = (uint32_t) (rb - open_c + 2);
-          wdst[wcount] = rec;
-          ok = 1;
-        }
-      }
-      wcount += (uint32_t) __shfl(ok, 0, 64);
-      open = false;
-    }
-    const bool up = v > vprev && v >= m && g >= a.begin;
-    if (__ballot(up) == 0) continue;
-    const uint64_t above = chg & ~((2ull << lane) - 1);   // change points after this row
-    const int e = above ? __builtin_ctzll(above) : 0;
-    const uint32_t ve = __shfl(v, e, 64);
-    const bool lmax = up && above != 0 && ve < v;
-    const uint64_t to_open = __ballot(up && above == 0);  // at most the last up row
-    if (to_open) {
-      const int ol = 63 - __builtin_clzll(to_open);
-      open = true;
-      open_c = gw + (uint64_t) j * 64 + ol;
-      open_v = __shfl(v, ol, 64);
-    }
-    bool acc = false;
-    if (lmax) acc = diverse_rows(t, g - 1, g + (uint64_t) (e - lane) - 1);
-    const uint64_t accm = __ballot(acc);
-    if (acc) {
-      GtSmaxRecord rec;
-      rec.lb = g - 1;
-      rec.lcp = v;
-      rec.width = (uint32_t) (e - lane + 1);
-      wdst[wcount + (uint32_t) __popcll(accm & lanemask_lt())] = rec;
-    }
-    wcount += (uint32_t) __popcll(accm);
-  }
-  if (open) {
-    uint32_t wc = wcount;
-    if (lane == 0) finish_open(t, a, open_c, open_v, wdst, &wc);
-    wcount = __shfl(wc, 0, 64);
-  }
-  return wcount;
-}
-
-// Per-lane path for the shard's edge tiles (rows >= end or N, row 0, the
-// pending plateau): the lane's 4 segments of 16 rows, exact per-row logic.
-__device__ static uint32_t edge_rows(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                     const uint8_t *sL, GtSmaxRecord *wdst) {
+// Per-lane detection over the lane's 4 segments of 16 rows: the SWAR fast
+// path in interior tiles, exact per-row logic in the shard's edge tiles (rows
+// >= end or N, row 0, the pending plateau); then left-diversity, the wave's
+// row-order offsets and the record writes.
+__device__ static uint32_t lane_rows(const Win &t, const SmaxScanArgs &a, uint64_t g0,
+                                     const uint8_t *sL, GtSmaxRecord *wdst, bool interior,
+                                     uint32_t segpre) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   uint64_t cand = 0;
   bool pend_here = false;
   uint64_t pend_c = 0;
   uint32_t pend_l = 0;
-#pragma unroll
+#pragma unroll 1
   for (int r = 0; r < SMAX_SEGS; r++) {
     const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
     const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-    segment_candidates(t, a, sg, *reinterpret_cast<const uint4 *>(&sL[so]), r, cand,
-                       pend_here, pend_c, pend_l);
+    if (interior) {
+      if (!((segpre >> r) & 1u)) continue;
+      const uint32_t own = sg >= a.begin ? 0xffffu
+                         : (sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu);
+      uint32_t slow;
+      const uint32_t c16 = segment_fast(t, a, sg, so, sL, own, mf, &slow);
+      cand |= (uint64_t) c16 << (16 * r);
+      while (slow) {                     // plateau runs past the 20-row window
+        const int q = __builtin_ctz(slow);
+        slow &= slow - 1;
+        const uint64_t c = sg + q;
+        const uint32_t cur = lcp_exact(t, c);
+        int rel;
+        bool pend;
+        (void) plateau_end(t, c, cur, &rel, &pend);
+        if (pend) { pend_here = true; pend_c = c; pend_l = cur; }
+        else if (rel < 0) cand |= 1ull << (r * 16 + q);
+      }
+    } else {
+      segment_candidates(t, a, sg, *reinterpret_cast<const uint4 *>(&sL[so]), r, cand,
+                         pend_here, pend_c, pend_l);
+    }
   }
   uint64_t tmp = cand;
   while (tmp) {
@@ -692,8 +653,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     // ---- stage the prefetched tile, filter
     __syncthreads();               // LDS free (previous tile done), sFlags reset
     store_tile(sL, sB, R);
-    const uint32_t segpre = seg_ge(R.l0, mf) | seg_ge(R.l1, mf) | seg_ge(R.l2, mf) |
-                            seg_ge(R.l3, mf);
+    const uint32_t segpre_bits = (seg_ge(R.l0, mf) ? 1u : 0u) | (seg_ge(R.l1, mf) ? 2u : 0u) |
+                                 (seg_ge(R.l2, mf) ? 4u : 0u) | (seg_ge(R.l3, mf) ? 8u : 0u);
+    const uint32_t segpre = segpre_bits;
     const uint32_t f0 = seg_ffcount(R.l0), f1 = seg_ffcount(R.l1), f2 = seg_ffcount(R.l2),
                    f3 = seg_ffcount(R.l3);
     const uint32_t hff = tid < 5 ? seg_ffcount(R.h) : 0u;
@@ -749,13 +711,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     uint32_t wcount = 0;
     if (wave_pre) {
       const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-      if (!edge) {
-        const uint32_t wrow0 = SMAX_LH + wave * SMAX_WAVE_BYTES;
-        const uint32_t rank0 = t.rank ? t.rank[1 + wave * 256] : 0u;
-        wcount = wave_rows(t, a, rank0, g0 + wave * SMAX_WAVE_BYTES, wrow0, sL, wdst);
-      } else {
-        wcount = edge_rows(t, a, g0, sL, wdst);
-      }
+      wcount = lane_rows(t, a, g0, sL, wdst, !edge, segpre_bits);
     }
     if (lane == 0) a.tile_count[tile * 4 + wave] = wcount;
 
