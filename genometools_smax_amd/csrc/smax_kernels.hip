@@ -51,7 +51,8 @@
 #define SMAX_RH 64                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
-#define SMAX_LLV_CAP 1024                             // .llv values in LDS
+#define SMAX_LLV_CAP 512                              // .llv values in LDS
+#define SMAX_LIST 256                                 // per-wave start-list window
 #define SMAX_WSLOT 2048                               // records per (tile, wave) slot
 
 static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
@@ -71,8 +72,7 @@ struct SmaxScanArgs {
   uint64_t tile_first;       // first local tile holding an owned row
   uint32_t minlen;
   uint32_t num_tiles;
-  GtSmaxRecord *slots;       // [tile][wave][segment][lane][8] records
-  uint8_t *sub_count;        // [tile][wave][segment][lane] record counts
+  GtSmaxRecord *slots;       // [tile][wave][SMAX_WSLOT] records, row order
   uint32_t *tile_count;      // [tile][wave] record counts
   GtSmaxBoundary *bnd;
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
@@ -345,42 +345,6 @@ __device__ __forceinline__ uint32_t seg_ffcount(const uint4 v) {
          __popc(bytes_ff(v.w));
 }
 
-// Candidate detection for one 16-row segment read from LDS (rows sg..sg+15).
-__device__ __forceinline__ void segment_candidates(const Win &t, const SmaxScanArgs &a,
-                                                   uint64_t sg, const uint4 v, int r,
-                                                   uint64_t &cand, bool &pend_here,
-                                                   uint64_t &pend_c, uint32_t &pend_l) {
-  const uint32_t m = a.minlen;
-  const uint64_t lo8 = (uint64_t) v.x | ((uint64_t) v.y << 32);
-  const uint64_t hi8 = (uint64_t) v.z | ((uint64_t) v.w << 32);
-  uint32_t prevb = lcp_byte(t, sg - 1);
-  for (int q = 0; q < 16; q++) {
-    const uint64_t c = sg + q;
-    uint32_t cb = (uint32_t) (((q < 8) ? (lo8 >> (8 * q)) : (hi8 >> (8 * (q - 8)))) & 0xffu);
-    if (c >= a.N || c == 0) cb = 0;
-    const uint32_t pb = prevb;
-    prevb = cb;
-    if (cb < m && cb != 255) continue;
-    if (c < a.begin || c >= a.end) continue;
-    uint32_t cur;
-    if (cb != 255) {
-      if (cb <= pb) continue;                  // pb < 255 here
-      cur = cb;
-    } else {
-      cur = lcp_big(t, c);
-      if (cur < m) continue;
-      if (pb == 255 && lcp_big(t, c - 1) >= cur) continue;
-    }
-    int rel;
-    bool pend;
-    (void) plateau_end(t, c, cur, &rel, &pend);
-    if (pend) {
-      pend_here = true; pend_c = c; pend_l = cur;
-    } else if (rel < 0) {
-      cand |= 1ull << (r * 16 + q);
-    }
-  }
-}
 
 // SWAR byte compares: high bit of each byte where the relation holds.
 __device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t y) {
@@ -415,176 +379,155 @@ __device__ __forceinline__ bool diverse_rows(const Win &t, uint64_t lo, uint64_t
   return true;
 }
 
-// byte k (-1..19) of a 21-byte register window: pb = row -1, lo = rows 0..7,
-// hi = rows 8..15, x = rows 16..19
-__device__ __forceinline__ uint32_t win_byte(uint32_t pb, uint64_t lo, uint64_t hi, uint32_t x,
-                                             int k) {
-  if (k < 0) return pb;
-  if (k < 8) return (uint32_t) (lo >> (8 * k)) & 0xffu;
-  if (k < 16) return (uint32_t) (hi >> (8 * (k - 8))) & 0xffu;
-  return (x >> (8 * (k - 16))) & 0xffu;
-}
-
-// Emit one record into the segment's sub-slot (at most 8 per 16 rows).
-__device__ __forceinline__ void emit(GtSmaxRecord *sub, uint32_t &k, uint64_t lb, uint32_t lcp,
-                                     uint32_t width) {
-  GtSmaxRecord rec;
-  rec.lb = lb;
-  rec.lcp = lcp;
-  rec.width = width;
-  sub[k++] = rec;
-}
-
-// Interior-tile segment (16 rows sg..sg+15), SWAR over the rows' LCP bytes in
-// registers: rows sg..sg+19 (16 own rows + 4 look-ahead rows) and row sg-1.
-// Masks (bit q = row sg+q):
-//   GE  byte >= min(minlen,128)       UP  LCP[q] > LCP[q-1]
-//   EQN LCP[q+1] == LCP[q]            LTN LCP[q+1] < LCP[q]
-// Byte compares are exact except between two 255 bytes; those (rare) pairs
-// are fixed up with exact .llv values.  A start q ends its plateau at the
-// first row e >= q with EQN clear; it is a local maximum iff LTN bit e; the
-// BWT bytes of rows q-1..e (registers too) decide left-diversity, and the
-// record goes straight to the segment's sub-slot, in row order.  Plateaus
-// reaching row 19 are resolved exactly (plateau_end / diverse_rows).
-__device__ __forceinline__ uint32_t segment_fast(const Win &t, const SmaxScanArgs &a,
-                                                 uint64_t sg, uint32_t so, const uint8_t *sL,
-                                                 const uint8_t *sB, uint32_t ownmask,
-                                                 uint32_t mf, GtSmaxRecord *sub,
-                                                 bool &pend_here, uint64_t &pend_c,
-                                                 uint32_t &pend_l) {
+// Plateau-start mask of one interior 16-row segment (rows sg..sg+15), SWAR
+// over the LCP bytes of rows sg-1..sg+15 from LDS: bit q set iff
+// LCP[q] >= min(minlen,128) (exact for minlen <= 128) and LCP[q] > LCP[q-1].
+// Byte compares are exact except between two 255 bytes; those pairs are
+// fixed up with exact .llv values.
+__device__ __forceinline__ uint32_t segment_starts_fast(const Win &t, uint64_t sg, uint32_t so,
+                                                        const uint8_t *sL, uint32_t mf) {
   const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
-  const uint32_t x = *reinterpret_cast<const uint32_t *>(&sL[so + 16]);
   const uint32_t prevb = sL[so - 1];
-  const uint32_t w[5] = {v.x, v.y, v.z, v.w, x};
-  uint32_t GE = 0, UP = 0, EQN = 0, LTN = 0, FF = 0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t GE = 0, UP = 0, FF = 0;
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
+  for (int k = 0; k < 4; k++) {
     const uint32_t cur = w[k];
     const uint32_t prv = k == 0 ? ((cur << 8) | prevb) : __builtin_amdgcn_alignbyte(cur, w[k - 1], 3);
-    const uint32_t nxt = k == 4 ? (cur >> 8) : __builtin_amdgcn_alignbyte(w[k + 1], cur, 1);
     GE |= pack4(bytes_ge(cur, mf)) << (4 * k);
     UP |= pack4(bytes_lt(prv, cur)) << (4 * k);
-    EQN |= pack4(bytes_eq(nxt, cur)) << (4 * k);
-    LTN |= pack4(bytes_lt(nxt, cur)) << (4 * k);
     FF |= pack4(bytes_ff(cur)) << (4 * k);
   }
-  EQN &= 0x7ffffu;                       // row 19's successor is unknown
-  const bool pff = prevb == 255u;
-  if (FF | (pff ? 1u : 0u)) {
-    // exact compares where both bytes are 255
-    uint32_t fu = FF & ((FF << 1) | (pff ? 1u : 0u)) & 0xffffu;
-    uint32_t fn = FF & (FF >> 1) & 0x7ffffu;
-    while (fu) {
-      const int q = __builtin_ctz(fu);
-      fu &= fu - 1;
-      const uint32_t c = lcp_big(t, sg + q), p = lcp_big(t, sg + q - 1);
-      UP = (UP & ~(1u << q)) | ((c > p ? 1u : 0u) << q);
-    }
-    while (fn) {
-      const int q = __builtin_ctz(fn);
-      fn &= fn - 1;
-      const uint32_t c = lcp_big(t, sg + q), n = lcp_big(t, sg + q + 1);
-      EQN = (EQN & ~(1u << q)) | ((c == n ? 1u : 0u) << q);
-      LTN = (LTN & ~(1u << q)) | ((n < c ? 1u : 0u) << q);
-    }
+  uint32_t st = GE & UP;
+  // exact compares where both bytes are 255 (only matters for candidate rows)
+  uint32_t fu = FF & ((FF << 1) | (prevb == 255u ? 1u : 0u)) & GE;
+  while (fu) {
+    const int q = __builtin_ctz(fu);
+    fu &= fu - 1;
+    const uint32_t c = lcp_big(t, sg + q), p = lcp_big(t, sg + q - 1);
+    st = (st & ~(1u << q)) | ((c > p ? 1u : 0u) << q);
   }
-  uint32_t starts = GE & UP & ownmask;
-  if (starts == 0) return 0;
-  const uint64_t lo = (uint64_t) v.x | ((uint64_t) v.y << 32);
-  const uint64_t hi = (uint64_t) v.z | ((uint64_t) v.w << 32);
-  // BWT bytes of rows -1..19, loaded once the segment has a start
-  const uint4 bv = *reinterpret_cast<const uint4 *>(&sB[so]);
-  const uint32_t bx = *reinterpret_cast<const uint32_t *>(&sB[so + 16]);
-  const uint32_t bpb = sB[so - 1];
-  const uint64_t blo = (uint64_t) bv.x | ((uint64_t) bv.y << 32);
-  const uint64_t bhi = (uint64_t) bv.z | ((uint64_t) bv.w << 32);
-  uint32_t k = 0;
-  while (starts) {
-    const int q = __builtin_ctz(starts);
-    starts &= starts - 1;
-    const uint32_t cb = win_byte(prevb, lo, hi, x, q);
-    const uint32_t cur = cb < 255 ? cb : lcp_big(t, sg + q);
-    if (cur < a.minlen) continue;        // only when minlen > 128 (superset filter)
-    const int e = q + __builtin_ctz(~EQN >> q);
-    if (e >= 19) {                       // plateau runs past the window: exact
-      int rel;
-      bool pend;
-      const uint64_t j = plateau_end(t, sg + q, cur, &rel, &pend);
-      if (pend) { pend_here = true; pend_c = sg + q; pend_l = cur; }
-      else if (rel < 0 && diverse_rows(t, sg + q - 1, j))
-        emit(sub, k, sg + q - 1, cur, (uint32_t) (j - (sg + q) + 2));
-      continue;
-    }
-    if (!((LTN >> e) & 1u)) continue;    // a child interval follows: not leaf-only
-    Seen sn = {0, 0, 0, 0};
-    bool dup = false;
-    for (int r = q - 1; r <= e && !dup; r++) dup = seen_add(sn, win_byte(bpb, blo, bhi, bx, r));
-    if (!dup) emit(sub, k, sg + q - 1, cur, (uint32_t) (e - q + 2));
-  }
-  return k;
+  return st;
 }
 
-// Per-lane detection over the lane's 4 segments of 16 rows, records written
-// straight into the segment's sub-slot (8 records per 16 rows, the most a
-// segment can hold) -- row order is (segment, lane, row) within the wave, the
-// order K3 compacts in.  Interior tiles use the SWAR path; the shard's edge
-// tiles (rows >= end or N, row 0, the pending plateau) the exact per-row one.
-__device__ static uint32_t lane_rows(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                     const uint8_t *sL, const uint8_t *sB, GtSmaxRecord *wdst,
-                                     uint8_t *wcnt, bool interior, uint32_t segpre) {
+// Exact plateau-start mask of one edge-tile segment (rows >= end or N, row
+// 0, rows before begin): bit q iff begin <= c < end, LCP[c] >= minlen and
+// LCP[c] > LCP[c-1].
+__device__ __forceinline__ uint32_t segment_starts_exact(const Win &t, const SmaxScanArgs &a,
+                                                         uint64_t sg) {
+  uint32_t st = 0;
+  uint32_t prev = lcp_exact(t, sg - 1);
+  for (int q = 0; q < 16; q++) {
+    const uint64_t c = sg + q;
+    const uint32_t cur = lcp_exact(t, c);
+    if (c >= a.begin && c < a.end && cur >= a.minlen && cur > prev) st |= 1u << q;
+    prev = cur;
+  }
+  return st;
+}
+
+// Detection for one wave's 4096 rows, per segment round r (the 64 lanes'
+// segments r, rows lane-major = row order):
+//   1. each lane's 16-bit plateau-start mask (SWAR in interior tiles, exact
+//      per row in the shard's edge tiles);
+//   2. the wave compacts the starts, in row order, into an LDS list;
+//   3. the list is evaluated 64 starts per step, one per lane: exact plateau
+//      end in LDS, local-maximum test, left-diversity over BWT[lb..rb], the
+//      pending plateau at the shard end; accepted records are written in row
+//      order to the wave's slot (ballot prefix).
+// No lane loops over another lane's work: the per-start cost is spread over
+// all 64 lanes instead of serialising the wave on its busiest lane.
+__device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint64_t g0,
+                                       const uint8_t *sL, uint16_t *list, GtSmaxRecord *wdst,
+                                       bool interior, uint32_t segpre) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
-  bool pend_here = false;
-  uint64_t pend_c = 0;
-  uint32_t pend_l = 0;
-  uint32_t total = 0;
+  const uint64_t gw = g0 + wave * SMAX_WAVE_BYTES;
+  uint32_t wcount = 0;
 #pragma unroll 1
   for (int r = 0; r < SMAX_SEGS; r++) {
     const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-    const uint64_t sg = g0 + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
-    GtSmaxRecord *sub = wdst + (r * 64 + lane) * 8;
-    uint32_t k = 0;
+    const uint64_t sg = gw + r * 1024 + lane * 16;
+    uint32_t st = 0;
     if (interior) {
       if ((segpre >> r) & 1u) {
-        const uint32_t own = sg >= a.begin ? 0xffffu
-                           : (sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu);
-        k = segment_fast(t, a, sg, so, sL, sB, own, mf, sub, pend_here, pend_c, pend_l);
+        st = segment_starts_fast(t, sg, so, sL, mf);
+        if (sg < a.begin)
+          st &= sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
       }
     } else {
-      uint64_t cand = 0;
-      segment_candidates(t, a, sg, *reinterpret_cast<const uint4 *>(&sL[so]), 0, cand,
-                         pend_here, pend_c, pend_l);
-      while (cand) {
-        const int q = __builtin_ctzll(cand);
-        cand &= cand - 1;
-        const uint64_t c = sg + q;
-        const uint32_t cur = lcp_exact(t, c);
-        int rel;
-        bool pend;
-        const uint64_t j = plateau_end(t, c, cur, &rel, &pend);
-        if (diverse_rows(t, c - 1, j)) emit(sub, k, c - 1, cur, (uint32_t) (j - c + 2));
-      }
+      st = segment_starts_exact(t, a, sg);
     }
-    wcnt[r * 64 + lane] = (uint8_t) k;
-    total += k;
-  }
-  if (pend_here) {
-    Seen s = {0, 0, 0, 0};
-    bool dup = false;
-    for (uint64_t g = pend_c - 1; g < a.end && !dup; g++) dup = seen_add(s, bwt_at(t, g));
-    if (!dup) {
-      GtSmaxBoundary *b = a.bnd;
-      b->pend_c = pend_c;
-      b->pend_lcp = pend_l;
-      b->pend_div.seen[0] = s.w0; b->pend_div.seen[1] = s.w1;
-      b->pend_div.seen[2] = s.w2; b->pend_div.seen[3] = s.w3;
-      b->pend_div.dup = 0;
-      b->pend_valid = 1;
-    }
-  }
+    // compact the starts into the list (row order)
+    const uint32_t c = (uint32_t) __popc(st);
+    uint32_t incl = c;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
-  return total;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    const uint32_t nstart = __shfl(incl, 63, 64);
+    if (nstart == 0) continue;
+    const uint32_t rowbase = r * 1024 + lane * 16;     // row offset inside the wave
+    // windows of SMAX_LIST starts (a ramp can make every row a start)
+    for (uint32_t w0 = 0; w0 < nstart; w0 += SMAX_LIST) {
+      uint32_t pos = incl - c;
+      uint32_t bits = st;
+      while (bits) {
+        const int q = __builtin_ctz(bits);
+        bits &= bits - 1;
+        if (pos >= w0 && pos < w0 + SMAX_LIST) list[pos - w0] = (uint16_t) (rowbase + q);
+        pos++;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t nwin = nstart - w0 < SMAX_LIST ? nstart - w0 : SMAX_LIST;
+      // evaluate 64 starts per step
+      for (uint32_t i0 = 0; i0 < nwin; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        bool acc = false;
+        uint64_t cc = 0;
+        uint32_t cur = 0;
+        uint64_t j = 0;
+        if (i < nwin) {
+          cc = gw + list[i];
+          cur = lcp_exact(t, cc);
+          if (cur >= a.minlen) {
+            int rel;
+            bool pend;
+            j = plateau_end(t, cc, cur, &rel, &pend);
+            if (pend) {
+              Seen sn = {0, 0, 0, 0};
+              bool dup = false;
+              for (uint64_t g = cc - 1; g < a.end && !dup; g++) dup = seen_add(sn, bwt_at(t, g));
+              if (!dup) {
+                GtSmaxBoundary *b = a.bnd;
+                b->pend_c = cc;
+                b->pend_lcp = cur;
+                b->pend_div.seen[0] = sn.w0; b->pend_div.seen[1] = sn.w1;
+                b->pend_div.seen[2] = sn.w2; b->pend_div.seen[3] = sn.w3;
+                b->pend_div.dup = 0;
+                b->pend_valid = 1;
+              }
+            } else if (rel < 0) {
+              acc = diverse_rows(t, cc - 1, j);
+            }
+          }
+        }
+        const uint64_t am = __ballot(acc);
+        if (acc) {
+          GtSmaxRecord rec;
+          rec.lb = cc - 1;
+          rec.lcp = cur;
+          rec.width = (uint32_t) (j - cc + 2);
+          wdst[wcount + (uint32_t) __popcll(am & lanemask_lt())] = rec;
+        }
+        wcount += (uint32_t) __popcll(am);
+      }
+      __builtin_amdgcn_wave_barrier();   // list reused by the next window
+    }
+  }
+  return wcount;
 }
 
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
@@ -596,6 +539,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ uint32_t sHalo[5];
   __shared__ uint32_t sFlags;
   __shared__ uint32_t sLlvBase;
+  __shared__ uint16_t sList[SMAX_THREADS / 64][SMAX_LIST];   // per-wave start lists
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -680,18 +624,13 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
       __syncthreads();
     }
 
-    // ---- detection, diversity, records (per (segment, lane) sub-slots)
+    // ---- detection, diversity, records (per wave, row order)
     const uint64_t slot = tile * 4 + wave;
     GtSmaxRecord *wdst = a.slots + slot * (uint64_t) SMAX_WSLOT;
-    uint8_t *wcnt = a.sub_count + slot * 256;
     uint32_t wcount = 0;
-    if (wave_pre) {
-      const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-      wcount = lane_rows(t, a, g0, sL, sB, wdst, wcnt, !edge, segpre_bits);
-    } else {
-#pragma unroll
-      for (int r = 0; r < SMAX_SEGS; r++) wcnt[r * 64 + lane] = 0;
-    }
+    const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
+    if (wave_pre || edge)
+      wcount = wave_detect(t, a, g0, sL, sList[wave], wdst, !edge, segpre_bits);
     if (lane == 0) a.tile_count[slot] = wcount;
 
     if (tid == 0) sFlags = 0;
@@ -711,40 +650,23 @@ __global__ void __launch_bounds__(SMAX_THREADS) smax_scan_kernel_w3(SmaxScanArgs
 
 // ------------------------------------------------------------ K3: compact
 
-// One wave per (tile, wave) slot, grid-stride: the slot's 256 sub-slots
-// (segment-major, then lane = row order) are prefix-summed in the wave and
-// copied to their final position (exclusive scan of the slot totals) ->
+// One wave per (tile, wave) slot, grid-stride: copy the slot's records (row
+// order) to their final position (exclusive scan of the slot counts) ->
 // ascending lb overall.  Also publishes the total.
 __global__ void __launch_bounds__(256)
-smax_compact_kernel(const GtSmaxRecord *slots, const uint8_t *sub_count,
-                    const uint32_t *slot_count, const uint64_t *slot_off, uint64_t nslots,
-                    GtSmaxRecord *out, uint64_t capacity, uint64_t *count) {
+smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
+                    const uint64_t *slot_off, uint64_t nslots, GtSmaxRecord *out,
+                    uint64_t capacity, uint64_t *count) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (blockIdx.x * (uint64_t) blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t) gridDim.x * blockDim.x) >> 6;
   for (uint64_t sl = wave; sl < nslots; sl += nwaves) {
-    const uint32_t tot = slot_count[sl];
+    const uint32_t cnt = slot_count[sl];
     const uint64_t off = slot_off[sl];
-    if (sl == nslots - 1 && lane == 0) *count = off + tot;
-    if (tot == 0) continue;
-    const uint8_t *cnt = sub_count + sl * 256;
+    if (sl == nslots - 1 && lane == 0) *count = off + cnt;
     const GtSmaxRecord *src = slots + sl * (uint64_t) SMAX_WSLOT;
-    uint32_t base = 0;
-#pragma unroll
-    for (int r = 0; r < SMAX_SEGS; r++) {
-      const uint32_t c = cnt[r * 64 + lane];
-      uint32_t incl = c;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += o;
-      }
-      const uint64_t o0 = off + base + incl - c;
-      const GtSmaxRecord *sub = src + (r * 64 + lane) * 8;
-      for (uint32_t i = 0; i < c; i++)
-        if (o0 + i < capacity) out[o0 + i] = sub[i];
-      base += __shfl(incl, 63, 64);
-    }
+    for (uint32_t i = lane; i < cnt; i += 64)
+      if (off + i < capacity) out[off + i] = src[i];
   }
 }
 
@@ -844,7 +766,6 @@ struct GtSmaxPlan {
   uint32_t grid, compact_grid;
   GtSmaxRecord *out;         // capacity records, ascending lb
   GtSmaxRecord *slots;       // num_tiles * 4 * SMAX_WSLOT
-  uint8_t *sub_count;        // num_tiles * 4 * 256
   uint32_t *tile_count;      // num_tiles * 4
   uint64_t *tile_off;        // num_tiles * 4
   uint64_t *count;
@@ -950,7 +871,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * 4 * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * 4 * (uint64_t) p->num_tiles));
-  HIPCHK(hipMalloc(&p->sub_count, 256 * 4 * (uint64_t) p->num_tiles));
+
   HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * 4 * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
@@ -992,7 +913,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->sub_count, p->tile_count, p->tile_off, p->count, p->bnd,
+  void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
                   p->llv_lo, p->err, p->scan_tmp};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
@@ -1018,7 +939,6 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.minlen = p->minlen;
   a.num_tiles = p->num_tiles;
   a.slots = p->slots;
-  a.sub_count = p->sub_count;
   a.tile_count = p->tile_count;
   a.bnd = p->bnd;
   a.dbg = p->dbg;
@@ -1051,8 +971,8 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
                                    (uint64_t) 0, (size_t) p->num_tiles * 4,
                                    rocprim::plus<uint64_t>(), s));
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->slots, p->sub_count, p->tile_count, p->tile_off,
-                       (uint64_t) p->num_tiles * 4, p->out, p->capacity, p->count);
+                       p->slots, p->tile_count, p->tile_off, (uint64_t) p->num_tiles * 4,
+                       p->out, p->capacity, p->count);
     HIPCHK(hipGetLastError());
   }
   p->runs++;
