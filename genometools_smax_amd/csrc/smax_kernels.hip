@@ -44,14 +44,14 @@
 #include "gt_smax_hip.h"
 
 #define SMAX_THREADS 256
-#define SMAX_SEGS 4                                   // uint4 per thread
+#define SMAX_SEGS 2                                   // 16-row segments per lane
 #define SMAX_WAVE_BYTES (SMAX_SEGS * 64 * 16)         // 4096 rows per wave
 #define SMAX_TILE (SMAX_THREADS * SMAX_SEGS * 16)     // 16384 rows per tile
 #define SMAX_LH 16                                    // left halo (bytes)
 #define SMAX_RH 64                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
-#define SMAX_LLV_CAP 512                              // .llv values in LDS
+#define SMAX_LLV_CAP SMAX_THREADS                     // .llv values in LDS (1 per lane)
 #define SMAX_LIST 256                                 // per-wave start-list window
 #define SMAX_WSLOT 2048                               // records per (tile, wave) slot
 
@@ -65,7 +65,7 @@ struct SmaxScanArgs {
   const uint8_t *bwt;
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
   uint64_t numllv;
-  const uint32_t *llv_lo;    // per tile: first llv index >= tile_g0 - LH
+  const uint2 *llv_win;      // per tile: {first llv index >= g0 - LH, entries in the window}
   uint64_t base, begin, end, N;
   uint64_t local_len;        // readable: [-PAD_FRONT, local_len + PAD_BACK)
   uint32_t *err;             // sticky error bits (bounds), read by the host
@@ -83,20 +83,44 @@ struct SmaxScanArgs {
 #define SMAX_ERR_LLV 1u        // a 255 byte without its .llv entry
 #define SMAX_ERR_RANGE 2u      // a table read outside the shard's rows
 
+// Rare-path global loads of the scan kernels, each with its own wait inside
+// one asm statement: hipcc sees no outstanding load, so it never places a
+// vmcnt(0) on the common path (which would also drain K1's in-flight DMA of
+// the next window); the wait is paid only when the load executes.
+__device__ __forceinline__ uint32_t gld_u8(const void *p) {
+  uint32_t v;
+  asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t gld_u32(const void *p) {
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint64_t gld_u64(const void *p) {
+  uint64_t v;
+  asm volatile("global_load_dwordx2 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+  return v;
+}
+// low dword of an .llv record's value (values < 2^32 are checked at plan time)
+__device__ __forceinline__ uint32_t llv_value(const GtSmaxLlv *e) {
+  return gld_u32(reinterpret_cast<const uint8_t *>(e) + 8);
+}
+
 // exact LCP value from the global .llv (binary search in [lo, hi))
 __device__ static uint32_t llv_search_global(const GtSmaxLlv *llv, uint64_t lo,
                                              uint64_t hi, uint64_t g, uint32_t *err) {
   const uint64_t stop = hi;
   while (lo < hi) {
     uint64_t mid = (lo + hi) >> 1;
-    uint64_t p = llv[mid].position;
+    uint64_t p = gld_u64(&llv[mid].position);
     if (p < g) lo = mid + 1; else hi = mid;
   }
-  if (lo >= stop || llv[lo].position != g) {   // never for a consistent index
+  if (lo >= stop || gld_u64(&llv[lo].position) != g) {   // never for a consistent index
     atomicOr(err, SMAX_ERR_LLV);
     return 255;
   }
-  return (uint32_t) llv[lo].value;
+  return llv_value(&llv[lo]);
 }
 
 // high bit of each byte of w that is >= m (1 <= m <= 128); exact
@@ -150,7 +174,7 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
     const uint32_t r = t.rank[chunk] + (uint32_t) cnt;
     if ((int) r < t.nval) return t.val[r];
     if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
-    return (uint32_t) t.llv[t.llv_base + r].value;
+    return llv_value(&t.llv[t.llv_base + r]);
   }
   return llv_search_global(t.llv, 0, t.numllv, g, t.err);
 }
@@ -161,7 +185,7 @@ __device__ __forceinline__ uint32_t lcp_byte(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
   if (t.L != nullptr && o >= 0 && o < SMAX_LDSB) return t.L[o];
   if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 0; }
-  return t.glcp[g - t.base];
+  return gld_u8(&t.glcp[g - t.base]);
 }
 
 __device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
@@ -173,7 +197,7 @@ __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
   if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
-  return t.gbwt[g - t.base];
+  return gld_u8(&t.gbwt[g - t.base]);
 }
 
 // Plateau scan from start c with exact value l: returns j (last row of the
@@ -216,28 +240,24 @@ __device__ __forceinline__ bool seen_add(Seen &s, uint32_t c) {
 // block (a wave's rows are segment-major, then lane): per-segment offsets
 // inside the wave, the wave's offset inside the block, the block total.
 __device__ __forceinline__ void block_scan_rows(const uint32_t c0, const uint32_t c1,
-                                                const uint32_t c2, const uint32_t c3,
                                                 uint32_t *o0, uint32_t *o1,
-                                                uint32_t *o2, uint32_t *o3,
                                                 uint32_t *wave_off, uint32_t *total,
                                                 uint32_t *sWave) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t wt = 0;
-  const uint32_t cs[4] = {c0, c1, c2, c3};
-  uint32_t os[4];
+  const uint64_t ltm = (1ull << lane) - 1;
+  uint32_t e0 = 0, t0 = 0, e1 = 0, t1 = 0;
+  // counts <= 16 per lane and segment: prefix over bit planes
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-    uint32_t incl = cs[r];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
-    }
-    os[r] = wt + incl - cs[r];
-    wt += __shfl(incl, 63, 64);
+  for (int b = 0; b < 5; b++) {
+    const uint64_t p0 = __ballot((c0 >> b) & 1u), p1 = __ballot((c1 >> b) & 1u);
+    e0 += (uint32_t) __popcll(p0 & ltm) << b;
+    t0 += (uint32_t) __popcll(p0) << b;
+    e1 += (uint32_t) __popcll(p1 & ltm) << b;
+    t1 += (uint32_t) __popcll(p1) << b;
   }
-  *o0 = os[0]; *o1 = os[1]; *o2 = os[2]; *o3 = os[3];
-  __syncthreads();                 // sWave free (previous users done)
+  *o0 = e0;
+  *o1 = t0 + e1;
+  const uint32_t wt = t0 + t1;
   if (lane == 0) sWave[wave] = wt;
   __syncthreads();
   uint32_t wo = 0, tot = 0;
@@ -291,50 +311,63 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
 
 // ------------------------------------------------------------ K1: scan
 
-// Tile registers: 4 x 16 B per lane of LCP and of BWT; halo chunks go to
-// threads 0..4 (LCP: 16 B left, 64 B right) and 5..9 (BWT).  Named fields,
-// no arrays: keeps the prefetch in VGPRs (arrays written under a condition
-// were demoted to scratch by hipcc).
-struct TileRegs {
-  uint4 l0, l1, l2, l3, b0, b1, b2, b3, h;
+// LDS-DMA (global_load_lds): global -> LDS with no VGPR destination, lane
+// i writing lds_base + i * size.  Issued from inline asm so that hipcc
+// neither counts it nor drains it at __syncthreads(): the next tile's window
+// stays in flight across the current tile's barriers, and the kernel waits
+// for it itself (s_waitcnt vmcnt(0) before the barrier that publishes it).
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) void *) p;
+}
+__device__ __forceinline__ void glds16(const void *g, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
+}
+__device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One tile's LDS window: LCP and BWT bytes of rows [g0 - LH, g0 + TILE + RH)
+// and the window's .llv values (rank order, first SMAX_LLV_CAP of them).
+struct SmaxWindow {
+  uint8_t L[SMAX_LDSB];
+  uint8_t B[SMAX_LDSB];
+  uint32_t val[SMAX_LLV_CAP];
 };
 
-__device__ __forceinline__ void load_tile(const uint8_t *lcp, const uint8_t *bwt,
-                                          uint64_t l0, TileRegs &R) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint8_t *ls = lcp + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
-  const uint8_t *bs = bwt + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
-  R.l0 = *reinterpret_cast<const uint4 *>(ls);
-  R.l1 = *reinterpret_cast<const uint4 *>(ls + 1024);
-  R.l2 = *reinterpret_cast<const uint4 *>(ls + 2048);
-  R.l3 = *reinterpret_cast<const uint4 *>(ls + 3072);
-  R.b0 = *reinterpret_cast<const uint4 *>(bs);
-  R.b1 = *reinterpret_cast<const uint4 *>(bs + 1024);
-  R.b2 = *reinterpret_cast<const uint4 *>(bs + 2048);
-  R.b3 = *reinterpret_cast<const uint4 *>(bs + 3072);
-  if (tid < 10) {
-    const int h = tid < 5 ? tid : tid - 5;
-    const int64_t off = (h == 0) ? -SMAX_LH : (int64_t) SMAX_TILE + (h - 1) * 16;
-    R.h = *reinterpret_cast<const uint4 *>((tid < 5 ? lcp : bwt) + l0 + off);
+// Issue the DMA of tile `l0` (local index) into window w: 16 B per lane per
+// instruction, 1 KiB per wave instruction; halos by a few lanes of waves
+// 0..3; the .llv values of {lo, n} (low dword of each record's value).
+__device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
+                                             uint32_t lo, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wl = lds_addr(w->L), wb = lds_addr(w->B), wv = lds_addr(w->val);
+  const uint8_t *ls = a.lcp + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
+  const uint8_t *bs = a.bwt + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) {
+    glds16(ls + r * 1024, wl + SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024);
+    glds16(bs + r * 1024, wb + SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024);
   }
-}
-
-__device__ __forceinline__ void store_tile(uint8_t *sL, uint8_t *sB, const TileRegs &R) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t o = SMAX_LH + wave * SMAX_WAVE_BYTES + lane * 16;
-  *reinterpret_cast<uint4 *>(&sL[o]) = R.l0;
-  *reinterpret_cast<uint4 *>(&sL[o + 1024]) = R.l1;
-  *reinterpret_cast<uint4 *>(&sL[o + 2048]) = R.l2;
-  *reinterpret_cast<uint4 *>(&sL[o + 3072]) = R.l3;
-  *reinterpret_cast<uint4 *>(&sB[o]) = R.b0;
-  *reinterpret_cast<uint4 *>(&sB[o + 1024]) = R.b1;
-  *reinterpret_cast<uint4 *>(&sB[o + 2048]) = R.b2;
-  *reinterpret_cast<uint4 *>(&sB[o + 3072]) = R.b3;
-  if (tid < 10) {
-    const int h = tid < 5 ? tid : tid - 5;
-    const int off = (h == 0) ? 0 : SMAX_LH + SMAX_TILE + (h - 1) * 16;
-    *reinterpret_cast<uint4 *>(&(tid < 5 ? sL : sB)[off]) = R.h;
+  if (wave == 0) {
+    if (lane == 0) glds16(a.lcp + l0 - SMAX_LH, wl);
+  } else if (wave == 1) {
+    if (lane < SMAX_RH / 16) glds16(a.lcp + l0 + SMAX_TILE + lane * 16, wl + SMAX_LH + SMAX_TILE);
+  } else if (wave == 2) {
+    if (lane == 0) glds16(a.bwt + l0 - SMAX_LH, wb);
+  } else {
+    if (lane < SMAX_RH / 16) glds16(a.bwt + l0 + SMAX_TILE + lane * 16, wb + SMAX_LH + SMAX_TILE);
   }
+  const uint32_t k = (uint32_t) threadIdx.x;
+  if (k < n && k < SMAX_LLV_CAP)
+    glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + k) + 8, wv + wave * 256);
 }
 
 __device__ __forceinline__ uint32_t seg_ge(const uint4 v, uint32_t mf) {
@@ -368,7 +401,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 __device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
   if ((int) r < t.nval) return t.val[r];
   if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
-  return (uint32_t) t.llv[t.llv_base + r].value;
+  return llv_value(&t.llv[t.llv_base + r]);
 }
 
 // diversity of BWT rows [lo, hi] (pairwise distinct symbols < 254)
@@ -426,6 +459,33 @@ __device__ __forceinline__ uint32_t segment_starts_exact(const Win &t, const Sma
   return st;
 }
 
+// 64-bit SWAR: high bit of each byte of x equal to the same byte of y
+__device__ __forceinline__ uint64_t bytes_eq64(uint64_t x, uint64_t y) {
+  return ((uint64_t) bytes_eq((uint32_t) (x >> 32), (uint32_t) (y >> 32)) << 32) |
+         bytes_eq((uint32_t) x, (uint32_t) y);
+}
+// 8 consecutive window bytes starting at LDS offset o (o + 11 inside the
+// window): three aligned dword reads, issued together
+__device__ __forceinline__ uint64_t lds_bytes8(const uint8_t *base, uint32_t o) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(base + (o & ~3u));
+  const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+  const uint32_t sh = o & 3u;
+  return ((uint64_t) __builtin_amdgcn_alignbyte(d2, d1, sh) << 32) |
+         __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+// left diversity of the first w (2..8) symbols of X: symbols < 254 pairwise
+// distinct
+__device__ __forceinline__ bool diverse8(uint64_t X, uint32_t w) {
+  for (uint32_t m = 1; m < w; m++) {
+    const uint32_t x = (uint32_t) (X >> (8 * m)) & 0xffu;
+    if (x >= 254) continue;
+    const uint64_t hit = bytes_eq64(X, x * 0x0101010101010101ull) &
+                         (0x8080808080808080ull >> (8 * (8 - m)));
+    if (hit != 0) return false;
+  }
+  return true;
+}
+
 // Detection for one wave's 4096 rows, per segment round r (the 64 lanes'
 // segments r, rows lane-major = row order):
 //   1. each lane's 16-bit plateau-start mask (SWAR in interior tiles, exact
@@ -459,14 +519,17 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
       st = segment_starts_exact(t, a, sg);
     }
     // compact the starts into the list (row order)
+    // exclusive prefix of the counts (<= 16) over bit planes: no LDS trips
     const uint32_t c = (uint32_t) __popc(st);
-    uint32_t incl = c;
+    const uint64_t ltm = lanemask_lt();
+    uint32_t excl = 0, nstart = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
+    for (int b = 0; b < 5; b++) {
+      const uint64_t pl = __ballot((c >> b) & 1u);
+      excl += (uint32_t) __popcll(pl & ltm) << b;
+      nstart += (uint32_t) __popcll(pl) << b;
     }
-    const uint32_t nstart = __shfl(incl, 63, 64);
+    const uint32_t incl = excl + c;
     if (nstart == 0) continue;
     const uint32_t rowbase = r * 1024 + lane * 16;     // row offset inside the wave
     // windows of SMAX_LIST starts (a ramp can make every row a start)
@@ -489,7 +552,34 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
         uint64_t cc = 0;
         uint32_t cur = 0;
         uint64_t j = 0;
-        if (i < nwin) {
+        bool slow = i < nwin && !interior;
+        if (interior && i < nwin) {
+          // fast path: start value, plateau of <= 7 rows and diversity over
+          // <= 8 BWT symbols from two 8-byte LDS windows (one LDS round trip).
+          // A plateau in an interior tile never reaches `end` within them.
+          const uint32_t co = SMAX_LH + wave * SMAX_WAVE_BYTES + list[i];
+          cc = gw + list[i];
+          const uint64_t LX = lds_bytes8(sL, co);
+          const uint64_t BX = lds_bytes8(t.B, co - 1);
+          const uint32_t cb = (uint32_t) LX & 0xffu;
+          if (cb == 255) {
+            slow = true;
+          } else if (cb >= a.minlen) {
+            cur = cb;
+            const uint64_t nx = LX >> 8;
+            const uint64_t ne = ~bytes_eq64(nx, cb * 0x0101010101010101ull) &
+                                0x0080808080808080ull;
+            if (ne == 0) {
+              slow = true;
+            } else {
+              const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
+              const uint32_t nb = (uint32_t) (nx >> (8 * k)) & 0xffu;
+              j = cc + k;
+              if (nb < cb) acc = diverse8(BX, k + 2);
+            }
+          }
+        }
+        if (slow) {
           cc = gw + list[i];
           cur = lcp_exact(t, cc);
           if (cur >= a.minlen) {
@@ -531,14 +621,12 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
 }
 
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sL[SMAX_LDSB];
-  __shared__ __attribute__((aligned(16))) uint8_t sB[SMAX_LDSB];
+  __shared__ __attribute__((aligned(16))) SmaxWindow sWin[2];   // double-buffered windows
+  __shared__ __attribute__((aligned(16))) uint32_t sInfo[2][2];  // .llv {lo, n} ring
   __shared__ uint16_t sRank[SMAX_NCHUNK];
-  __shared__ uint32_t sVal[SMAX_LLV_CAP];
   __shared__ uint32_t sWave[SMAX_THREADS / 64];
   __shared__ uint32_t sHalo[5];
   __shared__ uint32_t sFlags;
-  __shared__ uint32_t sLlvBase;
   __shared__ uint16_t sList[SMAX_THREADS / 64][SMAX_LIST];   // per-wave start lists
 
   const int tid = threadIdx.x;
@@ -546,63 +634,84 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   const int wave = tid >> 6;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint64_t stride = gridDim.x;
+  const uint64_t last = a.num_tiles - 1;
 
   uint64_t tile = blockIdx.x;
   if (tile >= a.num_tiles) return;
-  if (tid == 0) sFlags = 0;
 
   Win t;
   win_init(t, a);
-  t.L = sL;
-  t.B = sB;
-  t.val = sVal;
 
-  TileRegs R;
-  R.h = make_uint4(0, 0, 0, 0);
-  load_tile(a.lcp, a.bwt, (a.tile_first + tile) * (uint64_t) SMAX_TILE, R);
-  uint32_t llv_lo_next = tid == 0 ? a.llv_lo[tile] : 0;
+  // prologue: .llv windows of the first two tiles, then the first window
+  const uint32_t info0 = lds_addr(&sInfo[0][0]), info1 = lds_addr(&sInfo[1][0]);
+  if (tid < 2) glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + tid, info0);
+  else if (tid >= 64 && tid < 66)
+    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + (tile + stride <= last ? tile + stride
+                                                                               : last)) + (tid - 64),
+          info1);
+  if (tid == 0) sFlags = 0;
+  glds_wait();
+  __syncthreads();
+  issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[0],
+               __builtin_amdgcn_readfirstlane(sInfo[0][0]),
+               __builtin_amdgcn_readfirstlane(sInfo[0][1]));
 
-  for (;;) {
+  for (uint32_t it = 0;; it++) {
+    const uint32_t cur = it & 1u;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
     const uint64_t next = tile + stride;
+    SmaxWindow *W = &sWin[cur];
     t.g0 = g0;
+    t.L = W->L;
+    t.B = W->B;
+    t.val = W->val;
 
-    // ---- stage the prefetched tile, filter
-    __syncthreads();               // LDS free (previous tile done), sFlags reset
-    store_tile(sL, sB, R);
-    const uint32_t segpre_bits = (seg_ge(R.l0, mf) ? 1u : 0u) | (seg_ge(R.l1, mf) ? 2u : 0u) |
-                                 (seg_ge(R.l2, mf) ? 4u : 0u) | (seg_ge(R.l3, mf) ? 8u : 0u);
-    const uint32_t segpre = segpre_bits;
-    const uint32_t f0 = seg_ffcount(R.l0), f1 = seg_ffcount(R.l1), f2 = seg_ffcount(R.l2),
-                   f3 = seg_ffcount(R.l3);
-    const uint32_t hff = tid < 5 ? seg_ffcount(R.h) : 0u;
-    if ((f0 | f1 | f2 | f3 | hff) != 0) atomicOr(&sFlags, 2u);
-    if (tid < 5) sHalo[tid] = hff;
-    if (tid == 0) sLlvBase = llv_lo_next;
+    // ---- this tile's window has landed; the previous tile's readers are done
+    glds_wait();
     __syncthreads();
+    const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[cur][0]);
+    const uint32_t wn = __builtin_amdgcn_readfirstlane(sInfo[cur][1]);
+    const uint32_t nlo = __builtin_amdgcn_readfirstlane(sInfo[cur ^ 1u][0]);
+    const uint32_t nn = __builtin_amdgcn_readfirstlane(sInfo[cur ^ 1u][1]);
+    const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + lane * 16;
+    const uint4 v0 = *reinterpret_cast<const uint4 *>(&W->L[so]);
+    const uint4 v1 = *reinterpret_cast<const uint4 *>(&W->L[so + 1024]);
+    const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+    const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
+    uint32_t hff = 0;
+    if (tid < 5) {
+      const int off = tid == 0 ? 0 : SMAX_LH + SMAX_TILE + (tid - 1) * 16;
+      hff = seg_ffcount(*reinterpret_cast<const uint4 *>(&W->L[off]));
+      sHalo[tid] = hff;
+    }
+    if ((f0 | f1 | hff) != 0) atomicOr(&sFlags, 2u);
+    __syncthreads();   // sFlags, sHalo; sInfo[cur] read by everyone
     const bool has_ff = (sFlags & 2u) != 0 && !(a.dbg & 16u);
-    const bool wave_pre = __ballot(segpre != 0) != 0 && !(a.dbg & 2u);
+    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
+    t.llv_base = wlo;
 
-    // ---- prefetch the next tile: in flight during all of this tile's work
+    // ---- DMA of the next tile's window (and the .llv window of the tile
+    // after it): in flight during all of this tile's work
     if (next < a.num_tiles) {
-      load_tile(a.lcp, a.bwt, (a.tile_first + next) * (uint64_t) SMAX_TILE, R);
-      if (tid == 0) llv_lo_next = a.llv_lo[next];
+      issue_window(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[cur ^ 1u], nlo, nn);
+      const uint64_t n2 = next + stride <= last ? next + stride : last;
+      if (tid < 2)
+        glds4(reinterpret_cast<const uint32_t *>(a.llv_win + n2) + tid,
+              cur ? info1 : info0);
     }
 
-    // ---- .llv ranks of the window's 255 bytes and their values in LDS
+    // ---- .llv ranks of the window's 255 bytes (values already in LDS)
     t.rank = nullptr;
     t.nval = -1;
     if (has_ff) {
-      uint32_t o0, o1, o2, o3, wo, tot;
-      block_scan_rows(f0, f1, f2, f3, &o0, &o1, &o2, &o3, &wo, &tot, sWave);
-      // chunk 0 = left halo, 1..1024 = tile rows, 1025..1028 = right halo
+      uint32_t o0, o1, wo, tot;
+      block_scan_rows(f0, f1, &o0, &o1, &wo, &tot, sWave);
+      // chunk 0 = left halo, 1..TILE/16 = tile rows, then 4 right-halo chunks
       const uint32_t h0 = sHalo[0];
-      const uint32_t cb = 1 + wave * 256 + lane;
+      const uint32_t cb = 1 + wave * (SMAX_WAVE_BYTES / 16) + lane;
       sRank[cb] = (uint16_t) (h0 + wo + o0);
       sRank[cb + 64] = (uint16_t) (h0 + wo + o1);
-      sRank[cb + 128] = (uint16_t) (h0 + wo + o2);
-      sRank[cb + 192] = (uint16_t) (h0 + wo + o3);
       if (tid == 0) {
         sRank[0] = 0;
         uint32_t acc = h0 + tot;
@@ -610,16 +719,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
           sRank[1 + SMAX_TILE / 16 + k] = (uint16_t) acc;
           acc += sHalo[1 + k];
         }
-        sFlags = acc;              // total 255 bytes in the window (reuse)
       }
-      __syncthreads();
-      const uint32_t nff = sFlags;
-      t.llv_base = sLlvBase;
-      if (nff <= SMAX_LLV_CAP) {
-        for (uint32_t i = tid; i < nff; i += SMAX_THREADS)
-          sVal[i] = (uint32_t) a.llv[t.llv_base + i].value;
-        t.nval = (int) nff;
-      }
+      t.nval = (int) (wn < SMAX_LLV_CAP ? wn : SMAX_LLV_CAP);
       t.rank = sRank;
       __syncthreads();
     }
@@ -630,13 +731,14 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     uint32_t wcount = 0;
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
     if (wave_pre || edge)
-      wcount = wave_detect(t, a, g0, sL, sList[wave], wdst, !edge, segpre_bits);
+      wcount = wave_detect(t, a, g0, W->L, sList[wave], wdst, !edge, segpre_bits);
     if (lane == 0) a.tile_count[slot] = wcount;
 
     if (tid == 0) sFlags = 0;
     tile = next;
     if (tile >= a.num_tiles) break;
   }
+  glds_wait();
 }
 
 // K1 instantiations: 4 waves/SIMD (<= 128 VGPRs, 4 workgroups/CU, what the
@@ -674,7 +776,7 @@ smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
 
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
                                       uint64_t base, uint64_t tile_first,
-                                      uint32_t num_tiles, uint32_t *lo_out,
+                                      uint32_t num_tiles, uint2 *win_out,
                                       uint32_t *err) {
   const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (t < numllv) {
@@ -684,12 +786,18 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
   if (t >= num_tiles) return;
   const uint64_t g0 = base + (tile_first + t) * (uint64_t) SMAX_TILE;
   const uint64_t key = g0 >= SMAX_LH ? g0 - SMAX_LH : 0;
+  const uint64_t key2 = g0 + SMAX_TILE + SMAX_RH;
   uint64_t lo = 0, hi = numllv;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (llv[mid].position < key) lo = mid + 1; else hi = mid;
   }
-  lo_out[t] = (uint32_t) lo;
+  uint64_t lo2 = lo, hi2 = numllv;
+  while (lo2 < hi2) {
+    const uint64_t mid = (lo2 + hi2) >> 1;
+    if (llv[mid].position < key2) lo2 = mid + 1; else hi2 = mid;
+  }
+  win_out[t] = make_uint2((uint32_t) lo, (uint32_t) (lo2 - lo));
 }
 
 // ------------------------------------------------------------ stitch
@@ -770,7 +878,7 @@ struct GtSmaxPlan {
   uint64_t *tile_off;        // num_tiles * 4
   uint64_t *count;
   GtSmaxBoundary *bnd;
-  uint32_t *llv_lo;
+  uint2 *llv_win;
   uint32_t *err;
   void *scan_tmp;
   size_t scan_tmp_bytes;
@@ -877,7 +985,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
   HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMemset(p->bnd, 0, sizeof (GtSmaxBoundary)));
-  HIPCHK(hipMalloc(&p->llv_lo, sizeof (uint32_t) * p->num_tiles));
+  // + 2 zeroed entries: the dummy .llv record of K1's unconditional loads
+  HIPCHK(hipMalloc(&p->llv_win, sizeof (uint2) * (p->num_tiles + 2)));
+  HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(hipMalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
   HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
@@ -895,7 +1005,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     const unsigned blocks = (unsigned) ((work + 255) / 256);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
                        shard->llv_dev, shard->numllv, shard->base, p->tile_first,
-                       p->num_tiles, p->llv_lo, derr);
+                       p->num_tiles, p->llv_win, derr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   }
@@ -914,7 +1024,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
-                  p->llv_lo, p->err, p->scan_tmp};
+                  p->llv_win, p->err, p->scan_tmp};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -928,7 +1038,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.bwt = p->shard.bwt_dev;
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;
-  a.llv_lo = p->llv_lo;
+  a.llv_win = p->llv_win;
   a.base = p->shard.base;
   a.begin = p->shard.begin;
   a.end = p->shard.end;
