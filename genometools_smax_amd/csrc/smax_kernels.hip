@@ -404,6 +404,17 @@ __device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
   return llv_value(&t.llv[t.llv_base + r]);
 }
 
+// rank of window offset o among the window's 255 bytes (t.rank staged)
+__device__ __forceinline__ uint32_t rank_at(const Win &t, uint32_t o) {
+  const uint32_t chunk = o >> 4, within = o & 15;
+  const uint4 v = *reinterpret_cast<const uint4 *>(&t.L[chunk * 16]);
+  const uint64_t lo = (uint64_t) bytes_ff(v.x) | ((uint64_t) bytes_ff(v.y) << 32);
+  const uint64_t hi = (uint64_t) bytes_ff(v.z) | ((uint64_t) bytes_ff(v.w) << 32);
+  const uint32_t cnt = within < 8 ? __popcll(lo & ((1ull << (8 * within)) - 1))
+                                  : __popcll(lo) + __popcll(hi & ((1ull << (8 * (within - 8))) - 1));
+  return t.rank[chunk] + cnt;
+}
+
 // diversity of BWT rows [lo, hi] (pairwise distinct symbols < 254)
 __device__ __forceinline__ bool diverse_rows(const Win &t, uint64_t lo, uint64_t hi) {
   Seen s = {0, 0, 0, 0};
@@ -530,7 +541,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
       nstart += (uint32_t) __popcll(pl) << b;
     }
     const uint32_t incl = excl + c;
-    if (nstart == 0) continue;
+    if (nstart == 0 || (a.dbg & 8u)) { wcount += nstart & (a.dbg >> 9); continue; }
     const uint32_t rowbase = r * 1024 + lane * 16;     // row offset inside the wave
     // windows of SMAX_LIST starts (a ramp can make every row a start)
     for (uint32_t w0 = 0; w0 < nstart; w0 += SMAX_LIST) {
@@ -546,7 +557,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
       __builtin_amdgcn_wave_barrier();
       const uint32_t nwin = nstart - w0 < SMAX_LIST ? nstart - w0 : SMAX_LIST;
       // evaluate 64 starts per step
-      for (uint32_t i0 = 0; i0 < nwin; i0 += 64) {
+      for (uint32_t i0 = 0; i0 < nwin && !(a.dbg & 4u); i0 += 64) {
         const uint32_t i = i0 + lane;
         bool acc = false;
         uint64_t cc = 0;
@@ -563,7 +574,31 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
           const uint64_t BX = lds_bytes8(t.B, co - 1);
           const uint32_t cb = (uint32_t) LX & 0xffu;
           if (cb == 255) {
-            slow = true;
+            // .llv start: exact values by rank; a run of equal values >= 255
+            // is a run of 255 bytes, so its ranks are consecutive
+            if (t.rank == nullptr) {
+              slow = true;
+            } else {
+              const uint32_t r = rank_at(t, co);
+              const uint32_t v = llv_by_rank(t, r);
+              if (v >= a.minlen) {
+                cur = v;
+                uint32_t k = 0;
+                int rel = 0;
+                for (; k < 7; k++) {
+                  const uint32_t nb = (uint32_t) (LX >> (8 * (k + 1))) & 0xffu;
+                  if (nb != 255) { rel = -1; break; }
+                  const uint32_t nv = llv_by_rank(t, r + k + 1);
+                  if (nv != v) { rel = nv < v ? -1 : 1; break; }
+                }
+                if (rel == 0) {
+                  slow = true;
+                } else {
+                  j = cc + k;
+                  if (rel < 0) acc = diverse8(BX, k + 2);
+                }
+              }
+            }
           } else if (cb >= a.minlen) {
             cur = cb;
             const uint64_t nx = LX >> 8;
@@ -579,7 +614,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
             }
           }
         }
-        if (slow) {
+        if (slow && !(a.dbg & 32u)) {
           cc = gw + list[i];
           cur = lcp_exact(t, cc);
           if (cur >= a.minlen) {
