@@ -1008,6 +1008,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
     if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
     p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
+    if (getenv("GT_SMAX_VERBOSE"))
+      fprintf(stderr, "gt_smax: K1 %d CUs x %d blocks/CU -> grid %u, %u tiles\n", dev_cus,
+              per_cu, p->grid, p->num_tiles);
     const uint64_t cg = (uint64_t) p->num_tiles;              // 4 slots per block
     p->compact_grid = (uint32_t) (cg < 4096 ? (cg ? cg : 1) : 4096);
   }

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Diagnostic: workload statistics of the K1 detection path on a synthetic
+genome (GPU ESA, downloaded; numpy on the host).  Prints how many rows pass
+each filter stage, the plateau-start density per 1024-row wave round and
+the share of starts that leave the fast (<= 7-row plateau, byte) path."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import genometools_smax_amd as G
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "human"
+bases = int(float(sys.argv[2])) if len(sys.argv) > 2 else 300_000_000
+minlen = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+text = G.synth_genome(kind, bases, 1 if kind != "uniform" else 42)
+esa = G.DeviceEsa(text)
+d = esa.download()
+L = np.asarray(d["lcptab"], dtype=np.uint8)
+N = esa.nonspecials
+L = L[: N + 1].astype(np.int16)
+rows = N + 1
+print("rows %d  llv %d" % (rows, esa.numllv))
+ge = L >= minlen
+print("LCP>=minlen: %.3f" % ge.mean())
+prev = np.concatenate(([0], L[:-1]))
+start = ge & (L > prev)
+print("plateau starts: %d (%.4f of rows)" % (start.sum(), start.mean()))
+seg = rows // 16
+segge = ge[: seg * 16].reshape(seg, 16).any(1)
+print("16-row segments passing the filter: %.3f" % segge.mean())
+rnd = rows // 1024
+per = start[: rnd * 1024].reshape(rnd, 1024).sum(1)
+print("starts per 1024-row round: mean %.1f  p50 %d  p90 %d  p99 %d  max %d" %
+      (per.mean(), np.percentile(per, 50), np.percentile(per, 90), np.percentile(per, 99), per.max()))
+steps = np.ceil(per / 64)
+print("64-start evaluation steps per round: mean %.2f  (rounds with 0: %.3f)" %
+      (steps.mean(), (per == 0).mean()))
+idx = np.nonzero(start)[0]
+cb255 = (L[idx] == 255).mean()
+# plateau length from each start
+nxt = np.ones(len(idx), dtype=np.int64)
+eq = np.zeros(len(idx), dtype=bool)
+for k in range(1, 9):
+    j = np.minimum(idx + k, rows - 1)
+    same = L[j] == L[idx]
+    if k == 1:
+        eq = same
+    else:
+        eq &= same
+    nxt += eq
+print("starts with a 255 byte: %.4f   plateaus > 7 rows: %.4f" % (cb255, (nxt > 7).mean()))
+lm = np.zeros(len(idx), dtype=bool)
+endj = np.minimum(idx + nxt, rows - 1)
+lm = L[endj] < L[idx]
+print("local maxima among starts: %.3f  (width mean %.2f)" % (lm.mean(), (nxt[lm] + 1).mean()))
