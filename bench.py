@@ -17,7 +17,7 @@ by range (strong scaling): value = nonspecials / max-over-ranks step time.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 "roofline" for K1 (algorithmic bytes = 2 B per suffix row + 16 B per .llv
-entry, SURVEY.md §8(d), over the average K1 duration from HIP events recorded
+entry + 16 B per emitted record, SURVEY.md §8(d), over the average K1 duration from HIP events recorded
 on K1's stream during the timed region) and, at N = 1, "cpu_baseline": the
 oracle's single-core linear scan (oracle/smax_oracle.c orc_linsmax, the
 repo's CPU esa_linsmax restatement) timed on this host over the same tables.
@@ -150,7 +150,9 @@ def main():
         llv_pos = esa.download()["llvtab"][:, 0] if esa.numllv else np.zeros(0, np.uint64)
     llv_here = int(np.count_nonzero((llv_pos >= begin - 1) & (llv_pos <= end)))
     rows = end - begin + 1
-    alg_bytes = 2 * rows + 16 * llv_here
+    # 2 B per suffix row (LCP + BWT byte) + 16 B per .llv entry
+    # in range + 16 B per emitted interval record (K1's output)
+    alg_bytes = 2 * rows + 16 * llv_here + 16 * plan.fetch_count()
 
     stats = torch.tensor([elapsed, float(count), k1_ms / max(k1_n, 1)], dtype=torch.float64,
                          device="cuda")

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 rocpd databases into the summaries committed under
+profiles/.
+
+  rocpd_summary.py stats  DB OUT.csv            kernel-trace --stats table
+  rocpd_summary.py pmc    OUT.json KERNEL DB... per-launch HBM bytes of KERNEL
+
+For `pmc`, each DB is one `rocprofv3 --pmc <COUNTER>` pass (FETCH_SIZE and
+WRITE_SIZE do not fit one pass on gfx950).  FETCH_SIZE / WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
+(/opt/skills/guides/MI355X_MICROARCH.md, HBM section), so read bytes =
+2 x 1024 x FETCH_SIZE; write bytes = 1024 x WRITE_SIZE.
+"""
+import csv
+import json
+import sqlite3
+import sys
+
+
+def stats(db, out):
+    con = sqlite3.connect(db)
+    rows = con.execute("select name, total_calls, total_duration, average, percentage "
+                       "from top_kernels").fetchall()
+    with open(out, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "calls", "total_ns", "average_ns", "percent"])
+        for name, calls, tot, avg, pct in rows:
+            short = name.replace("(anonymous namespace)::", "")
+            if "rocprim" in short:
+                # rocprim trampoline: keep the wrapped algorithm's config name
+                key = short.split("wrapped_")[1].split("<")[0] if "wrapped_" in short else "kernel"
+                short = "rocprim::" + key
+            else:
+                short = short.split("(")[0]
+            w.writerow([short, calls, "%.0f" % tot, "%.1f" % avg, "%.2f" % pct])
+    print("wrote", out, len(rows), "kernels")
+
+
+def pmc(out, kernel, dbs):
+    res = {"kernel": kernel, "passes": {}}
+    for db in dbs:
+        con = sqlite3.connect(db)
+        rows = con.execute("select counter_name, value, duration from counters_collection "
+                           "where kernel_name like ?", ("%" + kernel + "%",)).fetchall()
+        for name, value, dur in rows:
+            res["passes"].setdefault(name, []).append(float(value))
+    fetch = res["passes"].get("FETCH_SIZE", [])
+    write = res["passes"].get("WRITE_SIZE", [])
+    if fetch:
+        res["fetch_kib_per_launch"] = sum(fetch) / len(fetch)
+        res["read_bytes_per_launch"] = 2 * 1024 * res["fetch_kib_per_launch"]
+    if write:
+        res["write_kib_per_launch"] = sum(write) / len(write)
+        res["write_bytes_per_launch"] = 1024 * res["write_kib_per_launch"]
+    if fetch and write:
+        res["hbm_bytes_per_launch"] = res["read_bytes_per_launch"] + res["write_bytes_per_launch"]
+    res["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                     "read = 2 x 1024 x FETCH_SIZE (gfx950 half-count correction), "
+                     "write = 1024 x WRITE_SIZE")
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "passes"}, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3])
+    else:
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4:])
