@@ -497,6 +497,113 @@ __device__ __forceinline__ bool diverse8(uint64_t X, uint32_t w) {
   return true;
 }
 
+// Evaluate list[0 .. nwin) (row offsets inside the wave, row order), 64
+// starts per step, one per lane: exact plateau end in LDS, local-maximum
+// test, left diversity over BWT[lb..rb], the pending plateau at the shard
+// end; accepted records are appended in row order to the wave's slot.
+__device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64_t g0,
+                                     const uint8_t *sL, const uint16_t *list, uint32_t nwin,
+                                     GtSmaxRecord *wdst, uint32_t wcount, bool interior) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t gw = g0 + wave * SMAX_WAVE_BYTES;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i0 = 0; i0 < nwin && !(a.dbg & 4u); i0 += 64) {
+    const uint32_t i = i0 + lane;
+    bool acc = false;
+    uint64_t cc = 0;
+    uint32_t cur = 0;
+    uint64_t j = 0;
+    bool slow = i < nwin && !interior;
+    if (interior && i < nwin) {
+      // fast path: start value, plateau of <= 7 rows and diversity over
+      // <= 8 BWT symbols from two 8-byte LDS windows (one LDS round trip).
+      // A plateau in an interior tile never reaches `end` within them.
+      const uint32_t co = SMAX_LH + wave * SMAX_WAVE_BYTES + list[i];
+      cc = gw + list[i];
+      const uint64_t LX = lds_bytes8(sL, co);
+      const uint64_t BX = lds_bytes8(t.B, co - 1);
+      const uint32_t cb = (uint32_t) LX & 0xffu;
+      if (cb == 255) {
+        // .llv start: exact values by rank; a run of equal values >= 255
+        // is a run of 255 bytes, so its ranks are consecutive
+        if (t.rank == nullptr) {
+          slow = true;
+        } else {
+          const uint32_t r = rank_at(t, co);
+          const uint32_t v = llv_by_rank(t, r);
+          if (v >= a.minlen) {
+            cur = v;
+            uint32_t k = 0;
+            int rel = 0;
+            for (; k < 7; k++) {
+              const uint32_t nb = (uint32_t) (LX >> (8 * (k + 1))) & 0xffu;
+              if (nb != 255) { rel = -1; break; }
+              const uint32_t nv = llv_by_rank(t, r + k + 1);
+              if (nv != v) { rel = nv < v ? -1 : 1; break; }
+            }
+            if (rel == 0) {
+              slow = true;
+            } else {
+              j = cc + k;
+              if (rel < 0) acc = diverse8(BX, k + 2);
+            }
+          }
+        }
+      } else if (cb >= a.minlen) {
+        cur = cb;
+        const uint64_t nx = LX >> 8;
+        const uint64_t ne = ~bytes_eq64(nx, cb * 0x0101010101010101ull) &
+                            0x0080808080808080ull;
+        if (ne == 0) {
+          slow = true;
+        } else {
+          const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
+          const uint32_t nb = (uint32_t) (nx >> (8 * k)) & 0xffu;
+          j = cc + k;
+          if (nb < cb) acc = diverse8(BX, k + 2);
+        }
+      }
+    }
+    if (slow && !(a.dbg & 32u)) {
+      cc = gw + list[i];
+      cur = lcp_exact(t, cc);
+      if (cur >= a.minlen) {
+        int rel;
+        bool pend;
+        j = plateau_end(t, cc, cur, &rel, &pend);
+        if (pend) {
+          Seen sn = {0, 0, 0, 0};
+          bool dup = false;
+          for (uint64_t g = cc - 1; g < a.end && !dup; g++) dup = seen_add(sn, bwt_at(t, g));
+          if (!dup) {
+            GtSmaxBoundary *b = a.bnd;
+            b->pend_c = cc;
+            b->pend_lcp = cur;
+            b->pend_div.seen[0] = sn.w0; b->pend_div.seen[1] = sn.w1;
+            b->pend_div.seen[2] = sn.w2; b->pend_div.seen[3] = sn.w3;
+            b->pend_div.dup = 0;
+            b->pend_valid = 1;
+          }
+        } else if (rel < 0) {
+          acc = diverse_rows(t, cc - 1, j);
+        }
+      }
+    }
+    const uint64_t am = __ballot(acc);
+    if (acc) {
+      GtSmaxRecord rec;
+      rec.lb = cc - 1;
+      rec.lcp = cur;
+      rec.width = (uint32_t) (j - cc + 2);
+      wdst[wcount + (uint32_t) __popcll(am & lanemask_lt())] = rec;
+    }
+    wcount += (uint32_t) __popcll(am);
+  }
+  __builtin_amdgcn_wave_barrier();   // list reused after this
+  return wcount;
+}
+
 // Detection for one wave's 4096 rows, per segment round r (the 64 lanes'
 // segments r, rows lane-major = row order):
 //   1. each lane's 16-bit plateau-start mask (SWAR in interior tiles, exact
@@ -515,6 +622,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint64_t gw = g0 + wave * SMAX_WAVE_BYTES;
   uint32_t wcount = 0;
+  uint32_t pend = 0;                 // starts queued in the list (all rounds)
 #pragma unroll 1
   for (int r = 0; r < SMAX_SEGS; r++) {
     const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
@@ -529,7 +637,6 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
     } else {
       st = segment_starts_exact(t, a, sg);
     }
-    // compact the starts into the list (row order)
     // exclusive prefix of the counts (<= 16) over bit planes: no LDS trips
     const uint32_t c = (uint32_t) __popc(st);
     const uint64_t ltm = lanemask_lt();
@@ -540,12 +647,27 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
       excl += (uint32_t) __popcll(pl & ltm) << b;
       nstart += (uint32_t) __popcll(pl) << b;
     }
-    const uint32_t incl = excl + c;
     if (nstart == 0 || (a.dbg & 8u)) { wcount += nstart & (a.dbg >> 9); continue; }
     const uint32_t rowbase = r * 1024 + lane * 16;     // row offset inside the wave
-    // windows of SMAX_LIST starts (a ramp can make every row a start)
+    if (pend + nstart > SMAX_LIST && pend != 0) {      // make room: evaluate the queue
+      wcount = eval_list(t, a, g0, sL, list, pend, wdst, wcount, interior);
+      pend = 0;
+    }
+    if (nstart <= SMAX_LIST) {
+      // queue this round's starts behind the pending ones (row order)
+      uint32_t pos = pend + excl;
+      uint32_t bits = st;
+      while (bits) {
+        const int q = __builtin_ctz(bits);
+        bits &= bits - 1;
+        list[pos++] = (uint16_t) (rowbase + q);
+      }
+      pend += nstart;
+      continue;
+    }
+    // a ramp can make every row a start: windows of SMAX_LIST starts
     for (uint32_t w0 = 0; w0 < nstart; w0 += SMAX_LIST) {
-      uint32_t pos = incl - c;
+      uint32_t pos = excl;
       uint32_t bits = st;
       while (bits) {
         const int q = __builtin_ctz(bits);
@@ -553,105 +675,11 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
         if (pos >= w0 && pos < w0 + SMAX_LIST) list[pos - w0] = (uint16_t) (rowbase + q);
         pos++;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
       const uint32_t nwin = nstart - w0 < SMAX_LIST ? nstart - w0 : SMAX_LIST;
-      // evaluate 64 starts per step
-      for (uint32_t i0 = 0; i0 < nwin && !(a.dbg & 4u); i0 += 64) {
-        const uint32_t i = i0 + lane;
-        bool acc = false;
-        uint64_t cc = 0;
-        uint32_t cur = 0;
-        uint64_t j = 0;
-        bool slow = i < nwin && !interior;
-        if (interior && i < nwin) {
-          // fast path: start value, plateau of <= 7 rows and diversity over
-          // <= 8 BWT symbols from two 8-byte LDS windows (one LDS round trip).
-          // A plateau in an interior tile never reaches `end` within them.
-          const uint32_t co = SMAX_LH + wave * SMAX_WAVE_BYTES + list[i];
-          cc = gw + list[i];
-          const uint64_t LX = lds_bytes8(sL, co);
-          const uint64_t BX = lds_bytes8(t.B, co - 1);
-          const uint32_t cb = (uint32_t) LX & 0xffu;
-          if (cb == 255) {
-            // .llv start: exact values by rank; a run of equal values >= 255
-            // is a run of 255 bytes, so its ranks are consecutive
-            if (t.rank == nullptr) {
-              slow = true;
-            } else {
-              const uint32_t r = rank_at(t, co);
-              const uint32_t v = llv_by_rank(t, r);
-              if (v >= a.minlen) {
-                cur = v;
-                uint32_t k = 0;
-                int rel = 0;
-                for (; k < 7; k++) {
-                  const uint32_t nb = (uint32_t) (LX >> (8 * (k + 1))) & 0xffu;
-                  if (nb != 255) { rel = -1; break; }
-                  const uint32_t nv = llv_by_rank(t, r + k + 1);
-                  if (nv != v) { rel = nv < v ? -1 : 1; break; }
-                }
-                if (rel == 0) {
-                  slow = true;
-                } else {
-                  j = cc + k;
-                  if (rel < 0) acc = diverse8(BX, k + 2);
-                }
-              }
-            }
-          } else if (cb >= a.minlen) {
-            cur = cb;
-            const uint64_t nx = LX >> 8;
-            const uint64_t ne = ~bytes_eq64(nx, cb * 0x0101010101010101ull) &
-                                0x0080808080808080ull;
-            if (ne == 0) {
-              slow = true;
-            } else {
-              const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
-              const uint32_t nb = (uint32_t) (nx >> (8 * k)) & 0xffu;
-              j = cc + k;
-              if (nb < cb) acc = diverse8(BX, k + 2);
-            }
-          }
-        }
-        if (slow && !(a.dbg & 32u)) {
-          cc = gw + list[i];
-          cur = lcp_exact(t, cc);
-          if (cur >= a.minlen) {
-            int rel;
-            bool pend;
-            j = plateau_end(t, cc, cur, &rel, &pend);
-            if (pend) {
-              Seen sn = {0, 0, 0, 0};
-              bool dup = false;
-              for (uint64_t g = cc - 1; g < a.end && !dup; g++) dup = seen_add(sn, bwt_at(t, g));
-              if (!dup) {
-                GtSmaxBoundary *b = a.bnd;
-                b->pend_c = cc;
-                b->pend_lcp = cur;
-                b->pend_div.seen[0] = sn.w0; b->pend_div.seen[1] = sn.w1;
-                b->pend_div.seen[2] = sn.w2; b->pend_div.seen[3] = sn.w3;
-                b->pend_div.dup = 0;
-                b->pend_valid = 1;
-              }
-            } else if (rel < 0) {
-              acc = diverse_rows(t, cc - 1, j);
-            }
-          }
-        }
-        const uint64_t am = __ballot(acc);
-        if (acc) {
-          GtSmaxRecord rec;
-          rec.lb = cc - 1;
-          rec.lcp = cur;
-          rec.width = (uint32_t) (j - cc + 2);
-          wdst[wcount + (uint32_t) __popcll(am & lanemask_lt())] = rec;
-        }
-        wcount += (uint32_t) __popcll(am);
-      }
-      __builtin_amdgcn_wave_barrier();   // list reused by the next window
+      wcount = eval_list(t, a, g0, sL, list, nwin, wdst, wcount, interior);
     }
   }
+  if (pend != 0) wcount = eval_list(t, a, g0, sL, list, pend, wdst, wcount, interior);
   return wcount;
 }
 
