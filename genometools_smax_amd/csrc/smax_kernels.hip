@@ -428,8 +428,9 @@ __device__ __forceinline__ bool diverse_rows(const Win &t, uint64_t lo, uint64_t
 // LCP[q] >= min(minlen,128) (exact for minlen <= 128) and LCP[q] > LCP[q-1].
 // Byte compares are exact except between two 255 bytes; those pairs are
 // fixed up with exact .llv values.
-__device__ __forceinline__ uint32_t segment_starts_fast(const Win &t, uint64_t sg, uint32_t so,
-                                                        const uint8_t *sL, uint32_t mf) {
+__device__ __forceinline__ uint32_t segment_starts_fast(const Win &t, uint32_t so,
+                                                        const uint8_t *sL, uint32_t mf,
+                                                        uint32_t crank, uint32_t *ffo) {
   const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
   const uint32_t prevb = sL[so - 1];
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -445,12 +446,16 @@ __device__ __forceinline__ uint32_t segment_starts_fast(const Win &t, uint64_t s
   uint32_t st = GE & UP;
   // exact compares where both bytes are 255 (only matters for candidate rows)
   uint32_t fu = FF & ((FF << 1) | (prevb == 255u ? 1u : 0u)) & GE;
+  // (rank of row q = the chunk's rank + 255 bytes before q; row q-1 is the
+  // 255 byte just before it)
   while (fu) {
     const int q = __builtin_ctz(fu);
     fu &= fu - 1;
-    const uint32_t c = lcp_big(t, sg + q), p = lcp_big(t, sg + q - 1);
+    const uint32_t rc = crank + (uint32_t) __popc(FF & ((1u << q) - 1));
+    const uint32_t c = llv_by_rank(t, rc), p = llv_by_rank(t, rc - 1);
     st = (st & ~(1u << q)) | ((c > p ? 1u : 0u) << q);
   }
+  *ffo = FF;
   return st;
 }
 
@@ -502,7 +507,8 @@ __device__ __forceinline__ bool diverse8(uint64_t X, uint32_t w) {
 // test, left diversity over BWT[lb..rb], the pending plateau at the shard
 // end; accepted records are appended in row order to the wave's slot.
 __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                     const uint8_t *sL, const uint16_t *list, uint32_t nwin,
+                                     const uint8_t *sL, const uint16_t *list,
+                                     const uint16_t *lrank, uint32_t nwin,
                                      GtSmaxRecord *wdst, uint32_t wcount, bool interior) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t gw = g0 + wave * SMAX_WAVE_BYTES;
@@ -530,7 +536,7 @@ __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64
         if (t.rank == nullptr) {
           slow = true;
         } else {
-          const uint32_t r = rank_at(t, co);
+          const uint32_t r = lrank[i];       // queued with the start
           const uint32_t v = llv_by_rank(t, r);
           if (v >= a.minlen) {
             cur = v;
@@ -616,7 +622,8 @@ __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64
 // No lane loops over another lane's work: the per-start cost is spread over
 // all 64 lanes instead of serialising the wave on its busiest lane.
 __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                       const uint8_t *sL, uint16_t *list, GtSmaxRecord *wdst,
+                                       const uint8_t *sL, uint16_t *list, uint16_t *lrank,
+                                       GtSmaxRecord *wdst,
                                        bool interior, uint32_t segpre) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
@@ -627,10 +634,11 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
   for (int r = 0; r < SMAX_SEGS; r++) {
     const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
     const uint64_t sg = gw + r * 1024 + lane * 16;
-    uint32_t st = 0;
+    uint32_t st = 0, ff = 0;
+    const uint32_t crank = (interior && t.rank != nullptr) ? t.rank[so >> 4] : 0u;
     if (interior) {
       if ((segpre >> r) & 1u) {
-        st = segment_starts_fast(t, sg, so, sL, mf);
+        st = segment_starts_fast(t, so, sL, mf, crank, &ff);
         if (sg < a.begin)
           st &= sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
       }
@@ -650,7 +658,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
     if (nstart == 0 || (a.dbg & 8u)) { wcount += nstart & (a.dbg >> 9); continue; }
     const uint32_t rowbase = r * 1024 + lane * 16;     // row offset inside the wave
     if (pend + nstart > SMAX_LIST && pend != 0) {      // make room: evaluate the queue
-      wcount = eval_list(t, a, g0, sL, list, pend, wdst, wcount, interior);
+      wcount = eval_list(t, a, g0, sL, list, lrank, pend, wdst, wcount, interior);
       pend = 0;
     }
     if (nstart <= SMAX_LIST) {
@@ -660,6 +668,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
       while (bits) {
         const int q = __builtin_ctz(bits);
         bits &= bits - 1;
+        if ((ff >> q) & 1u) lrank[pos] = (uint16_t) (crank + (uint32_t) __popc(ff & ((1u << q) - 1)));
         list[pos++] = (uint16_t) (rowbase + q);
       }
       pend += nstart;
@@ -672,14 +681,17 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
       while (bits) {
         const int q = __builtin_ctz(bits);
         bits &= bits - 1;
-        if (pos >= w0 && pos < w0 + SMAX_LIST) list[pos - w0] = (uint16_t) (rowbase + q);
+        if (pos >= w0 && pos < w0 + SMAX_LIST) {
+          if ((ff >> q) & 1u) lrank[pos - w0] = (uint16_t) (crank + (uint32_t) __popc(ff & ((1u << q) - 1)));
+          list[pos - w0] = (uint16_t) (rowbase + q);
+        }
         pos++;
       }
       const uint32_t nwin = nstart - w0 < SMAX_LIST ? nstart - w0 : SMAX_LIST;
-      wcount = eval_list(t, a, g0, sL, list, nwin, wdst, wcount, interior);
+      wcount = eval_list(t, a, g0, sL, list, lrank, nwin, wdst, wcount, interior);
     }
   }
-  if (pend != 0) wcount = eval_list(t, a, g0, sL, list, pend, wdst, wcount, interior);
+  if (pend != 0) wcount = eval_list(t, a, g0, sL, list, lrank, pend, wdst, wcount, interior);
   return wcount;
 }
 
@@ -691,6 +703,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ uint32_t sHalo[5];
   __shared__ uint32_t sFlags;
   __shared__ uint16_t sList[SMAX_THREADS / 64][SMAX_LIST];   // per-wave start lists
+  __shared__ uint16_t sLRank[SMAX_THREADS / 64][SMAX_LIST];  // .llv rank of 255-byte starts
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -794,7 +807,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     uint32_t wcount = 0;
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
     if (wave_pre || edge)
-      wcount = wave_detect(t, a, g0, W->L, sList[wave], wdst, !edge, segpre_bits);
+      wcount = wave_detect(t, a, g0, W->L, sList[wave], sLRank[wave], wdst, !edge,
+                           segpre_bits);
     if (lane == 0) a.tile_count[slot] = wcount;
 
     if (tid == 0) sFlags = 0;
