@@ -43,17 +43,18 @@
 
 #include "gt_smax_hip.h"
 
-#define SMAX_THREADS 256
+#define SMAX_THREADS 256                              // 4 independent waves per workgroup
 #define SMAX_SEGS 2                                   // 16-row segments per lane
-#define SMAX_WAVE_BYTES (SMAX_SEGS * 64 * 16)         // 4096 rows per wave
-#define SMAX_TILE (SMAX_THREADS * SMAX_SEGS * 16)     // 16384 rows per tile
+#define SMAX_WAVE_BYTES (SMAX_SEGS * 64 * 16)         // 2048 rows per wave tile
+#define SMAX_TILE SMAX_WAVE_BYTES                     // a tile is one wave's work
 #define SMAX_LH 16                                    // left halo (bytes)
-#define SMAX_RH 64                                    // right halo (bytes)
+#define SMAX_RH 16                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
-#define SMAX_LLV_CAP SMAX_THREADS                     // .llv values in LDS (1 per lane)
-#define SMAX_LIST 256                                 // per-wave start-list window
-#define SMAX_WSLOT 2048                               // records per (tile, wave) slot
+#define SMAX_LLV_CAP 64                               // .llv values in LDS (1 per lane)
+#define SMAX_LIST 128                                 // per-wave start-list window
+#define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
+                                                      // records are >= 2 rows apart)
 
 static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
@@ -341,33 +342,31 @@ struct SmaxWindow {
   uint32_t val[SMAX_LLV_CAP];
 };
 
-// Issue the DMA of tile `l0` (local index) into window w: 16 B per lane per
-// instruction, 1 KiB per wave instruction; halos by a few lanes of waves
-// 0..3; the .llv values of {lo, n} (low dword of each record's value).
+// Issue the DMA of tile `l0` (local index) into the calling wave's window
+// w: 16 B per lane per instruction (1 KiB per wave instruction), the two
+// 16-row halos, and the window's .llv values {lo, n} (low dword of each
+// record's value, at most SMAX_LLV_CAP).
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wl = lds_addr(w->L), wb = lds_addr(w->B), wv = lds_addr(w->val);
-  const uint8_t *ls = a.lcp + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
-  const uint8_t *bs = a.bwt + l0 + wave * SMAX_WAVE_BYTES + lane * 16;
+  const uint32_t wl = __builtin_amdgcn_readfirstlane(lds_addr(w->L));
+  const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w->B));
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val));
+  const uint8_t *ls = a.lcp + l0 + lane * 16;
+  const uint8_t *bs = a.bwt + l0 + lane * 16;
 #pragma unroll
   for (int r = 0; r < SMAX_SEGS; r++) {
-    glds16(ls + r * 1024, wl + SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024);
-    glds16(bs + r * 1024, wb + SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024);
+    glds16(ls + r * 1024, wl + SMAX_LH + r * 1024);
+    glds16(bs + r * 1024, wb + SMAX_LH + r * 1024);
   }
-  if (wave == 0) {
-    if (lane == 0) glds16(a.lcp + l0 - SMAX_LH, wl);
-  } else if (wave == 1) {
-    if (lane < SMAX_RH / 16) glds16(a.lcp + l0 + SMAX_TILE + lane * 16, wl + SMAX_LH + SMAX_TILE);
-  } else if (wave == 2) {
-    if (lane == 0) glds16(a.bwt + l0 - SMAX_LH, wb);
-  } else {
-    if (lane < SMAX_RH / 16) glds16(a.bwt + l0 + SMAX_TILE + lane * 16, wb + SMAX_LH + SMAX_TILE);
+  if (lane == 0) {
+    glds16(a.lcp + l0 - SMAX_LH, wl);
+    glds16(a.lcp + l0 + SMAX_TILE, wl + SMAX_LH + SMAX_TILE);
+    glds16(a.bwt + l0 - SMAX_LH, wb);
+    glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
   }
-  const uint32_t k = (uint32_t) threadIdx.x;
-  if (k < n && k < SMAX_LLV_CAP)
-    glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + k) + 8, wv + wave * 256);
+  if ((uint32_t) lane < n && lane < SMAX_LLV_CAP)
+    glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + lane) + 8, wv);
 }
 
 __device__ __forceinline__ uint32_t seg_ge(const uint4 v, uint32_t mf) {
@@ -511,7 +510,7 @@ __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64
                                      const uint16_t *lrank, uint32_t nwin,
                                      GtSmaxRecord *wdst, uint32_t wcount, bool interior) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t gw = g0 + wave * SMAX_WAVE_BYTES;
+  const uint64_t gw = g0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   for (uint32_t i0 = 0; i0 < nwin && !(a.dbg & 4u); i0 += 64) {
@@ -525,7 +524,7 @@ __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64
       // fast path: start value, plateau of <= 7 rows and diversity over
       // <= 8 BWT symbols from two 8-byte LDS windows (one LDS round trip).
       // A plateau in an interior tile never reaches `end` within them.
-      const uint32_t co = SMAX_LH + wave * SMAX_WAVE_BYTES + list[i];
+      const uint32_t co = SMAX_LH + list[i];
       cc = gw + list[i];
       const uint64_t LX = lds_bytes8(sL, co);
       const uint64_t BX = lds_bytes8(t.B, co - 1);
@@ -627,12 +626,12 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
                                        bool interior, uint32_t segpre) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
-  const uint64_t gw = g0 + wave * SMAX_WAVE_BYTES;
+  const uint64_t gw = g0;
   uint32_t wcount = 0;
   uint32_t pend = 0;                 // starts queued in the list (all rounds)
 #pragma unroll 1
   for (int r = 0; r < SMAX_SEGS; r++) {
-    const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + r * 1024 + lane * 16;
+    const uint32_t so = SMAX_LH + r * 1024 + lane * 16;
     const uint64_t sg = gw + r * 1024 + lane * 16;
     uint32_t st = 0, ff = 0;
     const uint32_t crank = (interior && t.rank != nullptr) ? t.rank[so >> 4] : 0u;
@@ -696,122 +695,114 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
 }
 
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
-  __shared__ __attribute__((aligned(16))) SmaxWindow sWin[2];   // double-buffered windows
-  __shared__ __attribute__((aligned(16))) uint32_t sInfo[2][2];  // .llv {lo, n} ring
-  __shared__ uint16_t sRank[SMAX_NCHUNK];
-  __shared__ uint32_t sWave[SMAX_THREADS / 64];
-  __shared__ uint32_t sHalo[5];
-  __shared__ uint32_t sFlags;
+  // every wave is an independent worker with its own double-buffered window:
+  // no workgroup barrier anywhere in K1
+  __shared__ __attribute__((aligned(16))) SmaxWindow sWin[SMAX_THREADS / 64][2];
+  __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_THREADS / 64][2][2];
+  __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
   __shared__ uint16_t sList[SMAX_THREADS / 64][SMAX_LIST];   // per-wave start lists
   __shared__ uint16_t sLRank[SMAX_THREADS / 64][SMAX_LIST];  // .llv rank of 255-byte starts
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
-  const uint64_t stride = gridDim.x;
+  const uint64_t stride = (uint64_t) gridDim.x * (SMAX_THREADS / 64);
   const uint64_t last = a.num_tiles - 1;
 
-  uint64_t tile = blockIdx.x;
+  uint64_t tile = (uint64_t) blockIdx.x * (SMAX_THREADS / 64) + wave;
   if (tile >= a.num_tiles) return;
 
   Win t;
   win_init(t, a);
+  uint16_t *rank = sRank[wave];
 
   // prologue: .llv windows of the first two tiles, then the first window
-  const uint32_t info0 = lds_addr(&sInfo[0][0]), info1 = lds_addr(&sInfo[1][0]);
-  if (tid < 2) glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + tid, info0);
-  else if (tid >= 64 && tid < 66)
+  const uint32_t info0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
+  const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
+  if (lane < 2) {
+    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + (tile + stride <= last ? tile + stride
-                                                                               : last)) + (tid - 64),
+                                                                                : last)) + lane,
           info1);
-  if (tid == 0) sFlags = 0;
+  }
   glds_wait();
-  __syncthreads();
-  issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[0],
-               __builtin_amdgcn_readfirstlane(sInfo[0][0]),
-               __builtin_amdgcn_readfirstlane(sInfo[0][1]));
+  issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0],
+               __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
+               __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]));
 
   for (uint32_t it = 0;; it++) {
     const uint32_t cur = it & 1u;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
     const uint64_t next = tile + stride;
-    SmaxWindow *W = &sWin[cur];
+    SmaxWindow *W = &sWin[wave][cur];
     t.g0 = g0;
     t.L = W->L;
     t.B = W->B;
     t.val = W->val;
 
-    // ---- this tile's window has landed; the previous tile's readers are done
+    // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
-    __syncthreads();
-    const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[cur][0]);
-    const uint32_t wn = __builtin_amdgcn_readfirstlane(sInfo[cur][1]);
-    const uint32_t nlo = __builtin_amdgcn_readfirstlane(sInfo[cur ^ 1u][0]);
-    const uint32_t nn = __builtin_amdgcn_readfirstlane(sInfo[cur ^ 1u][1]);
-    const uint32_t so = SMAX_LH + wave * SMAX_WAVE_BYTES + lane * 16;
-    const uint4 v0 = *reinterpret_cast<const uint4 *>(&W->L[so]);
-    const uint4 v1 = *reinterpret_cast<const uint4 *>(&W->L[so + 1024]);
-    const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
-    const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
-    uint32_t hff = 0;
-    if (tid < 5) {
-      const int off = tid == 0 ? 0 : SMAX_LH + SMAX_TILE + (tid - 1) * 16;
-      hff = seg_ffcount(*reinterpret_cast<const uint4 *>(&W->L[off]));
-      sHalo[tid] = hff;
-    }
-    if ((f0 | f1 | hff) != 0) atomicOr(&sFlags, 2u);
-    __syncthreads();   // sFlags, sHalo; sInfo[cur] read by everyone
-    const bool has_ff = (sFlags & 2u) != 0 && !(a.dbg & 16u);
-    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
-    t.llv_base = wlo;
+    const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][0]);
+    const uint32_t wn = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][1]);
+    const uint32_t nlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][0]);
+    const uint32_t nn = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][1]);
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
-    // after it): in flight during all of this tile's work
+    // after it, into the ring slot just read): in flight during all of this
+    // tile's work
     if (next < a.num_tiles) {
-      issue_window(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[cur ^ 1u], nlo, nn);
+      issue_window(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u], nlo, nn);
       const uint64_t n2 = next + stride <= last ? next + stride : last;
-      if (tid < 2)
-        glds4(reinterpret_cast<const uint32_t *>(a.llv_win + n2) + tid,
-              cur ? info1 : info0);
+      if (lane < 2)
+        glds4(reinterpret_cast<const uint32_t *>(a.llv_win + n2) + lane, cur ? info1 : info0);
     }
 
-    // ---- .llv ranks of the window's 255 bytes (values already in LDS)
+    // ---- filter and .llv ranks of the window's 255 bytes (values in LDS)
+    const uint32_t so = SMAX_LH + lane * 16;
+    const uint4 v0 = *reinterpret_cast<const uint4 *>(&W->L[so]);
+    const uint4 v1 = *reinterpret_cast<const uint4 *>(&W->L[so + 1024]);
+    const uint4 hv = *reinterpret_cast<const uint4 *>(&W->L[lane == 0 ? 0 : SMAX_LH + SMAX_TILE]);
+    const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+    const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
+    const uint32_t hl = __builtin_amdgcn_readfirstlane(seg_ffcount(hv));   // lane 0: left halo
+    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
+    t.llv_base = wlo;
     t.rank = nullptr;
     t.nval = -1;
-    if (has_ff) {
-      uint32_t o0, o1, wo, tot;
-      block_scan_rows(f0, f1, &o0, &o1, &wo, &tot, sWave);
-      // chunk 0 = left halo, 1..TILE/16 = tile rows, then 4 right-halo chunks
-      const uint32_t h0 = sHalo[0];
-      const uint32_t cb = 1 + wave * (SMAX_WAVE_BYTES / 16) + lane;
-      sRank[cb] = (uint16_t) (h0 + wo + o0);
-      sRank[cb + 64] = (uint16_t) (h0 + wo + o1);
-      if (tid == 0) {
-        sRank[0] = 0;
-        uint32_t acc = h0 + tot;
-        for (int k = 0; k < 4; k++) {
-          sRank[1 + SMAX_TILE / 16 + k] = (uint16_t) acc;
-          acc += sHalo[1 + k];
-        }
+    if (__ballot((f0 | f1) != 0) != 0 || hl != 0) {
+      // chunk 0 = left halo, 1..64 segment 0, 65..128 segment 1, 129 right halo
+      const uint64_t ltm = lanemask_lt();
+      uint32_t e0 = 0, t0 = 0, e1 = 0, t1 = 0;
+#pragma unroll
+      for (int b = 0; b < 5; b++) {
+        const uint64_t p0 = __ballot((f0 >> b) & 1u), p1 = __ballot((f1 >> b) & 1u);
+        e0 += (uint32_t) __popcll(p0 & ltm) << b;
+        t0 += (uint32_t) __popcll(p0) << b;
+        e1 += (uint32_t) __popcll(p1 & ltm) << b;
+        t1 += (uint32_t) __popcll(p1) << b;
       }
+      rank[1 + lane] = (uint16_t) (hl + e0);
+      rank[65 + lane] = (uint16_t) (hl + t0 + e1);
+      if (lane == 0) {
+        rank[0] = 0;
+        rank[1 + SMAX_TILE / 16] = (uint16_t) (hl + t0 + t1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       t.nval = (int) (wn < SMAX_LLV_CAP ? wn : SMAX_LLV_CAP);
-      t.rank = sRank;
-      __syncthreads();
+      t.rank = (a.dbg & 16u) ? nullptr : rank;
     }
 
-    // ---- detection, diversity, records (per wave, row order)
-    const uint64_t slot = tile * 4 + wave;
-    GtSmaxRecord *wdst = a.slots + slot * (uint64_t) SMAX_WSLOT;
+    // ---- detection, diversity, records (row order)
+    GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
     uint32_t wcount = 0;
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
     if (wave_pre || edge)
       wcount = wave_detect(t, a, g0, W->L, sList[wave], sLRank[wave], wdst, !edge,
                            segpre_bits);
-    if (lane == 0) a.tile_count[slot] = wcount;
+    if (lane == 0) a.tile_count[tile] = wcount;
 
-    if (tid == 0) sFlags = 0;
     tile = next;
     if (tile >= a.num_tiles) break;
   }
@@ -950,9 +941,9 @@ struct GtSmaxPlan {
   uint64_t tile_first;
   uint32_t grid, compact_grid;
   GtSmaxRecord *out;         // capacity records, ascending lb
-  GtSmaxRecord *slots;       // num_tiles * 4 * SMAX_WSLOT
-  uint32_t *tile_count;      // num_tiles * 4
-  uint64_t *tile_off;        // num_tiles * 4
+  GtSmaxRecord *slots;       // num_tiles * SMAX_WSLOT
+  uint32_t *tile_count;      // num_tiles
+  uint64_t *tile_off;        // num_tiles
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
@@ -1049,18 +1040,19 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu;
     const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
     if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
-    p->grid = (uint32_t) (g < p->num_tiles ? g : p->num_tiles);
+    const uint64_t wg = ((uint64_t) p->num_tiles + 3) / 4;   // workgroups with a tile per wave
+    p->grid = (uint32_t) (g < wg ? g : wg);
     if (getenv("GT_SMAX_VERBOSE"))
       fprintf(stderr, "gt_smax: K1 %d CUs x %d blocks/CU -> grid %u, %u tiles\n", dev_cus,
               per_cu, p->grid, p->num_tiles);
-    const uint64_t cg = (uint64_t) p->num_tiles;              // 4 slots per block
+    const uint64_t cg = ((uint64_t) p->num_tiles + 3) / 4;   // one wave per tile slot
     p->compact_grid = (uint32_t) (cg < 4096 ? (cg ? cg : 1) : 4096);
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
-  HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * 4 * (uint64_t) p->num_tiles));
-  HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * 4 * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
 
-  HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * 4 * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
   HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
@@ -1071,7 +1063,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
   HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
-                                 (uint64_t) 0, (size_t) p->num_tiles * 4,
+                                 (uint64_t) 0, (size_t) p->num_tiles,
                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
   HIPCHK(hipMalloc(&p->scan_tmp, p->scan_tmp_bytes ? p->scan_tmp_bytes : 16));
   HIPCHK(hipMalloc(&derr, sizeof (uint32_t)));
@@ -1158,10 +1150,10 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
     size_t bytes = p->scan_tmp_bytes;
     HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->tile_count, p->tile_off,
-                                   (uint64_t) 0, (size_t) p->num_tiles * 4,
+                                   (uint64_t) 0, (size_t) p->num_tiles,
                                    rocprim::plus<uint64_t>(), s));
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->slots, p->tile_count, p->tile_off, (uint64_t) p->num_tiles * 4,
+                       p->slots, p->tile_count, p->tile_off, (uint64_t) p->num_tiles,
                        p->out, p->capacity, p->count);
     HIPCHK(hipGetLastError());
   }
