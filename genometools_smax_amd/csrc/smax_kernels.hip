@@ -237,41 +237,6 @@ __device__ __forceinline__ bool seen_add(Seen &s, uint32_t c) {
   return (cur & bit) != 0;
 }
 
-// Exclusive prefix of per-(segment, lane) counts in row order within the
-// block (a wave's rows are segment-major, then lane): per-segment offsets
-// inside the wave, the wave's offset inside the block, the block total.
-__device__ __forceinline__ void block_scan_rows(const uint32_t c0, const uint32_t c1,
-                                                uint32_t *o0, uint32_t *o1,
-                                                uint32_t *wave_off, uint32_t *total,
-                                                uint32_t *sWave) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t ltm = (1ull << lane) - 1;
-  uint32_t e0 = 0, t0 = 0, e1 = 0, t1 = 0;
-  // counts <= 16 per lane and segment: prefix over bit planes
-#pragma unroll
-  for (int b = 0; b < 5; b++) {
-    const uint64_t p0 = __ballot((c0 >> b) & 1u), p1 = __ballot((c1 >> b) & 1u);
-    e0 += (uint32_t) __popcll(p0 & ltm) << b;
-    t0 += (uint32_t) __popcll(p0) << b;
-    e1 += (uint32_t) __popcll(p1 & ltm) << b;
-    t1 += (uint32_t) __popcll(p1) << b;
-  }
-  *o0 = e0;
-  *o1 = t0 + e1;
-  const uint32_t wt = t0 + t1;
-  if (lane == 0) sWave[wave] = wt;
-  __syncthreads();
-  uint32_t wo = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < SMAX_THREADS / 64; w++) {
-    const uint32_t ws = sWave[w];
-    if (w < wave) wo += ws;
-    tot += ws;
-  }
-  *wave_off = wo;
-  *total = tot;
-}
-
 // ------------------------------------------------------------ K0: head run
 
 // One lane: the boundary record's head (run of LCP == LCP[begin]), reset of
@@ -509,7 +474,7 @@ __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64
                                      const uint8_t *sL, const uint16_t *list,
                                      const uint16_t *lrank, uint32_t nwin,
                                      GtSmaxRecord *wdst, uint32_t wcount, bool interior) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   const uint64_t gw = g0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -624,7 +589,7 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
                                        const uint8_t *sL, uint16_t *list, uint16_t *lrank,
                                        GtSmaxRecord *wdst,
                                        bool interior, uint32_t segpre) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint64_t gw = g0;
   uint32_t wcount = 0;
@@ -820,23 +785,45 @@ __global__ void __launch_bounds__(SMAX_THREADS) smax_scan_kernel_w3(SmaxScanArgs
 
 // ------------------------------------------------------------ K3: compact
 
-// One wave per (tile, wave) slot, grid-stride: copy the slot's records (row
-// order) to their final position (exclusive scan of the slot counts) ->
-// ascending lb overall.  Also publishes the total.
+// One workgroup per SMAX_CPB consecutive tile slots: the slots' counts are
+// scanned in LDS, then all 256 threads copy the slots' records to their final
+// positions (slot found by binary search in the LDS prefix), consecutive
+// threads on consecutive output records -> ascending lb overall, coalesced.
+// Also publishes the total.
+#define SMAX_CPB 256
 __global__ void __launch_bounds__(256)
 smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
                     const uint64_t *slot_off, uint64_t nslots, GtSmaxRecord *out,
                     uint64_t capacity, uint64_t *count) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t wave = (blockIdx.x * (uint64_t) blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t) gridDim.x * blockDim.x) >> 6;
-  for (uint64_t sl = wave; sl < nslots; sl += nwaves) {
-    const uint32_t cnt = slot_count[sl];
-    const uint64_t off = slot_off[sl];
-    if (sl == nslots - 1 && lane == 0) *count = off + cnt;
-    const GtSmaxRecord *src = slots + sl * (uint64_t) SMAX_WSLOT;
-    for (uint32_t i = lane; i < cnt; i += 64)
-      if (off + i < capacity) out[off + i] = src[i];
+  __shared__ uint32_t sPre[SMAX_CPB + 1];
+  __shared__ uint32_t sWave[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t s0 = blockIdx.x * (uint64_t) SMAX_CPB;
+  const uint32_t c = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
+  const uint64_t base = slot_off[s0];
+  uint32_t incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) sWave[wave] = incl;
+  __syncthreads();
+  uint32_t wo = 0;
+  for (int w = 0; w < wave; w++) wo += sWave[w];
+  sPre[tid + 1] = wo + incl;
+  if (tid == 0) sPre[0] = 0;
+  __syncthreads();
+  const uint32_t total = sPre[SMAX_CPB];
+  if (tid == 0 && s0 + SMAX_CPB >= nslots) *count = base + total;
+  for (uint32_t r = tid; r < total; r += 256) {
+    uint32_t lo = 0, hi = SMAX_CPB;          // largest j with sPre[j] <= r
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sPre[mid] <= r) lo = mid; else hi = mid;
+    }
+    if (base + r < capacity)
+      out[base + r] = slots[(s0 + lo) * (uint64_t) SMAX_WSLOT + (r - sPre[lo])];
   }
 }
 
@@ -1048,8 +1035,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     if (getenv("GT_SMAX_VERBOSE"))
       fprintf(stderr, "gt_smax: K1 %d CUs x %d blocks/CU -> grid %u, %u tiles\n", dev_cus,
               per_cu, p->grid, p->num_tiles);
-    const uint64_t cg = ((uint64_t) p->num_tiles + 3) / 4;   // one wave per tile slot
-    p->compact_grid = (uint32_t) (cg < 4096 ? (cg ? cg : 1) : 4096);
+    p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
