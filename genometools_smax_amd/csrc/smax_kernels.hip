@@ -466,102 +466,118 @@ __device__ __forceinline__ bool diverse8(uint64_t X, uint32_t w) {
   return true;
 }
 
-// Evaluate list[0 .. nwin) (row offsets inside the wave, row order), 64
-// starts per step, one per lane: exact plateau end in LDS, local-maximum
-// test, left diversity over BWT[lb..rb], the pending plateau at the shard
-// end; accepted records are appended in row order to the wave's slot.
+// Exact evaluation of one plateau start (row offset `ro` inside the tile, its
+// .llv rank `rk` when its LCP byte is 255): *cur = LCP value, *j = last row of
+// the plateau; returns whether [c-1 .. j] is a supermaximal-repeat interval.
+// Interior tiles take the fast path (start value, plateau of <= 7 rows and
+// diversity over <= 8 BWT symbols from two 8-byte LDS windows, one LDS round
+// trip; a plateau in an interior tile never reaches `end` within them);
+// everything else the exact generic path, which also records the pending
+// plateau at the shard end.  A 255-byte start whose predecessor is also 255
+// is only a start if its exact value is larger (checked here).
+__device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t g0,
+                                  const uint8_t *sL, uint32_t ro, uint32_t rk, bool interior,
+                                  uint32_t *curo, uint64_t *jo) {
+  const uint64_t cc = g0 + ro;
+  bool acc = false, slow = !interior;
+  uint32_t cur = 0;
+  uint64_t j = cc;
+  if (interior) {
+    const uint32_t co = SMAX_LH + ro;
+    const uint64_t LX = lds_bytes8(sL, co);
+    const uint64_t BX = lds_bytes8(t.B, co - 1);
+    const uint32_t cb = (uint32_t) LX & 0xffu;
+    if (cb == 255) {
+      // .llv start: exact values by rank; a run of equal values >= 255
+      // is a run of 255 bytes, so its ranks are consecutive
+      if (t.rank == nullptr) {
+        slow = true;
+      } else {
+        const uint32_t v = llv_by_rank(t, rk);
+        const bool start = sL[co - 1] != 255 || llv_by_rank(t, rk - 1) < v;
+        if (start && v >= a.minlen) {
+          cur = v;
+          uint32_t k = 0;
+          int rel = 0;
+          for (; k < 7; k++) {
+            const uint32_t nb = (uint32_t) (LX >> (8 * (k + 1))) & 0xffu;
+            if (nb != 255) { rel = -1; break; }
+            const uint32_t nv = llv_by_rank(t, rk + k + 1);
+            if (nv != v) { rel = nv < v ? -1 : 1; break; }
+          }
+          if (rel == 0) {
+            slow = true;
+          } else {
+            j = cc + k;
+            if (rel < 0) acc = diverse8(BX, k + 2);
+          }
+        }
+      }
+    } else if (cb >= a.minlen) {
+      cur = cb;
+      const uint64_t nx = LX >> 8;
+      const uint64_t ne = ~bytes_eq64(nx, cb * 0x0101010101010101ull) &
+                          0x0080808080808080ull;
+      if (ne == 0) {
+        slow = true;
+      } else {
+        const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
+        const uint32_t nb = (uint32_t) (nx >> (8 * k)) & 0xffu;
+        j = cc + k;
+        if (nb < cb) acc = diverse8(BX, k + 2);
+      }
+    }
+  }
+  if (slow && !(a.dbg & 32u)) {
+    acc = false;
+    cur = lcp_exact(t, cc);
+    const bool start = !interior || lcp_exact(t, cc - 1) < cur;
+    if (start && cur >= a.minlen) {
+      int rel;
+      bool pend;
+      j = plateau_end(t, cc, cur, &rel, &pend);
+      if (pend) {
+        Seen sn = {0, 0, 0, 0};
+        bool dup = false;
+        for (uint64_t g = cc - 1; g < a.end && !dup; g++) dup = seen_add(sn, bwt_at(t, g));
+        if (!dup) {
+          GtSmaxBoundary *b = a.bnd;
+          b->pend_c = cc;
+          b->pend_lcp = cur;
+          b->pend_div.seen[0] = sn.w0; b->pend_div.seen[1] = sn.w1;
+          b->pend_div.seen[2] = sn.w2; b->pend_div.seen[3] = sn.w3;
+          b->pend_div.dup = 0;
+          b->pend_valid = 1;
+        }
+      } else if (rel < 0) {
+        acc = diverse_rows(t, cc - 1, j);
+      }
+    }
+  }
+  *curo = cur;
+  *jo = j;
+  return acc;
+}
+
+// Evaluate list[0 .. nwin) (row offsets inside the tile, row order), 64
+// starts per step, one per lane; accepted records are appended in row order
+// to the tile's slot.
 __device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64_t g0,
                                      const uint8_t *sL, const uint16_t *list,
                                      const uint16_t *lrank, uint32_t nwin,
                                      GtSmaxRecord *wdst, uint32_t wcount, bool interior) {
   const int lane = threadIdx.x & 63;
-  const uint64_t gw = g0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   for (uint32_t i0 = 0; i0 < nwin && !(a.dbg & 4u); i0 += 64) {
     const uint32_t i = i0 + lane;
     bool acc = false;
-    uint64_t cc = 0;
     uint32_t cur = 0;
     uint64_t j = 0;
-    bool slow = i < nwin && !interior;
-    if (interior && i < nwin) {
-      // fast path: start value, plateau of <= 7 rows and diversity over
-      // <= 8 BWT symbols from two 8-byte LDS windows (one LDS round trip).
-      // A plateau in an interior tile never reaches `end` within them.
-      const uint32_t co = SMAX_LH + list[i];
-      cc = gw + list[i];
-      const uint64_t LX = lds_bytes8(sL, co);
-      const uint64_t BX = lds_bytes8(t.B, co - 1);
-      const uint32_t cb = (uint32_t) LX & 0xffu;
-      if (cb == 255) {
-        // .llv start: exact values by rank; a run of equal values >= 255
-        // is a run of 255 bytes, so its ranks are consecutive
-        if (t.rank == nullptr) {
-          slow = true;
-        } else {
-          const uint32_t r = lrank[i];       // queued with the start
-          const uint32_t v = llv_by_rank(t, r);
-          if (v >= a.minlen) {
-            cur = v;
-            uint32_t k = 0;
-            int rel = 0;
-            for (; k < 7; k++) {
-              const uint32_t nb = (uint32_t) (LX >> (8 * (k + 1))) & 0xffu;
-              if (nb != 255) { rel = -1; break; }
-              const uint32_t nv = llv_by_rank(t, r + k + 1);
-              if (nv != v) { rel = nv < v ? -1 : 1; break; }
-            }
-            if (rel == 0) {
-              slow = true;
-            } else {
-              j = cc + k;
-              if (rel < 0) acc = diverse8(BX, k + 2);
-            }
-          }
-        }
-      } else if (cb >= a.minlen) {
-        cur = cb;
-        const uint64_t nx = LX >> 8;
-        const uint64_t ne = ~bytes_eq64(nx, cb * 0x0101010101010101ull) &
-                            0x0080808080808080ull;
-        if (ne == 0) {
-          slow = true;
-        } else {
-          const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
-          const uint32_t nb = (uint32_t) (nx >> (8 * k)) & 0xffu;
-          j = cc + k;
-          if (nb < cb) acc = diverse8(BX, k + 2);
-        }
-      }
-    }
-    if (slow && !(a.dbg & 32u)) {
-      cc = gw + list[i];
-      cur = lcp_exact(t, cc);
-      if (cur >= a.minlen) {
-        int rel;
-        bool pend;
-        j = plateau_end(t, cc, cur, &rel, &pend);
-        if (pend) {
-          Seen sn = {0, 0, 0, 0};
-          bool dup = false;
-          for (uint64_t g = cc - 1; g < a.end && !dup; g++) dup = seen_add(sn, bwt_at(t, g));
-          if (!dup) {
-            GtSmaxBoundary *b = a.bnd;
-            b->pend_c = cc;
-            b->pend_lcp = cur;
-            b->pend_div.seen[0] = sn.w0; b->pend_div.seen[1] = sn.w1;
-            b->pend_div.seen[2] = sn.w2; b->pend_div.seen[3] = sn.w3;
-            b->pend_div.dup = 0;
-            b->pend_valid = 1;
-          }
-        } else if (rel < 0) {
-          acc = diverse_rows(t, cc - 1, j);
-        }
-      }
-    }
+    if (i < nwin) acc = eval_start(t, a, g0, sL, list[i], lrank[i], interior, &cur, &j);
     const uint64_t am = __ballot(acc);
     if (acc) {
+      const uint64_t cc = g0 + list[i];
       GtSmaxRecord rec;
       rec.lb = cc - 1;
       rec.lcp = cur;
