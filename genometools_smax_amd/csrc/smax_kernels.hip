@@ -52,7 +52,7 @@
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
 #define SMAX_LLV_CAP 64                               // .llv values in LDS (1 per lane)
-#define SMAX_LIST 128                                 // per-wave start-list window
+#define SMAX_LIST 96                                  // per-wave start-list window
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
                                                       // records are >= 2 rows apart)
 
@@ -60,6 +60,7 @@ static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
 static_assert(GT_SMAX_PAD_FRONT >= SMAX_LH, "front padding covers the halo");
 static_assert(SMAX_LDSB % 16 == 0, "window is whole 16-byte chunks");
+static_assert(SMAX_LIST % 2 == 0, "u16 list pairs");
 
 struct SmaxScanArgs {
   const uint8_t *lcp;        // local tables: index i <-> global base+i
@@ -675,14 +676,195 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
   return wcount;
 }
 
+// ---- interior tiles: SWAR classification of every plateau start
+//
+// Most supermaximal-repeat intervals are two rows wide (a plateau of one
+// row: LCP[c-1] < LCP[c] > LCP[c+1]); their whole predicate is byte-local, so
+// each lane decides them for its 16 rows with SWAR compares on the LCP bytes
+// c-1, c, c+1 and the BWT bytes c-1, c ("D" rows).  Only starts that need
+// exact values or a longer scan -- a 255 LCP byte (.llv value), or a plateau
+// of >= 2 rows (LCP[c+1] == LCP[c]) -- are queued ("L" rows) and evaluated
+// exactly, 64 at a time (eval_start).  Records are then written in row
+// order by their owning lanes.
+#define SMAX_DLIST 64                                 // queued exact starts per tile
+
+static_assert(2 * SMAX_LIST * 2 <= 3 * SMAX_DLIST * 4, "wave_detect list fits the queue");
+
+// high bit of each byte >= 254 (WILDCARD / SEPARATOR / UNDEFBWTCHAR)
+__device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0x01010101u); }
+
+__device__ __forceinline__ void classify_segment(const uint8_t *L, const uint8_t *B, uint32_t so,
+                                                 uint32_t mf, bool all_exact, uint32_t *Dm,
+                                                 uint32_t *Lm, uint32_t *Fm) {
+  const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
+  const uint4 bv = *reinterpret_cast<const uint4 *>(&B[so]);
+  const uint32_t pb = L[so - 1], nb = L[so + 16], bp = B[so - 1];
+  const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+  const uint32_t b0 = bv.x, b1 = bv.y, b2 = bv.z, b3 = bv.w;
+  uint32_t D = 0, Lr = 0, F = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t cur = k == 0 ? w0 : k == 1 ? w1 : k == 2 ? w2 : w3;
+    const uint32_t prv = k == 0 ? ((w0 << 8) | pb)
+                       : __builtin_amdgcn_alignbyte(cur, k == 1 ? w0 : k == 2 ? w1 : w2, 3);
+    const uint32_t nxt = k == 3 ? ((w3 >> 8) | (nb << 24))
+                       : __builtin_amdgcn_alignbyte(k == 0 ? w1 : k == 1 ? w2 : w3, cur, 1);
+    const uint32_t bc = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : b3;
+    const uint32_t bpv = k == 0 ? ((b0 << 8) | bp)
+                       : __builtin_amdgcn_alignbyte(bc, k == 1 ? b0 : k == 2 ? b1 : b2, 3);
+    const uint32_t ff = bytes_ff(cur);
+    // start: LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] > LCP[c-1];
+    // a 255/255 pair is a possible start, settled exactly by eval_start
+    const uint32_t A = bytes_ge(cur, mf) & (bytes_lt(prv, cur) | (ff & bytes_ff(prv)));
+    const uint32_t eqn = bytes_eq(nxt, cur);
+    uint32_t d = A & ~ff & bytes_lt(nxt, cur) &
+                 (~bytes_eq(bpv, bc) | bytes_sp(bpv) | bytes_sp(bc)) & 0x80808080u;
+    uint32_t l = A & (ff | eqn);
+    if (all_exact) { d = 0; l = A; }
+    D |= pack4(d) << (4 * k);
+    Lr |= pack4(l) << (4 * k);
+    F |= pack4(ff) << (4 * k);
+  }
+  *Dm = D;
+  *Lm = Lr;
+  *Fm = F;
+}
+
+// exclusive prefix over the wave's lanes and total of a per-lane count < 32
+__device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
+  const uint64_t ltm = lanemask_lt();
+  uint32_t e = 0, t = 0;
+#pragma unroll
+  for (int b = 0; b < 5; b++) {
+    const uint64_t pl = __ballot((c >> b) & 1u);
+    e += (uint32_t) __popcll(pl & ltm) << b;
+    t += (uint32_t) __popcll(pl) << b;
+  }
+  *tot = t;
+  return e;
+}
+
+// Returns the tile's record count, or UINT32_MAX when more than SMAX_DLIST
+// starts need exact evaluation (the caller then runs wave_detect).
+// Only the tile's 16-row segments holding a byte >= min(minlen,128) are
+// classified: they are compacted (row order) so that each classification
+// step keeps all 64 lanes busy (about a third of the segments are active on
+// repeat-rich DNA, so one step usually covers the whole tile).
+__device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &a, uint64_t g0,
+                                              const uint8_t *sL, uint32_t *ent,
+                                              GtSmaxRecord *wdst, uint32_t segpre) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
+  const bool all_exact = a.minlen > 128;
+  uint32_t *res_lcp = ent + SMAX_DLIST, *res_w = ent + 2 * SMAX_DLIST;
+  uint8_t *segl = reinterpret_cast<uint8_t *>(ent + 3 * SMAX_DLIST);
+  // compact the active segments (id = round * 64 + lane, row order)
+  const uint64_t ltm = lanemask_lt();
+  const uint64_t m0 = __ballot(segpre & 1u), m1 = __ballot((segpre >> 1) & 1u);
+  const uint32_t n0 = (uint32_t) __popcll(m0), nseg = n0 + (uint32_t) __popcll(m1);
+  if (segpre & 1u) segl[__popcll(m0 & ltm)] = (uint8_t) lane;
+  if (segpre & 2u) segl[n0 + __popcll(m1 & ltm)] = (uint8_t) (64 + lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  uint32_t Dm0 = 0, Lm0 = 0, Dm1 = 0, Lm1 = 0, Lpre0 = 0, Lpre1 = 0, ro0 = 0, ro1 = 0;
+  uint32_t nL = 0;
+  const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if ((uint32_t) k >= nsteps) break;
+    const uint32_t i = k * 64 + lane;
+    uint32_t D = 0, Lq = 0, F = 0, ro = 0;
+    if (i < nseg) {
+      const uint32_t sid = segl[i];
+      ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
+      const uint32_t so = SMAX_LH + ro;
+      classify_segment(sL, t.B, so, mf, all_exact, &D, &Lq, &F);
+      const uint64_t sg = g0 + ro;
+      if (sg < a.begin) {
+        const uint32_t m = sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
+        D &= m;
+        Lq &= m;
+      }
+    }
+    uint32_t tot;
+    const uint32_t excl = wave_excl((uint32_t) __popc(Lq), &tot);
+    if (nL + tot <= SMAX_DLIST && Lq != 0) {
+      const uint32_t crank = (F != 0 && t.rank != nullptr) ? t.rank[(SMAX_LH + ro) >> 4] : 0u;
+      uint32_t pos = nL + excl, bits = Lq;
+      while (bits) {
+        const int q = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const uint32_t rk = ((F >> q) & 1u) ? crank + (uint32_t) __popc(F & ((1u << q) - 1)) : 0u;
+        ent[pos++] = (ro + (uint32_t) q) | (rk << 16);
+      }
+    }
+    if (k == 0) { Dm0 = D; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
+    else { Dm1 = D; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
+    nL += tot;
+  }
+  if (nL > SMAX_DLIST) return UINT32_MAX;
+  if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
+  // exact evaluation of the queued starts (one per lane)
+  if (nL != 0 && !(a.dbg & 4u)) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if ((uint32_t) lane < nL) {
+      const uint32_t e = ent[lane];
+      const uint32_t ro = e & 0xffffu;
+      uint32_t cur;
+      uint64_t j;
+      const bool acc = eval_start(t, a, g0, sL, ro, e >> 16, true, &cur, &j);
+      res_lcp[lane] = acc ? cur : 0u;
+      res_w[lane] = (uint32_t) (j - (g0 + ro) + 2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // records in row order, written by the owning lanes
+  uint32_t wcount = 0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if ((uint32_t) k >= nsteps) break;
+    const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1;
+    const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
+    uint32_t acc = D, bits = Lq, idx = Lpre;
+    while (bits) {
+      const int q = __builtin_ctz(bits);
+      bits &= bits - 1;
+      if (res_lcp[idx++] != 0) acc |= 1u << q;
+    }
+    uint32_t tot;
+    uint32_t pos = wcount + wave_excl((uint32_t) __popc(acc), &tot);
+    bits = acc;
+    while (bits) {
+      const int q = __builtin_ctz(bits);
+      bits &= bits - 1;
+      GtSmaxRecord rec;
+      rec.lb = g0 + ro + q - 1;
+      if ((D >> q) & 1u) {
+        rec.lcp = sL[SMAX_LH + ro + q];
+        rec.width = 2;
+      } else {
+        const uint32_t i = Lpre + (uint32_t) __popc(Lq & ((1u << q) - 1));
+        rec.lcp = res_lcp[i];
+        rec.width = res_w[i];
+      }
+      wdst[pos++] = rec;
+    }
+    wcount += tot;
+  }
+  return wcount;
+}
+
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   // every wave is an independent worker with its own double-buffered window:
   // no workgroup barrier anywhere in K1
   __shared__ __attribute__((aligned(16))) SmaxWindow sWin[SMAX_THREADS / 64][2];
   __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_THREADS / 64][2][2];
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
-  __shared__ uint16_t sList[SMAX_THREADS / 64][SMAX_LIST];   // per-wave start lists
-  __shared__ uint16_t sLRank[SMAX_THREADS / 64][SMAX_LIST];  // .llv rank of 255-byte starts
+  // per wave: wave_detect's start list + ranks (2 x SMAX_LIST u16), or
+  // wave_detect_direct's queue and results (3 x SMAX_DLIST u32)
+  __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * SMAX_DLIST + 2 * 64 / 4];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -779,9 +961,11 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
     uint32_t wcount = 0;
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-    if (wave_pre || edge)
-      wcount = wave_detect(t, a, g0, W->L, sList[wave], sLRank[wave], wdst, !edge,
-                           segpre_bits);
+    uint16_t *qlist = reinterpret_cast<uint16_t *>(sQueue[wave]);
+    if (!edge && wave_pre && !(a.dbg & 128u))
+      wcount = wave_detect_direct(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
+    if (edge || (wave_pre && ((a.dbg & 128u) || wcount == UINT32_MAX)))
+      wcount = wave_detect(t, a, g0, W->L, qlist, qlist + SMAX_LIST, wdst, !edge, segpre_bits);
     if (lane == 0) a.tile_count[tile] = wcount;
 
     tile = next;

@@ -55,3 +55,12 @@ lm = np.zeros(len(idx), dtype=bool)
 endj = np.minimum(idx + nxt, rows - 1)
 lm = L[endj] < L[idx]
 print("local maxima among starts: %.3f  (width mean %.2f)" % (lm.mean(), (nxt[lm] + 1).mean()))
+nxt1 = L[np.minimum(idx + 1, rows - 1)]
+eqn = nxt1 == L[idx]
+ffs = L[idx] == 255
+print("starts with LCP[c+1]==LCP[c]: %.3f   with 255 byte: %.3f   -> exact queue %.3f" %
+      (eqn.mean(), ffs.mean(), (eqn | ffs).mean()))
+per_tile = np.bincount((idx[eqn | ffs] // 2048), minlength=rows // 2048 + 1)
+print("exact-queue starts per 2048-row tile: mean %.1f p50 %d p90 %d p99 %d max %d; tiles > 64: %.4f" %
+      (per_tile.mean(), np.percentile(per_tile, 50), np.percentile(per_tile, 90),
+       np.percentile(per_tile, 99), per_tile.max(), (per_tile > 64).mean()))
