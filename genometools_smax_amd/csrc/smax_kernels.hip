@@ -51,7 +51,7 @@
 #define SMAX_RH 16                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
-#define SMAX_LLV_CAP 64                               // .llv values in LDS (1 per lane)
+#define SMAX_LLV_CAP 56                               // .llv values in LDS (1 per lane)
 #define SMAX_LIST 96                                  // per-wave start-list window
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
                                                       // records are >= 2 rows apart)
@@ -758,6 +758,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   const bool all_exact = a.minlen > 128;
   uint32_t *res_lcp = ent + SMAX_DLIST, *res_w = ent + 2 * SMAX_DLIST;
   uint8_t *segl = reinterpret_cast<uint8_t *>(ent + 3 * SMAX_DLIST);
+  // accepted exact starts, one 16-bit row mask per compacted segment
+  uint32_t *accw = ent + 3 * SMAX_DLIST + 2 * 64 / 4;
   // compact the active segments (id = round * 64 + lane, row order)
   const uint64_t ltm = lanemask_lt();
   const uint64_t m0 = __ballot(segpre & 1u), m1 = __ballot((segpre >> 1) & 1u);
@@ -795,7 +797,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         const int q = __builtin_ctz(bits);
         bits &= bits - 1;
         const uint32_t rk = ((F >> q) & 1u) ? crank + (uint32_t) __popc(F & ((1u << q) - 1)) : 0u;
-        ent[pos++] = (ro + (uint32_t) q) | (rk << 16);
+        ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
       }
     }
     if (k == 0) { Dm0 = D; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
@@ -804,18 +806,21 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   }
   if (nL > SMAX_DLIST) return UINT32_MAX;
   if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
-  // exact evaluation of the queued starts (one per lane)
+  // exact evaluation of the queued starts (one per lane); accepted ones set
+  // their row bit in their segment's mask
   if (nL != 0 && !(a.dbg & 4u)) {
+    accw[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if ((uint32_t) lane < nL) {
       const uint32_t e = ent[lane];
-      const uint32_t ro = e & 0xffffu;
+      const uint32_t ro = e & 0x7ffu, si = (e >> 11) & 0x7fu;
       uint32_t cur;
       uint64_t j;
-      const bool acc = eval_start(t, a, g0, sL, ro, e >> 16, true, &cur, &j);
-      res_lcp[lane] = acc ? cur : 0u;
+      const bool acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
+      res_lcp[lane] = cur;
       res_w[lane] = (uint32_t) (j - (g0 + ro) + 2);
+      if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -827,15 +832,12 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     if ((uint32_t) k >= nsteps) break;
     const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1;
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
-    uint32_t acc = D, bits = Lq, idx = Lpre;
-    while (bits) {
-      const int q = __builtin_ctz(bits);
-      bits &= bits - 1;
-      if (res_lcp[idx++] != 0) acc |= 1u << q;
-    }
+    const uint32_t si = k * 64 + lane;
+    uint32_t acc = D;
+    if (Lq != 0 && !(a.dbg & 4u)) acc |= (accw[si >> 1] >> (16u * (si & 1u))) & 0xffffu;
     uint32_t tot;
     uint32_t pos = wcount + wave_excl((uint32_t) __popc(acc), &tot);
-    bits = acc;
+    uint32_t bits = acc;
     while (bits) {
       const int q = __builtin_ctz(bits);
       bits &= bits - 1;
@@ -864,7 +866,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
   // per wave: wave_detect's start list + ranks (2 x SMAX_LIST u16), or
   // wave_detect_direct's queue and results (3 x SMAX_DLIST u32)
-  __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * SMAX_DLIST + 2 * 64 / 4];
+  __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * SMAX_DLIST + 2 * 64 / 4 + 64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
