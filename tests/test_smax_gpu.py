@@ -124,3 +124,40 @@ def test_errors_are_reported():
         G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.n + 5, 8)
     with pytest.raises(G.SmaxError):
         G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 0)
+
+
+def _triplicated_text(rng, nwords):
+    # words occurring three times, each copy closed by a separator: every
+    # suffix inside a word shares exactly the rest of the word with its two
+    # copies, so a third of the suffix rows are plateaus of 2 rows -- far more
+    # exact-evaluation starts per tile than the direct path queues
+    parts = []
+    for _ in range(nwords):
+        w = rng.integers(0, 4, int(rng.integers(24, 40)), dtype=np.uint8)
+        for _ in range(3 if rng.random() < 0.8 else 2):
+            parts.append(w)
+            parts.append(np.array([255], dtype=np.uint8))
+    return np.concatenate(parts)
+
+
+def test_exact_queue_overflow_falls_back():
+    rng = np.random.default_rng(11)
+    e = O.Esa(_triplicated_text(rng, 1500))
+    for minlen in (2, 10, 20):
+        want = _cpu(e, minlen)
+        for shards in (1, 3):
+            assert np.array_equal(_gpu(e, minlen, shards), want), (minlen, shards)
+
+
+@pytest.mark.parametrize("dbg", [64, 128])
+def test_detection_paths_agree(monkeypatch, dbg):
+    # GT_SMAX_DEBUG=128: every interior tile through the start-list path;
+    # 64: every tile through the exact edge path.  Same answers required.
+    monkeypatch.setenv("GT_SMAX_DEBUG", str(dbg))
+    e = oracle_esa("at1MB")
+    for minlen in (5, 20, 256):
+        assert np.array_equal(_gpu(e, minlen, 2), _cpu(e, minlen)), minlen
+    rng = np.random.default_rng(5)
+    e2 = O.Esa(_repetitive_text(rng, 60000, 0.001))
+    for minlen in (3, 20, 300):
+        assert np.array_equal(_gpu(e2, minlen), _cpu(e2, minlen)), minlen
