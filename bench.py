@@ -58,6 +58,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=3_200_000_000,
                     help="max suffix rows timed on the CPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: stage the boundary records through host memory (multi-rank "
+                         "rehearsal on one GPU; the measured configuration is nccl = RCCL)")
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="all ranks on cuda:0 (rehearsal only)")
     args = ap.parse_args()
 
     import numpy as np
@@ -78,11 +83,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world))
+    if args.one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     # ---- setup (untimed): synthetic genome -> GPU ESA
     t0 = time.time()
@@ -103,15 +113,26 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
     send = recv = None
+    staged = world > 1 and args.dist_backend == "gloo"
     if world > 1:
         send = torch.zeros(G.BOUNDARY_BYTES, dtype=torch.uint8, device="cuda")
         recv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8, device="cuda")
+        if staged:
+            hsend = torch.zeros(G.BOUNDARY_BYTES, dtype=torch.uint8)
+            hrecv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8)
 
     def step():
         plan.run(sptr)
         if world > 1:
+            # the one exchange step: all-gather of the fixed-size boundary
+            # records, then the stitch kernel resolves spanning plateaus
             plan.copy_boundary(send.data_ptr(), sptr)
-            dist.all_gather_into_tensor(recv, send)
+            if staged:
+                hsend.copy_(send)
+                dist.all_gather_into_tensor(hrecv, hsend)
+                recv.copy_(hrecv)
+            else:
+                dist.all_gather_into_tensor(recv, send)
             plan.stitch(recv.data_ptr(), world, rank, sptr)
 
     # first pass sizes the output exactly (re-plan on overflow)
@@ -155,7 +176,7 @@ def main():
     alg_bytes = 2 * rows + 16 * llv_here + 16 * plan.fetch_count()
 
     stats = torch.tensor([elapsed, float(count), k1_ms / max(k1_n, 1)], dtype=torch.float64,
-                         device="cuda")
+                         device="cpu" if staged else "cuda")
     if dist:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
