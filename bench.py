@@ -229,7 +229,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": cfg["workload"], "minlen": minlen, "totallength": n,
                        "nonspecials": N, "llv_entries": esa.numllv, "global_batch": N,
-                       "parallelism": "sa-range-shard x%d + RCCL all-gather stitch" % world
+                       "parallelism": "sa-range-shard x%d + %s all-gather stitch"
+                       % (world, "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)")
                        if world > 1 else "single GPU"},
             "smax_intervals": count,
             "supermax_repeats_per_s": count / (elapsed / args.steps),
