@@ -851,7 +851,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         rec.lcp = res_lcp[i];
         rec.width = res_w[i];
       }
-      wdst[pos++] = rec;
+      if (!(a.dbg & 4096u)) wdst[pos] = rec;
+      pos++;
     }
     wcount += tot;
   }
@@ -968,7 +969,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
       wcount = wave_detect_direct(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
     if (edge || (wave_pre && ((a.dbg & 128u) || wcount == UINT32_MAX)))
       wcount = wave_detect(t, a, g0, W->L, qlist, qlist + SMAX_LIST, wdst, !edge, segpre_bits);
-    if (lane == 0) a.tile_count[tile] = wcount;
+    if (lane == 0 && !(a.dbg & 4096u)) a.tile_count[tile] = wcount;
 
     tile = next;
     if (tile >= a.num_tiles) break;
@@ -1336,7 +1337,12 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     if (p->dbg & 256u)
       hipLaunchKernelGGL(smax_scan_kernel_w3, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
     else
-      hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
+      {
+        // diagnostic: extra dynamic LDS lowers residency (occupancy sensitivity)
+        const char *pad = getenv("GT_SMAX_LDS_PAD");
+        const unsigned lp = pad ? (unsigned) strtoul(pad, NULL, 0) : 0u;
+        hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+      }
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
     size_t bytes = p->scan_tmp_bytes;
