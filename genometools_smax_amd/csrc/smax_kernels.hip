@@ -65,6 +65,7 @@ static_assert(SMAX_LIST % 2 == 0, "u16 list pairs");
 struct SmaxScanArgs {
   const uint8_t *lcp;        // local tables: index i <-> global base+i
   const uint8_t *bwt;
+  const uint64_t *bwtpk;     // packed BWT, 16 rows per u64 (index local_row/16 + 1), or null
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
   uint64_t numllv;
   const uint2 *llv_win;      // per tile: {first llv index >= g0 - LH, entries in the window}
@@ -143,7 +144,8 @@ struct Win {
   uint64_t numllv, base, N, end, local_len;
   uint32_t *err;
   const uint8_t *L;           // LDS window: index o = g - g0 + LH
-  const uint8_t *B;
+  const uint8_t *B;           // BWT bytes of the window (byte kernel), or
+  const uint64_t *P;          // packed BWT of the window, 16 rows per word
   const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
   const uint32_t *val;        // LDS .llv values in rank order (nval of them)
   int nval;                   // -1: values not staged (read global by rank)
@@ -154,7 +156,7 @@ struct Win {
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
-  t.L = nullptr; t.B = nullptr; t.rank = nullptr; t.val = nullptr; t.nval = -1;
+  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr; t.nval = -1;
   t.g0 = 0; t.llv_base = 0;
 }
 
@@ -195,8 +197,16 @@ __device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
   return b < 255 ? b : lcp_big(t, g);
 }
 
+// Packed BWT (DNA): per 16 rows one u64 -- bits 2q..2q+1 the symbol code of
+// row q (0..3), bit 32+q set when row q holds a special symbol (254/255,
+// unique for left diversity; decoded as 254).
+__device__ __forceinline__ uint32_t pk_sym(uint64_t w, uint32_t q) {
+  return ((w >> (32 + q)) & 1u) ? 254u : (uint32_t) (w >> (2 * q)) & 3u;
+}
+
 __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
+  if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(t.P[o >> 4], (uint32_t) (o & 15));
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
   if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
   return gld_u8(&t.gbwt[g - t.base]);
@@ -302,9 +312,14 @@ __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" 
 
 // One tile's LDS window: LCP and BWT bytes of rows [g0 - LH, g0 + TILE + RH)
 // and the window's .llv values (rank order, first SMAX_LLV_CAP of them).
-struct SmaxWindow {
+struct SmaxWindow {            // byte BWT (any alphabet)
   uint8_t L[SMAX_LDSB];
   uint8_t B[SMAX_LDSB];
+  uint32_t val[SMAX_LLV_CAP];
+};
+struct SmaxWindowPk {          // packed BWT (DNA): 0.5 B per row
+  uint8_t L[SMAX_LDSB];
+  uint64_t P[SMAX_LDSB / 16];
   uint32_t val[SMAX_LLV_CAP];
 };
 
@@ -312,27 +327,45 @@ struct SmaxWindow {
 // w: 16 B per lane per instruction (1 KiB per wave instruction), the two
 // 16-row halos, and the window's .llv values {lo, n} (low dword of each
 // record's value, at most SMAX_LLV_CAP).
-__device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
-                                             uint32_t lo, uint32_t n) {
+static_assert(SMAX_LH == 16 && SMAX_RH == 16 && SMAX_TILE == 2048,
+              "packed window: one halo group each side, 128 tile groups");
+__device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0, uint8_t *L,
+                                              uint32_t *val, uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
-  const uint32_t wl = __builtin_amdgcn_readfirstlane(lds_addr(w->L));
-  const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w->B));
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val));
+  const uint32_t wl = __builtin_amdgcn_readfirstlane(lds_addr(L));
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(val));
   const uint8_t *ls = a.lcp + l0 + lane * 16;
-  const uint8_t *bs = a.bwt + l0 + lane * 16;
 #pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++) {
-    glds16(ls + r * 1024, wl + SMAX_LH + r * 1024);
-    glds16(bs + r * 1024, wb + SMAX_LH + r * 1024);
-  }
+  for (int r = 0; r < SMAX_SEGS; r++) glds16(ls + r * 1024, wl + SMAX_LH + r * 1024);
   if (lane == 0) {
     glds16(a.lcp + l0 - SMAX_LH, wl);
     glds16(a.lcp + l0 + SMAX_TILE, wl + SMAX_LH + SMAX_TILE);
-    glds16(a.bwt + l0 - SMAX_LH, wb);
-    glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
   }
   if ((uint32_t) lane < n && lane < SMAX_LLV_CAP)
     glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + lane) + 8, wv);
+}
+__device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
+                                             uint32_t lo, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w->B));
+  const uint8_t *bs = a.bwt + l0 + lane * 16;
+  issue_lcp_llv(a, l0, w->L, w->val, lo, n);
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) glds16(bs + r * 1024, wb + SMAX_LH + r * 1024);
+  if (lane == 0) {
+    glds16(a.bwt + l0 - SMAX_LH, wb);
+    glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
+  }
+}
+__device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
+                                             uint32_t lo, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wp = __builtin_amdgcn_readfirstlane(lds_addr(w->P));
+  // groups l0/16 .. l0/16 + 129 of the packed array (index = local_row/16 + 1)
+  const uint64_t *ps = a.bwtpk + l0 / 16;
+  issue_lcp_llv(a, l0, w->L, w->val, lo, n);
+  glds16(ps + lane * 2, wp);                             // groups 0 .. 127
+  if (lane == 0) glds16(ps + 128, wp + 1024);            // groups 128, 129
 }
 
 __device__ __forceinline__ uint32_t seg_ge(const uint4 v, uint32_t mf) {
@@ -486,7 +519,23 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
   if (interior) {
     const uint32_t co = SMAX_LH + ro;
     const uint64_t LX = lds_bytes8(sL, co);
-    const uint64_t BX = lds_bytes8(t.B, co - 1);
+    // BWT symbols of rows c-1 .. c+6 as bytes (specials as 254)
+    uint64_t BX;
+    if (t.P != nullptr) {
+      const uint32_t o = co - 1, gi = o >> 4, q = o & 15u;
+      const uint64_t w0 = t.P[gi], w1 = t.P[gi + 1];
+      const uint64_t c64 = (w0 & 0xffffffffull) | (w1 << 32);
+      const uint32_t codes = (uint32_t) (c64 >> (2 * q)) & 0xffffu;
+      const uint32_t sp = (uint32_t) (((w0 >> 32) & 0xffffu) | (((w1 >> 32) & 0xffffu) << 16)) >> q;
+      BX = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t sym = ((sp >> k) & 1u) ? 254u : (codes >> (2 * k)) & 3u;
+        BX |= sym << (8 * k);
+      }
+    } else {
+      BX = lds_bytes8(t.B, co - 1);
+    }
     const uint32_t cb = (uint32_t) LX & 0xffu;
     if (cb == 255) {
       // .llv start: exact values by rank; a run of equal values >= 255
@@ -693,14 +742,43 @@ static_assert(2 * SMAX_LIST * 2 <= 3 * SMAX_DLIST * 4, "wave_detect list fits th
 // high bit of each byte >= 254 (WILDCARD / SEPARATOR / UNDEFBWTCHAR)
 __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0x01010101u); }
 
-__device__ __forceinline__ void classify_segment(const uint8_t *L, const uint8_t *B, uint32_t so,
+// 16 2-bit fields -> 16 bits: bit q = any bit of field q
+__device__ __forceinline__ uint32_t fields2_any(uint32_t x) {
+  uint32_t t = (x | (x >> 1)) & 0x55555555u;
+  t = (t | (t >> 1)) & 0x33333333u;
+  t = (t | (t >> 2)) & 0x0f0f0f0fu;
+  t = (t | (t >> 4)) & 0x00ff00ffu;
+  return (t | (t >> 8)) & 0x0000ffffu;
+}
+
+// BWT[c-1] != BWT[c] or either special, for the 16 rows of segment `so`
+__device__ __forceinline__ uint32_t segment_div2(const Win &t, uint32_t so) {
+  if (t.P != nullptr) {
+    const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1];
+    const uint32_t c = (uint32_t) w, pc = (uint32_t) (pw >> 30) & 3u;
+    const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu, psp = (uint32_t) (pw >> 47) & 1u;
+    return fields2_any(c ^ ((c << 2) | pc)) | sp | ((sp << 1) | psp);
+  }
+  const uint4 bv = *reinterpret_cast<const uint4 *>(&t.B[so]);
+  const uint32_t bp = t.B[so - 1];
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t bc = k == 0 ? bv.x : k == 1 ? bv.y : k == 2 ? bv.z : bv.w;
+    const uint32_t bpv = k == 0 ? ((bv.x << 8) | bp)
+                       : __builtin_amdgcn_alignbyte(bc, k == 1 ? bv.x : k == 2 ? bv.y : bv.z, 3);
+    r |= pack4((~bytes_eq(bpv, bc) | bytes_sp(bpv) | bytes_sp(bc)) & 0x80808080u) << (4 * k);
+  }
+  return r;
+}
+
+__device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
                                                  uint32_t mf, bool all_exact, uint32_t *Dm,
                                                  uint32_t *Lm, uint32_t *Fm) {
+  const uint8_t *L = t.L;
   const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
-  const uint4 bv = *reinterpret_cast<const uint4 *>(&B[so]);
-  const uint32_t pb = L[so - 1], nb = L[so + 16], bp = B[so - 1];
+  const uint32_t pb = L[so - 1], nb = L[so + 16];
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  const uint32_t b0 = bv.x, b1 = bv.y, b2 = bv.z, b3 = bv.w;
   uint32_t D = 0, Lr = 0, F = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -709,23 +787,18 @@ __device__ __forceinline__ void classify_segment(const uint8_t *L, const uint8_t
                        : __builtin_amdgcn_alignbyte(cur, k == 1 ? w0 : k == 2 ? w1 : w2, 3);
     const uint32_t nxt = k == 3 ? ((w3 >> 8) | (nb << 24))
                        : __builtin_amdgcn_alignbyte(k == 0 ? w1 : k == 1 ? w2 : w3, cur, 1);
-    const uint32_t bc = k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : b3;
-    const uint32_t bpv = k == 0 ? ((b0 << 8) | bp)
-                       : __builtin_amdgcn_alignbyte(bc, k == 1 ? b0 : k == 2 ? b1 : b2, 3);
     const uint32_t ff = bytes_ff(cur);
     // start: LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] > LCP[c-1];
     // a 255/255 pair is a possible start, settled exactly by eval_start
     const uint32_t A = bytes_ge(cur, mf) & (bytes_lt(prv, cur) | (ff & bytes_ff(prv)));
     const uint32_t eqn = bytes_eq(nxt, cur);
-    uint32_t d = A & ~ff & bytes_lt(nxt, cur) &
-                 (~bytes_eq(bpv, bc) | bytes_sp(bpv) | bytes_sp(bc)) & 0x80808080u;
-    uint32_t l = A & (ff | eqn);
-    if (all_exact) { d = 0; l = A; }
+    const uint32_t d = A & ~ff & bytes_lt(nxt, cur) & 0x80808080u;
+    const uint32_t l = A & (ff | eqn);
     D |= pack4(d) << (4 * k);
-    Lr |= pack4(l) << (4 * k);
+    Lr |= pack4(all_exact ? A : l) << (4 * k);
     F |= pack4(ff) << (4 * k);
   }
-  *Dm = D;
+  *Dm = (all_exact || D == 0) ? 0u : D & segment_div2(t, so);
   *Lm = Lr;
   *Fm = F;
 }
@@ -780,7 +853,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       const uint32_t sid = segl[i];
       ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
       const uint32_t so = SMAX_LH + ro;
-      classify_segment(sL, t.B, so, mf, all_exact, &D, &Lq, &F);
+      classify_segment(t, so, mf, all_exact, &D, &Lq, &F);
       const uint64_t sg = g0 + ro;
       if (sg < a.begin) {
         const uint32_t m = sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
@@ -859,10 +932,15 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   return wcount;
 }
 
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = W->B; t.P = nullptr; }
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = W->P; t.B = nullptr; }
+
+// WinT: SmaxWindowPk (packed DNA BWT) or SmaxWindow (byte BWT, any alphabet)
+template <typename WinT>
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   // every wave is an independent worker with its own double-buffered window:
   // no workgroup barrier anywhere in K1
-  __shared__ __attribute__((aligned(16))) SmaxWindow sWin[SMAX_THREADS / 64][2];
+  __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_THREADS / 64][2];
   __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_THREADS / 64][2][2];
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
   // per wave: wave_detect's start list + ranks (2 x SMAX_LIST u16), or
@@ -901,10 +979,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
     const uint64_t next = tile + stride;
-    SmaxWindow *W = &sWin[wave][cur];
+    WinT *W = &sWin[wave][cur];
     t.g0 = g0;
     t.L = W->L;
-    t.B = W->B;
+    set_bwt_window(t, W);
     t.val = W->val;
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
@@ -977,13 +1055,46 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   glds_wait();
 }
 
-// K1 instantiations: 4 waves/SIMD (<= 128 VGPRs, 4 workgroups/CU, what the
-// LDS budget allows) is the default; the unconstrained build is kept for A/B.
+// K1 instantiations.  Packed DNA BWT (0.5 B/row of BWT traffic, 8.1 KB of LDS
+// per wave) at 4 waves/SIMD is the default; the 5-wave build (which the LDS
+// budget allows) currently spills VGPRs and is slower -- kept for A/B
+// (GT_SMAX_DEBUG=256).  Byte BWT (any alphabet): 4 waves/SIMD.
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel(SmaxScanArgs a) {
-  smax_scan_body(a);
+  smax_scan_body<SmaxWindowPk>(a);
 }
-__global__ void __launch_bounds__(SMAX_THREADS) smax_scan_kernel_w3(SmaxScanArgs a) {
-  smax_scan_body(a);
+__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_pk5(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk>(a);
+}
+__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindow>(a);
+}
+
+// ------------------------------------------------------------ BWT packing
+
+// Plan-time packing of a DNA shard's BWT for K1's windows: group gi holds
+// local rows 16(gi-1) .. 16(gi-1)+15 as 2-bit codes + a special mask (see
+// pk_sym).  Sets *flag when a row of [0, local_len) holds a symbol in
+// [4, 254), i.e. the alphabet is not DNA (K1 then keeps byte BWT windows).
+__global__ void __launch_bounds__(256)
+smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, uint64_t *pk,
+                     uint32_t *flag) {
+  const uint64_t gi = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (gi >= ngroups) return;
+  const int64_t r0 = ((int64_t) gi - 1) * 16;
+  const uint4 v = *reinterpret_cast<const uint4 *>(bwt + r0);
+  uint32_t code = 0, sp = 0;
+  bool other = false;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+    const uint32_t b = (w >> (8 * (k & 3))) & 0xffu;
+    const int64_t row = r0 + k;
+    if (b >= 254) sp |= 1u << k;
+    else code |= (b & 3u) << (2 * k);
+    if (b > 3 && b < 254 && row >= 0 && (uint64_t) row < local_len) other = true;
+  }
+  pk[gi] = (uint64_t) code | ((uint64_t) sp << 32);
+  if (other) atomicOr(flag, 1u);
 }
 
 // ------------------------------------------------------------ K3: compact
@@ -1137,6 +1248,8 @@ struct GtSmaxPlan {
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
+  uint64_t *bwtpk;           // packed BWT (DNA shards), else null
+  bool pk;
   uint32_t *err;
   void *scan_tmp;
   size_t scan_tmp_bytes;
@@ -1224,8 +1337,25 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     int dev_cus = 0, per_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
                                  shard->device));
+    // packed BWT when the shard's alphabet is DNA ({0..3} plus specials)
+    {
+      const uint64_t ngroups = shard->local_len / 16 + 131;
+      uint32_t *flag = NULL, hflag = 0;
+      HIPCHK(hipMalloc(&p->bwtpk, sizeof (uint64_t) * ngroups));
+      HIPCHK(hipMalloc(&flag, sizeof (uint32_t)));
+      HIPCHK(hipMemset(flag, 0, sizeof (uint32_t)));
+      hipLaunchKernelGGL(smax_pack_bwt_kernel, dim3((unsigned) ((ngroups + 255) / 256)), dim3(256),
+                         0, 0, shard->bwt_dev, shard->local_len, ngroups, p->bwtpk, flag);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpy(&hflag, flag, sizeof hflag, hipMemcpyDeviceToHost));
+      (void) hipFree(flag);
+      p->pk = hflag == 0 && !(p->dbg & 8192u);
+      if (!p->pk) { (void) hipFree(p->bwtpk); p->bwtpk = NULL; }
+    }
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, (p->dbg & 256u) ? smax_scan_kernel_w3 : smax_scan_kernel, SMAX_THREADS, 0));
+        &per_cu, !p->pk ? smax_scan_kernel_bytes : (p->dbg & 256u) ? smax_scan_kernel_pk5
+                                                                   : smax_scan_kernel,
+        SMAX_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
     // 8 generations of resident workgroups: the dispatcher hands a finished
     // slot the next workgroup, which balances tiles of uneven cost (measured
@@ -1236,8 +1366,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     const uint64_t wg = ((uint64_t) p->num_tiles + 3) / 4;   // workgroups with a tile per wave
     p->grid = (uint32_t) (g < wg ? g : wg);
     if (getenv("GT_SMAX_VERBOSE"))
-      fprintf(stderr, "gt_smax: K1 %d CUs x %d blocks/CU -> grid %u, %u tiles\n", dev_cus,
-              per_cu, p->grid, p->num_tiles);
+      fprintf(stderr, "gt_smax: K1 %s BWT, %d CUs x %d blocks/CU -> grid %u, %u tiles\n",
+              p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
@@ -1288,7 +1418,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
-                  p->llv_win, p->err, p->scan_tmp};
+                  p->llv_win, p->err, p->scan_tmp, p->bwtpk};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -1300,6 +1430,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   SmaxScanArgs a;
   a.lcp = p->shard.lcp_dev;
   a.bwt = p->shard.bwt_dev;
+  a.bwtpk = p->pk ? p->bwtpk : nullptr;
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;
   a.llv_win = p->llv_win;
@@ -1334,15 +1465,17 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
-    if (p->dbg & 256u)
-      hipLaunchKernelGGL(smax_scan_kernel_w3, dim3(p->grid), dim3(SMAX_THREADS), 0, s, a);
-    else
-      {
-        // diagnostic: extra dynamic LDS lowers residency (occupancy sensitivity)
-        const char *pad = getenv("GT_SMAX_LDS_PAD");
-        const unsigned lp = pad ? (unsigned) strtoul(pad, NULL, 0) : 0u;
+    {
+      // diagnostic: extra dynamic LDS lowers residency (occupancy sensitivity)
+      const char *pad = getenv("GT_SMAX_LDS_PAD");
+      const unsigned lp = pad ? (unsigned) strtoul(pad, NULL, 0) : 0u;
+      if (p->pk && (p->dbg & 256u))
+        hipLaunchKernelGGL(smax_scan_kernel_pk5, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+      else if (p->pk)
         hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
-      }
+      else
+        hipLaunchKernelGGL(smax_scan_kernel_bytes, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+    }
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
     size_t bytes = p->scan_tmp_bytes;
