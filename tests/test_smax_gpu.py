@@ -149,10 +149,11 @@ def test_exact_queue_overflow_falls_back():
             assert np.array_equal(_gpu(e, minlen, shards), want), (minlen, shards)
 
 
-@pytest.mark.parametrize("dbg", [64, 128])
+@pytest.mark.parametrize("dbg", [64, 128, 8192])
 def test_detection_paths_agree(monkeypatch, dbg):
     # GT_SMAX_DEBUG=128: every interior tile through the start-list path;
-    # 64: every tile through the exact edge path.  Same answers required.
+    # 64: every tile through the exact edge path; 8192: byte BWT windows
+    # instead of packed ones.  Same answers required.
     monkeypatch.setenv("GT_SMAX_DEBUG", str(dbg))
     e = oracle_esa("at1MB")
     for minlen in (5, 20, 256):
@@ -161,3 +162,20 @@ def test_detection_paths_agree(monkeypatch, dbg):
     e2 = O.Esa(_repetitive_text(rng, 60000, 0.001))
     for minlen in (3, 20, 300):
         assert np.array_equal(_gpu(e2, minlen), _cpu(e2, minlen)), minlen
+
+
+def test_protein_alphabet_uses_byte_windows():
+    # sigma = 20 (not DNA): K1 keeps byte BWT windows
+    rng = np.random.default_rng(21)
+    fam = [rng.integers(0, 20, int(rng.integers(30, 300)), dtype=np.uint8) for _ in range(8)]
+    t = rng.integers(0, 20, 120000, dtype=np.uint8)
+    for _ in range(300):
+        f = fam[int(rng.integers(0, len(fam)))]
+        at = int(rng.integers(0, len(t) - len(f)))
+        t[at:at + len(f)] = f
+    t[rng.random(len(t)) < 0.002] = 255
+    e = O.Esa(t)
+    for minlen in (2, 8, 30, 256):
+        want = _cpu(e, minlen)
+        for shards in (1, 4):
+            assert np.array_equal(_gpu(e, minlen, shards), want), (minlen, shards)
