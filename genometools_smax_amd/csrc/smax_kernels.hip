@@ -78,6 +78,8 @@ struct SmaxScanArgs {
   GtSmaxRecord *slots;       // [tile][wave][SMAX_WSLOT] records, row order
   uint32_t *tile_count;      // [tile][wave] record counts
   GtSmaxBoundary *bnd;
+  uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
+  uint32_t *defer_count;     // reset by K0
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
 
@@ -257,6 +259,7 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   Win t;
   win_init(t, a);
   GtSmaxBoundary *b = a.bnd;
+  *a.defer_count = 0;
   b->pend_valid = 0;
   b->shard_begin = a.begin;
   b->shard_end = a.end;
@@ -936,6 +939,45 @@ __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = W-
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = W->P; t.B = nullptr; }
 
 // WinT: SmaxWindowPk (packed DNA BWT) or SmaxWindow (byte BWT, any alphabet)
+// Filter and .llv ranks of a landed window (one wave): per-lane segment
+// "any byte >= min(minlen,128)" bits, and the window's 255-byte ranks in
+// `rank` (values already in LDS) when it holds any 255 byte.
+__device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
+                                                   uint32_t wlo, uint32_t wn) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
+  const uint32_t so = SMAX_LH + lane * 16;
+  const uint4 v0 = *reinterpret_cast<const uint4 *>(&t.L[so]);
+  const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
+  const uint4 hv = *reinterpret_cast<const uint4 *>(&t.L[lane == 0 ? 0 : SMAX_LH + SMAX_TILE]);
+  const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+  const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
+  const uint32_t hl = __builtin_amdgcn_readfirstlane(seg_ffcount(hv));   // lane 0: left halo
+  t.llv_base = wlo;
+  t.rank = nullptr;
+  t.nval = -1;
+  if (__ballot((f0 | f1) != 0) != 0 || hl != 0) {
+    // chunk 0 = left halo, 1..64 segment 0, 65..128 segment 1, 129 right halo
+    uint32_t t0, t1;
+    const uint32_t e0 = wave_excl(f0, &t0), e1 = wave_excl(f1, &t1);
+    rank[1 + lane] = (uint16_t) (hl + e0);
+    rank[65 + lane] = (uint16_t) (hl + t0 + e1);
+    if (lane == 0) {
+      rank[0] = 0;
+      rank[1 + SMAX_TILE / 16] = (uint16_t) (hl + t0 + t1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    t.nval = (int) (wn < SMAX_LLV_CAP ? wn : SMAX_LLV_CAP);
+    t.rank = (a.dbg & 16u) ? nullptr : rank;
+  }
+  return segpre_bits;
+}
+
+// K1 body.  Interior tiles whose starts the direct path covers are finished
+// here; shard-edge tiles and tiles with more exact starts than the direct
+// path queues are deferred to K1b (their generic path is kept out of K1,
+// whose register budget it would otherwise set).
 template <typename WinT>
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   // every wave is an independent worker with its own double-buffered window:
@@ -943,13 +985,12 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_THREADS / 64][2];
   __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_THREADS / 64][2][2];
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
-  // per wave: wave_detect's start list + ranks (2 x SMAX_LIST u16), or
-  // wave_detect_direct's queue and results (3 x SMAX_DLIST u32)
+  // per wave: wave_detect_direct's queue and results (3 x SMAX_DLIST u32),
+  // compacted segment ids and accepted masks
   __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * SMAX_DLIST + 2 * 64 / 4 + 64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint64_t stride = (uint64_t) gridDim.x * (SMAX_THREADS / 64);
   const uint64_t last = a.num_tiles - 1;
 
@@ -1002,58 +1043,70 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
         glds4(reinterpret_cast<const uint32_t *>(a.llv_win + n2) + lane, cur ? info1 : info0);
     }
 
-    // ---- filter and .llv ranks of the window's 255 bytes (values in LDS)
-    const uint32_t so = SMAX_LH + lane * 16;
-    const uint4 v0 = *reinterpret_cast<const uint4 *>(&W->L[so]);
-    const uint4 v1 = *reinterpret_cast<const uint4 *>(&W->L[so + 1024]);
-    const uint4 hv = *reinterpret_cast<const uint4 *>(&W->L[lane == 0 ? 0 : SMAX_LH + SMAX_TILE]);
-    const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
-    const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
-    const uint32_t hl = __builtin_amdgcn_readfirstlane(seg_ffcount(hv));   // lane 0: left halo
+    const uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
-    t.llv_base = wlo;
-    t.rank = nullptr;
-    t.nval = -1;
-    if (__ballot((f0 | f1) != 0) != 0 || hl != 0) {
-      // chunk 0 = left halo, 1..64 segment 0, 65..128 segment 1, 129 right halo
-      const uint64_t ltm = lanemask_lt();
-      uint32_t e0 = 0, t0 = 0, e1 = 0, t1 = 0;
-#pragma unroll
-      for (int b = 0; b < 5; b++) {
-        const uint64_t p0 = __ballot((f0 >> b) & 1u), p1 = __ballot((f1 >> b) & 1u);
-        e0 += (uint32_t) __popcll(p0 & ltm) << b;
-        t0 += (uint32_t) __popcll(p0) << b;
-        e1 += (uint32_t) __popcll(p1 & ltm) << b;
-        t1 += (uint32_t) __popcll(p1) << b;
-      }
-      rank[1 + lane] = (uint16_t) (hl + e0);
-      rank[65 + lane] = (uint16_t) (hl + t0 + e1);
-      if (lane == 0) {
-        rank[0] = 0;
-        rank[1 + SMAX_TILE / 16] = (uint16_t) (hl + t0 + t1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      t.nval = (int) (wn < SMAX_LLV_CAP ? wn : SMAX_LLV_CAP);
-      t.rank = (a.dbg & 16u) ? nullptr : rank;
-    }
 
     // ---- detection, diversity, records (row order)
     GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
     uint32_t wcount = 0;
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-    uint16_t *qlist = reinterpret_cast<uint16_t *>(sQueue[wave]);
-    if (!edge && wave_pre && !(a.dbg & 128u))
+    bool defer = edge || (wave_pre && (a.dbg & 128u));
+    if (!defer && wave_pre) {
       wcount = wave_detect_direct(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
-    if (edge || (wave_pre && ((a.dbg & 128u) || wcount == UINT32_MAX)))
-      wcount = wave_detect(t, a, g0, W->L, qlist, qlist + SMAX_LIST, wdst, !edge, segpre_bits);
-    if (lane == 0 && !(a.dbg & 4096u)) a.tile_count[tile] = wcount;
+      defer = wcount == UINT32_MAX;
+    }
+    if (lane == 0) {
+      if (defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
+      else if (!(a.dbg & 4096u)) a.tile_count[tile] = wcount;
+    }
 
     tile = next;
     if (tile >= a.num_tiles) break;
   }
   glds_wait();
 }
+
+// K1b: the deferred tiles (shard edges, exact-queue overflow), one wave per
+// tile through the generic start-list path (exact at row 0, begin, end and
+// N; records the pending plateau at the shard end).  Byte BWT windows.
+__global__ void __launch_bounds__(SMAX_THREADS)
+smax_defer_kernel(SmaxScanArgs a) {
+  __shared__ __attribute__((aligned(16))) SmaxWindow sWin[SMAX_THREADS / 64];
+  __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
+  __shared__ uint16_t sList[SMAX_THREADS / 64][2 * SMAX_LIST];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t n = *a.defer_count;
+  Win t;
+  win_init(t, a);
+  for (uint32_t i = blockIdx.x * (SMAX_THREADS / 64) + wave; i < n;
+       i += gridDim.x * (SMAX_THREADS / 64)) {
+    const uint64_t tile = a.defer_list[i];
+    const uint2 info = a.llv_win[tile];
+    const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
+    const uint64_t g0 = a.base + l0;
+    SmaxWindow *W = &sWin[wave];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // previous tile's LDS reads done
+    issue_window(a, l0, W, __builtin_amdgcn_readfirstlane(info.x),
+                 __builtin_amdgcn_readfirstlane(info.y));
+    glds_wait();
+    t.g0 = g0;
+    t.L = W->L;
+    t.B = W->B;
+    t.P = nullptr;
+    t.val = W->val;
+    const uint32_t segpre_bits = prepare_window(t, a, sRank[wave], info.x, info.y);
+    const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
+    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
+    uint32_t wcount = 0;
+    if (edge || wave_pre)
+      wcount = wave_detect(t, a, g0, W->L, sList[wave], sList[wave] + SMAX_LIST,
+                           a.slots + tile * (uint64_t) SMAX_WSLOT, !edge, segpre_bits);
+    if (lane == 0 && !(a.dbg & 4096u)) a.tile_count[tile] = wcount;
+  }
+  glds_wait();
+}
+
 
 // K1 instantiations.  Packed DNA BWT (0.5 B/row of BWT traffic, 8.1 KB of LDS
 // per wave) at 4 waves/SIMD is the default; the 5-wave build (which the LDS
@@ -1240,7 +1293,7 @@ struct GtSmaxPlan {
   uint64_t capacity;
   uint32_t num_tiles;
   uint64_t tile_first;
-  uint32_t grid, compact_grid;
+  uint32_t grid, compact_grid, defer_grid;
   GtSmaxRecord *out;         // capacity records, ascending lb
   GtSmaxRecord *slots;       // num_tiles * SMAX_WSLOT
   uint32_t *tile_count;      // num_tiles
@@ -1250,6 +1303,8 @@ struct GtSmaxPlan {
   uint2 *llv_win;
   uint64_t *bwtpk;           // packed BWT (DNA shards), else null
   bool pk;
+  uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
+  uint32_t *defer_count;
   uint32_t *err;
   void *scan_tmp;
   size_t scan_tmp_bytes;
@@ -1369,6 +1424,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       fprintf(stderr, "gt_smax: K1 %s BWT, %d CUs x %d blocks/CU -> grid %u, %u tiles\n",
               p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
+    const uint64_t dg = ((uint64_t) p->num_tiles + 3) / 4;
+    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 4 ? dg : (uint64_t) dev_cus * 4);
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
@@ -1384,6 +1441,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(hipMalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
+  HIPCHK(hipMalloc(&p->defer_list, sizeof (uint32_t) * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->defer_count, sizeof (uint32_t)));
+  HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
   HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
                                  (uint64_t) 0, (size_t) p->num_tiles,
                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
@@ -1418,7 +1478,8 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
-                  p->llv_win, p->err, p->scan_tmp, p->bwtpk};
+                  p->llv_win, p->err, p->scan_tmp, p->bwtpk, p->defer_list,
+                  p->defer_count};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -1446,6 +1507,8 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.slots = p->slots;
   a.tile_count = p->tile_count;
   a.bnd = p->bnd;
+  a.defer_list = p->defer_list;
+  a.defer_count = p->defer_count;
   a.dbg = p->dbg;
   return a;
 }
@@ -1478,6 +1541,9 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
+    // K1b: deferred tiles (a few per shard; grid-stride over the device count)
+    hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
+    HIPCHK(hipGetLastError());
     size_t bytes = p->scan_tmp_bytes;
     HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->tile_count, p->tile_off,
                                    (uint64_t) 0, (size_t) p->num_tiles,
