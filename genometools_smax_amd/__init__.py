@@ -132,6 +132,8 @@ def lib():
         L.gt_smax_plan_copy_boundary.argtypes = [vp, vp, vp]
         L.gt_smax_plan_error_bits.argtypes = [vp]
         L.gt_smax_plan_error_bits.restype = ctypes.c_uint32
+        L.gt_smax_plan_deferred_tiles.argtypes = [vp]
+        L.gt_smax_plan_deferred_tiles.restype = ctypes.c_uint32
         _lib = L
     return _lib
 
@@ -409,6 +411,9 @@ class SmaxPlan:
 
     def error_bits(self):
         return lib().gt_smax_plan_error_bits(self.plan)
+
+    def deferred_tiles(self):
+        return lib().gt_smax_plan_deferred_tiles(self.plan)
 
     def fetch_count(self):
         c = ctypes.c_uint64()

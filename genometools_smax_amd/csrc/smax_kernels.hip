@@ -1651,6 +1651,14 @@ fail:
   return -1;
 }
 
+extern "C" uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *p) {
+  uint32_t n = 0;
+  if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;
+  if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0xffffffffu;
+  return n;
+}
+
 extern "C" uint32_t gt_smax_plan_error_bits(GtSmaxPlan *p) {
   uint32_t e = 0;
   if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;

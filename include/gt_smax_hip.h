@@ -198,6 +198,10 @@ int gt_smax_plan_fetch_count(GtSmaxPlan *plan, uint64_t *count);
  * 2 = a table read outside the shard's rows. */
 uint32_t gt_smax_plan_error_bits(GtSmaxPlan *plan);
 
+/* Diagnostic: tiles the last run handed from K1 to the generic kernel K1b
+ * (shard edges and tiles with more exact-evaluation starts than K1 queues). */
+uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *plan);
+
 #ifdef __cplusplus
 }
 #endif

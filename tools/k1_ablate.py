@@ -22,6 +22,9 @@ for rnd in range(3):
         os.environ["GT_SMAX_DEBUG"] = str(v)
         p = esa.plan(20)
         p.run(); torch.cuda.synchronize()
+        if rnd == 0:
+            print("dbg=%d: %d of %d tiles deferred to K1b" % (v, p.deferred_tiles(), p.num_tiles),
+                  flush=True)
         if p.error_bits():
             print("dbg=%d: device error bits 0x%x" % (v, p.error_bits()), flush=True)
         p.enable_timing(10)
