@@ -826,16 +826,17 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
 // classified: they are compacted (row order) so that each classification
 // step keeps all 64 lanes busy (about a third of the segments are active on
 // repeat-rich DNA, so one step usually covers the whole tile).
+template <int DL>
 __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &a, uint64_t g0,
                                               const uint8_t *sL, uint32_t *ent,
                                               GtSmaxRecord *wdst, uint32_t segpre) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const bool all_exact = a.minlen > 128;
-  uint32_t *res_lcp = ent + SMAX_DLIST, *res_w = ent + 2 * SMAX_DLIST;
-  uint8_t *segl = reinterpret_cast<uint8_t *>(ent + 3 * SMAX_DLIST);
+  uint32_t *res_lcp = ent + DL, *res_w = ent + 2 * DL;
+  uint8_t *segl = reinterpret_cast<uint8_t *>(ent + 3 * DL);
   // accepted exact starts, one 16-bit row mask per compacted segment
-  uint32_t *accw = ent + 3 * SMAX_DLIST + 2 * 64 / 4;
+  uint32_t *accw = ent + 3 * DL + 2 * 64 / 4;
   // compact the active segments (id = round * 64 + lane, row order)
   const uint64_t ltm = lanemask_lt();
   const uint64_t m0 = __ballot(segpre & 1u), m1 = __ballot((segpre >> 1) & 1u);
@@ -866,7 +867,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     }
     uint32_t tot;
     const uint32_t excl = wave_excl((uint32_t) __popc(Lq), &tot);
-    if (nL + tot <= SMAX_DLIST && Lq != 0) {
+    if (nL + tot <= DL && Lq != 0) {
       const uint32_t crank = (F != 0 && t.rank != nullptr) ? t.rank[(SMAX_LH + ro) >> 4] : 0u;
       uint32_t pos = nL + excl, bits = Lq;
       while (bits) {
@@ -880,7 +881,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     else { Dm1 = D; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
     nL += tot;
   }
-  if (nL > SMAX_DLIST) return UINT32_MAX;
+  if (nL > DL) return UINT32_MAX;
   if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
   // exact evaluation of the queued starts (one per lane); accepted ones set
   // their row bit in their segment's mask
@@ -888,15 +889,18 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     accw[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if ((uint32_t) lane < nL) {
-      const uint32_t e = ent[lane];
-      const uint32_t ro = e & 0x7ffu, si = (e >> 11) & 0x7fu;
-      uint32_t cur;
-      uint64_t j;
-      const bool acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
-      res_lcp[lane] = cur;
-      res_w[lane] = (uint32_t) (j - (g0 + ro) + 2);
-      if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
+    for (uint32_t i0 = 0; i0 < nL; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      if (i < nL) {
+        const uint32_t e = ent[i];
+        const uint32_t ro = e & 0x7ffu, si = (e >> 11) & 0x7fu;
+        uint32_t cur;
+        uint64_t j;
+        const bool acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
+        res_lcp[i] = cur;
+        res_w[i] = (uint32_t) (j - (g0 + ro) + 2);
+        if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1052,7 +1056,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
     bool defer = edge || (wave_pre && (a.dbg & 128u));
     if (!defer && wave_pre) {
-      wcount = wave_detect_direct(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
+      wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
       defer = wcount == UINT32_MAX;
     }
     if (lane == 0) {
@@ -1073,7 +1077,8 @@ __global__ void __launch_bounds__(SMAX_THREADS)
 smax_defer_kernel(SmaxScanArgs a) {
   __shared__ __attribute__((aligned(16))) SmaxWindow sWin[SMAX_THREADS / 64];
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
-  __shared__ uint16_t sList[SMAX_THREADS / 64][2 * SMAX_LIST];
+  // direct-path queue (256 exact starts) or the generic path's start list
+  __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * 256 + 2 * 64 / 4 + 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t n = *a.defer_count;
@@ -1098,10 +1103,15 @@ smax_defer_kernel(SmaxScanArgs a) {
     const uint32_t segpre_bits = prepare_window(t, a, sRank[wave], info.x, info.y);
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
-    uint32_t wcount = 0;
-    if (edge || wave_pre)
-      wcount = wave_detect(t, a, g0, W->L, sList[wave], sList[wave] + SMAX_LIST,
-                           a.slots + tile * (uint64_t) SMAX_WSLOT, !edge, segpre_bits);
+    GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
+    uint16_t *qlist = reinterpret_cast<uint16_t *>(sQueue[wave]);
+    uint32_t wcount = UINT32_MAX;
+    if (!edge && wave_pre && !(a.dbg & 128u))
+      wcount = wave_detect_direct<256>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
+    if (wcount == UINT32_MAX)
+      wcount = (edge || wave_pre) ? wave_detect(t, a, g0, W->L, qlist, qlist + SMAX_LIST, wdst,
+                                                !edge, segpre_bits)
+                                  : 0u;
     if (lane == 0 && !(a.dbg & 4096u)) a.tile_count[tile] = wcount;
   }
   glds_wait();
@@ -1425,7 +1435,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
               p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
     const uint64_t dg = ((uint64_t) p->num_tiles + 3) / 4;
-    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 4 ? dg : (uint64_t) dev_cus * 4);
+    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 16 ? dg : (uint64_t) dev_cus * 16);
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));

@@ -64,3 +64,13 @@ per_tile = np.bincount((idx[eqn | ffs] // 2048), minlength=rows // 2048 + 1)
 print("exact-queue starts per 2048-row tile: mean %.1f p50 %d p90 %d p99 %d max %d; tiles > 64: %.4f" %
       (per_tile.mean(), np.percentile(per_tile, 50), np.percentile(per_tile, 90),
        np.percentile(per_tile, 99), per_tile.max(), (per_tile > 64).mean()))
+# plateau length (rows) of the exact-queue starts
+eqi = idx[eqn & ~ffs]
+plen = np.ones(len(eqi), dtype=np.int64)
+alive = np.ones(len(eqi), dtype=bool)
+for k in range(1, 16):
+    j = np.minimum(eqi + k, rows - 1)
+    alive &= L[j] == L[eqi]
+    plen += alive
+print("plateau rows of LCP[c+1]==LCP[c] starts: 2: %.3f  3: %.3f  4-7: %.3f  8+: %.3f" %
+      ((plen == 2).mean(), (plen == 3).mean(), ((plen >= 4) & (plen <= 7)).mean(), (plen >= 8).mean()))
