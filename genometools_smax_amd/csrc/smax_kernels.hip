@@ -754,35 +754,63 @@ __device__ __forceinline__ uint32_t fields2_any(uint32_t x) {
   return (t | (t >> 8)) & 0x0000ffffu;
 }
 
-// BWT[c-1] != BWT[c] or either special, for the 16 rows of segment `so`
-__device__ __forceinline__ uint32_t segment_div2(const Win &t, uint32_t so) {
+// Left diversity of the 16 rows c of segment `so` for the two interval
+// shapes decided here: *div2 = {BWT[c-1], BWT[c]} pairwise distinct (specials
+// unique), *div3 = {BWT[c-1], BWT[c], BWT[c+1]} pairwise distinct.
+__device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t *div2,
+                                            uint32_t *div3) {
   if (t.P != nullptr) {
-    const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1];
-    const uint32_t c = (uint32_t) w, pc = (uint32_t) (pw >> 30) & 3u;
-    const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu, psp = (uint32_t) (pw >> 47) & 1u;
-    return fields2_any(c ^ ((c << 2) | pc)) | sp | ((sp << 1) | psp);
+    const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1], nw = t.P[(so >> 4) + 1];
+    const uint32_t c = (uint32_t) w, pc = (uint32_t) (pw >> 30) & 3u, nc = (uint32_t) nw & 3u;
+    const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
+    const uint32_t spm1 = ((sp << 1) | ((uint32_t) (pw >> 47) & 1u)) & 0xffffu;   // row q-1
+    const uint32_t spp1 = (sp >> 1) | (((uint32_t) (nw >> 32) & 1u) << 15);       // row q+1
+    const uint32_t cp = (c << 2) | pc, cn = (c >> 2) | (nc << 30);
+    const uint32_t ne1 = fields2_any(c ^ cp);                // q-1 vs q
+    const uint32_t ne1n = fields2_any(c ^ cn);               // q vs q+1
+    const uint32_t ne2 = fields2_any(cp ^ cn);               // q-1 vs q+1
+    const uint32_t d2 = ne1 | sp | spm1;
+    *div2 = d2;
+    *div3 = d2 & (ne1n | sp | spp1) & (ne2 | spm1 | spp1);
+    return;
   }
   const uint4 bv = *reinterpret_cast<const uint4 *>(&t.B[so]);
-  const uint32_t bp = t.B[so - 1];
-  uint32_t r = 0;
+  const uint32_t bp = t.B[so - 1], bn = t.B[so + 16];
+  uint32_t r2 = 0, r3 = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t bc = k == 0 ? bv.x : k == 1 ? bv.y : k == 2 ? bv.z : bv.w;
     const uint32_t bpv = k == 0 ? ((bv.x << 8) | bp)
                        : __builtin_amdgcn_alignbyte(bc, k == 1 ? bv.x : k == 2 ? bv.y : bv.z, 3);
-    r |= pack4((~bytes_eq(bpv, bc) | bytes_sp(bpv) | bytes_sp(bc)) & 0x80808080u) << (4 * k);
+    const uint32_t bnx = k == 3 ? ((bv.w >> 8) | (bn << 24))
+                       : __builtin_amdgcn_alignbyte(k == 0 ? bv.y : k == 1 ? bv.z : bv.w, bc, 1);
+    const uint32_t sc = bytes_sp(bc), sp = bytes_sp(bpv), sn = bytes_sp(bnx);
+    const uint32_t d2 = ~bytes_eq(bpv, bc) | sc | sp;
+    const uint32_t d3 = d2 & (~bytes_eq(bnx, bc) | sc | sn) & (~bytes_eq(bnx, bpv) | sp | sn);
+    r2 |= pack4(d2 & 0x80808080u) << (4 * k);
+    r3 |= pack4(d3 & 0x80808080u) << (4 * k);
   }
-  return r;
+  *div2 = r2;
+  *div3 = r3;
 }
 
+// Classification of the 16 rows c of segment `so` (byte compares exact except
+// between two 255 bytes):
+//   *Dm  records [c-1 .. c]:   start, LCP[c+1] < LCP[c], div2
+//   *D2m records [c-1 .. c+1]: start, LCP[c+1] == LCP[c] > LCP[c+2], div3
+//   *Lm  starts needing exact evaluation: 255 byte, or LCP[c] == LCP[c+1] ==
+//        LCP[c+2] (plateau of >= 3 rows)
+//   *Fm  255 bytes (ranks)
+// where start = LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] >
+// LCP[c-1] (a 255/255 pair is a possible start, settled by eval_start).
 __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
                                                  uint32_t mf, bool all_exact, uint32_t *Dm,
-                                                 uint32_t *Lm, uint32_t *Fm) {
+                                                 uint32_t *D2m, uint32_t *Lm, uint32_t *Fm) {
   const uint8_t *L = t.L;
   const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
-  const uint32_t pb = L[so - 1], nb = L[so + 16];
+  const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  uint32_t D = 0, Lr = 0, F = 0;
+  uint32_t D = 0, D2 = 0, Lr = 0, F = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t cur = k == 0 ? w0 : k == 1 ? w1 : k == 2 ? w2 : w3;
@@ -790,18 +818,29 @@ __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
                        : __builtin_amdgcn_alignbyte(cur, k == 1 ? w0 : k == 2 ? w1 : w2, 3);
     const uint32_t nxt = k == 3 ? ((w3 >> 8) | (nb << 24))
                        : __builtin_amdgcn_alignbyte(k == 0 ? w1 : k == 1 ? w2 : w3, cur, 1);
+    const uint32_t nx2 = k == 3 ? ((w3 >> 16) | (nb << 16) | (nb2 << 24))
+                       : __builtin_amdgcn_alignbyte(k == 0 ? w1 : k == 1 ? w2 : w3, cur, 2);
     const uint32_t ff = bytes_ff(cur);
-    // start: LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] > LCP[c-1];
-    // a 255/255 pair is a possible start, settled exactly by eval_start
     const uint32_t A = bytes_ge(cur, mf) & (bytes_lt(prv, cur) | (ff & bytes_ff(prv)));
-    const uint32_t eqn = bytes_eq(nxt, cur);
-    const uint32_t d = A & ~ff & bytes_lt(nxt, cur) & 0x80808080u;
-    const uint32_t l = A & (ff | eqn);
+    const uint32_t eqn = bytes_eq(nxt, cur), eqn2 = bytes_eq(nx2, cur);
+    const uint32_t Ae = A & ~ff;
+    const uint32_t d = Ae & bytes_lt(nxt, cur) & 0x80808080u;
+    const uint32_t d2 = Ae & eqn & bytes_lt(nx2, cur) & 0x80808080u;
+    const uint32_t l = A & (ff | (eqn & eqn2));
     D |= pack4(d) << (4 * k);
+    D2 |= pack4(d2) << (4 * k);
     Lr |= pack4(all_exact ? A : l) << (4 * k);
     F |= pack4(ff) << (4 * k);
   }
-  *Dm = (all_exact || D == 0) ? 0u : D & segment_div2(t, so);
+  if (all_exact || (D | D2) == 0) {
+    *Dm = 0;
+    *D2m = 0;
+  } else {
+    uint32_t div2, div3;
+    segment_div(t, so, &div2, &div3);
+    *Dm = D & div2;
+    *D2m = D2 & div3;
+  }
   *Lm = Lr;
   *Fm = F;
 }
@@ -845,23 +884,27 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   if (segpre & 2u) segl[n0 + __popcll(m1 & ltm)] = (uint8_t) (64 + lane);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones
   uint32_t Dm0 = 0, Lm0 = 0, Dm1 = 0, Lm1 = 0, Lpre0 = 0, Lpre1 = 0, ro0 = 0, ro1 = 0;
+  uint32_t W30 = 0, W31 = 0;
   uint32_t nL = 0;
   const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
     const uint32_t i = k * 64 + lane;
-    uint32_t D = 0, Lq = 0, F = 0, ro = 0;
+    uint32_t D = 0, D3 = 0, Lq = 0, F = 0, ro = 0;
     if (i < nseg) {
       const uint32_t sid = segl[i];
       ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
       const uint32_t so = SMAX_LH + ro;
-      classify_segment(t, so, mf, all_exact, &D, &Lq, &F);
+      classify_segment(t, so, mf, all_exact, &D, &D3, &Lq, &F);
+      D |= D3;
       const uint64_t sg = g0 + ro;
       if (sg < a.begin) {
         const uint32_t m = sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
         D &= m;
+        D3 &= m;
         Lq &= m;
       }
     }
@@ -877,8 +920,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
       }
     }
-    if (k == 0) { Dm0 = D; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
-    else { Dm1 = D; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
+    if (k == 0) { Dm0 = D; W30 = D3; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
+    else { Dm1 = D; W31 = D3; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
     nL += tot;
   }
   if (nL > DL) return UINT32_MAX;
@@ -910,7 +953,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
-    const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1;
+    const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1, W3 = k == 0 ? W30 : W31;
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
     const uint32_t si = k * 64 + lane;
     uint32_t acc = D;
@@ -925,7 +968,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       rec.lb = g0 + ro + q - 1;
       if ((D >> q) & 1u) {
         rec.lcp = sL[SMAX_LH + ro + q];
-        rec.width = 2;
+        rec.width = 2 + ((W3 >> q) & 1u);
       } else {
         const uint32_t i = Lpre + (uint32_t) __popc(Lq & ((1u << q) - 1));
         rec.lcp = res_lcp[i];
