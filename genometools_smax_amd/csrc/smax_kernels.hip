@@ -796,53 +796,57 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
 
 // Classification of the 16 rows c of segment `so` (byte compares exact except
 // between two 255 bytes):
-//   *Dm  records [c-1 .. c]:   start, LCP[c+1] < LCP[c], div2
-//   *D2m records [c-1 .. c+1]: start, LCP[c+1] == LCP[c] > LCP[c+2], div3
+//   *Dm  records [c-1 .. c] and [c-1 .. c+1] (D3 marks the latter): start,
+//        then LCP[c+1] < LCP[c], or LCP[c+1] == LCP[c] > LCP[c+2]; with the
+//        matching left diversity
 //   *Lm  starts needing exact evaluation: 255 byte, or LCP[c] == LCP[c+1] ==
 //        LCP[c+2] (plateau of >= 3 rows)
 //   *Fm  255 bytes (ranks)
 // where start = LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] >
 // LCP[c-1] (a 255/255 pair is a possible start, settled by eval_start).
+// Only two byte relations are computed, each row against its predecessor
+// (UP: LCP[r-1] < LCP[r], EQ: LCP[r-1] == LCP[r]) for rows 0..17; the
+// relations of c with c+1 and of c+1 with c+2 are the same bits shifted.
 __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
                                                  uint32_t mf, bool all_exact, uint32_t *Dm,
-                                                 uint32_t *D2m, uint32_t *Lm, uint32_t *Fm) {
+                                                 uint32_t *D3m, uint32_t *Lm, uint32_t *Fm) {
   const uint8_t *L = t.L;
   const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
   const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  uint32_t D = 0, D2 = 0, Lr = 0, F = 0;
+  uint32_t UP = 0, EQ = 0, GE = 0, FF = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t cur = k == 0 ? w0 : k == 1 ? w1 : k == 2 ? w2 : w3;
     const uint32_t prv = k == 0 ? ((w0 << 8) | pb)
                        : __builtin_amdgcn_alignbyte(cur, k == 1 ? w0 : k == 2 ? w1 : w2, 3);
-    const uint32_t nxt = k == 3 ? ((w3 >> 8) | (nb << 24))
-                       : __builtin_amdgcn_alignbyte(k == 0 ? w1 : k == 1 ? w2 : w3, cur, 1);
-    const uint32_t nx2 = k == 3 ? ((w3 >> 16) | (nb << 16) | (nb2 << 24))
-                       : __builtin_amdgcn_alignbyte(k == 0 ? w1 : k == 1 ? w2 : w3, cur, 2);
-    const uint32_t ff = bytes_ff(cur);
-    const uint32_t A = bytes_ge(cur, mf) & (bytes_lt(prv, cur) | (ff & bytes_ff(prv)));
-    const uint32_t eqn = bytes_eq(nxt, cur), eqn2 = bytes_eq(nx2, cur);
-    const uint32_t Ae = A & ~ff;
-    const uint32_t d = Ae & bytes_lt(nxt, cur) & 0x80808080u;
-    const uint32_t d2 = Ae & eqn & bytes_lt(nx2, cur) & 0x80808080u;
-    const uint32_t l = A & (ff | (eqn & eqn2));
-    D |= pack4(d) << (4 * k);
-    D2 |= pack4(d2) << (4 * k);
-    Lr |= pack4(all_exact ? A : l) << (4 * k);
-    F |= pack4(ff) << (4 * k);
+    UP |= pack4(bytes_lt(prv, cur)) << (4 * k);
+    EQ |= pack4(bytes_eq(prv, cur)) << (4 * k);
+    GE |= pack4(bytes_ge(cur, mf)) << (4 * k);
+    FF |= pack4(bytes_ff(cur)) << (4 * k);
   }
-  if (all_exact || (D | D2) == 0) {
+  // rows 16, 17 against their predecessors
+  const uint32_t b15 = w3 >> 24;
+  UP |= (b15 < nb ? 1u << 16 : 0u) | (nb < nb2 ? 1u << 17 : 0u);
+  EQ |= (b15 == nb ? 1u << 16 : 0u) | (nb == nb2 ? 1u << 17 : 0u);
+  const uint32_t FFP = FF & ((FF << 1) | (pb == 255u ? 1u : 0u));   // 255 after 255
+  const uint32_t A = GE & (UP | FFP) & 0xffffu;
+  const uint32_t Ae = A & ~FF;
+  const uint32_t eqn = EQ >> 1, dn = ~((UP | EQ) >> 1);            // vs row c+1
+  const uint32_t eqn1 = EQ >> 2, dn1 = ~((UP | EQ) >> 2);          // c+1 vs c+2
+  const uint32_t D = Ae & dn & 0xffffu;
+  const uint32_t D3 = Ae & eqn & dn1 & 0xffffu;
+  *Lm = all_exact ? A : (A & (FF | (eqn & eqn1)));
+  *Fm = FF;
+  if (all_exact || (D | D3) == 0) {
     *Dm = 0;
-    *D2m = 0;
+    *D3m = 0;
   } else {
     uint32_t div2, div3;
     segment_div(t, so, &div2, &div3);
-    *Dm = D & div2;
-    *D2m = D2 & div3;
+    *Dm = (D & div2) | (D3 & div3);
+    *D3m = D3 & div3;
   }
-  *Lm = Lr;
-  *Fm = F;
 }
 
 // exclusive prefix over the wave's lanes and total of a per-lane count < 32
@@ -899,7 +903,6 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
       const uint32_t so = SMAX_LH + ro;
       classify_segment(t, so, mf, all_exact, &D, &D3, &Lq, &F);
-      D |= D3;
       const uint64_t sg = g0 + ro;
       if (sg < a.begin) {
         const uint32_t m = sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
