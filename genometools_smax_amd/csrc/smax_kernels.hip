@@ -12,7 +12,7 @@
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
 // One pass = four launches on one stream, no host synchronisation:
-//   K0 smax_head_kernel   one lane: the shard's boundary head record
+//   K0 smax_head_kernel   one lane: per-run resets (K1b computes the boundary head)
 //   K1 smax_scan_kernel   the streaming kernel (HBM bound, see below)
 //   K2 rocPRIM exclusive scan of the per-tile interval counts
 //   K3 smax_compact_kernel ordered copy of the tiles' records -> ascending lb
@@ -254,13 +254,12 @@ __device__ __forceinline__ bool seen_add(Seen &s, uint32_t c) {
 
 // One lane: the boundary record's head (run of LCP == LCP[begin]), reset of
 // the pending slot and of the overflow cursor.  Runs before K1.
-__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
-  if (threadIdx.x != 0) return;
+// The shard's boundary head (run of LCP == LCP[begin] at the shard start),
+// one lane, global reads.
+__device__ static void compute_head(const SmaxScanArgs &a) {
   Win t;
   win_init(t, a);
   GtSmaxBoundary *b = a.bnd;
-  *a.defer_count = 0;
-  b->pend_valid = 0;
   b->shard_begin = a.begin;
   b->shard_end = a.end;
   const uint32_t v = lcp_exact(t, a.begin);
@@ -287,6 +286,16 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   b->head_div.seen[0] = s.w0; b->head_div.seen[1] = s.w1;
   b->head_div.seen[2] = s.w2; b->head_div.seen[3] = s.w3;
   b->head_div.dup = dup;
+}
+
+// K0: per-run resets ahead of K1 (the pending-plateau slot, which any K1 or
+// K1b wave may fill, and K1's deferral count); for an empty shard (begin ==
+// end) also the boundary head, otherwise computed by K1b.
+__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a, int with_head) {
+  if (threadIdx.x != 0) return;
+  a.bnd->pend_valid = 0;
+  *a.defer_count = 0;
+  if (with_head) compute_head(a);
 }
 
 // ------------------------------------------------------------ K1: scan
@@ -1128,6 +1137,7 @@ smax_defer_kernel(SmaxScanArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t n = *a.defer_count;
+  if (blockIdx.x == 0 && threadIdx.x == 0) compute_head(a);
   Win t;
   win_init(t, a);
   for (uint32_t i = blockIdx.x * (SMAX_THREADS / 64) + wave; i < n;
@@ -1576,9 +1586,10 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
   HIPCHK(hipSetDevice(p->shard.device));
   {
     SmaxScanArgs a = plan_args(p);
-    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
+    const int empty = p->shard.begin >= p->shard.end;
+    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a, empty);
     HIPCHK(hipGetLastError());
-    if (p->shard.begin >= p->shard.end) {
+    if (empty) {
       HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
       return 0;
     }
