@@ -858,18 +858,19 @@ __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
   }
 }
 
-// exclusive prefix over the wave's lanes and total of a per-lane count < 32
+// exclusive prefix over the wave's lanes and total of a per-lane count:
+// DPP inclusive scan (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast 15/31 across rows) -- VALU only, no ballots or scalar popcounts
 __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
-  const uint64_t ltm = lanemask_lt();
-  uint32_t e = 0, t = 0;
-#pragma unroll
-  for (int b = 0; b < 5; b++) {
-    const uint64_t pl = __ballot((c >> b) & 1u);
-    e += (uint32_t) __popcll(pl & ltm) << b;
-    t += (uint32_t) __popcll(pl) << b;
-  }
-  *tot = t;
-  return e;
+  int x = (int) c;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  *tot = (uint32_t) __builtin_amdgcn_readlane(x, 63);
+  return (uint32_t) x - c;
 }
 
 // Returns the tile's record count, or UINT32_MAX when more than SMAX_DLIST
