@@ -384,8 +384,9 @@ __device__ __forceinline__ uint32_t seg_ge(const uint4 v, uint32_t mf) {
   return bytes_ge(v.x, mf) | bytes_ge(v.y, mf) | bytes_ge(v.z, mf) | bytes_ge(v.w, mf);
 }
 __device__ __forceinline__ uint32_t seg_ffcount(const uint4 v) {
-  return __popc(bytes_ff(v.x)) + __popc(bytes_ff(v.y)) + __popc(bytes_ff(v.z)) +
-         __popc(bytes_ff(v.w));
+  // flags at bits 7,15,23,31 of each word: merge the four words, one popcount
+  return __popc((bytes_ff(v.x) >> 7) | (bytes_ff(v.y) >> 6) | (bytes_ff(v.z) >> 5) |
+                (bytes_ff(v.w) >> 4));
 }
 
 
@@ -1011,12 +1012,15 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
   const uint4 hv = *reinterpret_cast<const uint4 *>(&t.L[lane == 0 ? 0 : SMAX_LH + SMAX_TILE]);
   const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
-  const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
-  const uint32_t hl = __builtin_amdgcn_readfirstlane(seg_ffcount(hv));   // lane 0: left halo
   t.llv_base = wlo;
   t.rank = nullptr;
   t.nval = -1;
-  if (__ballot((f0 | f1) != 0) != 0 || hl != 0) {
+  // no .llv entry in the window: no 255 byte (in a consistent index; a
+  // stray 255 still resolves exactly through the global .llv search)
+  if (wn == 0) return segpre_bits;
+  const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
+  const uint32_t hl = __builtin_amdgcn_readfirstlane(seg_ffcount(hv));   // lane 0: left halo
+  {
     // chunk 0 = left halo, 1..64 segment 0, 65..128 segment 1, 129 right halo
     uint32_t t0, t1;
     const uint32_t e0 = wave_excl(f0, &t0), e1 = wave_excl(f1, &t1);
