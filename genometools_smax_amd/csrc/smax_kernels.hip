@@ -804,19 +804,19 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
   *div3 = r3;
 }
 
-// Classification of the 16 rows c of segment `so` (byte compares exact except
-// between two 255 bytes):
+// Classification of the 16 rows c of segment `so`:
 //   *Dm  records [c-1 .. c] and [c-1 .. c+1] (D3 marks the latter): start,
 //        then LCP[c+1] < LCP[c], or LCP[c+1] == LCP[c] > LCP[c+2]; with the
 //        matching left diversity
-//   *Lm  starts needing exact evaluation: 255 byte, or LCP[c] == LCP[c+1] ==
-//        LCP[c+2] (plateau of >= 3 rows)
+//   *Lm  starts needing exact evaluation: plateaus of >= 3 rows (LCP[c] ==
+//        LCP[c+1] == LCP[c+2])
 //   *Fm  255 bytes (ranks)
 // where start = LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] >
-// LCP[c-1] (a 255/255 pair is a possible start, settled by eval_start).
-// Only two byte relations are computed, each row against its predecessor
-// (UP: LCP[r-1] < LCP[r], EQ: LCP[r-1] == LCP[r]) for rows 0..17; the
-// relations of c with c+1 and of c+1 with c+2 are the same bits shifted.
+// LCP[c-1].  Only two relations are computed, each row against its
+// predecessor (UP: LCP[r-1] < LCP[r], EQ: LCP[r-1] == LCP[r]) for rows
+// 0..17; successor relations are the same bits shifted.  Byte compares are
+// exact except between two 255 bytes: those pairs (rare) are re-decided
+// from the exact .llv values by rank (crank = 255 bytes before the segment).
 __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
                                                  uint32_t mf, bool all_exact, uint32_t *Dm,
                                                  uint32_t *D3m, uint32_t *Lm, uint32_t *Fm) {
@@ -839,16 +839,33 @@ __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
   const uint32_t b15 = w3 >> 24;
   UP |= (b15 < nb ? 1u << 16 : 0u) | (nb < nb2 ? 1u << 17 : 0u);
   EQ |= (b15 == nb ? 1u << 16 : 0u) | (nb == nb2 ? 1u << 17 : 0u);
-  const uint32_t FFP = FF & ((FF << 1) | (pb == 255u ? 1u : 0u));   // 255 after 255
-  const uint32_t A = GE & (UP | FFP) & 0xffffu;
-  const uint32_t Ae = A & ~FF;
+  const uint32_t F18 = FF | (nb == 255u ? 1u << 16 : 0u) | (nb2 == 255u ? 1u << 17 : 0u);
+  uint32_t FFP = F18 & ((F18 << 1) | (pb == 255u ? 1u : 0u));    // 255 after 255
+  bool unresolved = false;
+  if (F18 != 0 && t.rank == nullptr) {
+    unresolved = true;                      // no ranks staged: exact queue instead
+  } else if (FFP != 0) {
+    {
+      const uint32_t crank = t.rank[so >> 4];
+      while (FFP) {
+        const int r = __builtin_ctz(FFP);
+        FFP &= FFP - 1;
+        const uint32_t rk = crank + (uint32_t) __popc(F18 & ((1u << r) - 1));
+        const uint32_t vr = llv_by_rank(t, rk), vp = llv_by_rank(t, rk - 1);
+        UP = (UP & ~(1u << r)) | ((vp < vr ? 1u : 0u) << r);
+        EQ = (EQ & ~(1u << r)) | ((vp == vr ? 1u : 0u) << r);
+      }
+    }
+  }
+  const uint32_t A = GE & (UP | (unresolved ? FF & ((FF << 1) | (pb == 255u ? 1u : 0u)) : 0u))
+                     & 0xffffu;
   const uint32_t eqn = EQ >> 1, dn = ~((UP | EQ) >> 1);            // vs row c+1
   const uint32_t eqn1 = EQ >> 2, dn1 = ~((UP | EQ) >> 2);          // c+1 vs c+2
-  const uint32_t D = Ae & dn & 0xffffu;
-  const uint32_t D3 = Ae & eqn & dn1 & 0xffffu;
-  *Lm = all_exact ? A : (A & (FF | (eqn & eqn1)));
+  const uint32_t D = A & dn & 0xffffu;
+  const uint32_t D3 = A & eqn & dn1 & 0xffffu;
+  *Lm = (all_exact || unresolved) ? A : (A & eqn & eqn1);
   *Fm = FF;
-  if (all_exact || (D | D3) == 0) {
+  if (all_exact || unresolved || (D | D3) == 0) {
     *Dm = 0;
     *D3m = 0;
   } else {
@@ -901,7 +918,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   __builtin_amdgcn_wave_barrier();
   // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones
   uint32_t Dm0 = 0, Lm0 = 0, Dm1 = 0, Lm1 = 0, Lpre0 = 0, Lpre1 = 0, ro0 = 0, ro1 = 0;
-  uint32_t W30 = 0, W31 = 0;
+  uint32_t W30 = 0, W31 = 0, F0 = 0, F1 = 0;
   uint32_t nL = 0;
   const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
 #pragma unroll
@@ -934,8 +951,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
       }
     }
-    if (k == 0) { Dm0 = D; W30 = D3; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
-    else { Dm1 = D; W31 = D3; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
+    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
+    else { Dm1 = D; W31 = D3; F1 = F; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
     nL += tot;
   }
   if (nL > DL) return UINT32_MAX;
@@ -968,6 +985,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
     const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1, W3 = k == 0 ? W30 : W31;
+    const uint32_t Fk = k == 0 ? F0 : F1;
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
     const uint32_t si = k * 64 + lane;
     uint32_t acc = D;
@@ -981,7 +999,10 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       GtSmaxRecord rec;
       rec.lb = g0 + ro + q - 1;
       if ((D >> q) & 1u) {
-        rec.lcp = sL[SMAX_LH + ro + q];
+        const uint32_t b = sL[SMAX_LH + ro + q];
+        rec.lcp = b < 255 ? b
+                          : llv_by_rank(t, t.rank[(SMAX_LH + ro) >> 4] +
+                                               (uint32_t) __popc(Fk & ((1u << q) - 1)));
         rec.width = 2 + ((W3 >> q) & 1u);
       } else {
         const uint32_t i = Lpre + (uint32_t) __popc(Lq & ((1u << q) - 1));
