@@ -139,6 +139,28 @@ __device__ __forceinline__ uint32_t bytes_ff(uint32_t w) {
   return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu) & 0x80808080u;
 }
 
+// SWAR byte compares: high bit of each byte where the relation holds.
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t y) {
+  const uint32_t z = x ^ y;
+  return ~(((z & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z | 0x7f7f7f7fu) & 0x80808080u;
+}
+
+// 64-bit SWAR: high bit of each byte of x equal to the same byte of y
+__device__ __forceinline__ uint64_t bytes_eq64(uint64_t x, uint64_t y) {
+  return ((uint64_t) bytes_eq((uint32_t) (x >> 32), (uint32_t) (y >> 32)) << 32) |
+         bytes_eq((uint32_t) x, (uint32_t) y);
+}
+
+// 8 consecutive window bytes starting at LDS offset o (o + 11 inside the
+// window): three aligned dword reads, issued together
+__device__ __forceinline__ uint64_t lds_bytes8(const uint8_t *base, uint32_t o) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(base + (o & ~3u));
+  const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+  const uint32_t sh = o & 3u;
+  return ((uint64_t) __builtin_amdgcn_alignbyte(d2, d1, sh) << 32) |
+         __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+
 struct Win {
   const uint8_t *glcp;        // global (local-indexed) tables
   const uint8_t *gbwt;
@@ -222,6 +244,24 @@ __device__ static uint64_t plateau_end(const Win &t, uint64_t c, uint32_t l,
   const uint32_t lb = l < 255 ? l : 255;
   uint64_t j = c;
   *pending = false;
+  // long plateaus inside the LDS window: 8 rows per step (exact: lb < 255,
+  // rows j+1 .. j+8 all below end and N)
+  if (lb < 255 && t.L != nullptr) {
+    const uint64_t splat = lb * 0x0101010101010101ull;
+    for (;;) {
+      const int64_t o = win_off(t, j + 1);
+      if (o < 0 || o + 11 >= SMAX_LDSB || j + 8 >= t.end || j + 8 >= t.N) break;
+      const uint64_t ne = ~bytes_eq64(lds_bytes8(t.L, (uint32_t) o), splat) &
+                          0x8080808080808080ull;
+      if (ne != 0) {
+        const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
+        const uint32_t nb = t.L[o + k];
+        *rel = nb < lb ? -1 : 1;
+        return j + k;
+      }
+      j += 8;
+    }
+  }
   for (;;) {
     const uint64_t g = j + 1;
     const uint32_t nb = lcp_byte(t, g);
@@ -390,11 +430,6 @@ __device__ __forceinline__ uint32_t seg_ffcount(const uint4 v) {
 }
 
 
-// SWAR byte compares: high bit of each byte where the relation holds.
-__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t y) {
-  const uint32_t z = x ^ y;
-  return ~(((z & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z | 0x7f7f7f7fu) & 0x80808080u;
-}
 __device__ __forceinline__ uint32_t bytes_lt(uint32_t x, uint32_t y) {   // x < y
   const uint32_t H = 0x80808080u;
   const uint32_t d = (x | H) - (y & ~H);      // per byte 128 + xl - yl, no borrow
@@ -486,20 +521,6 @@ __device__ __forceinline__ uint32_t segment_starts_exact(const Win &t, const Sma
   return st;
 }
 
-// 64-bit SWAR: high bit of each byte of x equal to the same byte of y
-__device__ __forceinline__ uint64_t bytes_eq64(uint64_t x, uint64_t y) {
-  return ((uint64_t) bytes_eq((uint32_t) (x >> 32), (uint32_t) (y >> 32)) << 32) |
-         bytes_eq((uint32_t) x, (uint32_t) y);
-}
-// 8 consecutive window bytes starting at LDS offset o (o + 11 inside the
-// window): three aligned dword reads, issued together
-__device__ __forceinline__ uint64_t lds_bytes8(const uint8_t *base, uint32_t o) {
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(base + (o & ~3u));
-  const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
-  const uint32_t sh = o & 3u;
-  return ((uint64_t) __builtin_amdgcn_alignbyte(d2, d1, sh) << 32) |
-         __builtin_amdgcn_alignbyte(d1, d0, sh);
-}
 // left diversity of the first w (2..8) symbols of X: symbols < 254 pairwise
 // distinct
 __device__ __forceinline__ bool diverse8(uint64_t X, uint32_t w) {
