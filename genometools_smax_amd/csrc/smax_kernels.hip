@@ -51,7 +51,7 @@
 #define SMAX_RH 16                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
-#define SMAX_LLV_CAP 56                               // .llv values in LDS (1 per lane)
+#define SMAX_LLV_CAP 112                              // .llv values staged in K1's LDS (u16)
 #define SMAX_LIST 96                                  // per-wave start-list window
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
                                                       // records are >= 2 rows apart)
@@ -67,6 +67,7 @@ struct SmaxScanArgs {
   const uint8_t *bwt;
   const uint64_t *bwtpk;     // packed BWT, 16 rows per u64 (index local_row/16 + 1), or null
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
+  const uint16_t *llv16;     // their values as u16 (plan time; windows with larger ones defer)
   uint64_t numllv;
   const uint2 *llv_win;      // per tile: {first llv index >= g0 - LH, entries in the window}
   uint64_t base, begin, end, N;
@@ -171,7 +172,8 @@ struct Win {
   const uint8_t *B;           // BWT bytes of the window (byte kernel), or
   const uint64_t *P;          // packed BWT of the window, 16 rows per word
   const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
-  const uint32_t *val;        // LDS .llv values in rank order (nval of them)
+  const uint32_t *val;        // LDS .llv values in rank order (nval of them), or
+  const uint16_t *val16;      // the same as u16 (K1 windows: values < 65536)
   int nval;                   // -1: values not staged (read global by rank)
   uint64_t g0;                // global row of the tile start
   uint64_t llv_base;          // first llv entry of the window
@@ -180,7 +182,8 @@ struct Win {
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
-  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr; t.nval = -1;
+  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr;
+  t.val16 = nullptr; t.nval = -1;
   t.g0 = 0; t.llv_base = 0;
 }
 
@@ -200,7 +203,7 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
     if (within < 8) cnt = __popcll(lo & ((1ull << (8 * within)) - 1));
     else cnt = __popcll(lo) + __popcll(hi & ((1ull << (8 * (within - 8))) - 1));
     const uint32_t r = t.rank[chunk] + (uint32_t) cnt;
-    if ((int) r < t.nval) return t.val[r];
+    if ((int) r < t.nval) return t.val16 != nullptr ? t.val16[r] : t.val[r];
     if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
     return llv_value(&t.llv[t.llv_base + r]);
   }
@@ -367,22 +370,27 @@ __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" 
 struct SmaxWindow {            // byte BWT (any alphabet)
   uint8_t L[SMAX_LDSB];
   uint8_t B[SMAX_LDSB];
-  uint32_t val[SMAX_LLV_CAP];
+  uint16_t val16[SMAX_LLV_CAP];
 };
 struct SmaxWindowPk {          // packed BWT (DNA): 0.5 B per row
   uint8_t L[SMAX_LDSB];
   uint64_t P[SMAX_LDSB / 16];
-  uint32_t val[SMAX_LLV_CAP];
+  uint16_t val16[SMAX_LLV_CAP];
 };
 
 // Issue the DMA of tile `l0` (local index) into the calling wave's window
 // w: 16 B per lane per instruction (1 KiB per wave instruction), the two
 // 16-row halos, and the window's .llv values {lo, n} (low dword of each
 // record's value, at most SMAX_LLV_CAP).
+struct SmaxWindowFull {        // K1b: byte BWT and every .llv value of the window
+  uint8_t L[SMAX_LDSB];
+  uint8_t B[SMAX_LDSB];
+  uint32_t val[SMAX_LDSB];
+};
 static_assert(SMAX_LH == 16 && SMAX_RH == 16 && SMAX_TILE == 2048,
               "packed window: one halo group each side, 128 tile groups");
 __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0, uint8_t *L,
-                                              uint32_t *val, uint32_t lo, uint32_t n) {
+                                              uint16_t *val, uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
   const uint32_t wl = __builtin_amdgcn_readfirstlane(lds_addr(L));
   const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(val));
@@ -393,15 +401,17 @@ __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0
     glds16(a.lcp + l0 - SMAX_LH, wl);
     glds16(a.lcp + l0 + SMAX_TILE, wl + SMAX_LH + SMAX_TILE);
   }
-  if ((uint32_t) lane < n && lane < SMAX_LLV_CAP)
-    glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + lane) + 8, wv);
+  // u16 copies of the values (plan-time array; K1 defers windows holding a
+  // value >= 65536): two per lane from the even index at or below lo
+  if (n != 0 && lane < SMAX_LLV_CAP / 2 && (uint32_t) (2 * lane) < n + 1)
+    glds4(a.llv16 + (lo & ~1u) + 2 * lane, wv);
 }
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
   const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w->B));
   const uint8_t *bs = a.bwt + l0 + lane * 16;
-  issue_lcp_llv(a, l0, w->L, w->val, lo, n);
+  issue_lcp_llv(a, l0, w->L, w->val16, lo, n);
 #pragma unroll
   for (int r = 0; r < SMAX_SEGS; r++) glds16(bs + r * 1024, wb + SMAX_LH + r * 1024);
   if (lane == 0) {
@@ -409,13 +419,31 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
     glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
   }
 }
+__device__ __forceinline__ void issue_window_full(const SmaxScanArgs &a, uint64_t l0,
+                                                  SmaxWindowFull *w, uint32_t lo, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w->B));
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val));
+  const uint8_t *bs = a.bwt + l0 + lane * 16;
+  issue_lcp_llv(a, l0, w->L, reinterpret_cast<uint16_t *>(w->val), lo, 0);
+#pragma unroll
+  for (int r = 0; r < SMAX_SEGS; r++) glds16(bs + r * 1024, wb + SMAX_LH + r * 1024);
+  if (lane == 0) {
+    glds16(a.bwt + l0 - SMAX_LH, wb);
+    glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
+  }
+  const uint32_t m = n < SMAX_LDSB ? n : SMAX_LDSB;
+  for (uint32_t i0 = 0; i0 < m; i0 += 64)
+    if (i0 + lane < m)
+      glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + i0 + lane) + 8, wv + i0 * 4);
+}
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
   const uint32_t wp = __builtin_amdgcn_readfirstlane(lds_addr(w->P));
   // groups l0/16 .. l0/16 + 129 of the packed array (index = local_row/16 + 1)
   const uint64_t *ps = a.bwtpk + l0 / 16;
-  issue_lcp_llv(a, l0, w->L, w->val, lo, n);
+  issue_lcp_llv(a, l0, w->L, w->val16, lo, n);
   glds16(ps + lane * 2, wp);                             // groups 0 .. 127
   if (lane == 0) glds16(ps + 128, wp + 1024);            // groups 128, 129
 }
@@ -445,7 +473,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 __device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
-  if ((int) r < t.nval) return t.val[r];
+  if ((int) r < t.nval) return t.val16 != nullptr ? t.val16[r] : t.val[r];
   if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
   return llv_value(&t.llv[t.llv_base + r]);
 }
@@ -1046,7 +1074,8 @@ __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = 
 // "any byte >= min(minlen,128)" bits, and the window's 255-byte ranks in
 // `rank` (values already in LDS) when it holds any 255 byte.
 __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
-                                                   uint32_t wlo, uint32_t wn) {
+                                                   uint32_t wlo, uint32_t wn,
+                                                   uint32_t cap = SMAX_LLV_CAP) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint32_t so = SMAX_LH + lane * 16;
@@ -1074,7 +1103,11 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    t.nval = (int) (wn < SMAX_LLV_CAP ? wn : SMAX_LLV_CAP);
+    t.nval = (int) (wn < cap ? wn : cap);
+    if (t.val16 != nullptr) {            // staged from the even index below wlo
+      t.val16 += wlo & 1u;
+      if ((uint32_t) t.nval > cap - (wlo & 1u)) t.nval = (int) (cap - (wlo & 1u));
+    }
     t.rank = (a.dbg & 16u) ? nullptr : rank;
   }
   return segpre_bits;
@@ -1130,14 +1163,17 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     t.g0 = g0;
     t.L = W->L;
     set_bwt_window(t, W);
-    t.val = W->val;
+    t.val = nullptr;
+    t.val16 = W->val16;
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
+    // .llv window {lo, n | bit 31: a value >= 65536}
     const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][0]);
-    const uint32_t wn = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][1]);
+    const uint32_t wnf = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][1]);
+    const uint32_t wn = wnf & 0x7fffffffu;
     const uint32_t nlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][0]);
-    const uint32_t nn = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][1]);
+    const uint32_t nn = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][1]) & 0x7fffffffu;
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
@@ -1156,7 +1192,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
     uint32_t wcount = 0;
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-    bool defer = edge || (wave_pre && (a.dbg & 128u));
+    // windows with more .llv values than K1 stages go to K1b (which stages
+    // all of them): K1 then never waits on a global .llv read
+    bool defer = edge || (wave_pre && ((a.dbg & 128u) || wnf > SMAX_LLV_CAP));
     if (!defer && wave_pre) {
       wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
       defer = wcount == UINT32_MAX;
@@ -1177,7 +1215,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
 // N; records the pending plateau at the shard end).  Byte BWT windows.
 __global__ void __launch_bounds__(SMAX_THREADS)
 smax_defer_kernel(SmaxScanArgs a) {
-  __shared__ __attribute__((aligned(16))) SmaxWindow sWin[SMAX_THREADS / 64];
+  __shared__ __attribute__((aligned(16))) SmaxWindowFull sWin[SMAX_THREADS / 64];
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
   // direct-path queue (256 exact starts) or the generic path's start list
   __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * 256 + 2 * 64 / 4 + 64];
@@ -1190,20 +1228,22 @@ smax_defer_kernel(SmaxScanArgs a) {
   for (uint32_t i = blockIdx.x * (SMAX_THREADS / 64) + wave; i < n;
        i += gridDim.x * (SMAX_THREADS / 64)) {
     const uint64_t tile = a.defer_list[i];
-    const uint2 info = a.llv_win[tile];
+    uint2 info = a.llv_win[tile];
+    info.y &= 0x7fffffffu;                                  // drop the wide-value flag
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
     const uint64_t g0 = a.base + l0;
-    SmaxWindow *W = &sWin[wave];
+    SmaxWindowFull *W = &sWin[wave];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // previous tile's LDS reads done
-    issue_window(a, l0, W, __builtin_amdgcn_readfirstlane(info.x),
-                 __builtin_amdgcn_readfirstlane(info.y));
+    issue_window_full(a, l0, W, __builtin_amdgcn_readfirstlane(info.x),
+                      __builtin_amdgcn_readfirstlane(info.y));
     glds_wait();
     t.g0 = g0;
     t.L = W->L;
     t.B = W->B;
     t.P = nullptr;
     t.val = W->val;
-    const uint32_t segpre_bits = prepare_window(t, a, sRank[wave], info.x, info.y);
+    t.val16 = nullptr;
+    const uint32_t segpre_bits = prepare_window(t, a, sRank[wave], info.x, info.y, SMAX_LDSB);
     const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
     GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
@@ -1309,6 +1349,14 @@ smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
 
 // ------------------------------------------------------------ llv index
 
+// u16 copies of the .llv values (larger values are flagged per tile by the
+// index kernel; those windows never read this array)
+__global__ void __launch_bounds__(256)
+smax_llv16_kernel(const GtSmaxLlv *llv, uint64_t numllv, uint16_t *out) {
+  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (i < numllv) out[i] = (uint16_t) llv[i].value;
+}
+
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
                                       uint64_t base, uint64_t tile_first,
                                       uint32_t num_tiles, uint2 *win_out,
@@ -1332,7 +1380,10 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
     const uint64_t mid = (lo2 + hi2) >> 1;
     if (llv[mid].position < key2) lo2 = mid + 1; else hi2 = mid;
   }
-  win_out[t] = make_uint2((uint32_t) lo, (uint32_t) (lo2 - lo));
+  uint32_t wide = 0;                       // K1 stages values as u16
+  for (uint64_t k = lo; k < lo2; k++)
+    if (llv[k].value > 0xffffull) { wide = 0x80000000u; break; }
+  win_out[t] = make_uint2((uint32_t) lo, (uint32_t) (lo2 - lo) | wide);
 }
 
 // ------------------------------------------------------------ stitch
@@ -1416,6 +1467,7 @@ struct GtSmaxPlan {
   uint2 *llv_win;
   uint64_t *bwtpk;           // packed BWT (DNA shards), else null
   bool pk;
+  uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
   uint32_t *defer_count;
   uint32_t *err;
@@ -1570,6 +1622,11 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   {
     const uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
     const unsigned blocks = (unsigned) ((work + 255) / 256);
+    HIPCHK(hipMalloc(&p->llv16, sizeof (uint16_t) * (shard->numllv + 4)));
+    HIPCHK(hipMemset(p->llv16, 0, sizeof (uint16_t) * (shard->numllv + 4)));
+    if (shard->numllv)
+      hipLaunchKernelGGL(smax_llv16_kernel, dim3((unsigned) ((shard->numllv + 255) / 256)),
+                         dim3(256), 0, 0, shard->llv_dev, shard->numllv, p->llv16);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
                        shard->llv_dev, shard->numllv, shard->base, p->tile_first,
                        p->num_tiles, p->llv_win, derr);
@@ -1591,7 +1648,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
-                  p->llv_win, p->err, p->scan_tmp, p->bwtpk, p->defer_list,
+                  p->llv_win, p->err, p->scan_tmp, p->bwtpk, p->llv16, p->defer_list,
                   p->defer_count};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
@@ -1605,6 +1662,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.lcp = p->shard.lcp_dev;
   a.bwt = p->shard.bwt_dev;
   a.bwtpk = p->pk ? p->bwtpk : nullptr;
+  a.llv16 = p->llv16;
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;
   a.llv_win = p->llv_win;
