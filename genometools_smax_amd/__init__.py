@@ -134,6 +134,7 @@ def lib():
         L.gt_smax_plan_error_bits.restype = ctypes.c_uint32
         L.gt_smax_plan_deferred_tiles.argtypes = [vp]
         L.gt_smax_plan_deferred_tiles.restype = ctypes.c_uint32
+        L.gt_smax_plan_debug_tiles.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_uint32)]
         _lib = L
     return _lib
 
@@ -414,6 +415,17 @@ class SmaxPlan:
 
     def deferred_tiles(self):
         return lib().gt_smax_plan_deferred_tiles(self.plan)
+
+    def debug_tiles(self):
+        """Diagnostic: (per-tile counts, deferred tile ids) of the last run."""
+        import numpy as np
+        counts = np.zeros(self.num_tiles, dtype=np.uint32)
+        deferred = np.zeros(self.num_tiles, dtype=np.uint32)
+        n = ctypes.c_uint32()
+        if lib().gt_smax_plan_debug_tiles(self.plan, counts.ctypes.data, deferred.ctypes.data,
+                                          ctypes.byref(n)) != 0:
+            raise SmaxError("gt_smax_plan_debug_tiles failed")
+        return counts, deferred[: n.value].copy()
 
     def fetch_count(self):
         c = ctypes.c_uint64()

@@ -52,7 +52,6 @@
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
 #define SMAX_LLV_CAP 112                              // .llv values staged in K1's LDS (u16)
-#define SMAX_LIST 96                                  // per-wave start-list window
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
                                                       // records are >= 2 rows apart)
 
@@ -60,7 +59,6 @@ static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
 static_assert(GT_SMAX_PAD_FRONT >= SMAX_LH, "front padding covers the halo");
 static_assert(SMAX_LDSB % 16 == 0, "window is whole 16-byte chunks");
-static_assert(SMAX_LIST % 2 == 0, "u16 list pairs");
 
 struct SmaxScanArgs {
   const uint8_t *lcp;        // local tables: index i <-> global base+i
@@ -337,7 +335,7 @@ __device__ static void compute_head(const SmaxScanArgs &a) {
 __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a, int with_head) {
   if (threadIdx.x != 0) return;
   a.bnd->pend_valid = 0;
-  *a.defer_count = 0;
+  if (!(a.dbg & 16384u)) *a.defer_count = 0;   // diagnostic: K1b alone on K1's last list
   if (with_head) compute_head(a);
 }
 
@@ -382,11 +380,6 @@ struct SmaxWindowPk {          // packed BWT (DNA): 0.5 B per row
 // w: 16 B per lane per instruction (1 KiB per wave instruction), the two
 // 16-row halos, and the window's .llv values {lo, n} (low dword of each
 // record's value, at most SMAX_LLV_CAP).
-struct SmaxWindowFull {        // K1b: byte BWT and every .llv value of the window
-  uint8_t L[SMAX_LDSB];
-  uint8_t B[SMAX_LDSB];
-  uint32_t val[SMAX_LDSB];
-};
 static_assert(SMAX_LH == 16 && SMAX_RH == 16 && SMAX_TILE == 2048,
               "packed window: one halo group each side, 128 tile groups");
 __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0, uint8_t *L,
@@ -418,24 +411,6 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
     glds16(a.bwt + l0 - SMAX_LH, wb);
     glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
   }
-}
-__device__ __forceinline__ void issue_window_full(const SmaxScanArgs &a, uint64_t l0,
-                                                  SmaxWindowFull *w, uint32_t lo, uint32_t n) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w->B));
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val));
-  const uint8_t *bs = a.bwt + l0 + lane * 16;
-  issue_lcp_llv(a, l0, w->L, reinterpret_cast<uint16_t *>(w->val), lo, 0);
-#pragma unroll
-  for (int r = 0; r < SMAX_SEGS; r++) glds16(bs + r * 1024, wb + SMAX_LH + r * 1024);
-  if (lane == 0) {
-    glds16(a.bwt + l0 - SMAX_LH, wb);
-    glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
-  }
-  const uint32_t m = n < SMAX_LDSB ? n : SMAX_LDSB;
-  for (uint32_t i0 = 0; i0 < m; i0 += 64)
-    if (i0 + lane < m)
-      glds4(reinterpret_cast<const uint8_t *>(a.llv + lo + i0 + lane) + 8, wv + i0 * 4);
 }
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                              uint32_t lo, uint32_t n) {
@@ -495,58 +470,6 @@ __device__ __forceinline__ bool diverse_rows(const Win &t, uint64_t lo, uint64_t
   for (uint64_t g = lo; g <= hi; g++)
     if (seen_add(s, bwt_at(t, g))) return false;
   return true;
-}
-
-// Plateau-start mask of one interior 16-row segment (rows sg..sg+15), SWAR
-// over the LCP bytes of rows sg-1..sg+15 from LDS: bit q set iff
-// LCP[q] >= min(minlen,128) (exact for minlen <= 128) and LCP[q] > LCP[q-1].
-// Byte compares are exact except between two 255 bytes; those pairs are
-// fixed up with exact .llv values.
-__device__ __forceinline__ uint32_t segment_starts_fast(const Win &t, uint32_t so,
-                                                        const uint8_t *sL, uint32_t mf,
-                                                        uint32_t crank, uint32_t *ffo) {
-  const uint4 v = *reinterpret_cast<const uint4 *>(&sL[so]);
-  const uint32_t prevb = sL[so - 1];
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t GE = 0, UP = 0, FF = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t cur = w[k];
-    const uint32_t prv = k == 0 ? ((cur << 8) | prevb) : __builtin_amdgcn_alignbyte(cur, w[k - 1], 3);
-    GE |= pack4(bytes_ge(cur, mf)) << (4 * k);
-    UP |= pack4(bytes_lt(prv, cur)) << (4 * k);
-    FF |= pack4(bytes_ff(cur)) << (4 * k);
-  }
-  uint32_t st = GE & UP;
-  // exact compares where both bytes are 255 (only matters for candidate rows)
-  uint32_t fu = FF & ((FF << 1) | (prevb == 255u ? 1u : 0u)) & GE;
-  // (rank of row q = the chunk's rank + 255 bytes before q; row q-1 is the
-  // 255 byte just before it)
-  while (fu) {
-    const int q = __builtin_ctz(fu);
-    fu &= fu - 1;
-    const uint32_t rc = crank + (uint32_t) __popc(FF & ((1u << q) - 1));
-    const uint32_t c = llv_by_rank(t, rc), p = llv_by_rank(t, rc - 1);
-    st = (st & ~(1u << q)) | ((c > p ? 1u : 0u) << q);
-  }
-  *ffo = FF;
-  return st;
-}
-
-// Exact plateau-start mask of one edge-tile segment (rows >= end or N, row
-// 0, rows before begin): bit q iff begin <= c < end, LCP[c] >= minlen and
-// LCP[c] > LCP[c-1].
-__device__ __forceinline__ uint32_t segment_starts_exact(const Win &t, const SmaxScanArgs &a,
-                                                         uint64_t sg) {
-  uint32_t st = 0;
-  uint32_t prev = lcp_exact(t, sg - 1);
-  for (int q = 0; q < 16; q++) {
-    const uint64_t c = sg + q;
-    const uint32_t cur = lcp_exact(t, c);
-    if (c >= a.begin && c < a.end && cur >= a.minlen && cur > prev) st |= 1u << q;
-    prev = cur;
-  }
-  return st;
 }
 
 // left diversity of the first w (2..8) symbols of X: symbols < 254 pairwise
@@ -671,122 +594,6 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
   return acc;
 }
 
-// Evaluate list[0 .. nwin) (row offsets inside the tile, row order), 64
-// starts per step, one per lane; accepted records are appended in row order
-// to the tile's slot.
-__device__ static uint32_t eval_list(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                     const uint8_t *sL, const uint16_t *list,
-                                     const uint16_t *lrank, uint32_t nwin,
-                                     GtSmaxRecord *wdst, uint32_t wcount, bool interior) {
-  const int lane = threadIdx.x & 63;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  for (uint32_t i0 = 0; i0 < nwin && !(a.dbg & 4u); i0 += 64) {
-    const uint32_t i = i0 + lane;
-    bool acc = false;
-    uint32_t cur = 0;
-    uint64_t j = 0;
-    if (i < nwin) acc = eval_start(t, a, g0, sL, list[i], lrank[i], interior, &cur, &j);
-    const uint64_t am = __ballot(acc);
-    if (acc) {
-      const uint64_t cc = g0 + list[i];
-      GtSmaxRecord rec;
-      rec.lb = cc - 1;
-      rec.lcp = cur;
-      rec.width = (uint32_t) (j - cc + 2);
-      wdst[wcount + (uint32_t) __popcll(am & lanemask_lt())] = rec;
-    }
-    wcount += (uint32_t) __popcll(am);
-  }
-  __builtin_amdgcn_wave_barrier();   // list reused after this
-  return wcount;
-}
-
-// Detection for one wave's 4096 rows, per segment round r (the 64 lanes'
-// segments r, rows lane-major = row order):
-//   1. each lane's 16-bit plateau-start mask (SWAR in interior tiles, exact
-//      per row in the shard's edge tiles);
-//   2. the wave compacts the starts, in row order, into an LDS list;
-//   3. the list is evaluated 64 starts per step, one per lane: exact plateau
-//      end in LDS, local-maximum test, left-diversity over BWT[lb..rb], the
-//      pending plateau at the shard end; accepted records are written in row
-//      order to the wave's slot (ballot prefix).
-// No lane loops over another lane's work: the per-start cost is spread over
-// all 64 lanes instead of serialising the wave on its busiest lane.
-__device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                       const uint8_t *sL, uint16_t *list, uint16_t *lrank,
-                                       GtSmaxRecord *wdst,
-                                       bool interior, uint32_t segpre) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
-  const uint64_t gw = g0;
-  uint32_t wcount = 0;
-  uint32_t pend = 0;                 // starts queued in the list (all rounds)
-#pragma unroll 1
-  for (int r = 0; r < SMAX_SEGS; r++) {
-    const uint32_t so = SMAX_LH + r * 1024 + lane * 16;
-    const uint64_t sg = gw + r * 1024 + lane * 16;
-    uint32_t st = 0, ff = 0;
-    const uint32_t crank = (interior && t.rank != nullptr) ? t.rank[so >> 4] : 0u;
-    if (interior) {
-      if ((segpre >> r) & 1u) {
-        st = segment_starts_fast(t, so, sL, mf, crank, &ff);
-        if (sg < a.begin)
-          st &= sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
-      }
-    } else {
-      st = segment_starts_exact(t, a, sg);
-    }
-    // exclusive prefix of the counts (<= 16) over bit planes: no LDS trips
-    const uint32_t c = (uint32_t) __popc(st);
-    const uint64_t ltm = lanemask_lt();
-    uint32_t excl = 0, nstart = 0;
-#pragma unroll
-    for (int b = 0; b < 5; b++) {
-      const uint64_t pl = __ballot((c >> b) & 1u);
-      excl += (uint32_t) __popcll(pl & ltm) << b;
-      nstart += (uint32_t) __popcll(pl) << b;
-    }
-    if (nstart == 0 || (a.dbg & 8u)) { wcount += nstart & (a.dbg >> 9); continue; }
-    const uint32_t rowbase = r * 1024 + lane * 16;     // row offset inside the wave
-    if (pend + nstart > SMAX_LIST && pend != 0) {      // make room: evaluate the queue
-      wcount = eval_list(t, a, g0, sL, list, lrank, pend, wdst, wcount, interior);
-      pend = 0;
-    }
-    if (nstart <= SMAX_LIST) {
-      // queue this round's starts behind the pending ones (row order)
-      uint32_t pos = pend + excl;
-      uint32_t bits = st;
-      while (bits) {
-        const int q = __builtin_ctz(bits);
-        bits &= bits - 1;
-        if ((ff >> q) & 1u) lrank[pos] = (uint16_t) (crank + (uint32_t) __popc(ff & ((1u << q) - 1)));
-        list[pos++] = (uint16_t) (rowbase + q);
-      }
-      pend += nstart;
-      continue;
-    }
-    // a ramp can make every row a start: windows of SMAX_LIST starts
-    for (uint32_t w0 = 0; w0 < nstart; w0 += SMAX_LIST) {
-      uint32_t pos = excl;
-      uint32_t bits = st;
-      while (bits) {
-        const int q = __builtin_ctz(bits);
-        bits &= bits - 1;
-        if (pos >= w0 && pos < w0 + SMAX_LIST) {
-          if ((ff >> q) & 1u) lrank[pos - w0] = (uint16_t) (crank + (uint32_t) __popc(ff & ((1u << q) - 1)));
-          list[pos - w0] = (uint16_t) (rowbase + q);
-        }
-        pos++;
-      }
-      const uint32_t nwin = nstart - w0 < SMAX_LIST ? nstart - w0 : SMAX_LIST;
-      wcount = eval_list(t, a, g0, sL, list, lrank, nwin, wdst, wcount, interior);
-    }
-  }
-  if (pend != 0) wcount = eval_list(t, a, g0, sL, list, lrank, pend, wdst, wcount, interior);
-  return wcount;
-}
-
 // ---- interior tiles: SWAR classification of every plateau start
 //
 // Most supermaximal-repeat intervals are two rows wide (a plateau of one
@@ -799,7 +606,6 @@ __device__ static uint32_t wave_detect(const Win &t, const SmaxScanArgs &a, uint
 // order by their owning lanes.
 #define SMAX_DLIST 64                                 // queued exact starts per tile
 
-static_assert(2 * SMAX_LIST * 2 <= 3 * SMAX_DLIST * 4, "wave_detect list fits the queue");
 
 // high bit of each byte >= 254 (WILDCARD / SEPARATOR / UNDEFBWTCHAR)
 __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0x01010101u); }
@@ -1210,54 +1016,291 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   glds_wait();
 }
 
-// K1b: the deferred tiles (shard edges, exact-queue overflow), one wave per
-// tile through the generic start-list path (exact at row 0, begin, end and
-// N; records the pending plateau at the shard end).  Byte BWT windows.
+// K1b: the tiles K1 defers -- shard edges (row 0, begin, end, N), windows
+// with more .llv values than K1 stages, exact-queue overflow -- plus the
+// shard's boundary head.  One wave per tile, everything exact: the window's
+// LCP values are expanded to u32 in LDS (bytes, then the window's .llv
+// values scattered over their 255 bytes), so no rank arithmetic and no
+// lane-serial scan over a run of 255 bytes.  Per 64-row step every lane
+// decides one row (start: LCP[c] > LCP[c-1], LCP[c] >= minlen, c owned;
+// plateau end: LCP[c+1] != LCP[c]) into wave ballots; the starts are then
+// compacted (row order, 512 rows at a time) and evaluated 64 at a time:
+// plateau end from the ballot words, local maximum, left diversity over the
+// window's BWT bytes, the pending plateau at the shard end.  Plateaus that
+// run past the window take the generic global path (eval_start).
+#define SMAX_XQ 512                                   // rows per compaction round
+#define SMAX_XSTEPS ((SMAX_TILE + 64 + 63) / 64)      // ballot steps incl. right halo
+
+struct SmaxWindowX {
+  uint8_t L[SMAX_LDSB];
+  uint8_t B[SMAX_LDSB];
+  uint32_t X[SMAX_LDSB];        // exact LCP of window row o (0 outside [1, N))
+  uint64_t ne[SMAX_XSTEPS];     // bit b: LCP[row b + 1] != LCP[row b] (tile rows b)
+  uint64_t st[SMAX_TILE / 64];  // bit b: row b is an owned plateau start
+  uint16_t list[SMAX_XQ];
+};
+
+// Loads tile l0's window (rows g0-LH .. g0+TILE+RH-1) into W and expands the
+// exact LCP values.  Sets the error bit when the window's 255 bytes and its
+// .llv entries disagree.
+__device__ static void load_exact_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowX *W) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t g0 = a.base + l0;
+  const uint2 info = a.llv_win[l0 / SMAX_TILE - a.tile_first];
+  const uint32_t lo = info.x, n = info.y & 0x7fffffffu;
+  const uint64_t wb = g0 - SMAX_LH;
+  // every load of the window first (3 chunks of LCP and BWT per lane, the
+  // first 4 .llv entries per lane), then the LDS writes
+  uint4 lv[3], bv[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int i = lane + 64 * r;
+    if (r < 2 || i < SMAX_NCHUNK) {
+      const int64_t r0 = (int64_t) l0 - SMAX_LH + 16 * i;
+      lv[r] = *reinterpret_cast<const uint4 *>(a.lcp + r0);
+      bv[r] = *reinterpret_cast<const uint4 *>(a.bwt + r0);
+    } else {
+      lv[r] = make_uint4(0, 0, 0, 0);
+      bv[r] = lv[r];
+    }
+  }
+  uint4 ev[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t e = (uint32_t) lane + 64u * r;
+    ev[r] = e < n ? *reinterpret_cast<const uint4 *>(&a.llv[lo + e]) : make_uint4(0, 0, 0, 0);
+  }
+  uint32_t nff = 0;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int i = lane + 64 * r;
+    if (r == 2 && i >= SMAX_NCHUNK) break;
+    *reinterpret_cast<uint4 *>(&W->L[16 * i]) = lv[r];
+    *reinterpret_cast<uint4 *>(&W->B[16 * i]) = bv[r];
+    nff += seg_ffcount(lv[r]);
+    const int64_t gr = (int64_t) wb + 16 * i;                     // global row of the chunk
+    const uint32_t w[4] = {lv[r].x, lv[r].y, lv[r].z, lv[r].w};
+    const bool inner = gr >= 1 && gr + 16 <= (int64_t) a.N;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint4 x;
+      uint32_t *xe = &x.x;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int64_t g = gr + 4 * k + q;
+        const uint32_t byte = (w[k] >> (8 * q)) & 0xffu;
+        xe[q] = (inner || (g >= 1 && g < (int64_t) a.N)) ? byte : 0u;
+      }
+      *reinterpret_cast<uint4 *>(&W->X[16 * i + 4 * k]) = x;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // .llv values over their 255 bytes (entries of [g0-LH, g0+TILE+RH)); the
+  // record is {u64 position, u64 value}: x,y = position, z = value low dword
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t e = (uint32_t) lane + 64u * r;
+    const uint64_t pos = ((uint64_t) ev[r].y << 32) | ev[r].x;
+    const uint64_t o = pos - wb;
+    if (e < n && o < SMAX_LDSB && pos < a.N) W->X[o] = ev[r].z;
+  }
+  for (uint32_t e0 = 256; e0 < n; e0 += 256) {       // dense windows: 4 entries per lane per batch
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t e = e0 + (uint32_t) lane + 64u * r;
+      ev[r] = e < n ? *reinterpret_cast<const uint4 *>(&a.llv[lo + e]) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t e = e0 + (uint32_t) lane + 64u * r;
+      const uint64_t pos = ((uint64_t) ev[r].y << 32) | ev[r].x;
+      const uint64_t o = pos - wb;
+      if (e < n && o < SMAX_LDSB && pos < a.N) W->X[o] = ev[r].z;
+    }
+  }
+  uint32_t tot;
+  (void) wave_excl(nff, &tot);
+  // every 255 byte of [1, N) in the window has its entry (rows < 1 or >= N
+  // hold 0 bytes in a consistent index)
+  if (tot != n && lane == 0) atomicOr(a.err, SMAX_ERR_LLV);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// The boundary head from the exact window of the shard's first tile (the
+// run of LCP == LCP[begin]); runs leaving the window take compute_head.
+__device__ static void head_from_window(const SmaxScanArgs &a, const SmaxWindowX *W, uint64_t g0) {
+  if ((threadIdx.x & 63) != 0) return;
+  const uint64_t wb = g0 - SMAX_LH;
+  uint64_t o = a.begin - wb;
+  const uint32_t v = W->X[o];
+  Seen s = {0, 0, 0, 0};
+  uint64_t dup = 0, f = UINT64_MAX, nxt = 0;
+  if (v >= a.minlen && a.begin < a.end) {
+    for (;;) {
+      if (seen_add(s, W->B[o])) { dup = 1; break; }
+      if (o + 1 >= SMAX_LDSB) { compute_head(a); return; }
+      const uint32_t nx = W->X[o + 1];
+      if (nx != v) { f = wb + o + 1; nxt = nx; break; }
+      if (wb + o + 1 >= a.end) break;   // run covers the whole shard: passthrough
+      o++;
+    }
+  } else {
+    f = a.begin;
+    nxt = v;
+  }
+  GtSmaxBoundary *b = a.bnd;
+  b->shard_begin = a.begin;
+  b->shard_end = a.end;
+  b->head_v = v;
+  b->head_f = f;
+  b->head_next = nxt;
+  b->head_div.seen[0] = s.w0; b->head_div.seen[1] = s.w1;
+  b->head_div.seen[2] = s.w2; b->head_div.seen[3] = s.w3;
+  b->head_div.dup = dup;
+}
+
+// Exact evaluation of the plateau start at tile row b (window W, LCP value
+// cur); returns whether [c-1 .. j] is a supermaximal-repeat interval.
+__device__ static bool eval_start_x(const SmaxScanArgs &a, const Win &t, const SmaxWindowX *W,
+                                    uint64_t g0, uint32_t b, uint32_t *curo, uint64_t *jo) {
+  const uint32_t o = b + SMAX_LH;
+  const uint32_t cur = W->X[o];
+  // plateau end: first row >= b whose successor differs
+  uint32_t wi = b >> 6;
+  uint64_t m = W->ne[wi] >> (b & 63);
+  uint32_t jb = b;
+  while (m == 0 && wi + 1 < SMAX_XSTEPS) {
+    jb = (wi + 1) << 6;
+    m = W->ne[++wi];
+  }
+  jb += (uint32_t) __builtin_ctzll(m);
+  if (jb + SMAX_LH + 1 >= SMAX_LDSB) {
+    // the plateau leaves the window: generic exact path (global reads)
+    return eval_start(t, a, g0, W->L, b, 0, false, curo, jo);
+  }
+  *curo = cur;
+  const uint64_t c = g0 + b, j = g0 + jb;
+  *jo = j;
+  if (j >= a.end) {
+    // the plateau contains row `end`: pending, resolved by the stitch
+    Seen sn = {0, 0, 0, 0};
+    bool dup = false;
+    for (uint64_t g = c - 1; g < a.end && !dup; g++) dup = seen_add(sn, W->B[g - g0 + SMAX_LH]);
+    if (!dup) {
+      GtSmaxBoundary *bd = a.bnd;
+      bd->pend_c = c;
+      bd->pend_lcp = cur;
+      bd->pend_div.seen[0] = sn.w0; bd->pend_div.seen[1] = sn.w1;
+      bd->pend_div.seen[2] = sn.w2; bd->pend_div.seen[3] = sn.w3;
+      bd->pend_div.dup = 0;
+      bd->pend_valid = 1;
+    }
+    return false;
+  }
+  if (W->X[jb + SMAX_LH + 1] > cur) return false;   // not a local maximum
+  const uint32_t width = jb - b + 2;
+  if (width <= 8 && o + 10 < SMAX_LDSB) return diverse8(lds_bytes8(W->B, o - 1), width);
+  Seen sn = {0, 0, 0, 0};
+  for (uint32_t q = o - 1; q <= jb + SMAX_LH; q++)
+    if (seen_add(sn, W->B[q])) return false;
+  return true;
+}
+
 __global__ void __launch_bounds__(SMAX_THREADS)
 smax_defer_kernel(SmaxScanArgs a) {
-  __shared__ __attribute__((aligned(16))) SmaxWindowFull sWin[SMAX_THREADS / 64];
-  __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
-  // direct-path queue (256 exact starts) or the generic path's start list
-  __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * 256 + 2 * 64 / 4 + 64];
+  __shared__ __attribute__((aligned(16))) SmaxWindowX sWin[SMAX_THREADS / 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t n = *a.defer_count;
-  if (blockIdx.x == 0 && threadIdx.x == 0) compute_head(a);
+  SmaxWindowX *W = &sWin[wave];
   Win t;
   win_init(t, a);
+  if (blockIdx.x == gridDim.x - 1) {
+    // the last workgroup: the boundary head from the shard's first window
+    if (wave == 0) {
+      const uint64_t l0 = a.tile_first * (uint64_t) SMAX_TILE;
+      load_exact_window(a, l0, W);
+      head_from_window(a, W, a.base + l0);
+    }
+    return;
+  }
+  const uint32_t n = *a.defer_count;
+  const uint64_t ltm = lanemask_lt();
   for (uint32_t i = blockIdx.x * (SMAX_THREADS / 64) + wave; i < n;
-       i += gridDim.x * (SMAX_THREADS / 64)) {
+       i += (gridDim.x - 1) * (SMAX_THREADS / 64)) {
     const uint64_t tile = a.defer_list[i];
-    uint2 info = a.llv_win[tile];
-    info.y &= 0x7fffffffu;                                  // drop the wide-value flag
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
     const uint64_t g0 = a.base + l0;
-    SmaxWindowFull *W = &sWin[wave];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // previous tile's LDS reads done
-    issue_window_full(a, l0, W, __builtin_amdgcn_readfirstlane(info.x),
-                      __builtin_amdgcn_readfirstlane(info.y));
-    glds_wait();
+    const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
+    load_exact_window(a, l0, W);
+    uint64_t tmark = 0;   // diagnostic phase stamp (GT_SMAX_DEBUG 32768|65536 / |131072)
+    if ((a.dbg & 65536u)) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
     t.L = W->L;
     t.B = W->B;
     t.P = nullptr;
-    t.val = W->val;
+    t.rank = nullptr;     // 255 values beyond the window: global search
+    t.val = nullptr;
     t.val16 = nullptr;
-    const uint32_t segpre_bits = prepare_window(t, a, sRank[wave], info.x, info.y, SMAX_LDSB);
-    const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
+    t.nval = -1;
+    // ballots: plateau ends (tile rows + right halo) and owned starts
+#pragma unroll 4
+    for (uint32_t s = 0; s < SMAX_XSTEPS; s++) {
+      const uint32_t b = s * 64 + lane, o = b + SMAX_LH;
+      bool ne = true, st = false;
+      if (o + 1 < SMAX_LDSB) {
+        const uint32_t c = W->X[o], nx = W->X[o + 1], pv = W->X[o - 1];
+        const uint64_t g = g0 + b;
+        ne = nx != c;
+        st = b < SMAX_TILE && c > pv && c >= a.minlen && g >= a.begin && g < a.end;
+      }
+      const uint64_t nem = __ballot(ne), stm = __ballot(st);
+      if (lane == 0) {
+        W->ne[s] = nem;
+        if (s < SMAX_TILE / 64) W->st[s] = stm;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if ((a.dbg & 131072u)) tmark = __builtin_readcyclecounter();
     GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
-    uint16_t *qlist = reinterpret_cast<uint16_t *>(sQueue[wave]);
-    uint32_t wcount = UINT32_MAX;
-    if (!edge && wave_pre && !(a.dbg & 128u))
-      wcount = wave_detect_direct<256>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
-    if (wcount == UINT32_MAX)
-      wcount = (edge || wave_pre) ? wave_detect(t, a, g0, W->L, qlist, qlist + SMAX_LIST, wdst,
-                                                !edge, segpre_bits)
-                                  : 0u;
+    uint32_t wcount = 0;
+    for (uint32_t q0 = 0; q0 < SMAX_TILE; q0 += SMAX_XQ) {
+      // compact this round's starts (row order)
+      uint32_t ns = 0;
+      for (uint32_t s = q0 / 64; s < (q0 + SMAX_XQ) / 64; s++) {
+        const uint64_t m = W->st[s];
+        if ((m >> lane) & 1u) W->list[ns + (uint32_t) __popcll(m & ltm)] = (uint16_t) (s * 64 + lane);
+        ns += (uint32_t) __popcll(m);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+        bool acc = false;
+        uint32_t cur = 0, b = 0;
+        uint64_t j = 0;
+        if (i0 + lane < ns) {
+          b = W->list[i0 + lane];
+          acc = eval_start_x(a, t, W, g0, b, &cur, &j);
+        }
+        const uint64_t am = __ballot(acc);
+        if (acc) {
+          GtSmaxRecord rec;
+          rec.lb = g0 + b - 1;
+          rec.lcp = cur;
+          rec.width = (uint32_t) (j - (g0 + b) + 2);
+          if (!(a.dbg & 4096u)) wdst[wcount + (uint32_t) __popcll(am & ltm)] = rec;
+        }
+        wcount += (uint32_t) __popcll(am);
+      }
+      __builtin_amdgcn_wave_barrier();   // list reused
+    }
+    if (a.dbg & 32768u)   // diagnostic: per-tile cycles (/16), no counts
+      wcount = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
     if (lane == 0 && !(a.dbg & 4096u)) a.tile_count[tile] = wcount;
+    __builtin_amdgcn_wave_barrier();   // window reused by the next tile
   }
-  glds_wait();
 }
 
 
@@ -1590,7 +1633,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
               p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
     const uint64_t dg = ((uint64_t) p->num_tiles + 3) / 4;
-    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 16 ? dg : (uint64_t) dev_cus * 16);
+    // + 1: the last workgroup computes the boundary head
+    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 8 ? dg : (uint64_t) dev_cus * 8) + 1;
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
@@ -1704,7 +1748,9 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       // diagnostic: extra dynamic LDS lowers residency (occupancy sensitivity)
       const char *pad = getenv("GT_SMAX_LDS_PAD");
       const unsigned lp = pad ? (unsigned) strtoul(pad, NULL, 0) : 0u;
-      if (p->pk && (p->dbg & 256u))
+      if ((p->dbg & 16384u) && p->runs > 0)
+        ;   // diagnostic: re-run K1b on the first run's deferred tiles
+      else if (p->pk && (p->dbg & 256u))
         hipLaunchKernelGGL(smax_scan_kernel_pk5, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
       else if (p->pk)
         hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
@@ -1829,6 +1875,21 @@ extern "C" uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *p) {
   if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
     return 0xffffffffu;
   return n;
+}
+
+extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_t *deferred,
+                                        uint32_t *ndeferred) {
+  if (hipSetDevice(p->shard.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
+  if (counts && hipMemcpy(counts, p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  uint32_t n = 0;
+  if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (ndeferred) *ndeferred = n;
+  if (deferred && n && hipMemcpy(deferred, p->defer_list, sizeof (uint32_t) * n,
+                                 hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 0;
 }
 
 extern "C" uint32_t gt_smax_plan_error_bits(GtSmaxPlan *p) {

@@ -202,6 +202,13 @@ uint32_t gt_smax_plan_error_bits(GtSmaxPlan *plan);
  * (shard edges and tiles with more exact-evaluation starts than K1 queues). */
 uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *plan);
 
+/* Diagnostic: copies the last run's per-tile record counts (num_tiles
+ * entries; with GT_SMAX_DEBUG bit 32768 the deferred tiles hold K1b cycle
+ * stamps instead) and the deferred-tile list (capacity num_tiles) to host
+ * buffers (either may be NULL).  0 on success, -1 on a HIP error. */
+int gt_smax_plan_debug_tiles(GtSmaxPlan *plan, uint32_t *counts, uint32_t *deferred,
+                             uint32_t *ndeferred);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,3 +74,11 @@ for k in range(1, 16):
     plen += alive
 print("plateau rows of LCP[c+1]==LCP[c] starts: 2: %.3f  3: %.3f  4-7: %.3f  8+: %.3f" %
       ((plen == 2).mean(), (plen == 3).mean(), ((plen >= 4) & (plen <= 7)).mean(), (plen >= 8).mean()))
+# active 16-row segments per 2048-row tile (K1 classification steps of 64)
+nt = rows // 2048
+act = segge[: nt * 128].reshape(nt, 128).sum(1)
+print("active segments per tile: mean %.1f p10 %d p50 %d p90 %d; tiles needing 2 steps: %.3f, 0 steps: %.3f"
+      % (act.mean(), np.percentile(act, 10), np.percentile(act, 50), np.percentile(act, 90),
+         (act > 64).mean(), (act == 0).mean()))
+print("histogram of active segments per tile (bins of 16):",
+      np.bincount(np.minimum(act // 16, 8), minlength=9).tolist())
