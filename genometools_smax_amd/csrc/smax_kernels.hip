@@ -443,6 +443,14 @@ __device__ __forceinline__ uint32_t pack4(uint32_t m) {
   return (((m >> 7) * 0x00204081u) >> 21) & 0xfu;
 }
 
+// four byte-flag words (bits 7,15,23,31; word k = rows 4k..4k+3) -> 16-bit
+// row mask: dot products of the flag bytes with weights 2^q (VALU dot4)
+__device__ __forceinline__ uint32_t pack16(const uint32_t f[4]) {
+  const uint32_t lo = __builtin_amdgcn_udot4(f[1], 0x80402010u, __builtin_amdgcn_udot4(f[0], 0x08040201u, 0u, false), false);
+  const uint32_t hi = __builtin_amdgcn_udot4(f[3], 0x80402010u, __builtin_amdgcn_udot4(f[2], 0x08040201u, 0u, false), false);
+  return (lo >> 7) | (hi << 1);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   return (1ull << (threadIdx.x & 63)) - 1;
 }
@@ -679,17 +687,18 @@ __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
   const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
   const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  uint32_t UP = 0, EQ = 0, GE = 0, FF = 0;
+  uint32_t up[4], eq[4], ge[4], ff[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t cur = k == 0 ? w0 : k == 1 ? w1 : k == 2 ? w2 : w3;
     const uint32_t prv = k == 0 ? ((w0 << 8) | pb)
                        : __builtin_amdgcn_alignbyte(cur, k == 1 ? w0 : k == 2 ? w1 : w2, 3);
-    UP |= pack4(bytes_lt(prv, cur)) << (4 * k);
-    EQ |= pack4(bytes_eq(prv, cur)) << (4 * k);
-    GE |= pack4(bytes_ge(cur, mf)) << (4 * k);
-    FF |= pack4(bytes_ff(cur)) << (4 * k);
+    up[k] = bytes_lt(prv, cur);
+    eq[k] = bytes_eq(prv, cur);
+    ge[k] = bytes_ge(cur, mf);
+    ff[k] = bytes_ff(cur);
   }
+  uint32_t UP = pack16(up), EQ = pack16(eq), GE = pack16(ge), FF = pack16(ff);
   // rows 16, 17 against their predecessors
   const uint32_t b15 = w3 >> 24;
   UP |= (b15 < nb ? 1u << 16 : 0u) | (nb < nb2 ? 1u << 17 : 0u);
