@@ -372,7 +372,7 @@ struct SmaxWindow {            // byte BWT (any alphabet)
 };
 struct SmaxWindowPk {          // packed BWT (DNA): 0.5 B per row
   uint8_t L[SMAX_LDSB];
-  uint64_t P[SMAX_LDSB / 16];
+  uint64_t P[SMAX_LDSB / 16 + 2];   // + 2: the tail DMA moves 2 lanes x 16 B
   uint16_t val16[SMAX_LLV_CAP];
 };
 
@@ -412,6 +412,58 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
     glds16(a.bwt + l0 + SMAX_TILE, wb + SMAX_LH + SMAX_TILE);
   }
 }
+// Packed window of local tile start l0 in ONE asm statement (M0 and EXEC
+// set once per piece, SGPR base + per-lane VGPR offset; the instruction
+// offset moves the global and the LDS address alike): LCP rows
+// [l0-LH, l0+TILE+RH) as 1 KiB + 1 KiB + 32 B (2 lanes), packed BWT groups
+// l0/16 .. l0/16+131 as 1 KiB + 32 B (2 lanes), the window's .llv values as
+// u16 pairs (vlanes lanes x 4 B), and, if ibase != 0, the llv_win entry at
+// ibase (2 lanes x 4 B) into LDS address iaddr.
+__device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
+                                                uint32_t lo, uint32_t n, const void *ibase,
+                                                uint32_t iaddr, uint32_t v16, uint32_t v4) {
+  const uint32_t wl = __builtin_amdgcn_readfirstlane(lds_addr(w->L));
+  const uint32_t wp = __builtin_amdgcn_readfirstlane(lds_addr(w->P));
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val16));
+  const uint8_t *lb = a.lcp + l0 - SMAX_LH;
+  const uint8_t *pb = reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16);
+  const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~1u));
+  const uint32_t nl = n == 0 ? 0u : ((n + 2) / 2 < SMAX_LLV_CAP / 2 ? (n + 2) / 2 : SMAX_LLV_CAP / 2);
+  const uint64_t vmask = nl == 0 ? 0ull : (nl >= 64 ? ~0ull : (1ull << nl) - 1);
+  const uint64_t imask = ibase != nullptr ? 3ull : 0ull;
+  const uint8_t *ib = ibase != nullptr ? reinterpret_cast<const uint8_t *>(ibase) : lb;
+  uint32_t keep;
+  uint64_t ex;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_mov_b64 %1, exec\n\t"
+      "global_load_lds_dwordx4 %2, %8 offset:0\n\t"
+      "global_load_lds_dwordx4 %2, %8 offset:1024\n\t"
+      "s_mov_b32 m0, %5\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
+      "s_mov_b64 exec, 3\n\t"
+      "global_load_lds_dwordx4 %2, %9 offset:1024\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %8 offset:2048\n\t"
+      "s_mov_b64 exec, %11\n\t"
+      "s_mov_b32 m0, %6\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %3, %10 offset:0\n\t"
+      "s_mov_b64 exec, %13\n\t"
+      "s_mov_b32 m0, %7\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %3, %12 offset:0\n\t"
+      "s_mov_b64 exec, %1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep), "=&s"(ex)
+      : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+        "s"(vmask), "s"(ib), "s"(imask)
+      : "memory");
+}
+
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
@@ -680,9 +732,13 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
 // 0..17; successor relations are the same bits shifted.  Byte compares are
 // exact except between two 255 bytes: those pairs (rare) are re-decided
 // from the exact .llv values by rank (crank = 255 bytes before the segment).
-__device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
-                                                 uint32_t mf, bool all_exact, uint32_t *Dm,
-                                                 uint32_t *D3m, uint32_t *Lm, uint32_t *Fm) {
+struct SegRel {
+  uint32_t UP, EQ, GE, FF, F18, pb;
+};
+
+// Part 1: the relations of rows 0..17 of segment `so` to their predecessors
+// (byte compares), the >= min(minlen,128) filter and the 255 bytes.
+__device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t mf, SegRel &r) {
   const uint8_t *L = t.L;
   const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
   const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
@@ -698,37 +754,55 @@ __device__ __forceinline__ void classify_segment(const Win &t, uint32_t so,
     ge[k] = bytes_ge(cur, mf);
     ff[k] = bytes_ff(cur);
   }
-  uint32_t UP = pack16(up), EQ = pack16(eq), GE = pack16(ge), FF = pack16(ff);
+  r.UP = pack16(up);
+  r.EQ = pack16(eq);
+  r.GE = pack16(ge);
+  r.FF = pack16(ff);
   // rows 16, 17 against their predecessors
   const uint32_t b15 = w3 >> 24;
-  UP |= (b15 < nb ? 1u << 16 : 0u) | (nb < nb2 ? 1u << 17 : 0u);
-  EQ |= (b15 == nb ? 1u << 16 : 0u) | (nb == nb2 ? 1u << 17 : 0u);
-  const uint32_t F18 = FF | (nb == 255u ? 1u << 16 : 0u) | (nb2 == 255u ? 1u << 17 : 0u);
-  uint32_t FFP = F18 & ((F18 << 1) | (pb == 255u ? 1u : 0u));    // 255 after 255
+  r.UP |= (b15 < nb ? 1u << 16 : 0u) | (nb < nb2 ? 1u << 17 : 0u);
+  r.EQ |= (b15 == nb ? 1u << 16 : 0u) | (nb == nb2 ? 1u << 17 : 0u);
+  r.F18 = r.FF | (nb == 255u ? 1u << 16 : 0u) | (nb2 == 255u ? 1u << 17 : 0u);
+  r.pb = pb;
+}
+
+// Part 2, given the rank of the segment's first row among the window's 255
+// bytes (crank):
+//   *Dm  records [c-1 .. c] and [c-1 .. c+1] (D3 marks the latter): start,
+//        then LCP[c+1] < LCP[c], or LCP[c+1] == LCP[c] > LCP[c+2]; with the
+//        matching left diversity
+//   *Lm  starts needing exact evaluation: plateaus of >= 3 rows (LCP[c] ==
+//        LCP[c+1] == LCP[c+2])
+// where start = LCP[c] >= minlen (exact for minlen <= 128) and LCP[c] >
+// LCP[c-1].  Only two relations are computed, each row against its
+// predecessor (UP, EQ) for rows 0..17; successor relations are the same bits
+// shifted.  Byte compares are exact except between two 255 bytes: those
+// pairs (rare) are re-decided from the exact .llv values by rank.
+__device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r, uint32_t crank,
+                                             bool all_exact, uint32_t *Dm, uint32_t *D3m,
+                                             uint32_t *Lm) {
+  uint32_t UP = r.UP, EQ = r.EQ;
+  uint32_t FFP = r.F18 & ((r.F18 << 1) | (r.pb == 255u ? 1u : 0u));    // 255 after 255
   bool unresolved = false;
-  if (F18 != 0 && t.rank == nullptr) {
-    unresolved = true;                      // no ranks staged: exact queue instead
-  } else if (FFP != 0) {
-    {
-      const uint32_t crank = t.rank[so >> 4];
-      while (FFP) {
-        const int r = __builtin_ctz(FFP);
-        FFP &= FFP - 1;
-        const uint32_t rk = crank + (uint32_t) __popc(F18 & ((1u << r) - 1));
-        const uint32_t vr = llv_by_rank(t, rk), vp = llv_by_rank(t, rk - 1);
-        UP = (UP & ~(1u << r)) | ((vp < vr ? 1u : 0u) << r);
-        EQ = (EQ & ~(1u << r)) | ((vp == vr ? 1u : 0u) << r);
-      }
+  if (r.F18 != 0 && t.rank == nullptr) {
+    unresolved = true;                      // no ranks (inconsistent index): exact queue
+  } else {
+    while (FFP) {
+      const int q = __builtin_ctz(FFP);
+      FFP &= FFP - 1;
+      const uint32_t rk = crank + (uint32_t) __popc(r.F18 & ((1u << q) - 1));
+      const uint32_t vr = llv_by_rank(t, rk), vp = llv_by_rank(t, rk - 1);
+      UP = (UP & ~(1u << q)) | ((vp < vr ? 1u : 0u) << q);
+      EQ = (EQ & ~(1u << q)) | ((vp == vr ? 1u : 0u) << q);
     }
   }
-  const uint32_t A = GE & (UP | (unresolved ? FF & ((FF << 1) | (pb == 255u ? 1u : 0u)) : 0u))
+  const uint32_t A = r.GE & (UP | (unresolved ? r.FF & ((r.FF << 1) | (r.pb == 255u ? 1u : 0u)) : 0u))
                      & 0xffffu;
   const uint32_t eqn = EQ >> 1, dn = ~((UP | EQ) >> 1);            // vs row c+1
   const uint32_t eqn1 = EQ >> 2, dn1 = ~((UP | EQ) >> 2);          // c+1 vs c+2
   const uint32_t D = A & dn & 0xffffu;
   const uint32_t D3 = A & eqn & dn1 & 0xffffu;
   *Lm = (all_exact || unresolved) ? A : (A & eqn & eqn1);
-  *Fm = FF;
   if (all_exact || unresolved || (D | D3) == 0) {
     *Dm = 0;
     *D3m = 0;
@@ -782,19 +856,34 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   __builtin_amdgcn_wave_barrier();
   // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones
   uint32_t Dm0 = 0, Lm0 = 0, Dm1 = 0, Lm1 = 0, Lpre0 = 0, Lpre1 = 0, ro0 = 0, ro1 = 0;
-  uint32_t W30 = 0, W31 = 0, F0 = 0, F1 = 0;
+  uint32_t W30 = 0, W31 = 0, F0 = 0, F1 = 0, R0 = 0, R1 = 0;
   uint32_t nL = 0;
   const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
+  // 255-byte ranks: the left halo's count, then a prefix over the compacted
+  // segments in row order (an inactive segment holds no byte >= 128)
+  uint32_t fbase = 0;
+  uint16_t *rank = const_cast<uint16_t *>(t.rank);
+  if (rank != nullptr) fbase = __builtin_amdgcn_readfirstlane(seg_ffcount(*reinterpret_cast<const uint4 *>(t.L)));
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
     const uint32_t i = k * 64 + lane;
-    uint32_t D = 0, D3 = 0, Lq = 0, F = 0, ro = 0;
+    uint32_t D = 0, D3 = 0, Lq = 0, ro = 0;
+    SegRel rel = {0, 0, 0, 0, 0, 0};
     if (i < nseg) {
       const uint32_t sid = segl[i];
       ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
-      const uint32_t so = SMAX_LH + ro;
-      classify_segment(t, so, mf, all_exact, &D, &D3, &Lq, &F);
+      classify_rel(t, SMAX_LH + ro, mf, rel);
+    }
+    uint32_t crank = 0;
+    if (rank != nullptr) {
+      uint32_t ftot;
+      crank = fbase + wave_excl((uint32_t) __popc(rel.FF), &ftot);
+      if (i < nseg) rank[(SMAX_LH + ro) >> 4] = (uint16_t) crank;
+      fbase += ftot;
+    }
+    if (i < nseg) {
+      classify_fin(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq);
       const uint64_t sg = g0 + ro;
       if (sg < a.begin) {
         const uint32_t m = sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
@@ -803,10 +892,10 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         Lq &= m;
       }
     }
+    const uint32_t F = rel.FF;
     uint32_t tot;
     const uint32_t excl = wave_excl((uint32_t) __popc(Lq), &tot);
     if (nL + tot <= DL && Lq != 0) {
-      const uint32_t crank = (F != 0 && t.rank != nullptr) ? t.rank[(SMAX_LH + ro) >> 4] : 0u;
       uint32_t pos = nL + excl, bits = Lq;
       while (bits) {
         const int q = __builtin_ctz(bits);
@@ -815,9 +904,13 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
       }
     }
-    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
-    else { Dm1 = D; W31 = D3; F1 = F; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
+    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; R0 = crank; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
+    else { Dm1 = D; W31 = D3; F1 = F; R1 = crank; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
     nL += tot;
+  }
+  if (rank != nullptr && lane == 0) {   // halo chunks (ranks of rows the slow paths may read)
+    rank[0] = 0;
+    rank[1 + SMAX_TILE / 16] = (uint16_t) fbase;
   }
   if (nL > DL) return UINT32_MAX;
   if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
@@ -849,7 +942,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
     const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1, W3 = k == 0 ? W30 : W31;
-    const uint32_t Fk = k == 0 ? F0 : F1;
+    const uint32_t Fk = k == 0 ? F0 : F1, Rk = k == 0 ? R0 : R1;
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
     const uint32_t si = k * 64 + lane;
     uint32_t acc = D;
@@ -865,8 +958,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       if ((D >> q) & 1u) {
         const uint32_t b = sL[SMAX_LH + ro + q];
         rec.lcp = b < 255 ? b
-                          : llv_by_rank(t, t.rank[(SMAX_LH + ro) >> 4] +
-                                               (uint32_t) __popc(Fk & ((1u << q) - 1)));
+                          : llv_by_rank(t, Rk + (uint32_t) __popc(Fk & ((1u << q) - 1)));
         rec.width = 2 + ((W3 >> q) & 1u);
       } else {
         const uint32_t i = Lpre + (uint32_t) __popc(Lq & ((1u << q) - 1));
@@ -881,49 +973,42 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   return wcount;
 }
 
+// next tile's window + the llv_win entry of the tile after it (ring slot iaddr)
+__device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
+                                           uint32_t lo, uint32_t n, const uint2 *info, uint32_t iaddr,
+                                           uint32_t v16, uint32_t v4) {
+  issue_window_pk(a, l0, w, lo, n, info, iaddr, v16, v4);
+}
+__device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
+                                           uint32_t lo, uint32_t n, const uint2 *info, uint32_t iaddr,
+                                           uint32_t v16, uint32_t v4) {
+  issue_window(a, l0, w, lo, n);
+  if ((threadIdx.x & 63) < 2) glds4(reinterpret_cast<const uint32_t *>(info) + (threadIdx.x & 63), iaddr);
+}
+
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = W->B; t.P = nullptr; }
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = W->P; t.B = nullptr; }
 
-// WinT: SmaxWindowPk (packed DNA BWT) or SmaxWindow (byte BWT, any alphabet)
-// Filter and .llv ranks of a landed window (one wave): per-lane segment
-// "any byte >= min(minlen,128)" bits, and the window's 255-byte ranks in
-// `rank` (values already in LDS) when it holds any 255 byte.
+// Filter of a landed window (one wave): per-lane segment "any byte >=
+// min(minlen,128)" bits; the .llv values are staged with the window, their
+// ranks are computed during the classification (wave_detect_direct).
 __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
-                                                   uint32_t wlo, uint32_t wn,
-                                                   uint32_t cap = SMAX_LLV_CAP) {
+                                                   uint32_t wlo, uint32_t wn) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint32_t so = SMAX_LH + lane * 16;
   const uint4 v0 = *reinterpret_cast<const uint4 *>(&t.L[so]);
   const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
-  const uint4 hv = *reinterpret_cast<const uint4 *>(&t.L[lane == 0 ? 0 : SMAX_LH + SMAX_TILE]);
   const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
   t.llv_base = wlo;
-  t.rank = nullptr;
-  t.nval = -1;
   // no .llv entry in the window: no 255 byte (in a consistent index; a
   // stray 255 still resolves exactly through the global .llv search)
-  if (wn == 0) return segpre_bits;
-  const uint32_t f0 = seg_ffcount(v0), f1 = seg_ffcount(v1);
-  const uint32_t hl = __builtin_amdgcn_readfirstlane(seg_ffcount(hv));   // lane 0: left halo
-  {
-    // chunk 0 = left halo, 1..64 segment 0, 65..128 segment 1, 129 right halo
-    uint32_t t0, t1;
-    const uint32_t e0 = wave_excl(f0, &t0), e1 = wave_excl(f1, &t1);
-    rank[1 + lane] = (uint16_t) (hl + e0);
-    rank[65 + lane] = (uint16_t) (hl + t0 + e1);
-    if (lane == 0) {
-      rank[0] = 0;
-      rank[1 + SMAX_TILE / 16] = (uint16_t) (hl + t0 + t1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+  t.rank = wn == 0 ? nullptr : rank;
+  t.nval = -1;
+  if (wn != 0) {
+    const uint32_t cap = SMAX_LLV_CAP - (wlo & 1u);   // staged from the even index below wlo
+    t.val16 += wlo & 1u;
     t.nval = (int) (wn < cap ? wn : cap);
-    if (t.val16 != nullptr) {            // staged from the even index below wlo
-      t.val16 += wlo & 1u;
-      if ((uint32_t) t.nval > cap - (wlo & 1u)) t.nval = (int) (cap - (wlo & 1u));
-    }
-    t.rank = (a.dbg & 16u) ? nullptr : rank;
   }
   return segpre_bits;
 }
@@ -969,6 +1054,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
                __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
                __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]));
 
+  const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
   for (uint32_t it = 0;; it++) {
     const uint32_t cur = it & 1u;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
@@ -994,13 +1080,25 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
     if (next < a.num_tiles) {
-      issue_window(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u], nlo, nn);
       const uint64_t n2 = next + stride <= last ? next + stride : last;
-      if (lane < 2)
-        glds4(reinterpret_cast<const uint32_t *>(a.llv_win + n2) + lane, cur ? info1 : info0);
+      issue_next(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u], nlo, nn,
+                 a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
 
-    const uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
+    uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
+    if (a.dbg & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
+      if (a.dbg & (1u << 17)) {
+        uint32_t x = segpre_bits;
+#pragma unroll
+        for (int q = 0; q < 64; q++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x));
+        segpre_bits = x - 64;
+      } else {
+        uint32_t y = a.minlen;
+#pragma unroll
+        for (int q = 0; q < 64; q++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(y));
+        if (y == 12345) segpre_bits = 0;
+      }
+    }
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
 
     // ---- detection, diversity, records (row order)
@@ -1611,7 +1709,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                                  shard->device));
     // packed BWT when the shard's alphabet is DNA ({0..3} plus specials)
     {
-      const uint64_t ngroups = shard->local_len / 16 + 131;
+      const uint64_t ngroups = shard->local_len / 16 + 134;
       uint32_t *flag = NULL, hflag = 0;
       HIPCHK(hipMalloc(&p->bwtpk, sizeof (uint64_t) * ngroups));
       HIPCHK(hipMalloc(&flag, sizeof (uint32_t)));
