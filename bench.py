@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--bases", type=int, default=None, help="override genome size")
     ap.add_argument("--minlen", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="skip the host-tables (PCIe-inclusive) leg")
     ap.add_argument("--cpu-sample", type=int, default=3_200_000_000,
                     help="max suffix rows timed on the CPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -213,6 +215,25 @@ def main():
                "sample": "oracle orc_linsmax (single core, -O3) over suffix rows [0,%d) of the same "
                          "tables: %.2fs" % (sample, t_cpu)}
 
+    # end-to-end through the drop-in boundary (host tables in memory -> H2D
+    # -> plan -> K0..K3 -> D2H of the (lcp, lb, rb) list): reported beside
+    # `value`, never as it
+    e2e = None
+    if host is not None and not args.no_end_to_end:
+        plan.close()
+        plan = None
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        iv = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], n, N, minlen, 1)
+        t_e2e = time.perf_counter() - t0
+        if len(iv) != count:
+            log("WARNING: end-to-end %d intervals != %d" % (len(iv), count))
+        e2e = {"value": N / t_e2e, "unit": "suffix-positions/s", "seconds": round(t_e2e, 4),
+               "path": "gt_smax_hip_enumerate_to_buffer: pageable host .lcp/.bwt/.llv -> H2D -> "
+                       "plan (pack, llv index) -> K0..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
+               "vs_cpu_baseline": (N / t_e2e) / cpu["value"] if cpu else None}
+        del iv
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -239,10 +260,12 @@ def main():
                          "kernel": "smax_scan_kernel", "kernel_avg_ms": k1_avg_ms,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
             "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2)},
         }
         print(json.dumps(out), flush=True)
-    plan.close()
+    if plan is not None:
+        plan.close()
     esa.release()
     if dist:
         dist.barrier()

@@ -79,6 +79,7 @@ struct SmaxScanArgs {
   GtSmaxBoundary *bnd;
   uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
   uint32_t *defer_count;     // reset by K0
+  uint32_t k1b_head;         // K1b: the last workgroup computes the boundary head
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
 
@@ -327,6 +328,24 @@ __device__ static void compute_head(const SmaxScanArgs &a) {
   b->head_div.seen[0] = s.w0; b->head_div.seen[1] = s.w1;
   b->head_div.seen[2] = s.w2; b->head_div.seen[3] = s.w3;
   b->head_div.dup = dup;
+}
+
+// The plan-time half of K1's deferral rule, shared by K1 and the static list
+// kernel: shard-edge tiles (row 0, begin, end, N: halos outside the shard)
+// and windows whose .llv entries K1 cannot stage (more than SMAX_LLV_CAP, or
+// a value >= 2^16: bit 31 of the llv_win count).
+__host__ __device__ __forceinline__ bool static_deferred(const SmaxScanArgs &a, uint64_t g0,
+                                                         uint32_t wnf) {
+  return g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u) ||
+         wnf > SMAX_LLV_CAP;
+}
+
+__global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, uint32_t *list,
+                                                                 uint32_t *count) {
+  const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (t >= a.num_tiles) return;
+  const uint64_t g0 = a.base + (a.tile_first + t) * (uint64_t) SMAX_TILE;
+  if (static_deferred(a, g0, a.llv_win[t].y)) list[atomicAdd(count, 1u)] = (uint32_t) t;
 }
 
 // K0: per-run resets ahead of K1 (the pending-plateau slot, which any K1 or
@@ -1104,15 +1123,17 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     // ---- detection, diversity, records (row order)
     GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
     uint32_t wcount = 0;
-    const bool edge = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u);
-    // windows with more .llv values than K1 stages go to K1b (which stages
-    // all of them): K1 then never waits on a global .llv read
-    bool defer = edge || (wave_pre && ((a.dbg & 128u) || wnf > SMAX_LLV_CAP));
-    if (!defer && wave_pre) {
+    // shard-edge tiles and windows with more .llv values than K1 stages
+    // belong to the static K1b list (plan time, smax_static_defer_kernel;
+    // run concurrently on the plan's side stream): K1 leaves them alone and
+    // never waits on a global .llv read
+    const bool stat = static_deferred(a, g0, wnf);
+    bool defer = !stat && wave_pre && (a.dbg & 128u);
+    if (!stat && !defer && wave_pre) {
       wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
-      defer = wcount == UINT32_MAX;
+      defer = wcount == UINT32_MAX;   // exact-queue overflow: runtime K1b list
     }
-    if (lane == 0) {
+    if (lane == 0 && !stat) {
       if (defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
       else if (!(a.dbg & 4096u)) a.tile_count[tile] = wcount;
     }
@@ -1323,7 +1344,7 @@ smax_defer_kernel(SmaxScanArgs a) {
   SmaxWindowX *W = &sWin[wave];
   Win t;
   win_init(t, a);
-  if (blockIdx.x == gridDim.x - 1) {
+  if (a.k1b_head && blockIdx.x == gridDim.x - 1) {
     // the last workgroup: the boundary head from the shard's first window
     if (wave == 0) {
       const uint64_t l0 = a.tile_first * (uint64_t) SMAX_TILE;
@@ -1335,7 +1356,7 @@ smax_defer_kernel(SmaxScanArgs a) {
   const uint32_t n = *a.defer_count;
   const uint64_t ltm = lanemask_lt();
   for (uint32_t i = blockIdx.x * (SMAX_THREADS / 64) + wave; i < n;
-       i += (gridDim.x - 1) * (SMAX_THREADS / 64)) {
+       i += (gridDim.x - a.k1b_head) * (SMAX_THREADS / 64)) {
     const uint64_t tile = a.defer_list[i];
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
     const uint64_t g0 = a.base + l0;
@@ -1620,6 +1641,11 @@ struct GtSmaxPlan {
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
   uint32_t *defer_count;
+  uint32_t *static_list;     // plan-time K1b list (edges, wide .llv windows) + count
+  uint32_t *static_count;
+  uint32_t n_static, static_grid;
+  hipStream_t side;          // K1b over the static list runs here, concurrent with K1
+  hipEvent_t fork, join;
   uint32_t *err;
   void *scan_tmp;
   size_t scan_tmp_bytes;
@@ -1629,6 +1655,8 @@ struct GtSmaxPlan {
   int nslots;
   uint64_t runs;
 };
+
+static SmaxScanArgs plan_args(GtSmaxPlan *p);
 
 extern "C" int gt_smax_device_count(void) {
   int n = 0;
@@ -1739,9 +1767,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       fprintf(stderr, "gt_smax: K1 %s BWT, %d CUs x %d blocks/CU -> grid %u, %u tiles\n",
               p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
+    // runtime K1b list (exact-queue overflow: ~1 tile in 10^4): grid-stride
     const uint64_t dg = ((uint64_t) p->num_tiles + 3) / 4;
-    // + 1: the last workgroup computes the boundary head
-    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 8 ? dg : (uint64_t) dev_cus * 8) + 1;
+    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 2 ? dg : (uint64_t) dev_cus * 2);
+    p->static_grid = (uint32_t) dev_cus * 8;   // capped below by the list length
   }
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
@@ -1787,6 +1816,25 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   if (herr & 1u) { seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
   if (herr & 2u) { seterr(errbuf, errlen, ".llv positions not strictly increasing"); goto fail; }
   (void) hipFree(derr);
+  derr = NULL;
+  // static K1b list (needs llv_win)
+  HIPCHK(hipMalloc(&p->static_list, sizeof (uint32_t) * ((uint64_t) p->num_tiles + 1)));
+  HIPCHK(hipMalloc(&p->static_count, sizeof (uint32_t)));
+  HIPCHK(hipMemset(p->static_count, 0, sizeof (uint32_t)));
+  {
+    SmaxScanArgs a = plan_args(p);
+    if (p->num_tiles > 0)
+      hipLaunchKernelGGL(smax_static_defer_kernel, dim3((p->num_tiles + 255) / 256), dim3(256), 0, 0,
+                       a, p->static_list, p->static_count);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(&p->n_static, p->static_count, sizeof (uint32_t), hipMemcpyDeviceToHost));
+    const uint32_t need = (p->n_static + 3) / 4;
+    // + 1: the last workgroup computes the boundary head
+    p->static_grid = (need < p->static_grid ? need : p->static_grid) + 1;
+  }
+  HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&p->join, hipEventDisableTiming));
   *planp = p;
   return 0;
 fail:
@@ -1800,7 +1848,13 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
                   p->llv_win, p->err, p->scan_tmp, p->bwtpk, p->llv16, p->defer_list,
-                  p->defer_count};
+                  p->defer_count, p->static_list, p->static_count};
+  if (p->side) {
+    (void) hipStreamSynchronize(p->side);
+    (void) hipStreamDestroy(p->side);
+  }
+  if (p->fork) (void) hipEventDestroy(p->fork);
+  if (p->join) (void) hipEventDestroy(p->join);
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -1831,6 +1885,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.bnd = p->bnd;
   a.defer_list = p->defer_list;
   a.defer_count = p->defer_count;
+  a.k1b_head = 0;
   a.dbg = p->dbg;
   return a;
 }
@@ -1849,6 +1904,9 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
       return 0;
     }
+    // fork point: after K0's resets (K1b over the static list then runs on
+    // the side stream, concurrent with K1; disjoint tiles)
+    HIPCHK(hipEventRecord(p->fork, s));
     const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
     {
@@ -1866,7 +1924,19 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
-    // K1b: deferred tiles (a few per shard; grid-stride over the device count)
+    HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
+    {
+      SmaxScanArgs b = a;
+      b.defer_list = p->static_list;
+      b.defer_count = p->static_count;
+      b.k1b_head = 1;
+      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, p->side, b);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(p->join, p->side));
+    // join (the static K1b finishes well inside K1), then K1b over K1's
+    // runtime list (exact-queue overflow)
+    HIPCHK(hipStreamWaitEvent(s, p->join, 0));
     hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
     HIPCHK(hipGetLastError());
     size_t bytes = p->scan_tmp_bytes;
