@@ -84,6 +84,19 @@ class GtSmaxBoundary(ctypes.Structure):
     ]
 
 
+class GtMaxpairsDevInput(ctypes.Structure):
+    _fields_ = [
+        ("lcp_dev", ctypes.c_void_p),
+        ("bwt_dev", ctypes.c_void_p),
+        ("llv_dev", ctypes.c_void_p),
+        ("numllv", ctypes.c_uint64),
+        ("suf_dev", ctypes.c_void_p),
+        ("suf_bytes", ctypes.c_int),
+        ("nonspecials", ctypes.c_uint64),
+        ("device", ctypes.c_int),
+    ]
+
+
 class GtSmaxRecord(ctypes.Structure):
     _fields_ = [("lb", ctypes.c_uint64), ("lcp", ctypes.c_uint32), ("width", ctypes.c_uint32)]
 
@@ -135,17 +148,31 @@ def lib():
         L.gt_smax_plan_deferred_tiles.argtypes = [vp]
         L.gt_smax_plan_deferred_tiles.restype = ctypes.c_uint32
         L.gt_smax_plan_debug_tiles.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_uint32)]
+        L.gt_maxpairs_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput), u32,
+                                                          ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
+        L.gt_maxpairs_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtMaxpairsDevInput),
+                                              u32, cs, sz]
+        L.gt_maxpairs_plan_delete.argtypes = [vp]
+        L.gt_maxpairs_plan_count.argtypes = [vp, vp]
+        L.gt_maxpairs_plan_total.argtypes = [vp, ctypes.POINTER(u64)]
+        L.gt_maxpairs_plan_emit.argtypes = [vp, vp, u64, vp]
+        L.gt_seqpos_map_dev.argtypes = [vp, u64, vp, u64, vp, ci, vp]
         _lib = L
     return _lib
 
 
 def exported_symbols():
-    """Every function include/gt_smax_hip.h declares (checked by tests)."""
+    """Every function the include/*.h headers declare (checked by tests)."""
+    import glob
     import re
-    hdr = os.path.join(os.path.dirname(_HERE), "include", "gt_smax_hip.h")
-    with open(hdr) as fh:
-        text = fh.read()
-    return sorted(set(re.findall(r"\b(gt_smax_\w+)\s*\(", text)))
+    names = set()
+    for hdr in sorted(glob.glob(os.path.join(os.path.dirname(_HERE), "include", "*.h"))):
+        with open(hdr) as fh:
+            text = fh.read()
+        text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)    # comments cite reference names
+        text = re.sub(r"//[^\n]*", " ", text)
+        names.update(re.findall(r"\b(gt_\w+)\s*\(", text))
+    return sorted(names)
 
 
 def _errbuf():
@@ -284,6 +311,88 @@ def enumerate_smax(lcptab, llvtab, bwttab, totallength, nonspecials, minlen, num
     arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).copy()
     lib().gt_smax_free(out)
     return arr
+
+
+def enumerate_maxpairs(lcptab, llvtab, bwttab, suftab, totallength, nonspecials, minlen):
+    """All maximal pairs of length >= minlen as an (k,3) uint64 array of
+    (len, pos1, pos2), pos1 < pos2 (gt_maxpairs_hip_enumerate_to_buffer; the
+    pair set of `gt repfind -l minlen`, in row order rather than the
+    reference's traversal order)."""
+    lcptab = np.ascontiguousarray(lcptab, dtype=np.uint8)
+    bwttab = np.ascontiguousarray(bwttab, dtype=np.uint8)
+    llvtab = np.ascontiguousarray(llvtab, dtype=np.uint64).reshape(-1, 2)
+    suftab = np.ascontiguousarray(suftab)
+    if suftab.dtype not in (np.uint32, np.uint64):
+        suftab = suftab.astype(np.uint64)
+    inp = GtSmaxInput()
+    inp.lcptab = lcptab.ctypes.data
+    inp.llvtab = llvtab.ctypes.data if len(llvtab) else None
+    inp.numllv = len(llvtab)
+    inp.bwttab = bwttab.ctypes.data
+    inp.suftab = suftab.ctypes.data
+    inp.suftab_bytes = suftab.dtype.itemsize
+    inp.totallength = int(totallength)
+    inp.nonspecials = int(nonspecials)
+    out = ctypes.c_void_p()
+    cnt = ctypes.c_uint64()
+    eb = _errbuf()
+    rc = lib().gt_maxpairs_hip_enumerate_to_buffer(ctypes.byref(inp), int(minlen), ctypes.byref(out),
+                                                   ctypes.byref(cnt), eb, len(eb))
+    _check(rc, eb)
+    n = cnt.value
+    if n == 0:
+        return np.zeros((0, 3), dtype=np.uint64)
+    buf = (ctypes.c_uint64 * (3 * n)).from_address(out.value)
+    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).copy()
+    lib().gt_smax_free(out)
+    return arr
+
+
+class MaxpairsPlan:
+    """Device-resident maximal pairs over HBM tables (gt_maxpairs_plan_*)."""
+
+    def __init__(self, lcp_ptr, bwt_ptr, llv_ptr, numllv, suf_ptr, suf_bytes, nonspecials, minlen,
+                 device=0):
+        inp = GtMaxpairsDevInput()
+        inp.lcp_dev, inp.bwt_dev, inp.llv_dev = lcp_ptr, bwt_ptr, llv_ptr
+        inp.numllv, inp.suf_dev, inp.suf_bytes = numllv, suf_ptr, suf_bytes
+        inp.nonspecials, inp.device = nonspecials, device
+        self._p = ctypes.c_void_p()
+        eb = _errbuf()
+        _check(lib().gt_maxpairs_plan_create(ctypes.byref(self._p), ctypes.byref(inp), int(minlen),
+                                             eb, len(eb)), eb)
+        self.device = device
+
+    def count(self, stream=0):
+        if lib().gt_maxpairs_plan_count(self._p, stream) != 0:
+            raise SmaxError("gt_maxpairs_plan_count failed")
+
+    def total(self):
+        t = ctypes.c_uint64()
+        if lib().gt_maxpairs_plan_total(self._p, ctypes.byref(t)) != 0:
+            raise SmaxError("gt_maxpairs_plan_total failed")
+        return t.value
+
+    def emit(self, out_ptr, capacity, stream=0):
+        if lib().gt_maxpairs_plan_emit(self._p, out_ptr, int(capacity), stream) != 0:
+            raise SmaxError("gt_maxpairs_plan_emit failed")
+
+    def close(self):
+        if self._p:
+            lib().gt_maxpairs_plan_delete(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def seqpos_map_dev(sep_ptr, nsep, pairs_ptr, count, out_ptr, device=0, stream=0):
+    """(len, pos1, pos2) -> (len, seqnum1, relpos1, seqnum2, relpos2) on the GPU."""
+    if lib().gt_seqpos_map_dev(sep_ptr, int(nsep), pairs_ptr, int(count), out_ptr, device, stream) != 0:
+        raise SmaxError("gt_seqpos_map_dev failed")
 
 
 def enumerate_index(index, minlen, num_gpus=1):
@@ -524,6 +633,13 @@ class DeviceEsa:
         end = N if end is None else end
         return SmaxPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
                         0, self.totallength + 1, begin, end, N, minlen, self.device, capacity)
+
+    def maxpairs_plan(self, minlen):
+        """Maximal pairs over the device tables (needs keep_suftab=True)."""
+        if not self.esa.suftab_dev:
+            raise SmaxError("maxpairs needs the suffix array: build with keep_suftab=True")
+        return MaxpairsPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
+                            self.esa.suftab_dev, 4, self.nonspecials, minlen, self.device)
 
     def release(self):
         if self.esa.lcptab_dev:

@@ -12,9 +12,16 @@
  *   -gpus N    number of GPUs / suffix-array shards (default 1)
  *   -intervals print "lcp lb rb" interval rows instead of pair lines
  * -smax excludes -r, -q, -spm, -samples, -extend as gt_option_exclude would.
- * Output: one line per occurrence pair of every supermaximal repeat, in the
- * format of gt_simpleexactselfmatchoutput (src/tools/gt_repfind.c:49-84,
- * src/match/querymatch.c:130-190): "len seqnum1 relpos1 F len seqnum2 relpos2".
+ * Without -smax the tool computes maximal pairs (the reference's default -f
+ * branch, gt_callenummaxpairs, src/tools/gt_repfind.c:553-562) on the GPU
+ * (gt_maxpairs_hip_enumerate); -r, -q, -spm, -samples
+ * and -extend are not part of this build.
+ * Output: one line per occurrence pair of every supermaximal repeat (or per
+ * maximal pair), in the format of gt_simpleexactselfmatchoutput
+ * (src/tools/gt_repfind.c:49-84, src/match/querymatch.c:130-190):
+ * "len seqnum1 relpos1 F len seqnum2 relpos2".  Maximal pairs come in
+ * suffix-array row order, not the reference's traversal order (same lines
+ * after sorting).
  * Errors: "gt repfind: error: <msg>" on stderr, exit status 1 (gt_tool_run).
  */
 #include <stdint.h>
@@ -24,6 +31,7 @@
 #include <time.h>
 
 #include "esa_reader.h"
+#include "gt_maxpairs_hip.h"
 #include "gt_smax_hip.h"
 
 typedef struct {
@@ -46,6 +54,31 @@ static uint64_t seqnum_of(const OutState *st, uint64_t p)
   return lo;
 }
 
+/* one pair line (gt_simpleexactselfmatchoutput: pos1 < pos2 after ordering,
+ * filtered when both are in one sequence and relpos1 > relpos2) */
+static void emit_pair(OutState *st, uint64_t len, uint64_t p1, uint64_t p2)
+{
+  uint64_t s1, s2, st1, st2;
+  if (p1 > p2) { uint64_t t = p1; p1 = p2; p2 = t; }
+  s1 = seqnum_of(st, p1);
+  s2 = seqnum_of(st, p2);
+  st1 = s1 == 0 ? 0 : st->sep[s1 - 1] + 1;
+  st2 = s2 == 0 ? 0 : st->sep[s2 - 1] + 1;
+  if (s1 == s2 && p1 - st1 > p2 - st2) return;
+  printf("%llu %llu %llu F %llu %llu %llu\n", (unsigned long long) len,
+         (unsigned long long) s1, (unsigned long long) (p1 - st1),
+         (unsigned long long) len, (unsigned long long) s2,
+         (unsigned long long) (p2 - st2));
+  st->npairs++;
+}
+
+/* GtMaxpairsFunc (GtProcessmaxpairs analogue) */
+static int emit_maxpair(void *data, uint64_t len, uint64_t pos1, uint64_t pos2)
+{
+  emit_pair((OutState *) data, len, pos1, pos2);
+  return 0;
+}
+
 /* GtSmaxIntervalFunc: emits the pair lines of one interval */
 static int emit_interval(void *data, uint64_t lcp, uint64_t lb, uint64_t rb)
 {
@@ -64,29 +97,16 @@ static int emit_interval(void *data, uint64_t lcp, uint64_t lb, uint64_t rb)
     st->occcap = w;
   }
   for (a = 0; a < w; a++) st->occ[a] = smax_esa_suffix(st->esa, lb + a);
-  for (a = 0; a < w; a++) {
-    for (b = a + 1; b < w; b++) {
-      uint64_t p1 = st->occ[a], p2 = st->occ[b], s1, s2, st1, st2;
-      if (p1 > p2) { uint64_t t = p1; p1 = p2; p2 = t; }
-      s1 = seqnum_of(st, p1);
-      s2 = seqnum_of(st, p2);
-      st1 = s1 == 0 ? 0 : st->sep[s1 - 1] + 1;
-      st2 = s2 == 0 ? 0 : st->sep[s2 - 1] + 1;
-      if (s1 == s2 && p1 - st1 > p2 - st2) continue;
-      printf("%llu %llu %llu F %llu %llu %llu\n", (unsigned long long) lcp,
-             (unsigned long long) s1, (unsigned long long) (p1 - st1),
-             (unsigned long long) lcp, (unsigned long long) s2,
-             (unsigned long long) (p2 - st2));
-      st->npairs++;
-    }
-  }
+  for (a = 0; a < w; a++)
+    for (b = a + 1; b < w; b++) emit_pair(st, lcp, st->occ[a], st->occ[b]);
   return 0;
 }
 
 static void usage(FILE *fp)
 {
-  fprintf(fp, "Usage: gt repfind -smax [options] -ii indexname\n"
-              "Compute supermaximal repeats.\n\n"
+  fprintf(fp, "Usage: gt repfind [options] -ii indexname\n"
+              "Compute maximal pairs (default) or supermaximal repeats (-smax).\n\n"
+              "-f         compute maximal forward repeats (default)\n"
               "-smax      compute supermaximal repeats (MI355X)\n"
               "-l         Specify minimum length of repeats\n"
               "           default: 20\n"
@@ -162,16 +182,21 @@ int main(int argc, char **argv)
       return fail(msg);
     }
   }
-  if (!smax) return fail("this build implements the -smax tool path only; use -smax");
   if (excluded != NULL) {
-    snprintf(msg, sizeof msg, "option \"-smax\" and option \"%s\" exclude each other", excluded);
+    if (smax)
+      snprintf(msg, sizeof msg, "option \"-smax\" and option \"%s\" exclude each other", excluded);
+    else
+      snprintf(msg, sizeof msg, "option \"%s\" is not part of this build (maximal pairs -f "
+               "and supermaximal repeats -smax only)", excluded);
     return fail(msg);
   }
+  if (!smax && intervals) return fail("option \"-intervals\" requires option \"-smax\"");
+  if (!smax && gpus > 1) return fail("option \"-gpus\" > 1 requires option \"-smax\"");
   if (indexname == NULL) return fail("option \"-ii\" is mandatory");
 
   setvbuf(stdout, outbuf, _IOFBF, sizeof outbuf);
   t0 = now_s();
-  if (smax_esa_open(&esa, indexname, !intervals, scan, errbuf, sizeof errbuf) != 0)
+  if (smax_esa_open(&esa, indexname, !intervals || !smax, scan, errbuf, sizeof errbuf) != 0)
     return fail(errbuf);
   smax_esa_input(&esa, &in);
   memset(&st, 0, sizeof st);
@@ -186,8 +211,10 @@ int main(int argc, char **argv)
            (unsigned long long) esa.totallength, (unsigned long long) esa.nonspecials,
            (unsigned long long) esa.numllv, gpus);
   }
-  if (gt_smax_hip_enumerate(&in, (unsigned int) minlen, gpus, emit_interval, &st,
-                            errbuf, sizeof errbuf) != 0) {
+  if ((smax ? gt_smax_hip_enumerate(&in, (unsigned int) minlen, gpus, emit_interval, &st,
+                                    errbuf, sizeof errbuf)
+            : gt_maxpairs_hip_enumerate(&in, (unsigned int) minlen, emit_maxpair, &st,
+                                        errbuf, sizeof errbuf)) != 0) {
     fflush(stdout);
     free((void *) st.sep);
     free(st.occ);
@@ -195,9 +222,11 @@ int main(int argc, char **argv)
     return fail(errbuf);
   }
   t1 = now_s();
-  if (verbose)
+  if (verbose && smax)
     printf("# smax intervals=%llu pairs=%llu time=%.3fs\n",
            (unsigned long long) st.nintervals, (unsigned long long) st.npairs, t1 - t0);
+  else if (verbose)
+    printf("# maximal pairs=%llu time=%.3fs\n", (unsigned long long) st.npairs, t1 - t0);
   fflush(stdout);
   free((void *) st.sep);
   free(st.occ);

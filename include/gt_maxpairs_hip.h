@@ -1,0 +1,106 @@
+/*
+ * gt_maxpairs_hip.h -- C-ABI of the MI355X maximal-pairs layer
+ * (`gt repfind -l N` without -smax) and of the
+ * on-device position formatting (§8(f) F4).
+ *
+ * Same conventions as gt_smax_hip.h: plain C types, 0 = success, -1 = error
+ * with the message in errbuf, input pointers borrowed for the call only, a
+ * non-zero callback return stops the enumeration and yields -1.
+ *
+ *  gt_maxpairs_hip_enumerate      replaces gt_enumeratemaxpairs /
+ *                                 gt_callenummaxpairs
+ *                                   src/match/esa-maxpairs.h:45-63,
+ *                                   src/match/esa-maxpairs.c:476-520
+ *                                 i.e. the bottom-up traversal
+ *                                   src/match/esa-bottomup-maxpairs.inc:136-264
+ *                                 with the leaf/branching-edge cartesian
+ *                                 products of src/match/esa-maxpairs.c:181-360.
+ *                                 The callback has the argument meaning of
+ *                                 GtProcessmaxpairs (src/match/esa-maxpairs.h:38-43):
+ *                                 (len, pos1, pos2), here with pos1 < pos2.
+ *                                 Pair SET identical to the reference; the
+ *                                 emission ORDER is by the later suffix-array
+ *                                 row, then descending earlier row (the
+ *                                 reference's is its traversal order), so
+ *                                 outputs compare equal after sorting.
+ *  gt_maxpairs_hip_enumerate_to_buffer  same, malloc'd (len,pos1,pos2) triples.
+ *
+ * A maximal pair of length L >= minlen is a pair of suffix-array rows
+ * i < j with L = min LCP[i+1..j] (the depth of their lowest common
+ * lcp-interval, so the two suffixes branch right after L symbols) whose
+ * left contexts differ: not (BWT[i] == BWT[j] < 254).  BWT >= 254 (wildcard,
+ * separator, or the undefined left context of position 0, the reference's
+ * INITIALCHAR) is unique, as in ISLEFTDIVERSE (src/match/esa-maxpairs.c:24-31).
+ */
+#ifndef GT_MAXPAIRS_HIP_H
+#define GT_MAXPAIRS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gt_smax_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* GtProcessmaxpairs analogue (without the encseq / GtError arguments). */
+typedef int (*GtMaxpairsFunc)(void *data, uint64_t len, uint64_t pos1, uint64_t pos2);
+
+/* in->suftab is required (4 or 8 bytes per entry). */
+int gt_maxpairs_hip_enumerate(const GtSmaxInput *in, unsigned int minlen,
+                              GtMaxpairsFunc cb, void *data,
+                              char *errbuf, size_t errlen);
+
+/* *len_pos1_pos2 receives 3*count uint64 (malloc'd; free with gt_smax_free). */
+int gt_maxpairs_hip_enumerate_to_buffer(const GtSmaxInput *in, unsigned int minlen,
+                                        uint64_t **len_pos1_pos2, uint64_t *count,
+                                        char *errbuf, size_t errlen);
+
+/* -------------------------------------------------- device-resident API */
+
+/* Tables in HBM, global rows 0..N (lcp_dev/bwt_dev as for GtSmaxDevShard
+ * with base 0; suftab entries of suf_bytes = 4 or 8 bytes). */
+typedef struct {
+  const uint8_t *lcp_dev;
+  const uint8_t *bwt_dev;
+  const GtSmaxLlv *llv_dev;
+  uint64_t numllv;
+  const void *suf_dev;
+  int suf_bytes;
+  uint64_t nonspecials;      /* N */
+  int device;
+} GtMaxpairsDevInput;
+
+typedef struct GtMaxpairsPlan GtMaxpairsPlan;
+
+/* Expands the exact LCP values (u32 per row, .llv applied) once. */
+int gt_maxpairs_plan_create(GtMaxpairsPlan **plan, const GtMaxpairsDevInput *in,
+                            unsigned int minlen, char *errbuf, size_t errlen);
+void gt_maxpairs_plan_delete(GtMaxpairsPlan *plan);
+
+/* Enqueue the counting pass (pairs per row + exclusive scan) on stream. */
+int gt_maxpairs_plan_count(GtMaxpairsPlan *plan, void *stream);
+
+/* Synchronises and returns the number of pairs of the last count pass. */
+int gt_maxpairs_plan_total(GtMaxpairsPlan *plan, uint64_t *total);
+
+/* Enqueue the emission pass: out_dev receives 3*total uint64
+ * (len, pos1 < pos2) triples; capacity is in triples (pairs beyond it are
+ * dropped).  Requires a preceding count pass. */
+int gt_maxpairs_plan_emit(GtMaxpairsPlan *plan, uint64_t *out_dev, uint64_t capacity,
+                          void *stream);
+
+/* F4: on-device sequence mapping of position pairs, the seqnum/relpos step
+ * of gt_querymatch_fill / gt_encseq_seqnum (src/match/querymatch.c:47-67,
+ * src/core/encseq.c:3815-3885): for each (len, pos1, pos2) triple with
+ * pos1 < pos2, writes (len, seqnum1, relpos1, seqnum2, relpos2) given the
+ * sorted separator positions sep_dev[0..nsep).  Asynchronous on stream. */
+int gt_seqpos_map_dev(const uint64_t *sep_dev, uint64_t nsep, const uint64_t *pairs_dev,
+                      uint64_t count, uint64_t *out_dev, int device, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

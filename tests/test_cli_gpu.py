@@ -39,6 +39,20 @@ def test_cli_atinsert_pairs(tmp_path, scan, width):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scan,width", [(False, 8), (True, 4)])
+def test_cli_maxpairs_matches_reference_golden(tmp_path, scan, width):
+    # `gt repfind -l 8 -ii Atinsert` (default -f: maximal pairs) == the
+    # reference's testdata/repfind-8-Atinsert.txt after sorting
+    idx = _index(tmp_path, "Atinsert.fna", width)
+    out = subprocess.run([CLI, "-l", "8", "-ii", idx] + (["-scan"] if scan else []), check=True,
+                         capture_output=True, text=True).stdout
+    with open(os.path.join(GOLDEN, "repfind-8-Atinsert.txt")) as fh:
+        want = _norm(fh)
+    mine = _norm(out.splitlines())
+    assert len(mine) == 452 and sorted(mine) == sorted(want)
+
+
+@pytest.mark.gpu
 def test_cli_at1mb_intervals_and_gpus(tmp_path):
     idx = _index(tmp_path, "at1MB")
     e = oracle_esa("at1MB")
@@ -55,6 +69,10 @@ def test_cli_errors(tmp_path):
     assert r.returncode == 1 and "gt repfind: error:" in r.stderr
     r = subprocess.run([CLI, "-smax", "-r", "-ii", "x"], capture_output=True, text=True)
     assert r.returncode == 1 and "exclude each other" in r.stderr
+    r = subprocess.run([CLI, "-l", "8", "-r", "-ii", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "not part of this build" in r.stderr
+    r = subprocess.run([CLI, "-intervals", "-ii", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "requires option" in r.stderr
     r = subprocess.run([CLI, "-smax", "-l", "0", "-ii", "x"], capture_output=True, text=True)
     assert r.returncode == 1
     r = subprocess.run([CLI, "-smax", "-ii", str(tmp_path / "missing")], capture_output=True, text=True)

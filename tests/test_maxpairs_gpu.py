@@ -1,0 +1,147 @@
+"""GPU parity for maximal pairs (`gt repfind -l N`) and the
+on-device seqnum/relpos mapping (F4), through the C-ABI.
+
+Pinned to the reference's own golden `testdata/repfind-8-Atinsert.txt`
+(`gt repfind -l 8` on Atinsert, 452 lines) after sorting, and to the
+oracle's restatement of the bottom-up maxpairs traversal
+(`orc_maxpairs`, src/match/esa-bottomup-maxpairs.inc:136-264) as a pair SET
+on fixtures and seeded texts with specials and .llv values.  The emission
+order differs from the reference's traversal order by design (row order),
+so every comparison is on sorted (len, pos1 < pos2) triples or sorted lines.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import genometools_smax_amd as G
+import oracle_lib as O
+from conftest import GOLDEN, oracle_esa
+
+pytestmark = pytest.mark.gpu
+
+
+def _norm(p):
+    p = np.asarray(p, dtype=np.uint64).reshape(-1, 3)
+    lo = np.minimum(p[:, 1], p[:, 2])
+    hi = np.maximum(p[:, 1], p[:, 2])
+    q = np.stack([p[:, 0], lo, hi], axis=1)
+    return q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]
+
+
+def _gpu(e, minlen, suf_dtype=np.uint64):
+    return G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab.astype(suf_dtype), e.n,
+                                e.nonspecials, minlen)
+
+
+def test_atinsert_matches_reference_golden():
+    e = oracle_esa("Atinsert.fna")
+    got = _gpu(e, 8)
+    lines = [" ".join(ln.split()) for ln in O.format_pairs(got, e.separators)]
+    with open(os.path.join(GOLDEN, "repfind-8-Atinsert.txt")) as fh:
+        want = [" ".join(ln.split()) for ln in fh if ln.strip()]
+    assert len(lines) == 452
+    assert sorted(lines) == sorted(want)
+
+
+@pytest.mark.parametrize("minlen", [4, 8, 12, 20, 40])
+def test_atinsert_pair_set(minlen):
+    e = oracle_esa("Atinsert.fna")
+    got = _gpu(e, minlen)
+    assert np.all(got[:, 1] < got[:, 2])
+    assert np.array_equal(_norm(got), _norm(O.maxpairs(e, minlen)))
+
+
+@pytest.mark.parametrize("minlen", [20, 50, 255, 300])
+def test_at1mb_pair_set(minlen):
+    e = oracle_esa("at1MB")
+    got = _gpu(e, minlen)
+    assert np.array_equal(_norm(got), _norm(O.maxpairs(e, minlen)))
+    if minlen == 20:
+        assert len(O.format_pairs(got, e.separators)) == 4507
+
+
+def test_suftab_4_bytes():
+    e = oracle_esa("at1MB")
+    assert np.array_equal(_norm(_gpu(e, 20, np.uint32)), _norm(_gpu(e, 20)))
+
+
+def _repetitive(rng, n, pspecial):
+    t = rng.integers(0, 4, n, dtype=np.uint8)
+    fams = [rng.integers(0, 4, int(rng.integers(40, 600)), dtype=np.uint8) for _ in range(5)]
+    for _ in range(n // 2000):
+        f = fams[int(rng.integers(0, len(fams)))]
+        at = int(rng.integers(0, n - len(f)))
+        cp = f.copy()
+        mut = rng.random(len(cp)) < 0.02
+        cp[mut] = rng.integers(0, 4, int(mut.sum()), dtype=np.uint8)
+        t[at:at + len(cp)] = cp
+    sp = rng.random(n) < pspecial
+    t[sp] = rng.choice(np.array([254, 255], dtype=np.uint8), int(sp.sum()))
+    return t
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_repetitive(seed):
+    rng = np.random.default_rng(300 + seed)
+    t = _repetitive(rng, int(rng.integers(20000, 80000)), [0.0, 0.001, 0.01, 0.05][seed])
+    e = O.Esa(t)
+    for minlen in (12, 30, 256):
+        assert np.array_equal(_norm(_gpu(e, minlen)), _norm(O.maxpairs(e, minlen))), minlen
+
+
+def test_long_lcp_values():
+    # an exact 1200-symbol duplication: pairs of length >= 255 need the .llv
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 4, 1200, dtype=np.uint8)
+    t = np.concatenate([rng.integers(0, 4, 5000, dtype=np.uint8), a, np.array([255], np.uint8),
+                        rng.integers(0, 4, 3000, dtype=np.uint8), a, np.array([254], np.uint8), a])
+    e = O.Esa(t)
+    assert len(e.llv) > 0
+    for minlen in (100, 255, 256, 1000, 1200, 1201):
+        assert np.array_equal(_norm(_gpu(e, minlen)), _norm(O.maxpairs(e, minlen))), minlen
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_small_edge_texts(seed):
+    rng = np.random.default_rng(40 + seed)
+    for _ in range(15):
+        n = int(rng.integers(1, 200))
+        t = rng.integers(0, int(rng.integers(1, 5)), n, dtype=np.uint8)
+        if rng.random() < 0.5:
+            t[rng.random(n) < 0.1] = 254
+        e = O.Esa(t)
+        for minlen in (1, 2, 5):
+            assert np.array_equal(_norm(_gpu(e, minlen)), _norm(O.maxpairs(e, minlen)))
+
+
+def test_device_resident_plan_and_seqpos_map():
+    import torch
+    e = oracle_esa("at1MB")
+    d = G.DeviceEsa(e.text, keep_suftab=True)
+    p = d.maxpairs_plan(20)
+    p.count()
+    total = p.total()
+    out = torch.empty(3 * total, dtype=torch.int64, device="cuda")
+    p.emit(out.data_ptr(), total)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64).reshape(-1, 3)
+    assert np.array_equal(_norm(got), _norm(O.maxpairs(e, 20)))
+    # F4: seqnum / relpos on the device == the oracle's formatter
+    sep = torch.from_numpy(e.separators.view(np.int64)).cuda()
+    mapped = torch.empty(5 * total, dtype=torch.int64, device="cuda")
+    G.seqpos_map_dev(sep.data_ptr(), len(e.separators), out.data_ptr(), total, mapped.data_ptr())
+    torch.cuda.synchronize()
+    m = mapped.cpu().numpy().view(np.uint64).reshape(-1, 5)
+    lines = ["%d %d %d F %d %d %d\n" % (r[0], r[1], r[2], r[0], r[3], r[4]) for r in m]
+    assert sorted(lines) == sorted(O.format_pairs(got, e.separators))
+    p.close()
+    d.release()
+
+
+def test_errors_are_reported():
+    e = oracle_esa("Atinsert.fna")
+    with pytest.raises(G.SmaxError):
+        G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab, e.n, e.n + 5, 8)
+    with pytest.raises(G.SmaxError):
+        G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab, e.n, e.nonspecials, 0)
