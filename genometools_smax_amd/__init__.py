@@ -113,6 +113,11 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise SmaxError("HIP library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+        # torch first: its bundled HIP runtime (soname libamdhip64.so.7) then
+        # also serves this library.  Loaded the other way round, torch's
+        # libtorch_hip (NEEDED libamdhip64.so, RPATH $ORIGIN) would map a
+        # second HIP/HSA runtime into the process and find no GPU.
+        import torch  # noqa: F401
         L = ctypes.CDLL(LIB_PATH)
         vp, u64, u32, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_int
         cs, sz = ctypes.c_char_p, ctypes.c_size_t

@@ -16,9 +16,11 @@
 // "block" (the maximal run with LCP >= minlen) keeping the running minimum
 // of LCP, i.e. the depth of the lowest common interval with row i, and
 // counts (pass 1) or writes (pass 2) the pairs whose left contexts differ.
-// Pass 1 + an exclusive scan give every row its output offset, so pass 2
-// writes the pairs without atomics.  Rows outside blocks (most rows of
-// non-repetitive input) exit after one load.  The walk reads X (exact LCP,
+// The rows with LCP[j] >= minlen (the only ones with a non-empty walk) are
+// listed first (16 rows per thread per 16-byte load, per-workgroup counts,
+// scan, ordered write); then one lane per listed row counts its pairs, an
+// exclusive scan of the counts gives every row its output offset, and the
+// emission pass writes the pairs without atomics.  The walk reads X (exact LCP,
 // u32) and BWT 8 rows per step (neighbouring lanes walk neighbouring rows:
 // each step of a wave is one contiguous segment), so the loop-carried
 // minimum never waits on a single load.
@@ -84,58 +86,147 @@ __device__ __forceinline__ uint64_t suf_at(const void *S, uint64_t k) {
   return (uint64_t) reinterpret_cast<const SufT *>(S)[k];
 }
 
-// Pass 1 (EMIT = false): cnt[j] = number of maximal pairs (i, j), i < j.
-// Pass 2 (EMIT = true): writes them at off[j] as (len, pos1 < pos2).
+// Walk of row j: counts (EMIT = false) or writes at out[o..] (EMIT = true)
+// the maximal pairs (i, j), i < j.  The early exit reads the LCP byte only
+// (exact below 255), so rows outside blocks cost one byte.
 template <bool EMIT, typename SufT>
-__global__ void __launch_bounds__(256)
-mp_walk_kernel(const uint32_t *X, const uint8_t *B, const void *S, uint64_t N, uint32_t minlen,
-               uint64_t *cnt, const uint64_t *off, uint64_t *out, uint64_t capacity) {
-  const uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (j >= N) return;
+__device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *X, const uint8_t *B,
+                                            const void *S, uint64_t j, uint32_t minlen,
+                                            uint64_t o, uint64_t *out, uint64_t capacity) {
+  const uint32_t m8 = lcp[j];
+  if (j == 0 || (m8 < 255u && m8 < minlen)) return 0;
   uint32_t m = X[j];                       // depth of the pair (j-1, j)
-  uint64_t c = 0;
-  if (j > 0 && m >= minlen) {
-    const uint32_t bj = B[j];
-    const bool uj = bj >= 254u;            // unique left context
-    const uint64_t o = EMIT ? off[j] : 0;
-    const uint64_t sj = EMIT ? suf_at<SufT>(S, j) : 0;
-    int64_t i = (int64_t) j - 1;
-    bool more = true;
-    while (more) {
-      uint32_t xi[MP_STEP], bi[MP_STEP];
-      uint64_t si[MP_STEP];
+  if (m < minlen) return 0;
+  uint32_t c = 0;
+  const uint32_t bj = B[j];
+  const bool uj = bj >= 254u;              // unique left context
+  const uint64_t sj = EMIT ? suf_at<SufT>(S, j) : 0;
+  int64_t i = (int64_t) j - 1;
+  bool more = true;
+  while (more) {
+    uint32_t xi[MP_STEP], bi[MP_STEP];
+    uint64_t si[MP_STEP];
 #pragma unroll
-      for (int q = 0; q < MP_STEP; q++) {
-        const int64_t r = i - q;
-        xi[q] = r >= 0 ? X[r] : 0u;
-        bi[q] = r >= 0 ? (uint32_t) B[r] : 0u;
-        si[q] = (EMIT && r >= 0) ? suf_at<SufT>(S, (uint64_t) r) : 0;
-      }
-#pragma unroll
-      for (int q = 0; q < MP_STEP; q++) {
-        if (!more) break;
-        // row i-q pairs with j at depth m = min LCP[i-q+1 .. j]
-        if (uj || bi[q] != bj) {
-          if (EMIT && o + c < capacity) {
-            uint64_t *w = out + 3 * (o + c);
-            w[0] = m;
-            w[1] = si[q] < sj ? si[q] : sj;
-            w[2] = si[q] < sj ? sj : si[q];
-          }
-          c++;
-        }
-        m = xi[q] < m ? xi[q] : m;         // X[0] == 0 ends every walk
-        if (m < minlen) more = false;
-      }
-      i -= MP_STEP;
+    for (int q = 0; q < MP_STEP; q++) {
+      const int64_t r = i - q;
+      xi[q] = r >= 0 ? X[r] : 0u;
+      bi[q] = r >= 0 ? (uint32_t) B[r] : 0u;
+      si[q] = (EMIT && r >= 0) ? suf_at<SufT>(S, (uint64_t) r) : 0;
     }
+#pragma unroll
+    for (int q = 0; q < MP_STEP; q++) {
+      if (!more) break;
+      // row i-q pairs with j at depth m = min LCP[i-q+1 .. j]
+      if (uj || bi[q] != bj) {
+        if (EMIT && o + c < capacity) {
+          uint64_t *w = out + 3 * (o + c);
+          w[0] = m;
+          w[1] = si[q] < sj ? si[q] : sj;
+          w[2] = si[q] < sj ? sj : si[q];
+        }
+        c++;
+      }
+      m = xi[q] < m ? xi[q] : m;           // X[0] == 0 ends every walk
+      if (m < minlen) more = false;
+    }
+    i -= MP_STEP;
   }
-  if (!EMIT) cnt[j] = c;
+  return c;
 }
 
-__global__ void mp_total_kernel(const uint64_t *cnt, const uint64_t *off, uint64_t N,
+// workgroup-wide exclusive prefix (u64) of one value per thread; *total = sum
+__device__ __forceinline__ uint64_t mp_block_excl(uint64_t v, uint64_t *total) {
+  __shared__ uint64_t sW[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) sW[wave] = incl;
+  __syncthreads();
+  uint64_t wo = 0;
+  for (int w = 0; w < wave; w++) wo += sW[w];
+  *total = sW[0] + sW[1] + sW[2] + sW[3];
+  return wo + incl - v;
+}
+
+// Candidate rows (LCP[j] >= minlen, j >= 1: rows whose walk is not empty),
+// found per workgroup of MP_WG_ROWS rows: every thread tests 16 consecutive
+// rows with one 16-byte LCP load (byte >= min(minlen, 255), exact below
+// 255).  Pass A counts them per workgroup, pass B (after a scan of those
+// counts) writes them to one global list in row order.  The walks then run
+// one lane per candidate row (passes C and D), so neighbouring lanes walk
+// neighbouring rows (coalesced) and a long block spreads over the device.
+#define MP_ROWS 16
+#define MP_WG_ROWS (256 * MP_ROWS)
+
+__device__ __forceinline__ uint32_t mp_candidates(const uint8_t *lcp, uint64_t j0, uint64_t N,
+                                                  uint32_t mf) {
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (j0 + MP_ROWS <= N) {
+    v = *reinterpret_cast<const uint4 *>(lcp + j0);
+  } else {
+    for (int q = 0; q < MP_ROWS; q++)
+      if (j0 + q < N) reinterpret_cast<uint8_t *>(&v)[q] = lcp[j0 + q];
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < MP_ROWS; q++)
+    m |= (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= mf ? 1u : 0u) << q;
+  if (j0 == 0) m &= ~1u;                   // row 0 has no earlier row
+  return m;
+}
+
+__global__ void __launch_bounds__(256)
+mp_cand_count_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, uint64_t *wg_cand) {
+  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) MP_ROWS;
+  uint64_t tot;
+  (void) mp_block_excl((uint64_t) __popc(mp_candidates(lcp, j0, N, mf)), &tot);
+  if (threadIdx.x == 0) wg_cand[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(256)
+mp_cand_write_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, const uint64_t *wg_cand_off,
+                     uint64_t *list) {
+  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) MP_ROWS;
+  uint32_t m = mp_candidates(lcp, j0, N, mf);
+  uint64_t tot;
+  uint64_t pos = wg_cand_off[blockIdx.x] + mp_block_excl((uint64_t) __popc(m), &tot);
+  while (m) {
+    const int q = __builtin_ctz(m);
+    m &= m - 1;
+    list[pos++] = j0 + q;
+  }
+}
+
+// Pass C: pairs per candidate row.
+template <typename SufT>
+__global__ void __launch_bounds__(256)
+mp_count_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint64_t *list,
+                uint64_t ncand, uint32_t minlen, uint32_t *cnt) {
+  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (e >= ncand) return;
+  cnt[e] = mp_walk<false, SufT>(lcp, X, B, nullptr, list[e], minlen, 0, nullptr, 0);
+}
+
+// Pass D: the pairs of every candidate row at its scanned offset,
+// (len, pos1 < pos2).
+template <typename SufT>
+__global__ void __launch_bounds__(256)
+mp_emit_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const void *S,
+               const uint64_t *list, uint64_t ncand, uint32_t minlen, const uint32_t *cnt,
+               const uint64_t *off, uint64_t *out, uint64_t capacity) {
+  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (e >= ncand || cnt[e] == 0) return;
+  (void) mp_walk<true, SufT>(lcp, X, B, S, list[e], minlen, off[e], out, capacity);
+}
+
+__global__ void mp_total_kernel(const uint32_t *cnt, const uint64_t *off, uint64_t n,
                                 uint64_t *total) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *total = N == 0 ? 0 : off[N - 1] + cnt[N - 1];
+  if (threadIdx.x == 0 && blockIdx.x == 0) *total = n == 0 ? 0 : off[n - 1] + cnt[n - 1];
 }
 
 // F4: (len, pos1, pos2) -> (len, seqnum1, relpos1, seqnum2, relpos2); seqnum
@@ -167,9 +258,14 @@ __global__ void __launch_bounds__(256) seqpos_map_kernel(const uint64_t *sep, ui
 struct GtMaxpairsPlan {
   GtMaxpairsDevInput in;
   unsigned int minlen;
-  uint32_t *X;          // N+1 exact LCP values
-  uint64_t *cnt, *off;  // N pair counts, N exclusive offsets
-  uint64_t *total;      // 1
+  uint32_t *X;                   // N+1 exact LCP values
+  uint64_t nwg;                  // candidate workgroups (MP_WG_ROWS rows)
+  uint64_t *wg_cand, *wg_cand_off;
+  uint64_t ncand;                // candidate rows (fixed by the tables and minlen)
+  uint64_t *list;                // ncand candidate rows, row order
+  uint32_t *cnt;                 // ncand pair counts
+  uint64_t *off;                 // ncand exclusive offsets
+  uint64_t *total;               // 1
   void *scan_tmp;
   size_t scan_tmp_bytes;
   bool counted;
@@ -180,7 +276,8 @@ static unsigned mp_blocks(uint64_t n) { return (unsigned) ((n + 255) / 256); }
 extern "C" void gt_maxpairs_plan_delete(GtMaxpairsPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
-  void *bufs[] = {p->X, p->cnt, p->off, p->total, p->scan_tmp};
+  void *bufs[] = {p->X, p->wg_cand, p->wg_cand_off, p->list, p->cnt, p->off, p->total,
+                  p->scan_tmp};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   free(p);
@@ -208,6 +305,10 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
     mp_seterr(errbuf, errlen, "minimum length must be >= 1");
     return -1;
   }
+  if ((uintptr_t) in->lcp_dev & 15) {
+    mp_seterr(errbuf, errlen, "device lcptab must be 16-byte aligned");
+    return -1;
+  }
   p = (GtMaxpairsPlan *) calloc(1, sizeof *p);
   if (p == NULL) {
     mp_seterr(errbuf, errlen, "out of memory");
@@ -217,8 +318,9 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
   p->minlen = minlen;
   MPCHK(hipSetDevice(in->device));
   MPCHK(hipMalloc(&p->X, sizeof (uint32_t) * (N + 1)));
-  MPCHK(hipMalloc(&p->cnt, sizeof (uint64_t) * (N + 1)));
-  MPCHK(hipMalloc(&p->off, sizeof (uint64_t) * (N + 1)));
+  p->nwg = (N + MP_WG_ROWS - 1) / MP_WG_ROWS;
+  MPCHK(hipMalloc(&p->wg_cand, sizeof (uint64_t) * (p->nwg + 1)));
+  MPCHK(hipMalloc(&p->wg_cand_off, sizeof (uint64_t) * (p->nwg + 1)));
   MPCHK(hipMalloc(&p->total, sizeof (uint64_t)));
   MPCHK(hipMemset(p->total, 0, sizeof (uint64_t)));
   MPCHK(hipMalloc(&derr, sizeof (uint32_t)));
@@ -231,11 +333,39 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
                        in->numllv, in->lcp_dev, N, p->X, derr);
     MPCHK(hipGetLastError());
   }
+  // candidate rows: their number sizes the per-candidate buffers (the tables
+  // are immutable for the plan's life; every count pass rebuilds the list)
   if (N > 0) {
-    MPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->cnt, p->off, (uint64_t) 0,
-                                  (size_t) N, rocprim::plus<uint64_t>(), (hipStream_t) 0));
+    size_t b1 = 0;
+    MPCHK(rocprim::exclusive_scan(nullptr, b1, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
+                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), (hipStream_t) 0));
+    p->scan_tmp_bytes = b1;
+    hipLaunchKernelGGL(mp_cand_count_kernel, dim3((unsigned) p->nwg), dim3(256), 0, 0, in->lcp_dev,
+                       N, minlen < 255u ? minlen : 255u, p->wg_cand);
+    MPCHK(hipGetLastError());
+    MPCHK(hipMalloc(&p->scan_tmp, b1 ? b1 : 16));
+    MPCHK(rocprim::exclusive_scan(p->scan_tmp, b1, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
+                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), (hipStream_t) 0));
+    uint64_t last[2];
+    MPCHK(hipMemcpy(&last[0], p->wg_cand + p->nwg - 1, sizeof (uint64_t), hipMemcpyDeviceToHost));
+    MPCHK(hipMemcpy(&last[1], p->wg_cand_off + p->nwg - 1, sizeof (uint64_t), hipMemcpyDeviceToHost));
+    p->ncand = last[0] + last[1];
   }
-  MPCHK(hipMalloc(&p->scan_tmp, p->scan_tmp_bytes ? p->scan_tmp_bytes : 16));
+  MPCHK(hipMalloc(&p->list, sizeof (uint64_t) * (p->ncand + 1)));
+  MPCHK(hipMalloc(&p->cnt, sizeof (uint32_t) * (p->ncand + 1)));
+  MPCHK(hipMalloc(&p->off, sizeof (uint64_t) * (p->ncand + 1)));
+  if (p->ncand > 0) {
+    size_t b2 = 0;
+    MPCHK(rocprim::exclusive_scan(nullptr, b2, p->cnt, p->off, (uint64_t) 0, (size_t) p->ncand,
+                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
+    if (b2 > p->scan_tmp_bytes) {
+      MPCHK(hipFree(p->scan_tmp));
+      p->scan_tmp = NULL;
+      MPCHK(hipMalloc(&p->scan_tmp, b2));
+      p->scan_tmp_bytes = b2;
+    }
+  }
+  if (p->scan_tmp == NULL) MPCHK(hipMalloc(&p->scan_tmp, 16));
   MPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   if (herr & 1u) { mp_seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
   if (herr & 2u) { mp_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
@@ -252,24 +382,28 @@ extern "C" int gt_maxpairs_plan_count(GtMaxpairsPlan *p, void *stream) {
   char *errbuf = NULL;
   size_t errlen = 0;
   hipStream_t s = (hipStream_t) stream;
-  const uint64_t N = p->in.nonspecials;
+  const uint64_t N = p->in.nonspecials, nc = p->ncand;
+  const uint32_t mf = p->minlen < 255u ? p->minlen : 255u;
   MPCHK(hipSetDevice(p->in.device));
-  if (N == 0) {
+  if (nc == 0) {
     MPCHK(hipMemsetAsync(p->total, 0, sizeof (uint64_t), s));
   } else {
-    if (p->in.suf_bytes == 8)
-      hipLaunchKernelGGL((mp_walk_kernel<false, uint64_t>), dim3(mp_blocks(N)), dim3(256), 0, s,
-                         p->X, p->in.bwt_dev, p->in.suf_dev, N, p->minlen, p->cnt, nullptr,
-                         nullptr, 0);
-    else
-      hipLaunchKernelGGL((mp_walk_kernel<false, uint32_t>), dim3(mp_blocks(N)), dim3(256), 0, s,
-                         p->X, p->in.bwt_dev, p->in.suf_dev, N, p->minlen, p->cnt, nullptr,
-                         nullptr, 0);
-    MPCHK(hipGetLastError());
     size_t bytes = p->scan_tmp_bytes;
-    MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->cnt, p->off, (uint64_t) 0, (size_t) N,
+    hipLaunchKernelGGL(mp_cand_count_kernel, dim3((unsigned) p->nwg), dim3(256), 0, s,
+                       p->in.lcp_dev, N, mf, p->wg_cand);
+    MPCHK(hipGetLastError());
+    MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
+                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), s));
+    hipLaunchKernelGGL(mp_cand_write_kernel, dim3((unsigned) p->nwg), dim3(256), 0, s,
+                       p->in.lcp_dev, N, mf, p->wg_cand_off, p->list);
+    MPCHK(hipGetLastError());
+    hipLaunchKernelGGL((mp_count_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->list, nc, p->minlen, p->cnt);
+    MPCHK(hipGetLastError());
+    bytes = p->scan_tmp_bytes;
+    MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->cnt, p->off, (uint64_t) 0, (size_t) nc,
                                   rocprim::plus<uint64_t>(), s));
-    hipLaunchKernelGGL(mp_total_kernel, dim3(1), dim3(64), 0, s, p->cnt, p->off, N, p->total);
+    hipLaunchKernelGGL(mp_total_kernel, dim3(1), dim3(64), 0, s, p->cnt, p->off, nc, p->total);
     MPCHK(hipGetLastError());
   }
   p->counted = true;
@@ -294,18 +428,18 @@ extern "C" int gt_maxpairs_plan_emit(GtMaxpairsPlan *p, uint64_t *out_dev, uint6
   char *errbuf = NULL;
   size_t errlen = 0;
   hipStream_t s = (hipStream_t) stream;
-  const uint64_t N = p->in.nonspecials;
+  const uint64_t nc = p->ncand;
   if (!p->counted) return -1;
   MPCHK(hipSetDevice(p->in.device));
-  if (N == 0 || capacity == 0) return 0;
+  if (nc == 0 || capacity == 0) return 0;
   if (p->in.suf_bytes == 8)
-    hipLaunchKernelGGL((mp_walk_kernel<true, uint64_t>), dim3(mp_blocks(N)), dim3(256), 0, s,
-                       p->X, p->in.bwt_dev, p->in.suf_dev, N, p->minlen, nullptr, p->off, out_dev,
-                       capacity);
+    hipLaunchKernelGGL((mp_emit_kernel<uint64_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->in.suf_dev, p->list, nc, p->minlen,
+                       p->cnt, p->off, out_dev, capacity);
   else
-    hipLaunchKernelGGL((mp_walk_kernel<true, uint32_t>), dim3(mp_blocks(N)), dim3(256), 0, s,
-                       p->X, p->in.bwt_dev, p->in.suf_dev, N, p->minlen, nullptr, p->off, out_dev,
-                       capacity);
+    hipLaunchKernelGGL((mp_emit_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->in.suf_dev, p->list, nc, p->minlen,
+                       p->cnt, p->off, out_dev, capacity);
   MPCHK(hipGetLastError());
   return 0;
 fail:
