@@ -821,13 +821,24 @@ __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r
   const uint32_t eqn1 = EQ >> 2, dn1 = ~((UP | EQ) >> 2);          // c+1 vs c+2
   const uint32_t D = A & dn & 0xffffu;
   const uint32_t D3 = A & eqn & dn1 & 0xffffu;
-  *Lm = (all_exact || unresolved) ? A : (A & eqn & eqn1);
-  if (all_exact || unresolved || (D | D3) == 0) {
+  if (A == 0) {
+    *Dm = 0;
+    *D3m = 0;
+    *Lm = 0;
+    return;
+  }
+  // left diversity of rows (c-1, c) and (c-1, c, c+1): every interval
+  // [c-1 .. j] needs the first, every plateau of >= 3 rows the second, so
+  // the exact queue only receives starts that can still be accepted (on
+  // repeat-rich DNA most plateau starts share their left symbols)
+  uint32_t div2, div3;
+  segment_div(t, so, &div2, &div3);
+  if (all_exact || unresolved) {
+    *Lm = A & div2;
     *Dm = 0;
     *D3m = 0;
   } else {
-    uint32_t div2, div3;
-    segment_div(t, so, &div2, &div3);
+    *Lm = A & eqn & eqn1 & div3;
     *Dm = (D & div2) | (D3 & div3);
     *D3m = D3 & div3;
   }
