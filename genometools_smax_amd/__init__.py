@@ -97,6 +97,18 @@ class GtMaxpairsDevInput(ctypes.Structure):
     ]
 
 
+_LEAF_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64,
+                            ctypes.c_uint64, ctypes.c_uint64)
+_BRANCH_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64,
+                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64)
+_ITV_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                           ctypes.c_uint64)
+
+
+class GtLcpitvVisitor(ctypes.Structure):
+    _fields_ = [("leaf_edge", _LEAF_CB), ("branching_edge", _BRANCH_CB), ("lcp_interval", _ITV_CB)]
+
+
 class GtSmaxRecord(ctypes.Structure):
     _fields_ = [("lb", ctypes.c_uint64), ("lcp", ctypes.c_uint32), ("width", ctypes.c_uint32)]
 
@@ -162,6 +174,10 @@ def lib():
         L.gt_maxpairs_plan_total.argtypes = [vp, ctypes.POINTER(u64)]
         L.gt_maxpairs_plan_emit.argtypes = [vp, vp, u64, vp]
         L.gt_seqpos_map_dev.argtypes = [vp, u64, vp, u64, vp, ci, vp]
+        L.gt_lcpitv_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput),
+                                                        ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
+        L.gt_esa_bottomup_hip.argtypes = [ctypes.POINTER(GtSmaxInput), ctypes.POINTER(GtLcpitvVisitor),
+                                          vp, cs, sz]
         _lib = L
     return _lib
 
@@ -398,6 +414,72 @@ def seqpos_map_dev(sep_ptr, nsep, pairs_ptr, count, out_ptr, device=0, stream=0)
     """(len, pos1, pos2) -> (len, seqnum1, relpos1, seqnum2, relpos2) on the GPU."""
     if lib().gt_seqpos_map_dev(sep_ptr, int(nsep), pairs_ptr, int(count), out_ptr, device, stream) != 0:
         raise SmaxError("gt_seqpos_map_dev failed")
+
+
+def _input(lcptab, llvtab, bwttab, suftab, totallength, nonspecials):
+    keep = []
+    lcptab = np.ascontiguousarray(lcptab, dtype=np.uint8)
+    llvtab = np.ascontiguousarray(llvtab, dtype=np.uint64).reshape(-1, 2)
+    keep += [lcptab, llvtab]
+    inp = GtSmaxInput()
+    inp.lcptab = lcptab.ctypes.data
+    inp.llvtab = llvtab.ctypes.data if len(llvtab) else None
+    inp.numllv = len(llvtab)
+    if bwttab is not None:
+        bwttab = np.ascontiguousarray(bwttab, dtype=np.uint8)
+        keep.append(bwttab)
+        inp.bwttab = bwttab.ctypes.data
+    if suftab is not None:
+        suftab = np.ascontiguousarray(suftab)
+        if suftab.dtype not in (np.uint32, np.uint64):
+            suftab = suftab.astype(np.uint64)
+        keep.append(suftab)
+        inp.suftab = suftab.ctypes.data
+        inp.suftab_bytes = suftab.dtype.itemsize
+    inp.totallength = int(totallength)
+    inp.nonspecials = int(nonspecials)
+    return inp, keep
+
+
+def enumerate_lcp_intervals(lcptab, llvtab, totallength, nonspecials):
+    """Every lcp-interval of depth > 0 with its father, bottom-up (pop)
+    order: (k,5) uint64 of (lcp, lb, rb, fatherlcp, fatherlb)
+    (gt_lcpitv_hip_enumerate_to_buffer)."""
+    inp, keep = _input(lcptab, llvtab, None, None, totallength, nonspecials)
+    out = ctypes.c_void_p()
+    cnt = ctypes.c_uint64()
+    eb = _errbuf()
+    _check(lib().gt_lcpitv_hip_enumerate_to_buffer(ctypes.byref(inp), ctypes.byref(out),
+                                                   ctypes.byref(cnt), eb, len(eb)), eb)
+    n = cnt.value
+    if n == 0:
+        return np.zeros((0, 5), dtype=np.uint64)
+    buf = (ctypes.c_uint64 * (5 * n)).from_address(out.value)
+    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 5).copy()
+    lib().gt_smax_free(out)
+    return arr
+
+
+def esa_bottomup(lcptab, llvtab, suftab, totallength, nonspecials, leaf_edge=None,
+                 branching_edge=None, lcp_interval=None):
+    """gt_esa_bottomup over the GPU lcp-interval tree (gt_esa_bottomup_hip):
+    leaf_edge(firstsucc, fd, flb, leafnumber), branching_edge(firstsucc, fd,
+    flb, sd, slb, srb), lcp_interval(lcp, lb, rb); a truthy return stops."""
+    inp, keep = _input(lcptab, llvtab, None, suftab, totallength, nonspecials)
+    v = GtLcpitvVisitor()
+    cbs = []
+    if leaf_edge is not None:
+        cbs.append(_LEAF_CB(lambda d, f, fd, flb, leaf: int(bool(leaf_edge(f, fd, flb, leaf)))))
+        v.leaf_edge = cbs[-1]
+    if branching_edge is not None:
+        cbs.append(_BRANCH_CB(lambda d, f, fd, flb, sd, slb, srb:
+                              int(bool(branching_edge(f, fd, flb, sd, slb, srb)))))
+        v.branching_edge = cbs[-1]
+    if lcp_interval is not None:
+        cbs.append(_ITV_CB(lambda d, lcp, lb, rb: int(bool(lcp_interval(lcp, lb, rb)))))
+        v.lcp_interval = cbs[-1]
+    eb = _errbuf()
+    _check(lib().gt_esa_bottomup_hip(ctypes.byref(inp), ctypes.byref(v), None, eb, len(eb)), eb)
 
 
 def enumerate_index(index, minlen, num_gpus=1):

@@ -251,6 +251,76 @@ uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
   return found;
 }
 
+/* Full event stream of gt_esa_bottomup (src/match/esa-bottomup.c:116-273)
+ * for a visitor with all three callbacks, as 7-word records:
+ *   (0, firstsucc, fd, flb, leafnumber, 0, 0)       visit_leaf_edge
+ *   (1, firstsucc, fd, flb, sd, slb, srb)           visit_branching_edge
+ *   (2, 0, lcp, lb, rb, 0, 0)                       visit_lcp_interval
+ * (F3 checker).  Returns the number of events; *ev is malloc'd. */
+uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
+                             uint64_t nonspecials, uint64_t **ev)
+{
+  BUStack st = {NULL, 0, 0};
+  BUItv *last = NULL;
+  BUItv lastcopy;
+  uint64_t idx, n = 0, alloc = 0, *e = NULL;
+  int firstedgefromroot = 1;
+#define EV(T, F, A, B, C, D, E)                                              \
+  do {                                                                       \
+    if (n + 1 > alloc) {                                                     \
+      alloc = alloc * 2 + 1024;                                              \
+      e = realloc(e, sizeof (uint64_t) * 7 * alloc);                         \
+    }                                                                        \
+    uint64_t *r_ = e + 7 * n++;                                              \
+    r_[0] = (T); r_[1] = (F); r_[2] = (A); r_[3] = (B); r_[4] = (C);          \
+    r_[5] = (D); r_[6] = (E);                                                \
+  } while (0)
+#define FIRSTEDGE(F)                                                         \
+  do {                                                                       \
+    if (BU_TOP(&st).lcp > 0 || !firstedgefromroot) (F) = 0;                  \
+    else { (F) = 1; firstedgefromroot = 0; }                                 \
+  } while (0)
+  bu_push(&st, 0, 0);
+  for (idx = 0; idx < nonspecials; idx++) {
+    uint64_t lcpvalue = lcp[idx + 1];
+    uint64_t prevsuffix = suftab[idx];
+    int firstedge;
+    if (lcpvalue <= BU_TOP(&st).lcp) {
+      FIRSTEDGE(firstedge);
+      EV(0, firstedge, BU_TOP(&st).lcp, BU_TOP(&st).lb, prevsuffix, 0, 0);
+    }
+    last = NULL;
+    while (lcpvalue < BU_TOP(&st).lcp) {
+      st.next--;
+      lastcopy = st.space[st.next];
+      last = &lastcopy;
+      last->rb = idx;
+      EV(2, 0, last->lcp, last->lb, last->rb, 0, 0);
+      if (lcpvalue <= BU_TOP(&st).lcp) {
+        FIRSTEDGE(firstedge);
+        EV(1, firstedge, BU_TOP(&st).lcp, BU_TOP(&st).lb, last->lcp, last->lb, last->rb);
+        last = NULL;
+      }
+    }
+    if (lcpvalue > BU_TOP(&st).lcp) {
+      if (last != NULL) {
+        uint64_t l = last->lcp, b = last->lb, r = last->rb;
+        bu_push(&st, lcpvalue, b);
+        EV(1, 1, BU_TOP(&st).lcp, BU_TOP(&st).lb, l, b, r);
+        last = NULL;
+      } else {
+        bu_push(&st, lcpvalue, idx);
+        EV(0, 1, BU_TOP(&st).lcp, BU_TOP(&st).lb, prevsuffix, 0, 0);
+      }
+    }
+  }
+  free(st.space);
+#undef EV
+#undef FIRSTEDGE
+  *ev = e;
+  return n;
+}
+
 /* --------------------------------------------------------- 3. brute force */
 
 static int is_spec(const uint8_t *t, uint64_t n, int64_t p)

@@ -179,3 +179,25 @@ def test_index_files_layout(tmp_path):
     assert np.array_equal(np.fromfile(idx + ".suf", dtype=np.uint64), e.suftab)
     O.index_fasta(os.path.join(GOLDEN, "Atinsert.fna"), idx + "4", suftab_bytes=4)
     assert np.array_equal(np.fromfile(idx + "4.suf", dtype=np.uint32).astype(np.uint64), e.suftab)
+
+
+@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB"])
+def test_bottomup_event_stream_shape(name):
+    # gt_esa_bottomup restatement (F3 checker): one leaf edge per suffix,
+    # one branching edge per popped interval, intervals in pop order
+    # (rb ascending, then depth descending), exactly one firstsucc root edge
+    e = oracle_esa(name)
+    ev = O.bottomup_events(e)
+    kinds = ev[:, 0]
+    assert int((kinds == 0).sum()) == e.nonspecials
+    assert int((kinds == 1).sum()) == int((kinds == 2).sum())
+    itv = ev[kinds == 2]
+    order = np.lexsort((-itv[:, 2].astype(np.int64), itv[:, 4]))
+    assert np.array_equal(order, np.arange(len(itv)))
+    root = ev[(kinds != 2) & (ev[:, 2] == 0)]
+    assert int(root[:, 1].sum()) == 1 and root[0, 1] == 1
+    # the smax intervals are exactly the lcp-intervals without a branching
+    # child that pass the diversity test: a subset of the intervals
+    sm = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8)
+    allitv = set(map(tuple, itv[:, 2:5].tolist()))
+    assert set(map(tuple, sm.tolist())) <= allitv
