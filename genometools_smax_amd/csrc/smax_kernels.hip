@@ -223,11 +223,14 @@ __device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
   return b < 255 ? b : lcp_big(t, g);
 }
 
-// Packed BWT (DNA): per 16 rows one u64 -- bits 2q..2q+1 the symbol code of
-// row q (0..3), bit 32+q set when row q holds a special symbol (254/255,
-// unique for left diversity; decoded as 254).
+// Packed BWT (DNA): per 16 rows one u64 in bit planes -- bit q the low bit
+// and bit 16+q the high bit of row q's symbol code (0..3), bit 32+q set when
+// row q holds a special symbol (254/255, unique for left diversity; decoded
+// as 254).  Planes make the row-vs-neighbour compares of the diversity tests
+// plain 16-bit shifts and xors (no 2-bit field compression).
 __device__ __forceinline__ uint32_t pk_sym(uint64_t w, uint32_t q) {
-  return ((w >> (32 + q)) & 1u) ? 254u : (uint32_t) (w >> (2 * q)) & 3u;
+  return ((w >> (32 + q)) & 1u) ? 254u
+                                : (uint32_t) (((w >> q) & 1u) | (((w >> (16 + q)) & 1u) << 1));
 }
 
 __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
@@ -588,13 +591,14 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
     if (t.P != nullptr) {
       const uint32_t o = co - 1, gi = o >> 4, q = o & 15u;
       const uint64_t w0 = t.P[gi], w1 = t.P[gi + 1];
-      const uint64_t c64 = (w0 & 0xffffffffull) | (w1 << 32);
-      const uint32_t codes = (uint32_t) (c64 >> (2 * q)) & 0xffffu;
+      const uint32_t a0 = (uint32_t) w0, a1 = (uint32_t) w1;
+      const uint32_t lo = (((a0 & 0xffffu) | (a1 << 16)) >> q) & 0xffu;
+      const uint32_t hi = (((a0 >> 16) | (a1 & 0xffff0000u)) >> q) & 0xffu;
       const uint32_t sp = (uint32_t) (((w0 >> 32) & 0xffffu) | (((w1 >> 32) & 0xffffu) << 16)) >> q;
       BX = 0;
 #pragma unroll
       for (int k = 0; k < 8; k++) {
-        const uint64_t sym = ((sp >> k) & 1u) ? 254u : (codes >> (2 * k)) & 3u;
+        const uint64_t sym = ((sp >> k) & 1u) ? 254u : ((lo >> k) & 1u) | (((hi >> k) & 1u) << 1);
         BX |= sym << (8 * k);
       }
     } else {
@@ -689,14 +693,6 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
 // high bit of each byte >= 254 (WILDCARD / SEPARATOR / UNDEFBWTCHAR)
 __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0x01010101u); }
 
-// 16 2-bit fields -> 16 bits: bit q = any bit of field q
-__device__ __forceinline__ uint32_t fields2_any(uint32_t x) {
-  uint32_t t = (x | (x >> 1)) & 0x55555555u;
-  t = (t | (t >> 1)) & 0x33333333u;
-  t = (t | (t >> 2)) & 0x0f0f0f0fu;
-  t = (t | (t >> 4)) & 0x00ff00ffu;
-  return (t | (t >> 8)) & 0x0000ffffu;
-}
 
 // Left diversity of the 16 rows c of segment `so` for the two interval
 // shapes decided here: *div2 = {BWT[c-1], BWT[c]} pairwise distinct (specials
@@ -705,14 +701,17 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
                                             uint32_t *div3) {
   if (t.P != nullptr) {
     const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1], nw = t.P[(so >> 4) + 1];
-    const uint32_t c = (uint32_t) w, pc = (uint32_t) (pw >> 30) & 3u, nc = (uint32_t) nw & 3u;
+    // both code planes at once (low plane bits 0..15, high plane 16..31)
+    const uint32_t c = (uint32_t) w, pc = (uint32_t) pw, nc = (uint32_t) nw;
     const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
     const uint32_t spm1 = ((sp << 1) | ((uint32_t) (pw >> 47) & 1u)) & 0xffffu;   // row q-1
     const uint32_t spp1 = (sp >> 1) | (((uint32_t) (nw >> 32) & 1u) << 15);       // row q+1
-    const uint32_t cp = (c << 2) | pc, cn = (c >> 2) | (nc << 30);
-    const uint32_t ne1 = fields2_any(c ^ cp);                // q-1 vs q
-    const uint32_t ne1n = fields2_any(c ^ cn);               // q vs q+1
-    const uint32_t ne2 = fields2_any(cp ^ cn);               // q-1 vs q+1
+    const uint32_t cp = ((c << 1) & 0xfffefffeu) | ((pc >> 15) & 0x00010001u);   // row q-1
+    const uint32_t cn = ((c >> 1) & 0x7fff7fffu) | ((nc << 15) & 0x80008000u);   // row q+1
+    const uint32_t x1 = c ^ cp, x1n = c ^ cn, x2 = cp ^ cn;
+    const uint32_t ne1 = (x1 | (x1 >> 16)) & 0xffffu;        // q-1 vs q
+    const uint32_t ne1n = (x1n | (x1n >> 16)) & 0xffffu;     // q vs q+1
+    const uint32_t ne2 = (x2 | (x2 >> 16)) & 0xffffu;        // q-1 vs q+1
     const uint32_t d2 = ne1 | sp | spm1;
     *div2 = d2;
     *div3 = d2 & (ne1n | sp | spp1) & (ne2 | spm1 | spp1);
@@ -1460,8 +1459,8 @@ __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_bytes(SmaxSc
 // ------------------------------------------------------------ BWT packing
 
 // Plan-time packing of a DNA shard's BWT for K1's windows: group gi holds
-// local rows 16(gi-1) .. 16(gi-1)+15 as 2-bit codes + a special mask (see
-// pk_sym).  Sets *flag when a row of [0, local_len) holds a symbol in
+// local rows 16(gi-1) .. 16(gi-1)+15 as two code bit planes + a special
+// mask (see pk_sym).  Sets *flag when a row of [0, local_len) holds a symbol in
 // [4, 254), i.e. the alphabet is not DNA (K1 then keeps byte BWT windows).
 __global__ void __launch_bounds__(256)
 smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, uint64_t *pk,
@@ -1478,7 +1477,7 @@ smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, u
     const uint32_t b = (w >> (8 * (k & 3))) & 0xffu;
     const int64_t row = r0 + k;
     if (b >= 254) sp |= 1u << k;
-    else code |= (b & 3u) << (2 * k);
+    else code |= ((b & 1u) << k) | (((b >> 1) & 1u) << (16 + k));   // bit planes
     if (b > 3 && b < 254 && row >= 0 && (uint64_t) row < local_len) other = true;
   }
   pk[gi] = (uint64_t) code | ((uint64_t) sp << 32);
