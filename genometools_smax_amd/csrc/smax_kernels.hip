@@ -1021,6 +1021,24 @@ __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = 
 // Filter of a landed window (one wave): per-lane segment "any byte >=
 // min(minlen,128)" bits; the .llv values are staged with the window, their
 // ranks are computed during the classification (wave_detect_direct).
+// rows of segment `so` (16 LCP bytes v) with LCP >= mf whose BWT differs
+// from the predecessor's (packed bit-plane window), or any 255 byte
+__device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint32_t so,
+                                              uint32_t mf) {
+  const uint32_t g[4] = {bytes_ge(v.x, mf), bytes_ge(v.y, mf), bytes_ge(v.z, mf),
+                         bytes_ge(v.w, mf)};
+  if ((g[0] | g[1] | g[2] | g[3]) == 0) return false;
+  const uint32_t ff = bytes_ff(v.x) | bytes_ff(v.y) | bytes_ff(v.z) | bytes_ff(v.w);
+  const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1];
+  const uint32_t c = (uint32_t) w, pc = (uint32_t) pw;
+  const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
+  const uint32_t spm1 = ((sp << 1) | ((uint32_t) (pw >> 47) & 1u)) & 0xffffu;
+  const uint32_t cp = ((c << 1) & 0xfffefffeu) | ((pc >> 15) & 0x00010001u);
+  const uint32_t x1 = c ^ cp;
+  const uint32_t d2 = ((x1 | (x1 >> 16)) & 0xffffu) | sp | spm1;
+  return ff != 0 || (pack16(g) & d2) != 0;
+}
+
 __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
                                                    uint32_t wlo, uint32_t wn) {
   const int lane = threadIdx.x & 63;
@@ -1028,7 +1046,17 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   const uint32_t so = SMAX_LH + lane * 16;
   const uint4 v0 = *reinterpret_cast<const uint4 *>(&t.L[so]);
   const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
-  const uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+  uint32_t segpre_bits;
+  if (t.P != nullptr && !(a.dbg & 1u)) {
+    // packed windows: a segment is classified only if some row c can start
+    // a record -- LCP[c] >= min(minlen,128) with BWT[c-1] != BWT[c] (or a
+    // special symbol) -- or it holds a 255 byte (the rank prefix of the
+    // classification counts the 255 bytes of active segments only)
+    segpre_bits = (seg_can_start(t, v0, so, mf) ? 1u : 0u) |
+                  (seg_can_start(t, v1, so + 1024, mf) ? 2u : 0u);
+  } else {
+    segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+  }
   t.llv_base = wlo;
   // no .llv entry in the window: no 255 byte (in a consistent index; a
   // stray 255 still resolves exactly through the global .llv search)

@@ -16,7 +16,7 @@ text = G.synth_genome(kind, bases, 1 if kind != "uniform" else 42)
 esa = G.DeviceEsa(text)
 res = {v: [] for v in variants}
 base_env = dict(os.environ)
-for rnd in range(3):
+for rnd in range(int(os.environ.get("ROUNDS", "3"))):
     for v in variants:
         os.environ.clear()
         os.environ.update(base_env)
@@ -32,4 +32,4 @@ for rnd in range(3):
         res[v].append(ms / n)
         p.close()
 for v in variants:
-    print("%-40s K1 ms: min %.4f med %.4f" % (v or "(default)", min(res[v]), sorted(res[v])[1]), flush=True)
+    print("%-40s K1 ms: min %.4f med %.4f" % (v or "(default)", min(res[v]), sorted(res[v])[len(res[v]) // 2]), flush=True)
