@@ -36,6 +36,7 @@
 // No MFMA: integer/byte work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -51,6 +52,11 @@
 #define SMAX_RH 16                                    // right halo (bytes)
 #define SMAX_LDSB (SMAX_LH + SMAX_TILE + SMAX_RH)     // LDS window bytes
 #define SMAX_NCHUNK (SMAX_LDSB / 16)                  // 16-byte window chunks
+// tile slot formats: K1 writes packed 8-byte records (row + 1 in the tile:
+// 11 bits, width: 21 bits, lcp: 32 bits; wider records send the tile to
+// K1b), K1b writes GtSmaxRecord (16 bytes) and flags its tile count
+#define SMAX_PK_WMAX ((1u << 21) - 1)
+#define SMAX_SLOT_WIDE 0x80000000u
 #define SMAX_LLV_CAP 112                              // .llv values staged in K1's LDS (u16)
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
                                                       // records are >= 2 rows apart)
@@ -867,7 +873,7 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
 template <int DL>
 __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &a, uint64_t g0,
                                               const uint8_t *sL, uint32_t *ent,
-                                              GtSmaxRecord *wdst, uint32_t segpre) {
+                                              uint64_t *wdst, uint32_t segpre) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const bool all_exact = a.minlen > 128;
@@ -945,6 +951,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
   // exact evaluation of the queued starts (one per lane); accepted ones set
   // their row bit in their segment's mask
+  bool wide = false;
   if (nL != 0 && !(a.dbg & 4u)) {
     accw[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -960,10 +967,14 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         res_lcp[i] = cur;
         res_w[i] = (uint32_t) (j - (g0 + ro) + 2);
         if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
+        wide |= acc && j - (g0 + ro) + 2 > SMAX_PK_WMAX;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    // a record wider than the packed slot format holds: the tile goes to
+    // K1b (16-byte records)
+    if (__ballot(wide) != 0) return UINT32_MAX;
   }
   // records in row order, written by the owning lanes
   uint32_t wcount = 0;
@@ -982,19 +993,19 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     while (bits) {
       const int q = __builtin_ctz(bits);
       bits &= bits - 1;
-      GtSmaxRecord rec;
-      rec.lb = g0 + ro + q - 1;
+      // packed slot record: row in the tile + 1 (11 bits) | width (21) | lcp (32)
+      uint32_t lcp, width;
       if ((D >> q) & 1u) {
         const uint32_t b = sL[SMAX_LH + ro + q];
-        rec.lcp = b < 255 ? b
-                          : llv_by_rank(t, Rk + (uint32_t) __popc(Fk & ((1u << q) - 1)));
-        rec.width = 2 + ((W3 >> q) & 1u);
+        lcp = b < 255 ? b : llv_by_rank(t, Rk + (uint32_t) __popc(Fk & ((1u << q) - 1)));
+        width = 2 + ((W3 >> q) & 1u);
       } else {
         const uint32_t i = Lpre + (uint32_t) __popc(Lq & ((1u << q) - 1));
-        rec.lcp = res_lcp[i];
-        rec.width = res_w[i];
+        lcp = res_lcp[i];
+        width = res_w[i];
       }
-      if (!(a.dbg & 4096u)) wdst[pos] = rec;
+      if (!(a.dbg & 4096u))
+        wdst[pos] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
       pos++;
     }
     wcount += tot;
@@ -1159,7 +1170,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
 
     // ---- detection, diversity, records (row order)
-    GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
+    uint64_t *wdst = reinterpret_cast<uint64_t *>(a.slots + tile * (uint64_t) SMAX_WSLOT);
     uint32_t wcount = 0;
     // shard-edge tiles and windows with more .llv values than K1 stages
     // belong to the static K1b list (plan time, smax_static_defer_kernel;
@@ -1464,7 +1475,8 @@ smax_defer_kernel(SmaxScanArgs a) {
     }
     if (a.dbg & 32768u)   // diagnostic: per-tile cycles (/16), no counts
       wcount = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
-    if (lane == 0 && !(a.dbg & 4096u)) a.tile_count[tile] = wcount;
+    if (lane == 0 && !(a.dbg & 4096u))
+      a.tile_count[tile] = wcount | ((a.dbg & 32768u) ? 0u : SMAX_SLOT_WIDE);   // 16-byte records
     __builtin_amdgcn_wave_barrier();   // window reused by the next tile
   }
 }
@@ -1523,12 +1535,15 @@ smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, u
 __global__ void __launch_bounds__(256)
 smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
                     const uint64_t *slot_off, uint64_t nslots, GtSmaxRecord *out,
-                    uint64_t capacity, uint64_t *count) {
+                    uint64_t capacity, uint64_t *count, uint64_t g00) {
   __shared__ uint32_t sPre[SMAX_CPB + 1];
   __shared__ uint32_t sWave[4];
+  __shared__ uint8_t sWide[SMAX_CPB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t s0 = blockIdx.x * (uint64_t) SMAX_CPB;
-  const uint32_t c = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
+  const uint32_t cw = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
+  const uint32_t c = cw & ~SMAX_SLOT_WIDE;
+  sWide[tid] = (cw & SMAX_SLOT_WIDE) ? 1 : 0;
   const uint64_t base = slot_off[s0];
   uint32_t incl = c;
 #pragma unroll
@@ -1551,8 +1566,19 @@ smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
       const uint32_t mid = (lo + hi) >> 1;
       if (sPre[mid] <= r) lo = mid; else hi = mid;
     }
-    if (base + r < capacity)
-      out[base + r] = slots[(s0 + lo) * (uint64_t) SMAX_WSLOT + (r - sPre[lo])];
+    if (base + r >= capacity) continue;
+    const uint64_t tile = s0 + lo;
+    if (sWide[lo]) {
+      out[base + r] = slots[tile * (uint64_t) SMAX_WSLOT + (r - sPre[lo])];
+    } else {
+      const uint64_t v =
+          reinterpret_cast<const uint64_t *>(slots + tile * (uint64_t) SMAX_WSLOT)[r - sPre[lo]];
+      GtSmaxRecord rec;
+      rec.lb = g00 + tile * (uint64_t) SMAX_TILE + (v & 0x7ffu) - 1;   // g00: global row of tile 0
+      rec.width = (uint32_t) (v >> 11) & SMAX_PK_WMAX;
+      rec.lcp = (uint32_t) (v >> 32);
+      out[base + r] = rec;
+    }
   }
 }
 
@@ -1659,6 +1685,11 @@ static void seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
       goto fail;                                                             \
     }                                                                        \
   } while (0)
+
+// tile record count without the slot-format flag (scan input)
+struct SmaxSlotCount {
+  __host__ __device__ uint64_t operator()(uint32_t c) const { return c & ~SMAX_SLOT_WIDE; }
+};
 
 struct GtSmaxPlan {
   GtSmaxDevShard shard;
@@ -1827,7 +1858,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMalloc(&p->defer_list, sizeof (uint32_t) * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->defer_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
-  HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes, p->tile_count, p->tile_off,
+  HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes,
+                                 rocprim::make_transform_iterator(p->tile_count, SmaxSlotCount()),
+                                 p->tile_off,
                                  (uint64_t) 0, (size_t) p->num_tiles,
                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
   HIPCHK(hipMalloc(&p->scan_tmp, p->scan_tmp_bytes ? p->scan_tmp_bytes : 16));
@@ -1978,12 +2011,15 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
     HIPCHK(hipGetLastError());
     size_t bytes = p->scan_tmp_bytes;
-    HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->tile_count, p->tile_off,
+    HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes,
+                                   rocprim::make_transform_iterator(p->tile_count, SmaxSlotCount()),
+                                   p->tile_off,
                                    (uint64_t) 0, (size_t) p->num_tiles,
                                    rocprim::plus<uint64_t>(), s));
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->slots, p->tile_count, p->tile_off, (uint64_t) p->num_tiles,
-                       p->out, p->capacity, p->count);
+                       p->out, p->capacity, p->count,
+                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE);
     HIPCHK(hipGetLastError());
   }
   p->runs++;
@@ -2098,6 +2134,8 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
   if (counts && hipMemcpy(counts, p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
+  if (counts && !(p->dbg & 32768u))
+    for (uint64_t i = 0; i < p->num_tiles; i++) counts[i] &= ~SMAX_SLOT_WIDE;   // slot-format flag
   uint32_t n = 0;
   if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   if (ndeferred) *ndeferred = n;
