@@ -156,6 +156,12 @@ static int map_table(SmaxEsa *esa, int slot, const char *indexname,
 int smax_esa_open(SmaxEsa *esa, const char *indexname, int need_suftab,
                   int scanfile, char *errbuf, size_t errlen)
 {
+  return smax_esa_open_tables(esa, indexname, need_suftab, 1, scanfile, errbuf, errlen);
+}
+
+int smax_esa_open_tables(SmaxEsa *esa, const char *indexname, int need_suftab,
+                         int need_bwt, int scanfile, char *errbuf, size_t errlen)
+{
   const void *p;
   uint64_t bytes, n;
   memset(esa, 0, sizeof *esa);
@@ -165,9 +171,11 @@ int smax_esa_open(SmaxEsa *esa, const char *indexname, int need_suftab,
   if (map_table(esa, 0, indexname, ".lcp", n + 1, 1, 0, &p, &bytes, errbuf, errlen))
     goto fail;
   esa->lcptab = p;
-  if (map_table(esa, 1, indexname, ".bwt", n + 1, 1, 0, &p, &bytes, errbuf, errlen))
-    goto fail;
-  esa->bwttab = p;
+  if (need_bwt) {
+    if (map_table(esa, 1, indexname, ".bwt", n + 1, 1, 0, &p, &bytes, errbuf, errlen))
+      goto fail;
+    esa->bwttab = p;
+  }
   if (map_table(esa, 2, indexname, ".llv", 0, 0, 1, &p, &bytes, errbuf, errlen))
     goto fail;
   if (bytes % sizeof (GtSmaxLlv) != 0) {

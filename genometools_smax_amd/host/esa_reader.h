@@ -36,6 +36,9 @@ typedef struct {
 /* 0 on success, -1 with a gt-style message in errbuf. */
 int smax_esa_open(SmaxEsa *esa, const char *indexname, int need_suftab,
                   int scanfile, char *errbuf, size_t errlen);
+/* Same, with the .bwt table optional (need_bwt == 0: esa->bwttab NULL). */
+int smax_esa_open_tables(SmaxEsa *esa, const char *indexname, int need_suftab,
+                         int need_bwt, int scanfile, char *errbuf, size_t errlen);
 void smax_esa_close(SmaxEsa *esa);
 uint64_t smax_esa_suffix(const SmaxEsa *esa, uint64_t idx);
 void smax_esa_input(const SmaxEsa *esa, GtSmaxInput *in);

@@ -80,3 +80,32 @@ def test_cli_errors(tmp_path):
     idx = _index(tmp_path, "Atinsert.fna", 4)
     r = subprocess.run([CLI, "-smax", "-ii", idx], capture_output=True, text=True)
     assert r.returncode == 1 and "number of mapped units" in r.stderr
+
+
+SFXMAP = os.path.join(G.BIN_DIR, "gt-sfxmap")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fasta", ["Atinsert.fna", "at1MB"])
+def test_sfxmap_enumlcpitvtree_bu(tmp_path, fasta):
+    # `gt dev sfxmap -enumlcpitvtreeBU -esa IDX`: the lcpitvs visitor's
+    # L/B lines (src/match/esa_lcpintervals_visitor.c:30-61), in the order of
+    # gt_esa_bottomup, from the GPU tree
+    idx = _index(tmp_path, fasta)
+    out = subprocess.run([SFXMAP, "-enumlcpitvtreeBU", "-esa", idx], check=True,
+                         capture_output=True, text=True).stdout.splitlines()
+    ev = O.bottomup_events(oracle_esa(fasta))
+    want = []
+    for r in ev:
+        if r[0] == 0:
+            want.append("L %d %d %d %d" % (r[1], r[2], r[3], r[4]))
+        elif r[0] == 1:
+            want.append("B %d %d %d %d %d" % (r[1], r[2], r[3], r[4], r[5]))
+    assert out == want
+
+
+def test_sfxmap_errors():
+    r = subprocess.run([SFXMAP, "-esa", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "gt sfxmap: error:" in r.stderr
+    r = subprocess.run([SFXMAP, "-enumlcpitvtreeBU"], capture_output=True, text=True)
+    assert r.returncode == 1 and "mandatory" in r.stderr
