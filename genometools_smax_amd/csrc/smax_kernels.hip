@@ -1038,8 +1038,9 @@ __device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint3
                                               uint32_t mf) {
   const uint32_t g[4] = {bytes_ge(v.x, mf), bytes_ge(v.y, mf), bytes_ge(v.z, mf),
                          bytes_ge(v.w, mf)};
-  if ((g[0] | g[1] | g[2] | g[3]) == 0) return false;
-  const uint32_t ff = bytes_ff(v.x) | bytes_ff(v.y) | bytes_ff(v.z) | bytes_ff(v.w);
+  // any 0xff byte: a zero byte of ~w (exact as an any-test)
+  const uint32_t ff = ((0xfefefefeu - v.x) & v.x) | ((0xfefefefeu - v.y) & v.y) |
+                      ((0xfefefefeu - v.z) & v.z) | ((0xfefefefeu - v.w) & v.w);
   const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1];
   const uint32_t c = (uint32_t) w, pc = (uint32_t) pw;
   const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
@@ -1047,7 +1048,7 @@ __device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint3
   const uint32_t cp = ((c << 1) & 0xfffefffeu) | ((pc >> 15) & 0x00010001u);
   const uint32_t x1 = c ^ cp;
   const uint32_t d2 = ((x1 | (x1 >> 16)) & 0xffffu) | sp | spm1;
-  return ff != 0 || (pack16(g) & d2) != 0;
+  return (ff & 0x80808080u) != 0 || (pack16(g) & d2) != 0;
 }
 
 __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
@@ -1057,16 +1058,16 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   const uint32_t so = SMAX_LH + lane * 16;
   const uint4 v0 = *reinterpret_cast<const uint4 *>(&t.L[so]);
   const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
-  uint32_t segpre_bits;
-  if (t.P != nullptr && !(a.dbg & 1u)) {
-    // packed windows: a segment is classified only if some row c can start
-    // a record -- LCP[c] >= min(minlen,128) with BWT[c-1] != BWT[c] (or a
-    // special symbol) -- or it holds a 255 byte (the rank prefix of the
+  uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+  if (t.P != nullptr && !(a.dbg & 1u) &&
+      __popcll(__ballot(segpre_bits & 1u)) + __popcll(__ballot(segpre_bits & 2u)) > 64) {
+    // more active segments than one classification step holds (packed
+    // windows): keep only segments where some row c can start a record --
+    // LCP[c] >= min(minlen,128) with BWT[c-1] != BWT[c] (or a special
+    // symbol) -- or that hold a 255 byte (the rank prefix of the
     // classification counts the 255 bytes of active segments only)
-    segpre_bits = (seg_can_start(t, v0, so, mf) ? 1u : 0u) |
-                  (seg_can_start(t, v1, so + 1024, mf) ? 2u : 0u);
-  } else {
-    segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
+    if ((segpre_bits & 1u) && !seg_can_start(t, v0, so, mf)) segpre_bits &= ~1u;
+    if ((segpre_bits & 2u) && !seg_can_start(t, v1, so + 1024, mf)) segpre_bits &= ~2u;
   }
   t.llv_base = wlo;
   // no .llv entry in the window: no 255 byte (in a consistent index; a
