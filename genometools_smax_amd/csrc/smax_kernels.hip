@@ -35,8 +35,6 @@
 //            the tile's slot (or the overflow area) -- K2/K3 place them.
 // No MFMA: integer/byte work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -56,6 +54,7 @@
 // 11 bits, width: 21 bits, lcp: 32 bits; wider records send the tile to
 // K1b), K1b writes GtSmaxRecord (16 bytes) and flags its tile count
 #define SMAX_PK_WMAX ((1u << 21) - 1)
+#define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
 #define SMAX_SLOT_WIDE 0x80000000u
 #define SMAX_LLV_CAP 112                              // .llv values staged in K1's LDS (u16)
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
@@ -82,6 +81,7 @@ struct SmaxScanArgs {
   uint32_t num_tiles;
   GtSmaxRecord *slots;       // [tile][wave][SMAX_WSLOT] records, row order
   uint32_t *tile_count;      // [tile][wave] record counts
+  uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), zeroed by K0
   GtSmaxBoundary *bnd;
   uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
   uint32_t *defer_count;     // reset by K0
@@ -360,8 +360,11 @@ __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, 
 // K0: per-run resets ahead of K1 (the pending-plateau slot, which any K1 or
 // K1b wave may fill, and K1's deferral count); for an empty shard (begin ==
 // end) also the boundary head, otherwise computed by K1b.
-__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a, int with_head) {
-  if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(256) smax_head_kernel(SmaxScanArgs a, int with_head,
+                                                        uint32_t nblock) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nblock) a.block_sum[i] = 0;
+  if (i != 0) return;
   a.bnd->pend_valid = 0;
   if (!(a.dbg & 16384u)) *a.defer_count = 0;   // diagnostic: K1b alone on K1's last list
   if (with_head) compute_head(a);
@@ -1185,7 +1188,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     }
     if (lane == 0 && !stat) {
       if (defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
-      else if (!(a.dbg & 4096u)) a.tile_count[tile] = wcount;
+      else if (!(a.dbg & 4096u)) {
+        a.tile_count[tile] = wcount;
+        if (wcount) atomicAdd(&a.block_sum[tile / SMAX_CPB], wcount);
+      }
     }
 
     tile = next;
@@ -1476,8 +1482,10 @@ smax_defer_kernel(SmaxScanArgs a) {
     }
     if (a.dbg & 32768u)   // diagnostic: per-tile cycles (/16), no counts
       wcount = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
-    if (lane == 0 && !(a.dbg & 4096u))
+    if (lane == 0 && !(a.dbg & 4096u)) {
       a.tile_count[tile] = wcount | ((a.dbg & 32768u) ? 0u : SMAX_SLOT_WIDE);   // 16-byte records
+      if (wcount && !(a.dbg & 32768u)) atomicAdd(&a.block_sum[tile / SMAX_CPB], wcount);
+    }
     __builtin_amdgcn_wave_barrier();   // window reused by the next tile
   }
 }
@@ -1532,20 +1540,26 @@ smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, u
 // positions (slot found by binary search in the LDS prefix), consecutive
 // threads on consecutive output records -> ascending lb overall, coalesced.
 // Also publishes the total.
-#define SMAX_CPB 256
 __global__ void __launch_bounds__(256)
 smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
-                    const uint64_t *slot_off, uint64_t nslots, GtSmaxRecord *out,
+                    const uint32_t *block_sum, uint64_t nslots, GtSmaxRecord *out,
                     uint64_t capacity, uint64_t *count, uint64_t g00) {
   __shared__ uint32_t sPre[SMAX_CPB + 1];
   __shared__ uint32_t sWave[4];
   __shared__ uint8_t sWide[SMAX_CPB];
+  __shared__ uint64_t sRed[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t s0 = blockIdx.x * (uint64_t) SMAX_CPB;
+  // this workgroup's output offset: the record counts of all earlier
+  // workgroups (summed per SMAX_CPB tiles by K1 / K1b)
+  uint64_t bs = 0;
+  for (uint32_t b = tid; b < blockIdx.x; b += 256) bs += block_sum[b];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
+  if (lane == 0) sRed[wave] = bs;
   const uint32_t cw = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
   const uint32_t c = cw & ~SMAX_SLOT_WIDE;
   sWide[tid] = (cw & SMAX_SLOT_WIDE) ? 1 : 0;
-  const uint64_t base = slot_off[s0];
   uint32_t incl = c;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -1560,6 +1574,7 @@ smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
   if (tid == 0) sPre[0] = 0;
   __syncthreads();
   const uint32_t total = sPre[SMAX_CPB];
+  const uint64_t base = sRed[0] + sRed[1] + sRed[2] + sRed[3];
   if (tid == 0 && s0 + SMAX_CPB >= nslots) *count = base + total;
   for (uint32_t r = tid; r < total; r += 256) {
     uint32_t lo = 0, hi = SMAX_CPB;          // largest j with sPre[j] <= r
@@ -1687,11 +1702,6 @@ static void seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
     }                                                                        \
   } while (0)
 
-// tile record count without the slot-format flag (scan input)
-struct SmaxSlotCount {
-  __host__ __device__ uint64_t operator()(uint32_t c) const { return c & ~SMAX_SLOT_WIDE; }
-};
-
 struct GtSmaxPlan {
   GtSmaxDevShard shard;
   unsigned int minlen;
@@ -1702,7 +1712,7 @@ struct GtSmaxPlan {
   GtSmaxRecord *out;         // capacity records, ascending lb
   GtSmaxRecord *slots;       // num_tiles * SMAX_WSLOT
   uint32_t *tile_count;      // num_tiles
-  uint64_t *tile_off;        // num_tiles
+  uint32_t *block_sum;       // compact_grid record sums (K1/K1b atomics, K3 offsets)
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
@@ -1717,8 +1727,6 @@ struct GtSmaxPlan {
   hipStream_t side;          // K1b over the static list runs here, concurrent with K1
   hipEvent_t fork, join;
   uint32_t *err;
-  void *scan_tmp;
-  size_t scan_tmp_bytes;
   uint32_t dbg;
   // optional K1 timing: event pairs recorded around the scan kernel
   hipEvent_t *ev;
@@ -1846,7 +1854,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
 
-  HIPCHK(hipMalloc(&p->tile_off, sizeof (uint64_t) * (uint64_t) p->num_tiles));
+  HIPCHK(hipMalloc(&p->block_sum, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
+  HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
   HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
   HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
@@ -1859,12 +1868,6 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMalloc(&p->defer_list, sizeof (uint32_t) * (uint64_t) p->num_tiles));
   HIPCHK(hipMalloc(&p->defer_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
-  HIPCHK(rocprim::exclusive_scan(nullptr, p->scan_tmp_bytes,
-                                 rocprim::make_transform_iterator(p->tile_count, SmaxSlotCount()),
-                                 p->tile_off,
-                                 (uint64_t) 0, (size_t) p->num_tiles,
-                                 rocprim::plus<uint64_t>(), (hipStream_t) 0));
-  HIPCHK(hipMalloc(&p->scan_tmp, p->scan_tmp_bytes ? p->scan_tmp_bytes : 16));
   HIPCHK(hipMalloc(&derr, sizeof (uint32_t)));
   HIPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
   if (shard->numllv > 0xffffffffull) {
@@ -1918,8 +1921,8 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->tile_count, p->tile_off, p->count, p->bnd,
-                  p->llv_win, p->err, p->scan_tmp, p->bwtpk, p->llv16, p->defer_list,
+  void *bufs[] = {p->out, p->slots, p->tile_count, p->block_sum, p->count, p->bnd,
+                  p->llv_win, p->err, p->bwtpk, p->llv16, p->defer_list,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
     (void) hipStreamSynchronize(p->side);
@@ -1954,6 +1957,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.num_tiles = p->num_tiles;
   a.slots = p->slots;
   a.tile_count = p->tile_count;
+  a.block_sum = p->block_sum;
   a.bnd = p->bnd;
   a.defer_list = p->defer_list;
   a.defer_count = p->defer_count;
@@ -1970,7 +1974,8 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
   {
     SmaxScanArgs a = plan_args(p);
     const int empty = p->shard.begin >= p->shard.end;
-    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a, empty);
+    hipLaunchKernelGGL(smax_head_kernel, dim3((p->compact_grid + 255) / 256 + 1), dim3(256), 0, s,
+                       a, empty, p->compact_grid);
     HIPCHK(hipGetLastError());
     if (empty) {
       HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
@@ -2011,14 +2016,8 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     HIPCHK(hipStreamWaitEvent(s, p->join, 0));
     hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
     HIPCHK(hipGetLastError());
-    size_t bytes = p->scan_tmp_bytes;
-    HIPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes,
-                                   rocprim::make_transform_iterator(p->tile_count, SmaxSlotCount()),
-                                   p->tile_off,
-                                   (uint64_t) 0, (size_t) p->num_tiles,
-                                   rocprim::plus<uint64_t>(), s));
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->slots, p->tile_count, p->tile_off, (uint64_t) p->num_tiles,
+                       p->slots, p->tile_count, p->block_sum, (uint64_t) p->num_tiles,
                        p->out, p->capacity, p->count,
                        p->shard.base + p->tile_first * (uint64_t) SMAX_TILE);
     HIPCHK(hipGetLastError());
