@@ -1,6 +1,5 @@
 set -e
 R=$GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $R/gpurun_out/gpu_tests.log 2>&1
-timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-end-to-end > $R/gpurun_out/bench.json 2> $R/gpurun_out/bench.err
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/prof_nt -o p -- python3 $R/tools/k1_once.py human 3e9 6 > $R/gpurun_out/once.log 2>&1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $R/gpurun_out/smoke.log 2>&1
+timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 2 --dist-backend gloo --one-gpu > $R/gpurun_out/bench_2r.json 2> $R/gpurun_out/bench_2r.err
+timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 3 --steps 5 --warmup 1 --dist-backend gloo --one-gpu --config c2 > $R/gpurun_out/bench_3r.json 2> $R/gpurun_out/bench_3r.err
