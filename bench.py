@@ -60,6 +60,8 @@ def main():
                     help="skip the host-tables (PCIe-inclusive) leg")
     ap.add_argument("--cpu-sample", type=int, default=3_200_000_000,
                     help="max suffix rows timed on the CPU")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads for the all-core CPU figure (the GPU box's CPU share is 16)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: stage the boundary records through host memory (multi-rank "
                          "rehearsal on one GPU; the measured configuration is nccl = RCCL)")
@@ -214,6 +216,22 @@ def main():
         cpu = {"value": sample / t_cpu, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
                "sample": "oracle orc_linsmax (single core, -O3) over suffix rows [0,%d) of the same "
                          "tables: %.2fs" % (sample, t_cpu)}
+        # all-core figure beside the single-core headline:
+        # orc_linsmax_mt, row ranges per pthread, same output
+        threads = min(len(os.sched_getaffinity(0)), args.cpu_threads)
+        if threads > 1:
+            t0 = time.perf_counter()
+            res_mt = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample,
+                                        minlen, threads=threads)
+            t_mt = time.perf_counter() - t0
+            if len(res_mt) != len(res):
+                log("WARNING: all-core CPU scan %d intervals != single-core %d"
+                    % (len(res_mt), len(res)))
+            cpu["all_cores"] = {"value": sample / t_mt, "cores": threads, "seconds": round(t_mt, 3),
+                                "sample": "orc_linsmax_mt (pthreads, equal row ranges) over the "
+                                          "same rows"}
+            del res_mt
+        del res
 
     # end-to-end through the drop-in boundary (host tables in memory -> H2D
     # -> plan -> K0..K3 -> D2H of the (lcp, lb, rb) list): reported beside

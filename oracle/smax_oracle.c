@@ -32,6 +32,7 @@
  *                           (src/tools/gt_repfind.c:49-84,
  *                           src/match/querymatch.c:130-190).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -88,11 +89,30 @@ static int leftdiverse(const uint8_t *bwt, uint64_t lb, uint64_t rb)
 /* L[k] = lcp(S[k-1],S[k]) for 1<=k<=N-1, L[0]=L[N]=0.
  * out: triples (lcp, lb, rb) in ascending lb, at most cap of them; returns the
  * total number found (may exceed cap). */
-uint64_t orc_linsmax(const uint8_t *lcpbytes, const OrcLlv *llv,
-                     uint64_t numllv, const uint8_t *bwt, uint64_t nonspecials,
-                     uint64_t minlen, uint64_t *out, uint64_t cap)
+/* Scan of the plateaus whose first row k (= lb+1) lies in [kbeg, kend);
+ * a plateau starting before kend is followed past it.  prev must be L[kbeg-1]
+ * and li any .llv index not beyond the first entry at position >= kbeg. */
+typedef struct { uint64_t *buf, n, cap; int grow; } OrcOut;
+
+static void orc_out_put(OrcOut *o, uint64_t l, uint64_t lb, uint64_t rb)
 {
-  uint64_t N = nonspecials, k, li = 0, found = 0, prev = 0;
+  if (o->n >= o->cap) {
+    if (!o->grow) { o->n++; return; }
+    o->cap = o->cap ? 2 * o->cap : 4096;
+    o->buf = realloc(o->buf, 3 * sizeof (uint64_t) * o->cap);
+  }
+  o->buf[3 * o->n] = l;
+  o->buf[3 * o->n + 1] = lb;
+  o->buf[3 * o->n + 2] = rb;
+  o->n++;
+}
+
+static void orc_linsmax_range(const uint8_t *lcpbytes, const OrcLlv *llv,
+                              uint64_t numllv, const uint8_t *bwt, uint64_t N,
+                              uint64_t minlen, uint64_t kbeg, uint64_t kend,
+                              uint64_t prev, uint64_t li, OrcOut *o)
+{
+  uint64_t k;
 #define ORC_L(IDX, VAR)                                                       \
   do {                                                                        \
     uint64_t ix_ = (IDX);                                                     \
@@ -101,9 +121,8 @@ uint64_t orc_linsmax(const uint8_t *lcpbytes, const OrcLlv *llv,
     else { while (li < numllv && llv[li].position < ix_) li++;                \
            VAR = llv[li].value; }                                             \
   } while (0)
-  if (N < 2) return 0;
-  k = 1;
-  while (k <= N - 1) {
+  k = kbeg;
+  while (k < kend) {
     uint64_t l, j, next;
     ORC_L(k, l);
     if (l > prev && l >= minlen) {
@@ -114,14 +133,8 @@ uint64_t orc_linsmax(const uint8_t *lcpbytes, const OrcLlv *llv,
         if (next != l) break;
         j++;
       }
-      if (next < l && leftdiverse(bwt, k - 1, j)) {
-        if (found < cap) {
-          out[3 * found] = l;
-          out[3 * found + 1] = k - 1;
-          out[3 * found + 2] = j;
-        }
-        found++;
-      }
+      if (next < l && leftdiverse(bwt, k - 1, j))
+        orc_out_put(o, l, k - 1, j);
       /* position j+1 starts a new comparison against L[j] == l */
       prev = l;
       k = j + 1;
@@ -131,7 +144,91 @@ uint64_t orc_linsmax(const uint8_t *lcpbytes, const OrcLlv *llv,
     k++;
   }
 #undef ORC_L
-  return found;
+}
+
+/* L[k] = lcp(S[k-1],S[k]) for 1<=k<=N-1, L[0]=L[N]=0.
+ * out: triples (lcp, lb, rb) in ascending lb, at most cap of them; returns the
+ * total number found (may exceed cap). */
+uint64_t orc_linsmax(const uint8_t *lcpbytes, const OrcLlv *llv,
+                     uint64_t numllv, const uint8_t *bwt, uint64_t nonspecials,
+                     uint64_t minlen, uint64_t *out, uint64_t cap)
+{
+  OrcOut o = {out, 0, cap, 0};
+  if (nonspecials < 2) return 0;
+  orc_linsmax_range(lcpbytes, llv, numllv, bwt, nonspecials, minlen,
+                    1, nonspecials, 0, 0, &o);
+  return o.n;
+}
+
+/* All-core form of orc_linsmax (the CPU baseline's multi-thread figure,
+ * SURVEY.md §8(d)): rows split in equal ranges, one pthread each; a plateau
+ * belongs to the range holding its first row (the GPU's shard rule) and is
+ * followed past the range end.  Output identical to orc_linsmax. */
+typedef struct {
+  const uint8_t *lcpbytes, *bwt; const OrcLlv *llv;
+  uint64_t numllv, N, minlen, kbeg, kend;
+  OrcOut o;
+} OrcTask;
+
+static uint64_t orc_llv_lower(const OrcLlv *llv, uint64_t numllv, uint64_t pos)
+{
+  uint64_t lo = 0, hi = numllv;
+  while (lo < hi) {
+    uint64_t mid = lo + (hi - lo) / 2;
+    if (llv[mid].position < pos) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+static void *orc_linsmax_task(void *arg)
+{
+  OrcTask *t = arg;
+  uint64_t prev = 0, li = orc_llv_lower(t->llv, t->numllv, t->kbeg - 1);
+  if (t->kbeg > 1 && t->kbeg - 1 < t->N) {
+    uint8_t b = t->lcpbytes[t->kbeg - 1];
+    prev = b < 255 ? b : t->llv[li].value;
+  }
+  orc_linsmax_range(t->lcpbytes, t->llv, t->numllv, t->bwt, t->N, t->minlen,
+                    t->kbeg, t->kend, prev, li, &t->o);
+  return NULL;
+}
+
+uint64_t orc_linsmax_mt(const uint8_t *lcpbytes, const OrcLlv *llv,
+                        uint64_t numllv, const uint8_t *bwt, uint64_t nonspecials,
+                        uint64_t minlen, uint64_t *out, uint64_t cap, int threads)
+{
+  OrcTask *t;
+  pthread_t *tid;
+  uint64_t N = nonspecials, total = 0, w = 0;
+  int i;
+  if (N < 2) return 0;
+  if (threads < 1) threads = 1;
+  t = calloc((size_t) threads, sizeof *t);
+  tid = calloc((size_t) threads, sizeof *tid);
+  for (i = 0; i < threads; i++) {
+    t[i].lcpbytes = lcpbytes; t[i].bwt = bwt; t[i].llv = llv;
+    t[i].numllv = numllv; t[i].N = N; t[i].minlen = minlen;
+    t[i].kbeg = 1 + (N - 1) * (uint64_t) i / (uint64_t) threads;
+    t[i].kend = 1 + (N - 1) * (uint64_t) (i + 1) / (uint64_t) threads;
+    t[i].o.grow = 1;
+    pthread_create(&tid[i], NULL, orc_linsmax_task, &t[i]);
+  }
+  for (i = 0; i < threads; i++) {
+    pthread_join(tid[i], NULL);
+    total += t[i].o.n;
+  }
+  for (i = 0; i < threads; i++) {
+    uint64_t m = t[i].o.n;
+    if (w < cap) {
+      uint64_t c = m < cap - w ? m : cap - w;
+      memcpy(out + 3 * w, t[i].o.buf, 3 * sizeof (uint64_t) * c);
+    }
+    w += m;
+    free(t[i].o.buf);
+  }
+  free(t);
+  free(tid);
+  return total;
 }
 
 /* --------------------------------------------- 2. bottom-up smax visitor */

@@ -31,6 +31,8 @@ def lib():
         L.orc_linsmax.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint64, _u8p, ctypes.c_uint64,
                                   ctypes.c_uint64, _u64p, ctypes.c_uint64]
         L.orc_linsmax.restype = ctypes.c_uint64
+        L.orc_linsmax_mt.argtypes = L.orc_linsmax.argtypes + [ctypes.c_int]
+        L.orc_linsmax_mt.restype = ctypes.c_uint64
         L.orc_bottomup_smax.argtypes = [_u64p, _u64p, _u8p, ctypes.c_uint64, ctypes.c_uint64,
                                         _u64p, ctypes.c_uint64]
         L.orc_bottomup_smax.restype = ctypes.c_uint64
@@ -105,12 +107,17 @@ def _triples(out, found):
     return out[: 3 * found].reshape(-1, 3).copy()
 
 
-def linsmax(lcpbytes, llv, bwt, nonspecials, minlen):
+def linsmax(lcpbytes, llv, bwt, nonspecials, minlen, threads=1):
+    """orc_linsmax; threads > 1 runs orc_linsmax_mt (same output, pthreads)."""
     llv = np.ascontiguousarray(llv, dtype=np.uint64).reshape(-1, 2)
     cap = max(16, nonspecials // 2 + 1)
     out = np.empty(3 * cap, dtype=np.uint64)
-    found = lib().orc_linsmax(_p(lcpbytes, _u8p), llv.ctypes.data_as(ctypes.c_void_p), len(llv),
-                              _p(bwt, _u8p), nonspecials, minlen, _p(out, _u64p), cap)
+    args = (_p(lcpbytes, _u8p), llv.ctypes.data_as(ctypes.c_void_p), len(llv),
+            _p(bwt, _u8p), nonspecials, minlen, _p(out, _u64p), cap)
+    if threads > 1:
+        found = lib().orc_linsmax_mt(*args, threads)
+    else:
+        found = lib().orc_linsmax(*args)
     assert found <= cap
     return _triples(out, found)
 

@@ -97,6 +97,23 @@ def test_linsmax_equals_bottomup_at1mb(minlen):
     assert np.array_equal(a, b)
 
 
+
+@pytest.mark.parametrize("threads", [2, 3, 7, 64])
+def test_linsmax_all_core_equals_single(threads):
+    """orc_linsmax_mt (bench's all-core CPU figure) == orc_linsmax, incl. ranges
+    that cut plateaus and .llv runs (tandem text: long plateaus, many .llv)."""
+    for name, minlen in (("at1MB", 20), ("at1MB", 256), ("Atinsert.fna", 1)):
+        e = oracle_esa(name)
+        a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        b = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen, threads=threads)
+        assert np.array_equal(a, b)
+    t = np.tile(np.array([0, 1, 2, 0, 3], np.uint8), 400)
+    e = O.Esa(t)
+    for minlen in (1, 300):
+        a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        b = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen, threads=threads)
+        assert np.array_equal(a, b)
+
 def _random_text(rng, n, sigma=4, pspecial=0.02):
     t = rng.integers(0, sigma, n, dtype=np.uint8)
     sp = rng.random(n) < pspecial

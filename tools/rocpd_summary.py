@@ -23,7 +23,7 @@ def stats(db, out):
                        "from top_kernels").fetchall()
     with open(out, "w", newline="") as fh:
         w = csv.writer(fh)
-        w.writerow(["kernel", "calls", "total_ns", "average_ns", "percent"])
+        w.writerow(["kernel", "calls", "total_us", "average_us", "percent"])
         for name, calls, tot, avg, pct in rows:
             short = name.replace("(anonymous namespace)::", "")
             if "rocprim" in short:
