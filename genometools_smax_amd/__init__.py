@@ -328,10 +328,22 @@ def enumerate_smax(lcptab, llvtab, bwttab, totallength, nonspecials, minlen, num
         if out.value:
             lib().gt_smax_free(out)
         return np.zeros((0, 3), dtype=np.uint64)
-    buf = (ctypes.c_uint64 * (3 * n)).from_address(out.value)
-    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).copy()
-    lib().gt_smax_free(out)
-    return arr
+    return np.asarray(_OwnedTriples(out.value, n))
+
+
+class _OwnedTriples:
+    """The C layer's malloc'd (k,3) uint64 triples exposed to numpy without a
+    copy; freed (gt_smax_free) when the last array view goes away."""
+
+    def __init__(self, ptr, k):
+        self._ptr = ptr
+        self.__array_interface__ = {"shape": (k, 3), "typestr": "<u8",
+                                    "data": (ptr, False), "version": 3}
+
+    def __del__(self):
+        if self._ptr:
+            lib().gt_smax_free(ctypes.c_void_p(self._ptr))
+            self._ptr = None
 
 
 def enumerate_maxpairs(lcptab, llvtab, bwttab, suftab, totallength, nonspecials, minlen):

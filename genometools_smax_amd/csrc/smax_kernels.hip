@@ -40,6 +40,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+
 #include "gt_smax_hip.h"
 
 #define SMAX_THREADS 256                              // 4 independent waves per workgroup
@@ -2162,6 +2168,19 @@ struct ShardRun {
   hipStream_t stream;
 };
 
+// Host work over [0, n) split in equal ranges, f(lo, hi) on up to 8 threads
+// (the inputs are host tables of up to ~10^10 rows).
+template <typename F>
+static void host_parallel_for(uint64_t n, F f) {
+  const unsigned nt = n < (1u << 16) ? 1u
+      : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; t++)
+    th.emplace_back([=] { f(n * t / nt, n * (t + 1) / nt); });
+  f(0, n / nt);
+  for (auto &x : th) x.join();
+}
+
 static int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
   if (in == NULL || in->lcptab == NULL || in->bwttab == NULL) {
     seterr(errbuf, errlen, "missing lcptab or bwttab");
@@ -2176,15 +2195,124 @@ static int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
            (unsigned long) in->nonspecials, (unsigned long) in->totallength);
     return -1;
   }
-  for (uint64_t i = 0; i < in->numllv; i++) {
-    if (in->llvtab[i].position > in->totallength ||
-        (i > 0 && in->llvtab[i].position <= in->llvtab[i - 1].position) ||
-        in->lcptab[in->llvtab[i].position] != 255) {
-      seterr(errbuf, errlen, "inconsistent .llv entry %lu", (unsigned long) i);
-      return -1;
+  std::vector<uint64_t> bad(8, UINT64_MAX);
+  std::atomic<unsigned> slot{0};
+  host_parallel_for(in->numllv, [&, in](uint64_t lo, uint64_t hi) {
+    uint64_t first = UINT64_MAX;
+    for (uint64_t i = lo; i < hi; i++) {
+      if (in->llvtab[i].position > in->totallength ||
+          (i > 0 && in->llvtab[i].position <= in->llvtab[i - 1].position) ||
+          in->lcptab[in->llvtab[i].position] != 255) {
+        first = i;
+        break;
+      }
     }
+    bad[slot.fetch_add(1) & 7] = first;
+  });
+  uint64_t first = *std::min_element(bad.begin(), bad.end());
+  if (first != UINT64_MAX) {
+    seterr(errbuf, errlen, "inconsistent .llv entry %lu", (unsigned long) first);
+    return -1;
   }
   return 0;
+}
+
+// Pageable host -> device through two pinned staging buffers: host threads
+// fill one while the DMA engine drains the other.  A plain hipMemcpyAsync
+// from pageable memory goes through the runtime's small staging buffer,
+// one chunk at a time, far below the link rate.  Returns after the copy.
+static hipError_t h2d_staged(void *dst, const void *src, uint64_t len, hipStream_t s) {
+  const uint64_t CH = 64ull << 20;
+  if (len < (16ull << 20)) {
+    hipError_t e = hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, s);
+    return e == hipSuccess ? hipStreamSynchronize(s) : e;
+  }
+  void *buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < 2 && e == hipSuccess; i++) {
+    e = hipHostMalloc(&buf[i], CH, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+  }
+  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += CH, k++) {
+    const int b = (int) (k & 1);
+    const uint64_t c = std::min(CH, len - off);
+    if (k >= 2 && (e = hipEventSynchronize(ev[b])) != hipSuccess) break;
+    const char *from = (const char *) src + off;
+    char *to = (char *) buf[b];
+    const uint64_t part = (c + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt && t * part < c; t++)
+      th.emplace_back([=] { memcpy(to + t * part, from + t * part, std::min(part, c - t * part)); });
+    memcpy(to, from, std::min(part, c));
+    for (auto &x : th) x.join();
+    e = hipMemcpyAsync((char *) dst + off, to, c, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(ev[b], s);
+  }
+  hipError_t e2 = hipStreamSynchronize(s);   // drain before the buffers go
+  if (e == hipSuccess) e = e2;
+  for (int i = 0; i < 2; i++) {
+    if (ev[i]) (void) hipEventDestroy(ev[i]);
+    if (buf[i]) (void) hipHostFree(buf[i]);
+  }
+  return e;
+}
+
+// GT_SMAX_TIMING=1: phase times of the host-table entry points on stderr.
+static double phase_clock() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static void phase_mark(const char *what, double *t) {
+  static int on = -1;
+  if (on < 0) on = getenv("GT_SMAX_TIMING") != NULL;
+  double now = phase_clock();
+  if (on) fprintf(stderr, "[gt_smax timing] %-10s %8.2f ms\n", what, (now - *t) * 1e3);
+  *t = now;
+}
+
+// Device records -> host (lcp, lb, rb) triples through two pinned chunks:
+// the DMA of chunk k+1 overlaps the threaded conversion of chunk k (which
+// also takes the first-touch faults of dst in parallel).
+static hipError_t d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt,
+                              hipStream_t s) {
+  const uint64_t CH = 4ull << 20;   // records per chunk (64 MiB)
+  void *buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  const uint64_t nch = (cnt + CH - 1) / CH;
+  for (int i = 0; i < 2 && i < (int) nch && e == hipSuccess; i++) {
+    e = hipHostMalloc(&buf[i], sizeof (GtSmaxRecord) * std::min(CH, cnt), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+  }
+  auto issue = [&](uint64_t j) {
+    const uint64_t c = std::min(CH, cnt - j * CH);
+    hipError_t r = hipMemcpyAsync(buf[j & 1], dev + j * CH, sizeof (GtSmaxRecord) * c,
+                                  hipMemcpyDeviceToHost, s);
+    return r == hipSuccess ? hipEventRecord(ev[j & 1], s) : r;
+  };
+  if (e == hipSuccess && nch > 0) e = issue(0);
+  for (uint64_t k = 0; e == hipSuccess && k < nch; k++) {
+    // chunk k+1 reuses the buffer of chunk k-1, whose conversion is done
+    if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
+    if ((e = hipEventSynchronize(ev[k & 1])) != hipSuccess) break;
+    const GtSmaxRecord *h = (const GtSmaxRecord *) buf[k & 1];
+    uint64_t *t0 = dst + 3 * k * CH;
+    host_parallel_for(std::min(CH, cnt - k * CH), [=](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; i++) {
+        t0[3 * i] = h[i].lcp;
+        t0[3 * i + 1] = h[i].lb;
+        t0[3 * i + 2] = h[i].lb + h[i].width - 1;
+      }
+    });
+  }
+  hipError_t e2 = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = e2;
+  for (int i = 0; i < 2; i++) {
+    if (ev[i]) (void) hipEventDestroy(ev[i]);
+    if (buf[i]) (void) hipHostFree(buf[i]);
+  }
+  return e;
 }
 
 static uint64_t llv_lower(const GtSmaxInput *in, uint64_t g) {
@@ -2217,6 +2345,7 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
   }
   if (nshards < 1) nshards = 1;
   if ((uint64_t) nshards > N - 1) nshards = (int) (N - 1);
+  double tph = phase_clock();
   runs = (ShardRun *) calloc((size_t) nshards, sizeof *runs);
   bnds = (GtSmaxBoundary *) calloc((size_t) nshards, sizeof *bnds);
   counts = (uint64_t *) calloc((size_t) nshards, sizeof *counts);
@@ -2236,16 +2365,14 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
     HIPCHK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
     if (gt_smax_dev_alloc_table(r->sh.device, len, &r->lcp, errbuf, errlen)) goto fail;
     if (gt_smax_dev_alloc_table(r->sh.device, len, &r->bwt, errbuf, errlen)) goto fail;
-    HIPCHK(hipMemcpyAsync(r->lcp, in->lcptab + base, len, hipMemcpyHostToDevice, r->stream));
+    HIPCHK(h2d_staged(r->lcp, in->lcptab + base, len, r->stream));
     {
       uint64_t blen = len <= in->totallength + 1 - base ? len : in->totallength + 1 - base;
-      HIPCHK(hipMemcpyAsync(r->bwt, in->bwttab + base, blen, hipMemcpyHostToDevice, r->stream));
+      HIPCHK(h2d_staged(r->bwt, in->bwttab + base, blen, r->stream));
     }
     HIPCHK(hipMalloc(&r->llv, sizeof (GtSmaxLlv) * (hi - lo + 1)));
     if (hi > lo)
-      HIPCHK(hipMemcpyAsync(r->llv, in->llvtab + lo, sizeof (GtSmaxLlv) * (hi - lo),
-                            hipMemcpyHostToDevice, r->stream));
-    HIPCHK(hipStreamSynchronize(r->stream));
+      HIPCHK(h2d_staged(r->llv, in->llvtab + lo, sizeof (GtSmaxLlv) * (hi - lo), r->stream));
     r->sh.lcp_dev = r->lcp;
     r->sh.bwt_dev = r->bwt;
     r->sh.llv_dev = r->llv;
@@ -2255,7 +2382,9 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
     r->sh.begin = begin;
     r->sh.end = end;
     r->sh.nonspecials = N;
+    phase_mark("h2d", &tph);
     if (gt_smax_plan_create(&r->plan, &r->sh, minlen, 0, errbuf, errlen)) goto fail;
+    phase_mark("plan", &tph);
     if (gt_smax_plan_run(r->plan, r->stream)) goto fail;
   }
   for (int s = 0; s < nshards; s++) {
@@ -2285,6 +2414,7 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
     }
     total += counts[s] + 1;   // +1 slot for a stitched interval
   }
+  phase_mark("run", &tph);
   trip = (uint64_t *) malloc(sizeof (uint64_t) * 3 * (total + 1));
   if (trip == NULL) {
     seterr(errbuf, errlen, "out of memory for %lu intervals", (unsigned long) total);
@@ -2293,19 +2423,10 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
   total = 0;
   for (int s = 0; s < nshards; s++) {
     ShardRun *r = &runs[s];
-    GtSmaxRecord *h = (GtSmaxRecord *) malloc(sizeof (GtSmaxRecord) * (counts[s] + 1));
-    if (h == NULL) { seterr(errbuf, errlen, "out of memory"); goto fail; }
     HIPCHK(hipSetDevice(r->sh.device));
     if (counts[s] > 0)
-      HIPCHK(hipMemcpy(h, r->plan->out, sizeof (GtSmaxRecord) * counts[s],
-                       hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < counts[s]; i++) {
-      trip[3 * total] = h[i].lcp;
-      trip[3 * total + 1] = h[i].lb;
-      trip[3 * total + 2] = h[i].lb + h[i].width - 1;
-      total++;
-    }
-    free(h);
+      HIPCHK(d2h_triples(trip + 3 * total, r->plan->out, counts[s], r->stream));
+    total += counts[s];
     GtSmaxRecord rec;
     if (stitch_resolve(bnds, nshards, s, minlen, &rec)) {
       trip[3 * total] = rec.lcp;
@@ -2314,6 +2435,7 @@ static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
       total++;
     }
   }
+  phase_mark("d2h+triples", &tph);
   *trip_out = trip;
   *count_out = total;
   trip = NULL;
@@ -2342,7 +2464,9 @@ extern "C" int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in,
                                                uint64_t **lcp_lb_rb,
                                                uint64_t *count, char *errbuf,
                                                size_t errlen) {
+  double tv = phase_clock();
   if (validate_input(in, errbuf, errlen)) return -1;
+  phase_mark("validate", &tv);
   if (minlen == 0) {
     seterr(errbuf, errlen, "minlen must be >= 1");
     return -1;
