@@ -2217,6 +2217,10 @@ static int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
   return 0;
 }
 
+#ifndef GT_SMAX_COPY_THREADS
+#define GT_SMAX_COPY_THREADS 8u    // 16 measured no faster (fill is memory-bound)
+#endif
+
 // Pageable host -> device through two pinned staging buffers: host threads
 // fill one while the DMA engine drains the other.  A plain hipMemcpyAsync
 // from pageable memory goes through the runtime's small staging buffer,
@@ -2234,7 +2238,7 @@ static hipError_t h2d_staged(void *dst, const void *src, uint64_t len, hipStream
     e = hipHostMalloc(&buf[i], CH, hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
   }
-  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const unsigned nt = std::max(1u, std::min(GT_SMAX_COPY_THREADS, std::thread::hardware_concurrency()));
   for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += CH, k++) {
     const int b = (int) (k & 1);
     const uint64_t c = std::min(CH, len - off);
