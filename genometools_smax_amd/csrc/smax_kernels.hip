@@ -1779,6 +1779,9 @@ static uint32_t plan_tiles(const GtSmaxDevShard *s, uint64_t *first) {
   return (uint32_t) (hi - lo + 1);
 }
 
+static double phase_clock();
+static void phase_mark(const char *what, double *t);
+
 extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                                    const GtSmaxDevShard *shard,
                                    unsigned int minlen, uint64_t capacity,
@@ -1814,6 +1817,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     const char *d = getenv("GT_SMAX_DEBUG");
     p->dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
   }
+  double tpc = phase_clock();
   HIPCHK(hipSetDevice(shard->device));
   {
     int dev_cus = 0, per_cu = 0;
@@ -1831,6 +1835,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpy(&hflag, flag, sizeof hflag, hipMemcpyDeviceToHost));
       (void) hipFree(flag);
+      phase_mark(" pack_bwt", &tpc);
       p->pk = hflag == 0 && !(p->dbg & 8192u);
       if (!p->pk) { (void) hipFree(p->bwtpk); p->bwtpk = NULL; }
     }
@@ -1856,8 +1861,11 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 2 ? dg : (uint64_t) dev_cus * 2);
     p->static_grid = (uint32_t) dev_cus * 8;   // capped below by the list length
   }
+  phase_mark(" occupancy", &tpc);
   HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
+  phase_mark(" out_alloc", &tpc);
   HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
+  phase_mark(" slot_alloc", &tpc);
   HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
 
   HIPCHK(hipMalloc(&p->block_sum, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
@@ -1899,6 +1907,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   (void) hipFree(derr);
   derr = NULL;
   // static K1b list (needs llv_win)
+  phase_mark(" llv_index", &tpc);
   HIPCHK(hipMalloc(&p->static_list, sizeof (uint32_t) * ((uint64_t) p->num_tiles + 1)));
   HIPCHK(hipMalloc(&p->static_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->static_count, 0, sizeof (uint32_t)));
@@ -1913,6 +1922,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     // + 1: the last workgroup computes the boundary head
     p->static_grid = (need < p->static_grid ? need : p->static_grid) + 1;
   }
+  phase_mark(" static_k1b", &tpc);
   HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&p->join, hipEventDisableTiming));
