@@ -179,3 +179,36 @@ def test_protein_alphabet_uses_byte_windows():
         want = _cpu(e, minlen)
         for shards in (1, 4):
             assert np.array_equal(_gpu(e, minlen, shards), want), (minlen, shards)
+
+
+def test_result_view_outlives_parent():
+    """enumerate_smax hands the C layer's buffer to numpy without a copy:
+    views keep it alive, and it is writable and C-contiguous."""
+    import gc
+    e = oracle_esa("at1MB")
+    a = _gpu(e, 20)
+    ref = _cpu(e, 20)
+    tail = a[-5:]
+    col = a[:, 1]
+    del a
+    gc.collect()
+    assert np.array_equal(tail, ref[-5:])
+    assert np.array_equal(col, ref[:, 1])
+    b = _gpu(e, 20)
+    assert b.flags.c_contiguous and b.flags.writeable
+    b[0, 0] += 1
+    assert b[0, 0] == ref[0, 0] + 1
+
+
+def test_host_path_multi_chunk_output():
+    """> 4 Mi intervals: the pinned D2H runs in several 4 Mi-record chunks
+    (and the H2D in many 64 MiB chunks); content equals the CPU oracle."""
+    text = G.synth_genome("human", 800_000_000, 3, threads=16)
+    esa = G.DeviceEsa(text, device=0, keep_suftab=False)
+    host = esa.download()
+    n, N = esa.totallength, esa.nonspecials
+    esa.release()
+    iv = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], n, N, 20, 1)
+    assert len(iv) > (4 << 20)
+    ref = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20, threads=8)
+    assert np.array_equal(iv, ref)
