@@ -374,11 +374,10 @@ def enumerate_maxpairs(lcptab, llvtab, bwttab, suftab, totallength, nonspecials,
     _check(rc, eb)
     n = cnt.value
     if n == 0:
+        if out.value:
+            lib().gt_smax_free(out)
         return np.zeros((0, 3), dtype=np.uint64)
-    buf = (ctypes.c_uint64 * (3 * n)).from_address(out.value)
-    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 3).copy()
-    lib().gt_smax_free(out)
-    return arr
+    return np.asarray(_OwnedTriples(out.value, n))
 
 
 class MaxpairsPlan:
