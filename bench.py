@@ -48,6 +48,21 @@ CONFIGS = {
 }
 
 
+def host_cpu():
+    """Host CPU identity for the cpu_baseline object."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
+
+
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
@@ -170,6 +185,9 @@ def main():
     elapsed = time.perf_counter() - t0
     k1_ms, k1_n = plan.kernel_ms()
     count = plan.fetch_count()
+    parity_ok = True
+    res = None
+    gpu_trip = plan.fetch_triples() if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
 
     # llv entries in this rank's rows (algorithmic bytes)
     host = None
@@ -200,27 +218,36 @@ def main():
     achieved = alg_bytes / (k1_avg_ms * 1e-3) / 1e9
 
     traffic = None
+    pmc_src = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
     if os.path.exists(pmc_path) and not args.bases:
         with open(pmc_path) as fh:
             pmc = json.load(fh)
         traffic = pmc.get("hbm_bytes_per_launch")
+        pmc_src = os.path.relpath(pmc_path, ROOT)
 
     cpu = None
+    sample_full = False
     if host is not None:
         import oracle_lib  # noqa: E402  (tests/: the checker, CPU baseline leg only)
         sample = min(N, args.cpu_sample)
+        sample_full = sample == N
         log("cpu baseline: oracle linsmax over %d rows (1 core)" % sample)
         t0 = time.perf_counter()
         res = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample, minlen)
         t_cpu = time.perf_counter() - t0
-        if sample == N and len(res) != count:
-            log("WARNING: GPU %d intervals != CPU oracle %d" % (count, len(res)))
-        elif sample == N:
-            log("GPU interval count matches the CPU oracle (%d)" % count)
+        if sample == N:
+            # bit-exact parity of the timed path's output (the plan's records)
+            if not np.array_equal(gpu_trip, res):
+                log("FAIL: GPU (%d intervals) differs from the CPU oracle (%d)"
+                    % (len(gpu_trip), len(res)))
+                parity_ok = False
+            else:
+                log("GPU interval array equals the CPU oracle's (%d intervals)" % len(res))
         cpu = {"value": sample / t_cpu, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
                "sample": "oracle orc_linsmax (single core, -O3) over suffix rows [0,%d) of the same "
                          "tables: %.2fs" % (sample, t_cpu)}
+        cpu.update(host_cpu())
         # all-core figure beside the single-core headline:
         # orc_linsmax_mt, row ranges per pthread, same output
         threads = min(len(os.sched_getaffinity(0)), args.cpu_threads)
@@ -229,14 +256,14 @@ def main():
             res_mt = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample,
                                         minlen, threads=threads)
             t_mt = time.perf_counter() - t0
-            if len(res_mt) != len(res):
-                log("WARNING: all-core CPU scan %d intervals != single-core %d"
+            if not np.array_equal(res_mt, res):
+                log("FAIL: all-core CPU scan (%d intervals) != single-core (%d)"
                     % (len(res_mt), len(res)))
+                parity_ok = False
             cpu["all_cores"] = {"value": sample / t_mt, "cores": threads, "seconds": round(t_mt, 3),
                                 "sample": "orc_linsmax_mt (pthreads, equal row ranges) over the "
                                           "same rows"}
             del res_mt
-        del res
 
     # end-to-end through the drop-in boundary (host tables in memory -> H2D
     # -> plan -> K0..K3 -> D2H of the (lcp, lb, rb) list): reported beside
@@ -249,14 +276,19 @@ def main():
         t0 = time.perf_counter()
         iv = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], n, N, minlen, 1)
         t_e2e = time.perf_counter() - t0
-        if len(iv) != count:
-            log("WARNING: end-to-end %d intervals != %d" % (len(iv), count))
+        if res is not None and sample == N and not np.array_equal(iv, res):
+            log("FAIL: end-to-end result (%d intervals) differs from the CPU oracle (%d)"
+                % (len(iv), len(res)))
+            parity_ok = False
         e2e = {"value": N / t_e2e, "unit": "suffix-positions/s", "seconds": round(t_e2e, 4),
                "path": "gt_smax_hip_enumerate_to_buffer: pageable host .lcp/.bwt/.llv -> H2D -> "
                        "plan (pack, llv index) -> K0..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
                "vs_cpu_baseline": (N / t_e2e) / cpu["value"] if cpu else None}
         del iv
 
+    if rank == 0 and not parity_ok:
+        log("parity failure: no bench line")
+        sys.exit(1)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -281,7 +313,16 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "smax_scan_kernel", "kernel_avg_ms": k1_avg_ms,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         # the same kernel priced by the HBM bytes it really moves
+                         # (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH §HBM)
+                         "achieved_by_traffic": (traffic / (k1_avg_ms * 1e-3) / 1e9
+                                                 if traffic else None),
+                         "frac_by_traffic": (traffic / (k1_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                             if traffic else None),
+                         "traffic_source": pmc_src},
+            "parity": ("bit-exact vs CPU oracle (plan records%s)" % (" + end-to-end" if e2e else "")
+                       if res is not None and sample_full else "not checked in this run"),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2)},

@@ -157,6 +157,7 @@ def lib():
         L.gt_smax_stitch_host.argtypes = [ctypes.POINTER(GtSmaxBoundary), ci, ci, u32,
                                           ctypes.POINTER(GtSmaxRecord)]
         L.gt_smax_plan_fetch_count.argtypes = [vp, ctypes.POINTER(u64)]
+        L.gt_smax_plan_fetch_triples.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
         L.gt_smax_plan_timing.argtypes = [vp, ci]
         L.gt_smax_plan_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci)]
         L.gt_smax_plan_copy_boundary.argtypes = [vp, vp, vp]
@@ -301,6 +302,19 @@ class EsaIndex:
 
 # ------------------------------------------------------------- host-buffer API
 
+def _check_lengths(totallength, nonspecials, lcptab=None, bwttab=None, suftab=None):
+    """The C layer reads totallength+1 table entries (nonspecials+1 of the
+    suffix array): refuse shorter host arrays instead of reading past them."""
+    n, N = int(totallength), int(nonspecials)
+    if n < 0 or N < 0 or N > n:
+        raise SmaxError("bad lengths: totallength=%d nonspecials=%d" % (n, N))
+    for name, tab, need in (("lcptab", lcptab, n + 1), ("bwttab", bwttab, n + 1),
+                            ("suftab", suftab, N + 1)):
+        if tab is not None and len(tab) < need:
+            raise SmaxError("%s holds %d entries, needs %d (totallength=%d, nonspecials=%d)"
+                            % (name, len(tab), need, n, N))
+
+
 def enumerate_smax(lcptab, llvtab, bwttab, totallength, nonspecials, minlen, num_gpus=1):
     """All smax intervals as an (k,3) uint64 array of (lcp, lb, rb), lb ascending.
 
@@ -308,6 +322,7 @@ def enumerate_smax(lcptab, llvtab, bwttab, totallength, nonspecials, minlen, num
     lcptab = np.ascontiguousarray(lcptab, dtype=np.uint8)
     bwttab = np.ascontiguousarray(bwttab, dtype=np.uint8)
     llvtab = np.ascontiguousarray(llvtab, dtype=np.uint64).reshape(-1, 2)
+    _check_lengths(totallength, nonspecials, lcptab, bwttab)
     inp = GtSmaxInput()
     inp.lcptab = lcptab.ctypes.data
     inp.llvtab = llvtab.ctypes.data if len(llvtab) else None
@@ -357,6 +372,7 @@ def enumerate_maxpairs(lcptab, llvtab, bwttab, suftab, totallength, nonspecials,
     suftab = np.ascontiguousarray(suftab)
     if suftab.dtype not in (np.uint32, np.uint64):
         suftab = suftab.astype(np.uint64)
+    _check_lengths(totallength, nonspecials, lcptab, bwttab, suftab)
     inp = GtSmaxInput()
     inp.lcptab = lcptab.ctypes.data
     inp.llvtab = llvtab.ctypes.data if len(llvtab) else None
@@ -431,6 +447,7 @@ def _input(lcptab, llvtab, bwttab, suftab, totallength, nonspecials):
     keep = []
     lcptab = np.ascontiguousarray(lcptab, dtype=np.uint8)
     llvtab = np.ascontiguousarray(llvtab, dtype=np.uint64).reshape(-1, 2)
+    _check_lengths(totallength, nonspecials, lcptab, bwttab, suftab)
     keep += [lcptab, llvtab]
     inp = GtSmaxInput()
     inp.lcptab = lcptab.ctypes.data
@@ -639,6 +656,17 @@ class SmaxPlan:
         if lib().gt_smax_plan_fetch_count(self.plan, ctypes.byref(c)) != 0:
             raise SmaxError("gt_smax_plan_fetch_count failed")
         return c.value
+
+    def fetch_triples(self):
+        """The plan's records (after run / stitch) as an (k,3) uint64 array of
+        (lcp, lb, rb), ascending lb (gt_smax_plan_fetch_triples)."""
+        k = self.fetch_count()
+        out = np.empty((max(k, 1), 3), dtype=np.uint64)
+        c = ctypes.c_uint64()
+        if lib().gt_smax_plan_fetch_triples(self.plan, out.ctypes.data, k, ctypes.byref(c)) != 0:
+            raise SmaxError("gt_smax_plan_fetch_triples failed (%d records, capacity %d)"
+                            % (c.value, self.capacity))
+        return out[: c.value]
 
     def close(self):
         if self.plan:

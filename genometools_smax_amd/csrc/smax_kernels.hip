@@ -11,28 +11,35 @@
 // BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
-// One pass = four launches on one stream, no host synchronisation:
-//   K0 smax_head_kernel   one lane: per-run resets (K1b computes the boundary head)
-//   K1 smax_scan_kernel   the streaming kernel (HBM bound, see below)
-//   K2 rocPRIM exclusive scan of the per-tile interval counts
-//   K3 smax_compact_kernel ordered copy of the tiles' records -> ascending lb
+// One pass = launches on one stream (plus a forked side stream), no host
+// synchronisation:
+//   K0  smax_head_kernel     per-run resets (pending-plateau slot, deferral
+//                            count, the 256-tile block sums)
+//   K1  smax_scan_kernel     the streaming kernel; K1b smax_defer_kernel over
+//                            the plan-time static list runs beside it on the
+//                            side stream (shard edges, dense-.llv windows) and
+//                            computes the boundary head
+//   K1b smax_defer_kernel    over K1's runtime list (exact-queue overflow)
+//   K3  smax_compact_kernel  ordered copy of the tiles' records -> ascending
+//                            lb, output offsets from the block sums
 //
-// K1: persistent 256-thread workgroups, static tile schedule (tile =
-// blockIdx.x + k*gridDim.x, 16384 suffix rows per tile) and no
-// inter-workgroup waits.  Per tile:
-//   stage    the prefetched LCP and BWT bytes (16 B/lane, coalesced, 1 KiB
-//            per wave instruction) -> LDS, plus a 16 B left / 64 B right halo;
-//            the NEXT tile's loads are issued right after, so they are in
-//            flight for the whole processing of this tile;
-//   .llv     a 255 byte is resolved in O(1): its rank among the window's 255
-//            bytes (per-16-byte-chunk prefix counts + a SWAR count) indexes
-//            the tile's .llv values, staged in LDS with one coalesced load;
-//   phase 1  SWAR filter "any byte >= minlen" per 16-byte segment, then per
-//            row the plateau-start test LCP[c] > LCP[c-1] and a scan to the
-//            plateau end in LDS; local maxima become candidates;
-//   phase 3  left-diversity: 256-bit seen-set over BWT[lb..rb] in LDS;
-//   output   block scan of per-row counts in row order, records written to
-//            the tile's slot (or the overflow area) -- K2/K3 place them.
+// K1: every wave is an independent worker on 2048-row tiles (tile = wave id
+// + k * waves in grid; 8 generations of resident 4-wave workgroups), no
+// workgroup barrier.  Per tile:
+//   window   LCP bytes (+16-row halos), packed BWT bit planes (DNA) or BWT
+//            bytes, and the window's .llv values (u16) go global -> LDS by
+//            LDS-DMA into one of the wave's two windows; the next tile's
+//            DMA is issued as soon as this one has landed;
+//   filter   per 16-row segment "any byte >= min(minlen,128)", refined to
+//            segments where a row can start a record when more than one
+//            64-lane step would be needed;
+//   classify active segments are compacted and classified with SWAR byte
+//            relations: 2- and 3-row intervals are decided in place (local
+//            maximum + left diversity from the bit planes); plateaus of
+//            >= 3 rows and 255 bytes (.llv values by rank) go to an exact
+//            queue, evaluated 64 starts at a time;
+//   output   owning lanes write packed 8-byte records in row order into the
+//            tile's slot; lane 0 adds the count to the 256-tile block sum.
 // No MFMA: integer/byte work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -2131,6 +2138,22 @@ extern "C" int gt_smax_plan_fetch_count(GtSmaxPlan *p, uint64_t *count) {
     fprintf(stderr, "gt_smax: inconsistent index (device error bits 0x%x)\n", e);
     return -1;
   }
+  return 0;
+fail:
+  return -1;
+}
+
+static hipError_t d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, hipStream_t s);
+
+extern "C" int gt_smax_plan_fetch_triples(GtSmaxPlan *p, uint64_t *lcp_lb_rb, uint64_t capacity,
+                                          uint64_t *count) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  uint64_t c = 0;
+  if (gt_smax_plan_fetch_count(p, &c)) return -1;
+  *count = c;
+  if (c > p->capacity || c > capacity) return -1;   // caller re-plans / enlarges
+  HIPCHK(d2h_triples(lcp_lb_rb, p->out, c, 0));
   return 0;
 fail:
   return -1;

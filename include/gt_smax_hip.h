@@ -194,6 +194,13 @@ int gt_smax_plan_copy_boundary(GtSmaxPlan *plan, void *dst_dev, void *stream);
  * -1 if the kernels flagged an inconsistent index (see error bits). */
 int gt_smax_plan_fetch_count(GtSmaxPlan *plan, uint64_t *count);
 
+/* Synchronises and copies the plan's records (after run / stitch) to host
+ * memory as (lcp, lb, rb) triples, ascending lb: 3*capacity uint64 at
+ * lcp_lb_rb.  *count receives the record count; -1 when it exceeds the
+ * plan's or the caller's capacity (nothing copied), or on a device error. */
+int gt_smax_plan_fetch_triples(GtSmaxPlan *plan, uint64_t *lcp_lb_rb,
+                               uint64_t capacity, uint64_t *count);
+
 /* Sticky device error bits: 1 = an .lcp byte 255 without its .llv entry,
  * 2 = a table read outside the shard's rows. */
 uint32_t gt_smax_plan_error_bits(GtSmaxPlan *plan);

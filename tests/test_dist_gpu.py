@@ -1,0 +1,159 @@
+"""Multi-rank device path of the sharded smax pass on one GPU.
+
+Each spawned rank (world_size 2 or 3, all on cuda:0, gloo process group)
+runs exactly the step bench.py runs per rank:
+
+    plan.run -> plan.copy_boundary -> all-gather of the boundary records
+             -> plan.stitch (smax_stitch_kernel) -> the rank's records
+
+The boundary records are staged through host memory for gloo (bench.py's
+--dist-backend gloo rehearsal; the driver's 8-GPU run uses RCCL on device
+memory, same bytes).  The ranks' record lists, concatenated in rank order,
+must equal the CPU oracle's single-shard answer bit for bit -- order
+included.  Two table layouts:
+  - shard-local tables (each rank holds LCP[begin-1 .. end], its BWT rows and
+    its .llv entries, as the host-table entry point uploads them), at1MB with
+    splits inside plateaus and a shard lying entirely inside one;
+  - full tables per rank (bench.py: the GPU suffixerator output, each rank
+    planning over its own range), 100 Mbp uniform and 30 Mbp human-like.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import genometools_smax_amd as G
+import oracle_lib as O
+from conftest import oracle_esa
+
+pytestmark = pytest.mark.gpu
+
+
+def _padded(host, length):
+    t = torch.zeros(G.PAD_FRONT + length + G.PAD_BACK, dtype=torch.uint8, device="cuda")
+    t[G.PAD_FRONT: G.PAD_FRONT + len(host)] = torch.from_numpy(np.ascontiguousarray(host))
+    return t, t.data_ptr() + G.PAD_FRONT
+
+
+def _exchange(plan, world, rank):
+    """The rank's step: run, all-gather of boundary records, stitch."""
+    stream = torch.cuda.current_stream().cuda_stream
+    plan.run(stream)
+    send = torch.zeros(G.BOUNDARY_BYTES, dtype=torch.uint8, device="cuda")
+    plan.copy_boundary(send.data_ptr(), stream)
+    hrecv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8)
+    dist.all_gather_into_tensor(hrecv, send.cpu())
+    recv = hrecv.cuda()
+    plan.stitch(recv.data_ptr(), world, rank, stream)
+    torch.cuda.synchronize()
+    return plan.fetch_triples()
+
+
+def _worker_local(rank, world, port, splits, minlen, name, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        e = oracle_esa(name)
+        N = e.nonspecials
+        begin, end = splits[rank], splits[rank + 1]
+        base = begin - 1
+        length = end - base + 1                      # LCP[begin-1 .. end]
+        lcp_t, lcp_p = _padded(e.lcpbytes[base: base + length], length)
+        bwt_t, bwt_p = _padded(e.bwt[base: min(base + length, e.n + 1)], length)
+        pos = e.llv[:, 0] if len(e.llv) else np.zeros(0, np.uint64)
+        mine = e.llv[(pos >= base) & (pos < base + length)]
+        llv_t = torch.from_numpy(np.ascontiguousarray(
+            np.vstack([mine, np.zeros((1, 2), np.uint64)]).view(np.int64))).cuda()
+        # capacity: at most one interval per two rows
+        plan = G.SmaxPlan(lcp_p, bwt_p, llv_t.data_ptr(), len(mine), base, length, begin, end, N,
+                          minlen, device=0, capacity=(end - begin) // 2 + 16)
+        trip = _exchange(plan, world, rank)
+        plan.close()
+        parts = [None] * world
+        dist.all_gather_object(parts, trip)
+        if rank == 0:
+            out_q.put(np.concatenate(parts).reshape(-1, 3))
+        del lcp_t, bwt_t, llv_t
+    finally:
+        dist.destroy_process_group()
+
+
+def _worker_full(rank, world, port, kind, bases, seed, minlen, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        text = G.synth_genome(kind, bases, seed, threads=4)
+        esa = G.DeviceEsa(text, device=0)
+        N = esa.nonspecials
+        begin = 1 + (N - 1) * rank // world           # bench.py's split rule
+        end = 1 + (N - 1) * (rank + 1) // world
+        plan = esa.plan(minlen, begin, end, capacity=(end - begin) // 2 + 16)
+        trip = _exchange(plan, world, rank)
+        plan.close()
+        parts = [None] * world
+        dist.all_gather_object(parts, trip)
+        if rank == 0:
+            host = esa.download()
+            want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen, threads=4)
+            out_q.put((np.concatenate(parts).reshape(-1, 3), want))
+        esa.release()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.start_processes(fn, args=(world, _free_port()) + args + (q,), nprocs=world, join=True,
+                       start_method="spawn")
+    return q.get()
+
+
+def _widest(name, minlen):
+    e = oracle_esa(name)
+    ref = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+    k = int(np.argmax(ref[:, 2] - ref[:, 1]))
+    return e, ref, [int(x) for x in ref[k]]
+
+
+@pytest.mark.parametrize("minlen", [8, 20])
+def test_two_ranks_local_tables_split_inside_plateau(minlen):
+    e, ref, (l, lb, rb) = _widest("at1MB", minlen)
+    assert rb - lb >= 2
+    got = _spawn(_worker_local, 2, [1, lb + 2, e.nonspecials], minlen, "at1MB")
+    assert np.array_equal(got, ref), (len(got), len(ref))
+
+
+def test_three_ranks_local_tables_passthrough_shard():
+    e, ref, (l, lb, rb) = _widest("at1MB", 8)
+    assert rb - lb >= 3
+    got = _spawn(_worker_local, 3, [1, lb + 2, lb + 3, e.nonspecials], 8, "at1MB")
+    assert np.array_equal(got, ref), (len(got), len(ref))
+
+
+def test_three_ranks_local_tables_even_split():
+    e = oracle_esa("at1MB")
+    N = e.nonspecials
+    ref = O.linsmax(e.lcpbytes, e.llv, e.bwt, N, 20)
+    got = _spawn(_worker_local, 3, [1 + (N - 1) * r // 3 for r in range(4)], 20, "at1MB")
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("world,kind,bases,seed", [(2, "uniform", 100_000_000, 42),
+                                                   (3, "human", 30_000_000, 5)])
+def test_full_tables_bench_split(world, kind, bases, seed):
+    got, want = _spawn(_worker_full, world, kind, bases, seed, 20)
+    assert len(want) > 100
+    assert np.array_equal(got, want), (len(got), len(want))
