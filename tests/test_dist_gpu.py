@@ -19,6 +19,7 @@ included.  Two table layouts:
 """
 import os
 import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -53,7 +54,7 @@ def _exchange(plan, world, rank):
     return plan.fetch_triples()
 
 
-def _worker_local(rank, world, port, splits, minlen, name, out_q):
+def _worker_local(rank, world, port, splits, minlen, name, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -77,13 +78,13 @@ def _worker_local(rank, world, port, splits, minlen, name, out_q):
         parts = [None] * world
         dist.all_gather_object(parts, trip)
         if rank == 0:
-            out_q.put(np.concatenate(parts).reshape(-1, 3))
+            np.savez(out_path, got=np.concatenate(parts).reshape(-1, 3))
         del lcp_t, bwt_t, llv_t
     finally:
         dist.destroy_process_group()
 
 
-def _worker_full(rank, world, port, kind, bases, seed, minlen, out_q):
+def _worker_full(rank, world, port, kind, bases, seed, minlen, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -101,7 +102,7 @@ def _worker_full(rank, world, port, kind, bases, seed, minlen, out_q):
         if rank == 0:
             host = esa.download()
             want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen, threads=4)
-            out_q.put((np.concatenate(parts).reshape(-1, 3), want))
+            np.savez(out_path, got=np.concatenate(parts).reshape(-1, 3), want=want)
         esa.release()
     finally:
         dist.destroy_process_group()
@@ -114,11 +115,15 @@ def _free_port():
 
 
 def _spawn(fn, world, *args):
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    mp.start_processes(fn, args=(world, _free_port()) + args + (q,), nprocs=world, join=True,
-                       start_method="spawn")
-    return q.get()
+    """Runs fn on world spawned ranks; rank 0 saves the result into a file
+    (a pipe-backed queue would block rank 0 on a large put while the parent
+    waits in join)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "result.npz")
+        mp.start_processes(fn, args=(world, _free_port()) + args + (out,), nprocs=world,
+                           join=True, start_method="spawn")
+        with np.load(out) as f:
+            return {k: f[k] for k in f.files}
 
 
 def _widest(name, minlen):
@@ -132,14 +137,14 @@ def _widest(name, minlen):
 def test_two_ranks_local_tables_split_inside_plateau(minlen):
     e, ref, (l, lb, rb) = _widest("at1MB", minlen)
     assert rb - lb >= 2
-    got = _spawn(_worker_local, 2, [1, lb + 2, e.nonspecials], minlen, "at1MB")
+    got = _spawn(_worker_local, 2, [1, lb + 2, e.nonspecials], minlen, "at1MB")["got"]
     assert np.array_equal(got, ref), (len(got), len(ref))
 
 
 def test_three_ranks_local_tables_passthrough_shard():
     e, ref, (l, lb, rb) = _widest("at1MB", 8)
     assert rb - lb >= 3
-    got = _spawn(_worker_local, 3, [1, lb + 2, lb + 3, e.nonspecials], 8, "at1MB")
+    got = _spawn(_worker_local, 3, [1, lb + 2, lb + 3, e.nonspecials], 8, "at1MB")["got"]
     assert np.array_equal(got, ref), (len(got), len(ref))
 
 
@@ -147,13 +152,14 @@ def test_three_ranks_local_tables_even_split():
     e = oracle_esa("at1MB")
     N = e.nonspecials
     ref = O.linsmax(e.lcpbytes, e.llv, e.bwt, N, 20)
-    got = _spawn(_worker_local, 3, [1 + (N - 1) * r // 3 for r in range(4)], 20, "at1MB")
+    got = _spawn(_worker_local, 3, [1 + (N - 1) * r // 3 for r in range(4)], 20, "at1MB")["got"]
     assert np.array_equal(got, ref)
 
 
 @pytest.mark.parametrize("world,kind,bases,seed", [(2, "uniform", 100_000_000, 42),
                                                    (3, "human", 30_000_000, 5)])
 def test_full_tables_bench_split(world, kind, bases, seed):
-    got, want = _spawn(_worker_full, world, kind, bases, seed, 20)
+    r = _spawn(_worker_full, world, kind, bases, seed, 20)
+    got, want = r["got"], r["want"]
     assert len(want) > 100
     assert np.array_equal(got, want), (len(got), len(want))
