@@ -87,6 +87,9 @@ def main():
                          "rehearsal on one GPU; the measured configuration is nccl = RCCL)")
     ap.add_argument("--one-gpu", action="store_true",
                     help="all ranks on cuda:0 (rehearsal only)")
+    ap.add_argument("--byte-bwt", action="store_true",
+                    help="plan from the byte BWT (plan-time packing) instead of the builder's "
+                         "packed BWT")
     args = ap.parse_args()
 
     import numpy as np
@@ -133,7 +136,15 @@ def main():
     # ---- this rank's suffix-array range
     begin = 1 + (N - 1) * rank // world
     end = 1 + (N - 1) * (rank + 1) // world
-    plan = esa.plan(minlen, begin, end)
+    # the builder emits the packed bit-plane BWT the scan streams (0.5 B/row),
+    # so creating the plan reads no BWT bytes: .llv index (u16 values, per-tile
+    # windows), the static K1b list and the plan's buffers (--byte-bwt: the
+    # plan packs the byte BWT itself, a plan-time pass over 1 B/row)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan = esa.plan(minlen, begin, end, packed=not args.byte_bwt)
+    torch.cuda.synchronize()
+    t_plan = time.perf_counter() - t0
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
     send = recv = None
@@ -166,7 +177,7 @@ def main():
     if cnt > plan.capacity:
         log("rank %d: %d intervals > capacity %d, re-planning" % (rank, cnt, plan.capacity))
         plan.close()
-        plan = esa.plan(minlen, begin, end, capacity=cnt + 16)
+        plan = esa.plan(minlen, begin, end, capacity=cnt + 16, packed=not args.byte_bwt)
 
     for _ in range(args.warmup):
         step()
@@ -281,8 +292,9 @@ def main():
                 % (len(iv), len(res)))
             parity_ok = False
         e2e = {"value": N / t_e2e, "unit": "suffix-positions/s", "seconds": round(t_e2e, 4),
-               "path": "gt_smax_hip_enumerate_to_buffer: pageable host .lcp/.bwt/.llv -> H2D -> "
-                       "plan (pack, llv index) -> K0..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
+               "path": "gt_smax_hip_enumerate_to_buffer: pageable host .lcp/.bwt/.llv -> H2D "
+                       "(.bwt packed to bit planes during the staged fill) -> plan (llv index) -> "
+                       "K0..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
                "vs_cpu_baseline": (N / t_e2e) / cpu["value"] if cpu else None}
         del iv
 
@@ -326,6 +338,10 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2)},
+            # plan creation over the resident tables, outside the timed steps
+            "plan_ms": round(t_plan * 1e3, 3),
+            "bwt_input": ("byte BWT, packed at plan time" if args.byte_bwt else
+                          "packed bit planes (0.5 B/row) emitted by the GPU ESA builder"),
         }
         print(json.dumps(out), flush=True)
     if plan is not None:

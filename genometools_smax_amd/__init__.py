@@ -62,6 +62,7 @@ class GtSmaxDevShard(ctypes.Structure):
         ("end", ctypes.c_uint64),
         ("nonspecials", ctypes.c_uint64),
         ("device", ctypes.c_int),
+        ("bwtpk_dev", ctypes.c_void_p),
     ]
 
 
@@ -94,6 +95,7 @@ class GtMaxpairsDevInput(ctypes.Structure):
         ("suf_bytes", ctypes.c_int),
         ("nonspecials", ctypes.c_uint64),
         ("device", ctypes.c_int),
+        ("bwtpk_dev", ctypes.c_void_p),
     ]
 
 
@@ -136,6 +138,8 @@ def lib():
         L.gt_smax_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput), u32, ci,
                                                       ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
         L.gt_smax_free.argtypes = [vp]
+        L.gt_smax_release_cache.argtypes = []
+        L.gt_smax_pack_bwt.argtypes = [vp, u64, vp]
         L.gt_smax_device_count.restype = ci
         L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
         L.gt_smax_dev_free_table.argtypes = [ci, vp]
@@ -575,9 +579,10 @@ class SmaxPlan:
     (DeviceTable, or torch tensors with PAD_FRONT/PAD_BACK slack)."""
 
     def __init__(self, lcp_ptr, bwt_ptr, llv_ptr, numllv, base, local_len, begin, end,
-                 nonspecials, minlen, device=0, capacity=0):
+                 nonspecials, minlen, device=0, capacity=0, bwtpk_ptr=None):
         sh = GtSmaxDevShard()
         sh.lcp_dev, sh.bwt_dev, sh.llv_dev = lcp_ptr, bwt_ptr, llv_ptr
+        sh.bwtpk_dev = bwtpk_ptr
         sh.numllv, sh.base, sh.local_len = int(numllv), int(base), int(local_len)
         sh.begin, sh.end, sh.nonspecials, sh.device = int(begin), int(end), int(nonspecials), device
         self.shard = sh
@@ -680,6 +685,24 @@ class SmaxPlan:
             pass
 
 
+def pk_groups(local_len):
+    """GT_SMAX_PK_GROUPS: u64 groups of a packed BWT of local_len rows."""
+    return int(local_len) // 16 + 134
+
+
+def pack_bwt(bwt):
+    """Host packing of a DNA BWT (gt_smax_pack_bwt): (groups, is_dna)."""
+    bwt = np.ascontiguousarray(bwt, dtype=np.uint8)
+    out = np.zeros(pk_groups(len(bwt)), dtype=np.uint64)
+    rc = lib().gt_smax_pack_bwt(bwt.ctypes.data, len(bwt), out.ctypes.data)
+    return out, rc == 0
+
+
+def release_cache():
+    """Frees the runtime's cached device and pinned buffers."""
+    lib().gt_smax_release_cache()
+
+
 def stitch_host(boundaries, shard_index, minlen):
     """Host form of the boundary stitch (pure function of the records)."""
     arr = (GtSmaxBoundary * len(boundaries))(*boundaries)
@@ -709,6 +732,7 @@ class GtSmaxEsaDev(ctypes.Structure):
         ("bwttab_dev", ctypes.c_void_p),
         ("llvtab_dev", ctypes.c_void_p),
         ("suftab_dev", ctypes.c_void_p),
+        ("bwtpk_dev", ctypes.c_void_p),
     ]
 
 
@@ -719,6 +743,7 @@ def _esa_lib():
         L.gt_smax_esa_build.argtypes = [ci, vp, u64, ci, ctypes.POINTER(GtSmaxEsaDev), cs, sz]
         L.gt_smax_esa_download.argtypes = [ctypes.POINTER(GtSmaxEsaDev), vp, vp, vp, vp, cs, sz]
         L.gt_smax_esa_release.argtypes = [ctypes.POINTER(GtSmaxEsaDev)]
+        L.gt_smax_esa_download_packed.argtypes = [ctypes.POINTER(GtSmaxEsaDev), vp, cs, sz]
         L.gt_smax_synth_total_length.argtypes = [ci, u64, ctypes.POINTER(u64)]
         L.gt_smax_synth_generate.argtypes = [ci, u64, u64, vp, u64, ctypes.POINTER(u64), ci]
         L._esa_ready = True
@@ -752,13 +777,24 @@ class DeviceEsa:
                                                eb, len(eb)), eb)
         return {"lcptab": lcp, "bwttab": bwt, "llvtab": llv[: self.numllv], "suftab": suf}
 
-    def plan(self, minlen, begin=None, end=None, capacity=0):
-        """Single-shard (or sub-range) smax plan over the device tables."""
+    def plan(self, minlen, begin=None, end=None, capacity=0, packed=True):
+        """Single-shard (or sub-range) smax plan over the device tables: the
+        builder's packed BWT (packed=False: the byte BWT, which the plan then
+        packs itself at plan time)."""
         N = self.nonspecials
         begin = 1 if begin is None else begin
         end = N if end is None else end
         return SmaxPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
-                        0, self.totallength + 1, begin, end, N, minlen, self.device, capacity)
+                        0, self.totallength + 1, begin, end, N, minlen, self.device, capacity,
+                        bwtpk_ptr=self.esa.bwtpk_dev if packed else None)
+
+    def packed_bwt(self):
+        """The builder's packed BWT groups (GT_SMAX_PK_GROUPS) on the host."""
+        out = np.empty(pk_groups(self.totallength + 1), dtype=np.uint64)
+        eb = _errbuf()
+        _check(_esa_lib().gt_smax_esa_download_packed(ctypes.byref(self.esa), out.ctypes.data,
+                                                      eb, len(eb)), eb)
+        return out
 
     def maxpairs_plan(self, minlen):
         """Maximal pairs over the device tables (needs keep_suftab=True)."""

@@ -22,7 +22,8 @@
 //      scattered back into the group's SA slots;
 //   4. Phi array + chunked Kasai (PLCP[i] >= PLCP[i-1]-1 within a chunk),
 //      comparing 32 symbols per step on the packed text;
-//   5. gathers for LCP (by SA) and BWT, stream compaction for .llv.
+//   5. gathers for LCP (by SA) and BWT -- bytes and the packed bit planes
+//      the smax scan streams -- and stream compaction for .llv.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -202,18 +203,31 @@ __global__ void k_plcp(const uint64_t *P, const uint64_t *S, const uint32_t *phi
   }
 }
 
+// LCP bytes, .llv flags, BWT bytes and the packed BWT (bit planes, layout of
+// GT_SMAX_PK_GROUPS in include/gt_smax_hip.h: group k/16 + 1 holds row k)
+// from three wave ballots -- 16 consecutive lanes are one group's rows
 __global__ void k_finish(const uint32_t *SA, const uint32_t *plcp, const uint8_t *T,
-                         uint64_t m, uint8_t *lcptab, uint8_t *bwttab,
+                         uint64_t m, uint8_t *lcptab, uint8_t *bwttab, uint64_t *bwtpk,
                          uint8_t *bigflag, unsigned long long *sum,
                          unsigned int *maxv) {
   uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   uint64_t v = 0;
+  uint32_t b = 0;
   if (k < m) {
     uint32_t s = SA[k];
     v = k == 0 ? 0 : plcp[s];
     lcptab[k] = v < 255 ? (uint8_t) v : 255;
     bigflag[k] = v >= 255;
-    bwttab[k] = s == 0 ? 254 : T[s - 1];
+    b = s == 0 ? 254 : T[s - 1];
+    bwttab[k] = (uint8_t) b;
+  }
+  {
+    const bool sp = k < m && b >= 254;
+    const uint64_t m0 = __ballot(!sp && (b & 1u)), m1 = __ballot(!sp && (b & 2u)), ms = __ballot(sp);
+    const uint32_t lane = threadIdx.x & 63;
+    if ((lane & 15) == 0)
+      bwtpk[k / 16 + 1] = ((m0 >> lane) & 0xffffull) | (((m1 >> lane) & 0xffffull) << 16) |
+                          (((ms >> lane) & 0xffffull) << 32);
   }
   // block reductions for averagelcp / maxbranchdepth (.prj)
   __shared__ unsigned long long ssum[256];
@@ -268,6 +282,8 @@ extern "C" void gt_smax_esa_release(GtSmaxEsaDev *e) {
   if (e->bwttab_dev) gt_smax_dev_free_table(e->device, e->bwttab_dev);
   if (e->llvtab_dev) (void) hipFree(e->llvtab_dev);
   if (e->suftab_dev) (void) hipFree(e->suftab_dev);
+  if (e->bwtpk_dev) (void) hipFree(e->bwtpk_dev);
+  e->bwtpk_dev = NULL;
   e->lcptab_dev = e->bwttab_dev = NULL;
   e->llvtab_dev = NULL;
   e->suftab_dev = NULL;
@@ -290,6 +306,7 @@ extern "C" int gt_smax_esa_build(int device, const uint8_t *text, uint64_t n,
   int rounds = 0;
   memset(out, 0, sizeof *out);
   out->device = device;
+  gt_smax_release_cache();   // the smax runtime's cached buffers: room for the build
   if (m >= 0xffffffffull) {
     seterr(errbuf, errlen, "text of %lu symbols exceeds the 32-bit suffix array "
            "path (n+1 < 2^32)", (unsigned long) n);
@@ -409,13 +426,15 @@ extern "C" int gt_smax_esa_build(int device, const uint8_t *text, uint64_t n,
     HIPCHK(hipGetLastError());
     if (gt_smax_dev_alloc_table(device, m, &out->lcptab_dev, errbuf, errlen)) goto fail;
     if (gt_smax_dev_alloc_table(device, m, &out->bwttab_dev, errbuf, errlen)) goto fail;
+    HIPCHK(hipMalloc(&out->bwtpk_dev, sizeof (uint64_t) * GT_SMAX_PK_GROUPS(m)));
+    HIPCHK(hipMemsetAsync(out->bwtpk_dev, 0, sizeof (uint64_t) * GT_SMAX_PK_GROUPS(m), s));
     HIPCHK(hipMalloc(&bigflag, m));
     HIPCHK(hipMalloc(&sumd, sizeof *sumd));
     HIPCHK(hipMalloc(&maxd, sizeof *maxd));
     HIPCHK(hipMemset(sumd, 0, sizeof *sumd));
     HIPCHK(hipMemset(maxd, 0, sizeof *maxd));
     hipLaunchKernelGGL(k_finish, dim3(blocks_for(m)), dim3(256), 0, s, SA, plcp, T, m,
-                       out->lcptab_dev, out->bwttab_dev, bigflag, sumd, maxd);
+                       out->lcptab_dev, out->bwttab_dev, out->bwtpk_dev, bigflag, sumd, maxd);
     HIPCHK(hipGetLastError());
     llvpos = hv;   // reuse
     hipLaunchKernelGGL(k_iota, dim3(blocks_for(m)), dim3(256), 0, s, valB, m);
@@ -501,5 +520,15 @@ extern "C" int gt_smax_esa_download(const GtSmaxEsaDev *e, uint8_t *lcptab,
   return 0;
 fail:
   free(s32);
+  return -1;
+}
+
+extern "C" int gt_smax_esa_download_packed(const GtSmaxEsaDev *e, uint64_t *pk, char *errbuf,
+                                           size_t errlen) {
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipMemcpy(pk, e->bwtpk_dev, sizeof (uint64_t) * GT_SMAX_PK_GROUPS(e->totallength + 1),
+                   hipMemcpyDeviceToHost));
+  return 0;
+fail:
   return -1;
 }

@@ -1,0 +1,29 @@
+// smax_internal.h -- internal interfaces between the kernels file
+// (smax_kernels.hip) and the host runtime (smax_runtime.cpp).  Not part of
+// the C-ABI.
+#ifndef GT_SMAX_INTERNAL_H
+#define GT_SMAX_INTERNAL_H
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gt_smax_hip.h"
+
+// Per-device caching allocator of the host runtime: plan buffers and staged
+// tables come from it, so back-to-back calls in one process reuse device
+// memory instead of hipMalloc/hipFree of multi-GB buffers per call.
+// smax_dev_free returns a block to the cache (or frees it when caching is
+// off, GT_SMAX_NO_CACHE=1); gt_smax_release_cache() frees everything cached.
+hipError_t smax_dev_alloc(void **ptr, size_t bytes);   // on the current device
+void smax_dev_free(void *ptr);                          // any device; NULL ok
+
+// Device records of a plan -> host (lcp, lb, rb) triples through the
+// device's pinned ring (the plan's work must be complete).
+hipError_t smax_d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, void *stream);
+
+// GT_SMAX_TIMING=1: phase times of the host-table entry points on stderr.
+double smax_phase_clock();
+void smax_phase_mark(const char *what, double *t);
+
+#endif

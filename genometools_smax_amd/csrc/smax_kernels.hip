@@ -48,12 +48,11 @@
 #include <string.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
-#include <thread>
 #include <vector>
 
 #include "gt_smax_hip.h"
+#include "smax_internal.h"
 
 #define SMAX_THREADS 256                              // 4 independent waves per workgroup
 #define SMAX_SEGS 2                                   // 16-row segments per lane
@@ -183,6 +182,7 @@ __device__ __forceinline__ uint64_t lds_bytes8(const uint8_t *base, uint32_t o) 
 struct Win {
   const uint8_t *glcp;        // global (local-indexed) tables
   const uint8_t *gbwt;
+  const uint64_t *gpk;        // packed BWT groups (index local_row/16 + 1), or null
   const GtSmaxLlv *llv;
   uint64_t numllv, base, N, end, local_len;
   uint32_t *err;
@@ -198,7 +198,7 @@ struct Win {
 };
 
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
-  t.glcp = a.lcp; t.gbwt = a.bwt; t.llv = a.llv; t.numllv = a.numllv;
+  t.glcp = a.lcp; t.gbwt = a.bwt; t.gpk = a.bwtpk; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
   t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr;
   t.val16 = nullptr; t.nval = -1;
@@ -257,7 +257,22 @@ __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(t.P[o >> 4], (uint32_t) (o & 15));
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
   if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
+  if (t.gpk != nullptr)
+    return pk_sym(gld_u64(&t.gpk[(g - t.base) / 16 + 1]), (uint32_t) ((g - t.base) & 15));
   return gld_u8(&t.gbwt[g - t.base]);
+}
+
+// the 16 rows of a packed group as BWT bytes (specials as 254)
+__device__ __forceinline__ uint4 pk_expand(uint64_t w) {
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) x |= pk_sym(w, (uint32_t) (4 * k + q)) << (8 * q);
+    o[k] = x;
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // Plateau scan from start c with exact value l: returns j (last row of the
@@ -1255,7 +1270,9 @@ __device__ static void load_exact_window(const SmaxScanArgs &a, uint64_t l0, Sma
     if (r < 2 || i < SMAX_NCHUNK) {
       const int64_t r0 = (int64_t) l0 - SMAX_LH + 16 * i;
       lv[r] = *reinterpret_cast<const uint4 *>(a.lcp + r0);
-      bv[r] = *reinterpret_cast<const uint4 *>(a.bwt + r0);
+      // packed shards: group l0/16 + i holds the chunk's 16 rows
+      bv[r] = a.bwtpk != nullptr ? pk_expand(a.bwtpk[l0 / 16 + i])
+                                 : *reinterpret_cast<const uint4 *>(a.bwt + r0);
     } else {
       lv[r] = make_uint4(0, 0, 0, 0);
       bv[r] = lv[r];
@@ -1730,7 +1747,7 @@ struct GtSmaxPlan {
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
   uint64_t *bwtpk;           // packed BWT (DNA shards), else null
-  bool pk;
+  bool pk, pk_owned;          // packed windows; bwtpk allocated by the plan
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
   uint32_t *defer_count;
@@ -1748,6 +1765,12 @@ struct GtSmaxPlan {
 };
 
 static SmaxScanArgs plan_args(GtSmaxPlan *p);
+
+// plan buffers come from the runtime's per-device cache (smax_internal.h)
+template <typename T>
+static hipError_t dalloc(T **p, size_t bytes) {
+  return smax_dev_alloc(reinterpret_cast<void **>(p), bytes);
+}
 
 extern "C" int gt_smax_device_count(void) {
   int n = 0;
@@ -1786,8 +1809,6 @@ static uint32_t plan_tiles(const GtSmaxDevShard *s, uint64_t *first) {
   return (uint32_t) (hi - lo + 1);
 }
 
-static double phase_clock();
-static void phase_mark(const char *what, double *t);
 
 extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                                    const GtSmaxDevShard *shard,
@@ -1810,8 +1831,14 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     free(p);
     return -1;
   }
-  if (((uintptr_t) shard->lcp_dev & 15) || ((uintptr_t) shard->bwt_dev & 15)) {
+  if (((uintptr_t) shard->lcp_dev & 15) || ((uintptr_t) shard->bwt_dev & 15) ||
+      ((uintptr_t) shard->bwtpk_dev & 15)) {
     seterr(errbuf, errlen, "device tables must be 16-byte aligned");
+    free(p);
+    return -1;
+  }
+  if (shard->lcp_dev == NULL || (shard->bwt_dev == NULL && shard->bwtpk_dev == NULL)) {
+    seterr(errbuf, errlen, "shard without an LCP or BWT table");
     free(p);
     return -1;
   }
@@ -1824,27 +1851,37 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     const char *d = getenv("GT_SMAX_DEBUG");
     p->dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
   }
-  double tpc = phase_clock();
+  double tpc = smax_phase_clock();
   HIPCHK(hipSetDevice(shard->device));
   {
     int dev_cus = 0, per_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
                                  shard->device));
-    // packed BWT when the shard's alphabet is DNA ({0..3} plus specials)
-    {
-      const uint64_t ngroups = shard->local_len / 16 + 134;
+    // packed BWT: the caller's (ESA builder, host staging), or packed here
+    // from the byte table when the shard's alphabet is DNA ({0..3} plus
+    // specials) -- a plan-time pass over the .bwt bytes
+    if (shard->bwtpk_dev != NULL && !((p->dbg & 8192u) && shard->bwt_dev != NULL)) {
+      p->bwtpk = const_cast<uint64_t *>(shard->bwtpk_dev);
+      p->pk = true;
+      p->pk_owned = false;
+    } else if (shard->bwt_dev == NULL) {
+      seterr(errbuf, errlen, "byte BWT requested (GT_SMAX_DEBUG 8192) but the shard has none");
+      goto fail;
+    } else {
+      p->pk_owned = true;
+      const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
       uint32_t *flag = NULL, hflag = 0;
-      HIPCHK(hipMalloc(&p->bwtpk, sizeof (uint64_t) * ngroups));
-      HIPCHK(hipMalloc(&flag, sizeof (uint32_t)));
+      HIPCHK(dalloc(&p->bwtpk, sizeof (uint64_t) * ngroups));
+      HIPCHK(dalloc(&flag, sizeof (uint32_t)));
       HIPCHK(hipMemset(flag, 0, sizeof (uint32_t)));
       hipLaunchKernelGGL(smax_pack_bwt_kernel, dim3((unsigned) ((ngroups + 255) / 256)), dim3(256),
                          0, 0, shard->bwt_dev, shard->local_len, ngroups, p->bwtpk, flag);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpy(&hflag, flag, sizeof hflag, hipMemcpyDeviceToHost));
-      (void) hipFree(flag);
-      phase_mark(" pack_bwt", &tpc);
+      smax_dev_free(flag);
+      smax_phase_mark(" pack_bwt", &tpc);
       p->pk = hflag == 0 && !(p->dbg & 8192u);
-      if (!p->pk) { (void) hipFree(p->bwtpk); p->bwtpk = NULL; }
+      if (!p->pk) { smax_dev_free(p->bwtpk); p->bwtpk = NULL; }
     }
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, !p->pk ? smax_scan_kernel_bytes : (p->dbg & 256u) ? smax_scan_kernel_pk5
@@ -1868,28 +1905,28 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 2 ? dg : (uint64_t) dev_cus * 2);
     p->static_grid = (uint32_t) dev_cus * 8;   // capped below by the list length
   }
-  phase_mark(" occupancy", &tpc);
-  HIPCHK(hipMalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
-  phase_mark(" out_alloc", &tpc);
-  HIPCHK(hipMalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
-  phase_mark(" slot_alloc", &tpc);
-  HIPCHK(hipMalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
+  smax_phase_mark(" occupancy", &tpc);
+  HIPCHK(dalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
+  smax_phase_mark(" out_alloc", &tpc);
+  HIPCHK(dalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
+  smax_phase_mark(" slot_alloc", &tpc);
+  HIPCHK(dalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
 
-  HIPCHK(hipMalloc(&p->block_sum, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
+  HIPCHK(dalloc(&p->block_sum, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
   HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
-  HIPCHK(hipMalloc(&p->count, sizeof (uint64_t)));
+  HIPCHK(dalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
-  HIPCHK(hipMalloc(&p->bnd, sizeof (GtSmaxBoundary)));
+  HIPCHK(dalloc(&p->bnd, sizeof (GtSmaxBoundary)));
   HIPCHK(hipMemset(p->bnd, 0, sizeof (GtSmaxBoundary)));
   // + 2 zeroed entries: the dummy .llv record of K1's unconditional loads
-  HIPCHK(hipMalloc(&p->llv_win, sizeof (uint2) * (p->num_tiles + 2)));
+  HIPCHK(dalloc(&p->llv_win, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
-  HIPCHK(hipMalloc(&p->err, sizeof (uint32_t)));
+  HIPCHK(dalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
-  HIPCHK(hipMalloc(&p->defer_list, sizeof (uint32_t) * (uint64_t) p->num_tiles));
-  HIPCHK(hipMalloc(&p->defer_count, sizeof (uint32_t)));
+  HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (uint64_t) p->num_tiles));
+  HIPCHK(dalloc(&p->defer_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
-  HIPCHK(hipMalloc(&derr, sizeof (uint32_t)));
+  HIPCHK(dalloc(&derr, sizeof (uint32_t)));
   HIPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
   if (shard->numllv > 0xffffffffull) {
     seterr(errbuf, errlen, "more than 2^32 .llv entries in one shard");
@@ -1898,7 +1935,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   {
     const uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
     const unsigned blocks = (unsigned) ((work + 255) / 256);
-    HIPCHK(hipMalloc(&p->llv16, sizeof (uint16_t) * (shard->numllv + 4)));
+    HIPCHK(dalloc(&p->llv16, sizeof (uint16_t) * (shard->numllv + 4)));
     HIPCHK(hipMemset(p->llv16, 0, sizeof (uint16_t) * (shard->numllv + 4)));
     if (shard->numllv)
       hipLaunchKernelGGL(smax_llv16_kernel, dim3((unsigned) ((shard->numllv + 255) / 256)),
@@ -1911,12 +1948,12 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   }
   if (herr & 1u) { seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
   if (herr & 2u) { seterr(errbuf, errlen, ".llv positions not strictly increasing"); goto fail; }
-  (void) hipFree(derr);
+  smax_dev_free(derr);
   derr = NULL;
   // static K1b list (needs llv_win)
-  phase_mark(" llv_index", &tpc);
-  HIPCHK(hipMalloc(&p->static_list, sizeof (uint32_t) * ((uint64_t) p->num_tiles + 1)));
-  HIPCHK(hipMalloc(&p->static_count, sizeof (uint32_t)));
+  smax_phase_mark(" llv_index", &tpc);
+  HIPCHK(dalloc(&p->static_list, sizeof (uint32_t) * ((uint64_t) p->num_tiles + 1)));
+  HIPCHK(dalloc(&p->static_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->static_count, 0, sizeof (uint32_t)));
   {
     SmaxScanArgs a = plan_args(p);
@@ -1929,14 +1966,14 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     // + 1: the last workgroup computes the boundary head
     p->static_grid = (need < p->static_grid ? need : p->static_grid) + 1;
   }
-  phase_mark(" static_k1b", &tpc);
+  smax_phase_mark(" static_k1b", &tpc);
   HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&p->join, hipEventDisableTiming));
   *planp = p;
   return 0;
 fail:
-  if (derr) (void) hipFree(derr);
+  if (derr) smax_dev_free(derr);
   gt_smax_plan_delete(p);
   return -1;
 }
@@ -1945,7 +1982,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->tile_count, p->block_sum, p->count, p->bnd,
-                  p->llv_win, p->err, p->bwtpk, p->llv16, p->defer_list,
+                  p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
     (void) hipStreamSynchronize(p->side);
@@ -1954,7 +1991,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p->fork) (void) hipEventDestroy(p->fork);
   if (p->join) (void) hipEventDestroy(p->join);
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-    if (bufs[i]) (void) hipFree(bufs[i]);
+    if (bufs[i]) smax_dev_free(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
   free(p->ev);
   free(p);
@@ -2143,7 +2180,6 @@ fail:
   return -1;
 }
 
-static hipError_t d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, hipStream_t s);
 
 extern "C" int gt_smax_plan_fetch_triples(GtSmaxPlan *p, uint64_t *lcp_lb_rb, uint64_t capacity,
                                           uint64_t *count) {
@@ -2153,7 +2189,7 @@ extern "C" int gt_smax_plan_fetch_triples(GtSmaxPlan *p, uint64_t *lcp_lb_rb, ui
   if (gt_smax_plan_fetch_count(p, &c)) return -1;
   *count = c;
   if (c > p->capacity || c > capacity) return -1;   // caller re-plans / enlarges
-  HIPCHK(d2h_triples(lcp_lb_rb, p->out, c, 0));
+  HIPCHK(smax_d2h_triples(lcp_lb_rb, p->out, c, 0));
   return 0;
 fail:
   return -1;
@@ -2189,347 +2225,4 @@ extern "C" uint32_t gt_smax_plan_error_bits(GtSmaxPlan *p) {
   if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;
   if (hipMemcpy(&e, p->err, sizeof e, hipMemcpyDeviceToHost) != hipSuccess) return 0xffffffffu;
   return e;
-}
-
-// ---------------------------------------------------- host-buffer API
-
-struct ShardRun {
-  GtSmaxDevShard sh;
-  uint8_t *lcp, *bwt;
-  GtSmaxLlv *llv;
-  GtSmaxPlan *plan;
-  hipStream_t stream;
-};
-
-// Host work over [0, n) split in equal ranges, f(lo, hi) on up to 8 threads
-// (the inputs are host tables of up to ~10^10 rows).
-template <typename F>
-static void host_parallel_for(uint64_t n, F f) {
-  const unsigned nt = n < (1u << 16) ? 1u
-      : std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < nt; t++)
-    th.emplace_back([=] { f(n * t / nt, n * (t + 1) / nt); });
-  f(0, n / nt);
-  for (auto &x : th) x.join();
-}
-
-static int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
-  if (in == NULL || in->lcptab == NULL || in->bwttab == NULL) {
-    seterr(errbuf, errlen, "missing lcptab or bwttab");
-    return -1;
-  }
-  if (in->numllv > 0 && in->llvtab == NULL) {
-    seterr(errbuf, errlen, "missing llvtab");
-    return -1;
-  }
-  if (in->nonspecials > in->totallength) {
-    seterr(errbuf, errlen, "nonspecials (%lu) exceeds totallength (%lu)",
-           (unsigned long) in->nonspecials, (unsigned long) in->totallength);
-    return -1;
-  }
-  std::vector<uint64_t> bad(8, UINT64_MAX);
-  std::atomic<unsigned> slot{0};
-  host_parallel_for(in->numllv, [&, in](uint64_t lo, uint64_t hi) {
-    uint64_t first = UINT64_MAX;
-    for (uint64_t i = lo; i < hi; i++) {
-      if (in->llvtab[i].position > in->totallength ||
-          (i > 0 && in->llvtab[i].position <= in->llvtab[i - 1].position) ||
-          in->lcptab[in->llvtab[i].position] != 255) {
-        first = i;
-        break;
-      }
-    }
-    bad[slot.fetch_add(1) & 7] = first;
-  });
-  uint64_t first = *std::min_element(bad.begin(), bad.end());
-  if (first != UINT64_MAX) {
-    seterr(errbuf, errlen, "inconsistent .llv entry %lu", (unsigned long) first);
-    return -1;
-  }
-  return 0;
-}
-
-#ifndef GT_SMAX_COPY_THREADS
-#define GT_SMAX_COPY_THREADS 8u    // 16 measured no faster (fill is memory-bound)
-#endif
-
-// Pageable host -> device through two pinned staging buffers: host threads
-// fill one while the DMA engine drains the other.  A plain hipMemcpyAsync
-// from pageable memory goes through the runtime's small staging buffer,
-// one chunk at a time, far below the link rate.  Returns after the copy.
-static hipError_t h2d_staged(void *dst, const void *src, uint64_t len, hipStream_t s) {
-  const uint64_t CH = 64ull << 20;
-  if (len < (16ull << 20)) {
-    hipError_t e = hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, s);
-    return e == hipSuccess ? hipStreamSynchronize(s) : e;
-  }
-  void *buf[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  hipError_t e = hipSuccess;
-  for (int i = 0; i < 2 && e == hipSuccess; i++) {
-    e = hipHostMalloc(&buf[i], CH, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-  }
-  const unsigned nt = std::max(1u, std::min(GT_SMAX_COPY_THREADS, std::thread::hardware_concurrency()));
-  for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += CH, k++) {
-    const int b = (int) (k & 1);
-    const uint64_t c = std::min(CH, len - off);
-    if (k >= 2 && (e = hipEventSynchronize(ev[b])) != hipSuccess) break;
-    const char *from = (const char *) src + off;
-    char *to = (char *) buf[b];
-    const uint64_t part = (c + nt - 1) / nt;
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt && t * part < c; t++)
-      th.emplace_back([=] { memcpy(to + t * part, from + t * part, std::min(part, c - t * part)); });
-    memcpy(to, from, std::min(part, c));
-    for (auto &x : th) x.join();
-    e = hipMemcpyAsync((char *) dst + off, to, c, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipEventRecord(ev[b], s);
-  }
-  hipError_t e2 = hipStreamSynchronize(s);   // drain before the buffers go
-  if (e == hipSuccess) e = e2;
-  for (int i = 0; i < 2; i++) {
-    if (ev[i]) (void) hipEventDestroy(ev[i]);
-    if (buf[i]) (void) hipHostFree(buf[i]);
-  }
-  return e;
-}
-
-// GT_SMAX_TIMING=1: phase times of the host-table entry points on stderr.
-static double phase_clock() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-static void phase_mark(const char *what, double *t) {
-  static int on = -1;
-  if (on < 0) on = getenv("GT_SMAX_TIMING") != NULL;
-  double now = phase_clock();
-  if (on) fprintf(stderr, "[gt_smax timing] %-10s %8.2f ms\n", what, (now - *t) * 1e3);
-  *t = now;
-}
-
-// Device records -> host (lcp, lb, rb) triples through two pinned chunks:
-// the DMA of chunk k+1 overlaps the threaded conversion of chunk k (which
-// also takes the first-touch faults of dst in parallel).
-static hipError_t d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt,
-                              hipStream_t s) {
-  const uint64_t CH = 4ull << 20;   // records per chunk (64 MiB)
-  void *buf[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  hipError_t e = hipSuccess;
-  const uint64_t nch = (cnt + CH - 1) / CH;
-  for (int i = 0; i < 2 && i < (int) nch && e == hipSuccess; i++) {
-    e = hipHostMalloc(&buf[i], sizeof (GtSmaxRecord) * std::min(CH, cnt), hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
-  }
-  auto issue = [&](uint64_t j) {
-    const uint64_t c = std::min(CH, cnt - j * CH);
-    hipError_t r = hipMemcpyAsync(buf[j & 1], dev + j * CH, sizeof (GtSmaxRecord) * c,
-                                  hipMemcpyDeviceToHost, s);
-    return r == hipSuccess ? hipEventRecord(ev[j & 1], s) : r;
-  };
-  if (e == hipSuccess && nch > 0) e = issue(0);
-  for (uint64_t k = 0; e == hipSuccess && k < nch; k++) {
-    // chunk k+1 reuses the buffer of chunk k-1, whose conversion is done
-    if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
-    if ((e = hipEventSynchronize(ev[k & 1])) != hipSuccess) break;
-    const GtSmaxRecord *h = (const GtSmaxRecord *) buf[k & 1];
-    uint64_t *t0 = dst + 3 * k * CH;
-    host_parallel_for(std::min(CH, cnt - k * CH), [=](uint64_t lo, uint64_t hi) {
-      for (uint64_t i = lo; i < hi; i++) {
-        t0[3 * i] = h[i].lcp;
-        t0[3 * i + 1] = h[i].lb;
-        t0[3 * i + 2] = h[i].lb + h[i].width - 1;
-      }
-    });
-  }
-  hipError_t e2 = hipStreamSynchronize(s);
-  if (e == hipSuccess) e = e2;
-  for (int i = 0; i < 2; i++) {
-    if (ev[i]) (void) hipEventDestroy(ev[i]);
-    if (buf[i]) (void) hipHostFree(buf[i]);
-  }
-  return e;
-}
-
-static uint64_t llv_lower(const GtSmaxInput *in, uint64_t g) {
-  uint64_t lo = 0, hi = in->numllv;
-  while (lo < hi) {
-    uint64_t mid = (lo + hi) >> 1;
-    if (in->llvtab[mid].position < g) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-static int run_shards(const GtSmaxInput *in, unsigned int minlen, int nshards,
-                      uint64_t **trip_out, uint64_t *count_out, char *errbuf,
-                      size_t errlen) {
-  const uint64_t N = in->nonspecials;
-  int ndev = gt_smax_device_count();
-  ShardRun *runs = NULL;
-  GtSmaxBoundary *bnds = NULL;
-  uint64_t *counts = NULL, total = 0, *trip = NULL;
-  int rc = -1;
-  *trip_out = NULL;
-  *count_out = 0;
-  if (ndev <= 0) {
-    seterr(errbuf, errlen, "no HIP device available");
-    return -1;
-  }
-  if (N < 2) {
-    *trip_out = (uint64_t *) malloc(sizeof (uint64_t));
-    return 0;
-  }
-  if (nshards < 1) nshards = 1;
-  if ((uint64_t) nshards > N - 1) nshards = (int) (N - 1);
-  double tph = phase_clock();
-  runs = (ShardRun *) calloc((size_t) nshards, sizeof *runs);
-  bnds = (GtSmaxBoundary *) calloc((size_t) nshards, sizeof *bnds);
-  counts = (uint64_t *) calloc((size_t) nshards, sizeof *counts);
-  if (!runs || !bnds || !counts) {
-    seterr(errbuf, errlen, "out of memory");
-    goto fail;
-  }
-  for (int s = 0; s < nshards; s++) {
-    ShardRun *r = &runs[s];
-    uint64_t begin = 1 + (N - 1) * (uint64_t) s / (uint64_t) nshards;
-    uint64_t end = 1 + (N - 1) * (uint64_t) (s + 1) / (uint64_t) nshards;
-    uint64_t base = begin - 1;
-    uint64_t len = end - base + 1;           // LCP[base .. end]
-    uint64_t lo = llv_lower(in, base), hi = llv_lower(in, base + len);
-    r->sh.device = s % ndev;
-    HIPCHK(hipSetDevice(r->sh.device));
-    HIPCHK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-    if (gt_smax_dev_alloc_table(r->sh.device, len, &r->lcp, errbuf, errlen)) goto fail;
-    if (gt_smax_dev_alloc_table(r->sh.device, len, &r->bwt, errbuf, errlen)) goto fail;
-    HIPCHK(h2d_staged(r->lcp, in->lcptab + base, len, r->stream));
-    {
-      uint64_t blen = len <= in->totallength + 1 - base ? len : in->totallength + 1 - base;
-      HIPCHK(h2d_staged(r->bwt, in->bwttab + base, blen, r->stream));
-    }
-    HIPCHK(hipMalloc(&r->llv, sizeof (GtSmaxLlv) * (hi - lo + 1)));
-    if (hi > lo)
-      HIPCHK(h2d_staged(r->llv, in->llvtab + lo, sizeof (GtSmaxLlv) * (hi - lo), r->stream));
-    r->sh.lcp_dev = r->lcp;
-    r->sh.bwt_dev = r->bwt;
-    r->sh.llv_dev = r->llv;
-    r->sh.numllv = hi - lo;
-    r->sh.base = base;
-    r->sh.local_len = len;
-    r->sh.begin = begin;
-    r->sh.end = end;
-    r->sh.nonspecials = N;
-    phase_mark("h2d", &tph);
-    if (gt_smax_plan_create(&r->plan, &r->sh, minlen, 0, errbuf, errlen)) goto fail;
-    phase_mark("plan", &tph);
-    if (gt_smax_plan_run(r->plan, r->stream)) goto fail;
-  }
-  for (int s = 0; s < nshards; s++) {
-    ShardRun *r = &runs[s];
-    HIPCHK(hipSetDevice(r->sh.device));
-    HIPCHK(hipStreamSynchronize(r->stream));
-    HIPCHK(hipMemcpy(&counts[s], r->plan->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(&bnds[s], r->plan->bnd, sizeof (GtSmaxBoundary), hipMemcpyDeviceToHost));
-    {
-      uint32_t e = 0;
-      HIPCHK(hipMemcpy(&e, r->plan->err, sizeof e, hipMemcpyDeviceToHost));
-      if (e != 0) {
-        seterr(errbuf, errlen, "inconsistent index: %s%s",
-               (e & 1u) ? "a .lcp byte 255 without its .llv entry " : "",
-               (e & 2u) ? "a table read outside the shard" : "");
-        goto fail;
-      }
-    }
-    if (counts[s] > r->plan->capacity) {   // re-run with exact capacity
-      uint64_t need = counts[s] + 1;
-      gt_smax_plan_delete(r->plan);
-      r->plan = NULL;
-      if (gt_smax_plan_create(&r->plan, &r->sh, minlen, need, errbuf, errlen)) goto fail;
-      if (gt_smax_plan_run(r->plan, r->stream)) goto fail;
-      HIPCHK(hipStreamSynchronize(r->stream));
-      HIPCHK(hipMemcpy(&counts[s], r->plan->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
-    }
-    total += counts[s] + 1;   // +1 slot for a stitched interval
-  }
-  phase_mark("run", &tph);
-  trip = (uint64_t *) malloc(sizeof (uint64_t) * 3 * (total + 1));
-  if (trip == NULL) {
-    seterr(errbuf, errlen, "out of memory for %lu intervals", (unsigned long) total);
-    goto fail;
-  }
-  total = 0;
-  for (int s = 0; s < nshards; s++) {
-    ShardRun *r = &runs[s];
-    HIPCHK(hipSetDevice(r->sh.device));
-    if (counts[s] > 0)
-      HIPCHK(d2h_triples(trip + 3 * total, r->plan->out, counts[s], r->stream));
-    total += counts[s];
-    GtSmaxRecord rec;
-    if (stitch_resolve(bnds, nshards, s, minlen, &rec)) {
-      trip[3 * total] = rec.lcp;
-      trip[3 * total + 1] = rec.lb;
-      trip[3 * total + 2] = rec.lb + rec.width - 1;
-      total++;
-    }
-  }
-  phase_mark("d2h+triples", &tph);
-  *trip_out = trip;
-  *count_out = total;
-  trip = NULL;
-  rc = 0;
-fail:
-  free(trip);
-  if (runs) {
-    for (int s = 0; s < nshards; s++) {
-      ShardRun *r = &runs[s];
-      if (r->plan) gt_smax_plan_delete(r->plan);
-      gt_smax_dev_free_table(r->sh.device, r->lcp);
-      gt_smax_dev_free_table(r->sh.device, r->bwt);
-      if (r->llv) { (void) hipSetDevice(r->sh.device); (void) hipFree(r->llv); }
-      if (r->stream) (void) hipStreamDestroy(r->stream);
-    }
-  }
-  free(runs);
-  free(bnds);
-  free(counts);
-  return rc;
-}
-
-extern "C" int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in,
-                                               unsigned int minlen,
-                                               int num_gpus,
-                                               uint64_t **lcp_lb_rb,
-                                               uint64_t *count, char *errbuf,
-                                               size_t errlen) {
-  double tv = phase_clock();
-  if (validate_input(in, errbuf, errlen)) return -1;
-  phase_mark("validate", &tv);
-  if (minlen == 0) {
-    seterr(errbuf, errlen, "minlen must be >= 1");
-    return -1;
-  }
-  return run_shards(in, minlen, num_gpus, lcp_lb_rb, count, errbuf, errlen);
-}
-
-extern "C" int gt_smax_hip_enumerate(const GtSmaxInput *in, unsigned int minlen,
-                                     int num_gpus, GtSmaxIntervalFunc cb,
-                                     void *data, char *errbuf, size_t errlen) {
-  uint64_t *trip = NULL, count = 0;
-  if (cb == NULL) {
-    seterr(errbuf, errlen, "no interval callback");
-    return -1;
-  }
-  if (gt_smax_hip_enumerate_to_buffer(in, minlen, num_gpus, &trip, &count,
-                                      errbuf, errlen))
-    return -1;
-  for (uint64_t i = 0; i < count; i++) {
-    if (cb(data, trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]) != 0) {
-      seterr(errbuf, errlen, "interval callback failed at interval %lu",
-             (unsigned long) i);
-      free(trip);
-      return -1;
-    }
-  }
-  free(trip);
-  return 0;
 }

@@ -1,0 +1,801 @@
+// smax_runtime.cpp -- host runtime behind the host-table entry points of
+// include/gt_smax_hip.h (gt_smax_hip_enumerate / _to_buffer), the drop-in
+// replacement of gt_esa_bottomup driving the smax visitor
+// (src/match/esa-bottomup.c:116-273, src/match/esa_visitor_rep.h:46-51).
+//
+// One call: validate the borrowed .lcp/.llv/.bwt tables, split the suffix
+// rows [1, N) into num_gpus shards, and give each used
+// device one host thread that
+//   1. stages its shards' tables into HBM through the device's persistent
+//      pinned ring (threaded host fill overlapping the DMA); the .bwt bytes
+//      are packed to their bit planes during the fill (0.5 B/row over PCIe
+//      and in HBM instead of 1 B/row), so no pass over byte BWT is left for
+//      the device;
+//   2. creates and runs each shard's plan (K0, K1 || static K1b, K1b, K3) on
+//      the device's stream;
+//   3. exchanges the 152-byte boundary records: an RCCL all-gather over the
+//      used devices (ncclAllGather on a communicator the library creates
+//      with ncclCommInitAll, cached for the process), or device-to-device
+//      copies when one device holds every shard; then the device stitch
+//      (smax_stitch_kernel) appends each shard's cross-shard interval;
+//   4. copies its shards' records to the caller's triple array at their
+//      global offsets (pinned ring, threaded conversion to (lcp, lb, rb)).
+// Callbacks then run on the calling thread in ascending lb, as the
+// reference's single-threaded traversal calls them.
+//
+// Device memory (tables, plan buffers) comes from a per-device caching
+// allocator and pinned staging buffers live for the process, so repeated
+// calls do not pay hipMalloc/hipHostMalloc of multi-GB buffers per call;
+// gt_smax_release_cache() returns everything (GT_SMAX_NO_CACHE=1: free
+// before return).
+#include <dlfcn.h>
+#include <emmintrin.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "gt_smax_hip.h"
+#include "smax_internal.h"
+
+namespace {
+
+void seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
+  if (errbuf == NULL || errlen == 0) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(errbuf, errlen, fmt, ap);
+  va_end(ap);
+}
+
+std::string hipmsg(const char *what, hipError_t e) {
+  char b[256];
+  snprintf(b, sizeof b, "%s: %s", what, hipGetErrorString(e));
+  return b;
+}
+
+bool env_on(const char *name) {
+  const char *v = getenv(name);
+  return v != NULL && *v && strcmp(v, "0") != 0;
+}
+
+// ------------------------------------------------------------ device cache
+
+struct Pool {
+  std::mutex mu;
+  std::unordered_map<void *, std::pair<int, size_t>> live;   // ptr -> (device, bytes)
+  std::multimap<std::pair<int, size_t>, void *> idle;        // (device, bytes) -> ptr
+};
+Pool &pool() {
+  static Pool *p = new Pool;   // never destroyed: frees may come from atexit paths
+  return *p;
+}
+
+size_t round_block(size_t bytes) {
+  if (bytes == 0) return 256;
+  if (bytes < (1u << 20)) return (bytes + 255) & ~(size_t) 255;
+  return (bytes + (2u << 20) - 1) & ~(size_t) ((2u << 20) - 1);
+}
+
+void release_idle(int device) {   // pool.mu held
+  Pool &P = pool();
+  int cur = -1;
+  (void) hipGetDevice(&cur);
+  for (auto it = P.idle.begin(); it != P.idle.end();) {
+    if (device >= 0 && it->first.first != device) { ++it; continue; }
+    (void) hipSetDevice(it->first.first);
+    (void) hipFree(it->second);
+    it = P.idle.erase(it);
+  }
+  if (cur >= 0) (void) hipSetDevice(cur);
+}
+
+// ------------------------------------------------------------ timing
+
+// ------------------------------------------------------------ per device
+
+constexpr uint64_t kStage = 64ull << 20;   // pinned staging chunk (bytes)
+
+struct DevCtx {
+  int device = -1;
+  std::mutex mu;                 // one call at a time uses the ring
+  hipStream_t stream = nullptr;
+  void *pin[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
+
+std::mutex g_ctx_mu;
+std::map<int, DevCtx *> g_ctx;
+
+hipError_t ctx_get(int device, DevCtx **out) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  auto it = g_ctx.find(device);
+  if (it != g_ctx.end()) { *out = it->second; return hipSuccess; }
+  DevCtx *c = new DevCtx;
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  for (int i = 0; i < 2 && e == hipSuccess; i++) {
+    e = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    for (int i = 0; i < 2; i++) {
+      if (c->pin[i]) (void) hipHostFree(c->pin[i]);
+      if (c->ev[i]) (void) hipEventDestroy(c->ev[i]);
+    }
+    if (c->stream) (void) hipStreamDestroy(c->stream);
+    delete c;
+    return e;
+  }
+  g_ctx[device] = c;
+  *out = c;
+  return hipSuccess;
+}
+
+// f(lo, hi) over [0, n) on nt threads (the calling thread takes the first part)
+template <typename F>
+void par_for(uint64_t n, unsigned nt, F f) {
+  if (nt <= 1 || n < (1u << 10)) { f(0, n); return; }
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; t++) th.emplace_back([=] { f(n * t / nt, n * (t + 1) / nt); });
+  f(0, n / nt);
+  for (auto &x : th) x.join();
+}
+
+unsigned copy_threads(int ndev) {
+  const char *v = getenv("GT_SMAX_COPY_THREADS");
+  unsigned total = v ? (unsigned) strtoul(v, NULL, 0) : 0u;
+  if (total == 0) total = 8u * (unsigned) std::max(1, std::min(ndev, 2));   // 16 measured no faster than 8 for one device
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  unsigned per = std::max(1u, std::min(total, hw) / (unsigned) std::max(1, ndev));
+  return std::min(per, 8u);
+}
+
+// Host -> device through the context's two pinned chunks: fill(off, n, buf)
+// writes destination bytes [off, off+n) into buf (on nt threads) while the
+// DMA engine drains the other chunk.  fill returns false to abort (*aborted).
+template <typename Fill>
+hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
+                     bool *aborted) {
+  hipError_t e = hipSuccess;
+  if (aborted) *aborted = false;
+  for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += kStage, k++) {
+    const int b = (int) (k & 1);
+    const uint64_t n = std::min(kStage, len - off);
+    if (k >= 2 && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
+    char *buf = (char *) c->pin[b];
+    std::atomic<bool> ok{true};
+    // split at 64-byte units (whole packed groups for the BWT fill)
+    const uint64_t units = (n + 63) / 64;
+    par_for(units, nt, [&, buf, off](uint64_t ulo, uint64_t uhi) {
+      const uint64_t lo = ulo * 64, hi = std::min(n, uhi * 64);
+      if (lo < hi && !fill(off + lo, hi - lo, buf + lo)) ok = false;
+    });
+    if (!ok) {
+      if (aborted) *aborted = true;
+      break;
+    }
+    e = hipMemcpyAsync((char *) dst + off, buf, n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(c->ev[b], c->stream);
+  }
+  hipError_t e2 = hipStreamSynchronize(c->stream);   // the ring is free again on return
+  return e == hipSuccess ? e2 : e;
+}
+
+// packed groups [g0, g1) of bwt[0 .. len) (layout: GT_SMAX_PK_GROUPS in
+// include/gt_smax_hip.h); false when a symbol in [4, 254) is seen
+bool pack_groups(const uint8_t *bwt, uint64_t len, uint64_t g0, uint64_t g1, uint64_t *out) {
+  const __m128i k3 = _mm_set1_epi8(3), k254 = _mm_set1_epi8((char) 254), z = _mm_setzero_si128();
+  __m128i bad = z;
+  bool badscalar = false;
+  for (uint64_t gi = g0; gi < g1; gi++) {
+    const int64_t r0 = ((int64_t) gi - 1) * 16;
+    uint64_t w = 0;
+    if (r0 >= 0 && (uint64_t) r0 + 16 <= len) {
+      const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i *>(bwt + r0));
+      const __m128i sp = _mm_cmpeq_epi8(_mm_max_epu8(v, k254), v);            // v >= 254
+      const __m128i gt3 = _mm_andnot_si128(_mm_cmpeq_epi8(_mm_subs_epu8(v, k3), z),
+                                           _mm_set1_epi8((char) 0xff));      // v > 3
+      bad = _mm_or_si128(bad, _mm_andnot_si128(sp, gt3));
+      const uint32_t spm = (uint32_t) _mm_movemask_epi8(sp);
+      const uint32_t lo = (uint32_t) _mm_movemask_epi8(_mm_slli_epi64(v, 7)) & ~spm;   // bit 0
+      const uint32_t hi = (uint32_t) _mm_movemask_epi8(_mm_slli_epi64(v, 6)) & ~spm;   // bit 1
+      w = (uint64_t) lo | ((uint64_t) hi << 16) | ((uint64_t) spm << 32);
+    } else {
+      for (int q = 0; q < 16; q++) {
+        const int64_t r = r0 + q;
+        if (r < 0 || (uint64_t) r >= len) continue;
+        const uint32_t b = bwt[r];
+        if (b >= 254) w |= 1ull << (32 + q);
+        else {
+          if (b > 3) badscalar = true;
+          w |= (uint64_t) (b & 1u) << q | (uint64_t) ((b >> 1) & 1u) << (16 + q);
+        }
+      }
+    }
+    out[gi - g0] = w;
+  }
+  return !badscalar && _mm_movemask_epi8(bad) == 0;
+}
+
+// device records -> host (lcp, lb, rb) triples through the pinned ring: the
+// DMA of chunk k+1 overlaps the threaded conversion of chunk k
+hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt,
+                       unsigned nt) {
+  const uint64_t CH = kStage / sizeof (GtSmaxRecord);
+  const uint64_t nch = (cnt + CH - 1) / CH;
+  hipError_t e = hipSuccess;
+  auto issue = [&](uint64_t j) {
+    const uint64_t n = std::min(CH, cnt - j * CH);
+    hipError_t r = hipMemcpyAsync(c->pin[j & 1], dev + j * CH, sizeof (GtSmaxRecord) * n,
+                                  hipMemcpyDeviceToHost, c->stream);
+    return r == hipSuccess ? hipEventRecord(c->ev[j & 1], c->stream) : r;
+  };
+  if (nch > 0) e = issue(0);
+  for (uint64_t k = 0; e == hipSuccess && k < nch; k++) {
+    if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
+    if ((e = hipEventSynchronize(c->ev[k & 1])) != hipSuccess) break;
+    const GtSmaxRecord *h = (const GtSmaxRecord *) c->pin[k & 1];
+    uint64_t *t0 = dst + 3 * k * CH;
+    par_for(std::min(CH, cnt - k * CH), nt, [=](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; i++) {
+        t0[3 * i] = h[i].lcp;
+        t0[3 * i + 1] = h[i].lb;
+        t0[3 * i + 2] = h[i].lb + h[i].width - 1;
+      }
+    });
+    // chunk k+2 reuses this buffer: issued only after this conversion
+  }
+  hipError_t e2 = hipStreamSynchronize(c->stream);
+  return e == hipSuccess ? e2 : e;
+}
+
+// ------------------------------------------------------------ RCCL
+
+struct Rccl {
+  bool tried = false, ok = false;
+  void *h = nullptr;
+  decltype(&ncclCommInitAll) init = nullptr;
+  decltype(&ncclAllGather) allgather = nullptr;
+  decltype(&ncclGetErrorString) errstr = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  std::vector<int> devs;              // device set of the cached communicators
+  std::vector<ncclComm_t> comms;
+};
+std::mutex g_rccl_mu;
+Rccl g_rccl;
+
+// Loads RCCL (the library torch already mapped, if any) on first use.
+bool rccl_load(std::string *err) {
+  if (g_rccl.tried) {
+    if (!g_rccl.ok) *err = "RCCL is not available";
+    return g_rccl.ok;
+  }
+  g_rccl.tried = true;
+  const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+  for (const char *n : names)
+    if ((g_rccl.h = dlopen(n, RTLD_NOW | RTLD_GLOBAL)) != nullptr) break;
+  if (g_rccl.h == nullptr) { *err = std::string("dlopen librccl: ") + dlerror(); return false; }
+  g_rccl.init = (decltype(g_rccl.init)) dlsym(g_rccl.h, "ncclCommInitAll");
+  g_rccl.allgather = (decltype(g_rccl.allgather)) dlsym(g_rccl.h, "ncclAllGather");
+  g_rccl.errstr = (decltype(g_rccl.errstr)) dlsym(g_rccl.h, "ncclGetErrorString");
+  g_rccl.destroy = (decltype(g_rccl.destroy)) dlsym(g_rccl.h, "ncclCommDestroy");
+  g_rccl.ok = g_rccl.init && g_rccl.allgather && g_rccl.errstr && g_rccl.destroy;
+  if (!g_rccl.ok) *err = "librccl lacks ncclCommInitAll/ncclAllGather";
+  return g_rccl.ok;
+}
+
+// communicators over devs (one rank per device, rank = position), cached
+bool rccl_comms(const std::vector<int> &devs, std::string *err) {
+  if (!rccl_load(err)) return false;
+  if (g_rccl.devs == devs && !g_rccl.comms.empty()) return true;
+  for (ncclComm_t c : g_rccl.comms) (void) g_rccl.destroy(c);
+  g_rccl.comms.assign(devs.size(), nullptr);
+  g_rccl.devs.clear();
+  ncclResult_t r = g_rccl.init(g_rccl.comms.data(), (int) devs.size(), devs.data());
+  if (r != ncclSuccess) {
+    *err = std::string("ncclCommInitAll: ") + g_rccl.errstr(r);
+    g_rccl.comms.clear();
+    return false;
+  }
+  g_rccl.devs = devs;
+  return true;
+}
+
+// ------------------------------------------------------------ validation
+
+int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
+  if (in == NULL || in->lcptab == NULL || in->bwttab == NULL) {
+    seterr(errbuf, errlen, "missing lcptab or bwttab");
+    return -1;
+  }
+  if (in->numllv > 0 && in->llvtab == NULL) {
+    seterr(errbuf, errlen, "missing llvtab");
+    return -1;
+  }
+  if (in->nonspecials > in->totallength) {
+    seterr(errbuf, errlen, "nonspecials (%lu) exceeds totallength (%lu)",
+           (unsigned long) in->nonspecials, (unsigned long) in->totallength);
+    return -1;
+  }
+  std::mutex mu;
+  uint64_t first = UINT64_MAX;
+  par_for(in->numllv, 8, [&, in](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; i++) {
+      if (in->llvtab[i].position > in->totallength ||
+          (i > 0 && in->llvtab[i].position <= in->llvtab[i - 1].position) ||
+          in->lcptab[in->llvtab[i].position] != 255) {
+        std::lock_guard<std::mutex> g(mu);
+        first = std::min(first, i);
+        break;
+      }
+    }
+  });
+  if (first != UINT64_MAX) {
+    seterr(errbuf, errlen, "inconsistent .llv entry %lu", (unsigned long) first);
+    return -1;
+  }
+  return 0;
+}
+
+uint64_t llv_lower(const GtSmaxInput *in, uint64_t g) {
+  uint64_t lo = 0, hi = in->numllv;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (in->llvtab[mid].position < g) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------ one call
+
+struct Shard {
+  uint64_t begin, end, base, len, lo, hi;
+  GtSmaxDevShard sh;
+  void *lcp = nullptr, *bwt = nullptr, *llv = nullptr;   // pool blocks (tables padded)
+  GtSmaxPlan *plan = nullptr;
+  uint64_t count = 0, offset = 0;
+};
+
+struct Call {
+  const GtSmaxInput *in;
+  unsigned minlen;
+  int nshards = 0, ndev = 0;
+  bool rccl = false;
+  std::vector<int> devs;          // device ordinal of each used device slot
+  std::vector<int> first;         // shards [first[d], first[d+1]) on device slot d
+  std::vector<Shard> sh;
+  std::vector<std::string> err;   // per device slot
+  std::atomic<bool> failed{false};
+  // phase barrier between the device threads (before the collective)
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t *trip = nullptr;
+  unsigned nt = 1;
+  double t0 = 0;
+};
+
+// all device threads meet here; returns false if any of them failed
+bool call_barrier(Call *C) {
+  std::unique_lock<std::mutex> g(C->mu);
+  if (++C->arrived == C->ndev) C->cv.notify_all();
+  else C->cv.wait(g, [C] { return C->arrived == C->ndev; });
+  return !C->failed.load();
+}
+
+void fail_dev(Call *C, int d, const std::string &m) {
+  if (C->err[d].empty()) C->err[d] = m;
+  C->failed = true;
+}
+
+#define DCHK(call)                                              \
+  do {                                                          \
+    hipError_t e_ = (call);                                     \
+    if (e_ != hipSuccess) { fail_dev(C, d, hipmsg(#call, e_)); goto out; } \
+  } while (0)
+
+hipError_t alloc_table(void **raw, uint64_t bytes) {
+  hipError_t e = smax_dev_alloc(raw, bytes + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK);
+  if (e != hipSuccess) return e;
+  char *p = (char *) *raw;
+  e = hipMemset(p, 0, GT_SMAX_PAD_FRONT);
+  if (e == hipSuccess) e = hipMemset(p + GT_SMAX_PAD_FRONT + bytes, 0, GT_SMAX_PAD_BACK);
+  return e;
+}
+
+// Phase 1 of device slot d: upload, plan, run, exchange, stitch, counts.
+void device_phase1(Call *C, int d) {
+  const GtSmaxInput *in = C->in;
+  DevCtx *c = nullptr;
+  char eb[512] = "";
+  bool voted = false;
+  const int dev = C->devs[d];
+  const int s0 = C->first[d], s1 = C->first[d + 1], kmax = C->first[1] - C->first[0];
+  void *send = nullptr, *recv = nullptr, *all = nullptr;
+  DCHK(hipSetDevice(dev));
+  DCHK(ctx_get(dev, &c));
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    double tp = smax_phase_clock();
+    for (int s = s0; s < s1; s++) {
+      Shard &S = C->sh[s];
+      DCHK(alloc_table(&S.lcp, S.len));
+      const char *lsrc = (const char *) in->lcptab + S.base;
+      DCHK(stage_h2d(c, (char *) S.lcp + GT_SMAX_PAD_FRONT, S.len, C->nt,
+                     [lsrc](uint64_t off, uint64_t n, char *buf) {
+                       memcpy(buf, lsrc + off, n);
+                       return true;
+                     }, nullptr));
+      // BWT: bit planes packed during the fill; a non-DNA alphabet aborts
+      // the packed upload and stages the bytes instead
+      const uint64_t ng = GT_SMAX_PK_GROUPS(S.len);
+      const uint8_t *bsrc = in->bwttab + S.base;
+      const uint64_t blen = S.len;
+      bool nondna = env_on("GT_SMAX_BYTE_BWT");
+      if (!nondna) {
+        DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
+        DCHK(stage_h2d(c, S.bwt, sizeof (uint64_t) * ng, C->nt,
+                       [bsrc, blen](uint64_t off, uint64_t n, char *buf) {
+                         return pack_groups(bsrc, blen, off / 8, (off + n) / 8, (uint64_t *) buf);
+                       }, &nondna));
+        S.sh.bwtpk_dev = nondna ? nullptr : (const uint64_t *) S.bwt;
+      }
+      if (nondna) {
+        smax_dev_free(S.bwt);
+        S.bwt = nullptr;
+        DCHK(alloc_table(&S.bwt, S.len));
+        DCHK(stage_h2d(c, (char *) S.bwt + GT_SMAX_PAD_FRONT, S.len, C->nt,
+                       [bsrc](uint64_t off, uint64_t n, char *buf) {
+                         memcpy(buf, bsrc + off, n);
+                         return true;
+                       }, nullptr));
+        S.sh.bwt_dev = (const uint8_t *) S.bwt + GT_SMAX_PAD_FRONT;
+      }
+      DCHK(smax_dev_alloc(&S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo + 1)));
+      if (S.hi > S.lo) {
+        const char *vsrc = (const char *) (in->llvtab + S.lo);
+        DCHK(stage_h2d(c, S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo), C->nt,
+                       [vsrc](uint64_t off, uint64_t n, char *buf) {
+                         memcpy(buf, vsrc + off, n);
+                         return true;
+                       }, nullptr));
+      }
+      S.sh.lcp_dev = (const uint8_t *) S.lcp + GT_SMAX_PAD_FRONT;
+      S.sh.llv_dev = (const GtSmaxLlv *) S.llv;
+      S.sh.numllv = S.hi - S.lo;
+      S.sh.base = S.base;
+      S.sh.local_len = S.len;
+      S.sh.begin = S.begin;
+      S.sh.end = S.end;
+      S.sh.nonspecials = in->nonspecials;
+      S.sh.device = dev;
+      if (d == 0) smax_phase_mark(s == s0 ? "h2d" : "h2d(next)", &tp);
+      if (gt_smax_plan_create(&S.plan, &S.sh, C->minlen, 0, eb, sizeof eb)) {
+        fail_dev(C, d, eb);
+        goto out;
+      }
+      if (d == 0) smax_phase_mark("plan", &tp);
+      if (gt_smax_plan_run(S.plan, c->stream)) { fail_dev(C, d, "plan run failed"); goto out; }
+    }
+    DCHK(hipStreamSynchronize(c->stream));
+    for (int s = s0; s < s1; s++) {
+      Shard &S = C->sh[s];
+      const uint32_t eb2 = gt_smax_plan_error_bits(S.plan);
+      if (eb2 != 0) {
+        snprintf(eb, sizeof eb, "inconsistent index: %s%s",
+                 (eb2 & 1u) ? "a .lcp byte 255 without its .llv entry " : "",
+                 (eb2 & 2u) ? "a table read outside the shard" : "");
+        fail_dev(C, d, eb);
+        goto out;
+      }
+      DCHK(hipMemcpy(&S.count, gt_smax_plan_count_dev(S.plan), sizeof (uint64_t),
+                     hipMemcpyDeviceToHost));
+      if (S.count + 1 > gt_smax_plan_capacity(S.plan)) {   // + 1: a stitched interval
+        gt_smax_plan_delete(S.plan);
+        S.plan = nullptr;
+        if (gt_smax_plan_create(&S.plan, &S.sh, C->minlen, S.count + 16, eb, sizeof eb)) {
+          fail_dev(C, d, eb);
+          goto out;
+        }
+        if (gt_smax_plan_run(S.plan, c->stream)) { fail_dev(C, d, "plan run failed"); goto out; }
+        DCHK(hipStreamSynchronize(c->stream));
+      }
+    }
+    if (d == 0) smax_phase_mark("run", &tp);
+    // ---- boundary exchange: device slot d's records at
+    // send[0 .. s1-s0), all slots gathered to recv[slot * kmax ..], then laid
+    // out in shard order in all[]
+    const size_t B = sizeof (GtSmaxBoundary);
+    DCHK(smax_dev_alloc(&send, B * kmax));
+    DCHK(smax_dev_alloc(&recv, B * kmax * C->ndev));
+    DCHK(smax_dev_alloc(&all, B * C->nshards));
+    DCHK(hipMemsetAsync(send, 0, B * kmax, c->stream));
+    for (int s = s0; s < s1; s++)
+      if (gt_smax_plan_copy_boundary(C->sh[s].plan, (char *) send + B * (s - s0), c->stream)) {
+        fail_dev(C, d, "boundary copy failed");
+        goto out;
+      }
+    voted = true;
+    if (!call_barrier(C)) goto out;          // every slot's plans ran: collective is safe
+    if (C->rccl) {
+      ncclResult_t r = g_rccl.allgather(send, recv, B * kmax, ncclUint8, g_rccl.comms[d], c->stream);
+      if (r != ncclSuccess) {
+        fail_dev(C, d, std::string("ncclAllGather: ") + g_rccl.errstr(r));
+        goto out;
+      }
+    } else {
+      DCHK(hipMemcpyAsync(recv, send, B * kmax, hipMemcpyDeviceToDevice, c->stream));
+    }
+    for (int e = 0; e < C->ndev; e++) {
+      const int n = C->first[e + 1] - C->first[e];
+      if (n > 0)
+        DCHK(hipMemcpyAsync((char *) all + B * C->first[e], (char *) recv + B * kmax * e, B * n,
+                            hipMemcpyDeviceToDevice, c->stream));
+    }
+    for (int s = s0; s < s1; s++)
+      if (gt_smax_plan_stitch(C->sh[s].plan, (const GtSmaxBoundary *) all, C->nshards, s,
+                              c->stream)) {
+        fail_dev(C, d, "stitch failed");
+        goto out;
+      }
+    for (int s = s0; s < s1; s++)
+      DCHK(hipMemcpyAsync(&C->sh[s].count, gt_smax_plan_count_dev(C->sh[s].plan),
+                          sizeof (uint64_t), hipMemcpyDeviceToHost, c->stream));
+    DCHK(hipStreamSynchronize(c->stream));
+    if (d == 0) smax_phase_mark("exchange", &tp);
+  }
+out:
+  if (!voted) call_barrier(C);   // a failed slot still meets the others (no collective then)
+  smax_dev_free(send);
+  smax_dev_free(recv);
+  smax_dev_free(all);
+}
+
+// Phase 2 of device slot d: its shards' records -> triples at their offsets.
+void device_phase2(Call *C, int d) {
+  DevCtx *c = nullptr;
+  const int dev = C->devs[d];
+  DCHK(hipSetDevice(dev));
+  DCHK(ctx_get(dev, &c));
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (int s = C->first[d]; s < C->first[d + 1]; s++) {
+      Shard &S = C->sh[s];
+      if (S.count > 0)
+        DCHK(d2h_triples(c, C->trip + 3 * S.offset, gt_smax_plan_records(S.plan), S.count, C->nt));
+    }
+  }
+out:
+  return;
+}
+
+template <typename F>
+void on_devices(Call *C, F f) {
+  if (C->ndev == 1) { f(C, 0); return; }
+  std::vector<std::thread> th;
+  for (int d = 0; d < C->ndev; d++) th.emplace_back(f, C, d);
+  for (auto &t : th) t.join();
+}
+
+int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **trip_out,
+             uint64_t *count_out, char *errbuf, size_t errlen) {
+  const uint64_t N = in->nonspecials;
+  const int avail = gt_smax_device_count();
+  *trip_out = NULL;
+  *count_out = 0;
+  if (avail <= 0) {
+    seterr(errbuf, errlen, "no HIP device available");
+    return -1;
+  }
+  if (N < 2) {
+    *trip_out = (uint64_t *) malloc(sizeof (uint64_t));
+    return *trip_out ? 0 : -1;
+  }
+  Call C;
+  C.in = in;
+  C.minlen = minlen;
+  C.nshards = std::max(1, num_gpus);
+  if ((uint64_t) C.nshards > N - 1) C.nshards = (int) (N - 1);
+  C.ndev = std::min(C.nshards, avail);
+  for (int d = 0; d < C.ndev; d++) C.devs.push_back(d);
+  // contiguous shard blocks per device slot, the first slots one larger
+  C.first.assign(C.ndev + 1, 0);
+  for (int d = 0; d < C.ndev; d++)
+    C.first[d + 1] = C.first[d] + C.nshards / C.ndev + (d < C.nshards % C.ndev ? 1 : 0);
+  C.err.assign(C.ndev, std::string());
+  C.nt = copy_threads(C.ndev);
+  C.sh.resize(C.nshards);
+  for (int s = 0; s < C.nshards; s++) {
+    Shard &S = C.sh[s];
+    memset(&S.sh, 0, sizeof S.sh);
+    S.begin = 1 + (N - 1) * (uint64_t) s / (uint64_t) C.nshards;
+    S.end = 1 + (N - 1) * (uint64_t) (s + 1) / (uint64_t) C.nshards;
+    S.base = S.begin - 1;
+    S.len = S.end - S.base + 1;               // LCP[base .. end], BWT[base .. end]
+    S.lo = llv_lower(in, S.base);
+    S.hi = llv_lower(in, S.base + S.len);
+  }
+  C.rccl = C.ndev > 1 || env_on("GT_SMAX_FORCE_RCCL");
+  if (C.rccl) {
+    std::lock_guard<std::mutex> g(g_rccl_mu);
+    std::string m;
+    if (!rccl_comms(C.devs, &m)) {
+      seterr(errbuf, errlen, "%s", m.c_str());
+      return -1;
+    }
+  }
+  int rc = -1;
+  std::unique_lock<std::mutex> rl(g_rccl_mu, std::defer_lock);
+  if (C.rccl) rl.lock();   // one call at a time on the cached communicators
+  on_devices(&C, device_phase1);
+  if (!C.failed) {
+    uint64_t total = 0;
+    for (auto &S : C.sh) { S.offset = total; total += S.count; }
+    C.trip = (uint64_t *) malloc(sizeof (uint64_t) * 3 * (total + 1));
+    if (C.trip == NULL) {
+      seterr(errbuf, errlen, "out of memory for %lu intervals", (unsigned long) total);
+    } else {
+      double tp = smax_phase_clock();
+      on_devices(&C, device_phase2);
+      smax_phase_mark("d2h+triples", &tp);
+      if (!C.failed) {
+        *trip_out = C.trip;
+        *count_out = total;
+        C.trip = NULL;
+        rc = 0;
+      }
+    }
+  }
+  if (rc != 0 && (errbuf == NULL || errlen == 0 || errbuf[0] == 0))
+    for (auto &m : C.err)
+      if (!m.empty()) { seterr(errbuf, errlen, "%s", m.c_str()); break; }
+  free(C.trip);
+  for (auto &S : C.sh) {
+    if (S.plan) gt_smax_plan_delete(S.plan);
+    smax_dev_free(S.lcp);
+    smax_dev_free(S.bwt);
+    smax_dev_free(S.llv);
+  }
+  if (env_on("GT_SMAX_NO_CACHE")) gt_smax_release_cache();
+  return rc;
+}
+
+}  // namespace
+
+// ============================================================ internal API
+
+hipError_t smax_dev_alloc(void **ptr, size_t bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const size_t sz = round_block(bytes);
+  Pool &P = pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  // reuse an idle block of this device of at most twice the size
+  auto it = P.idle.lower_bound({dev, sz});
+  if (it != P.idle.end() && it->first.first == dev && it->first.second <= 2 * sz) {
+    *ptr = it->second;
+    P.live[*ptr] = it->first;
+    P.idle.erase(it);
+    return hipSuccess;
+  }
+  e = hipMalloc(ptr, sz);
+  if (e == hipErrorOutOfMemory) {   // give the cached blocks back and retry
+    (void) hipGetLastError();
+    release_idle(dev);
+    e = hipMalloc(ptr, sz);
+  }
+  if (e != hipSuccess) { *ptr = nullptr; return e; }
+  P.live[*ptr] = {dev, sz};
+  return hipSuccess;
+}
+
+void smax_dev_free(void *ptr) {
+  if (ptr == nullptr) return;
+  Pool &P = pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  auto it = P.live.find(ptr);
+  if (it == P.live.end()) return;
+  const auto key = it->second;
+  P.live.erase(it);
+  static const bool nocache = env_on("GT_SMAX_NO_CACHE");
+  if (nocache) {
+    int cur = -1;
+    (void) hipGetDevice(&cur);
+    (void) hipSetDevice(key.first);
+    (void) hipFree(ptr);
+    if (cur >= 0) (void) hipSetDevice(cur);
+  } else {
+    P.idle.insert({key, ptr});
+  }
+}
+
+double smax_phase_clock() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void smax_phase_mark(const char *what, double *t) {
+  static const bool on = env_on("GT_SMAX_TIMING");
+  const double now = smax_phase_clock();
+  if (on) fprintf(stderr, "[gt_smax timing] %-12s %8.2f ms\n", what, (now - *t) * 1e3);
+  *t = now;
+}
+
+hipError_t smax_d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, void *stream) {
+  (void) stream;   // callers synchronised the plan's work already
+  int d = 0;
+  DevCtx *c = nullptr;
+  hipError_t e = hipGetDevice(&d);
+  if (e == hipSuccess) e = ctx_get(d, &c);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(c->mu);
+  return d2h_triples(c, dst, dev, cnt, copy_threads(1));
+}
+
+// ============================================================ C-ABI
+
+extern "C" int gt_smax_pack_bwt(const uint8_t *bwt, uint64_t len, uint64_t *pk) {
+  std::atomic<bool> ok{true};
+  par_for(GT_SMAX_PK_GROUPS(len), copy_threads(1), [&](uint64_t lo, uint64_t hi) {
+    if (!pack_groups(bwt, len, lo, hi, pk + lo)) ok = false;
+  });
+  return ok ? 0 : 1;
+}
+
+extern "C" void gt_smax_release_cache(void) {
+  {
+    Pool &P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    release_idle(-1);
+  }
+}
+
+extern "C" int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in, unsigned int minlen,
+                                               int num_gpus, uint64_t **lcp_lb_rb,
+                                               uint64_t *count, char *errbuf, size_t errlen) {
+  double tv = smax_phase_clock();
+  if (errbuf && errlen) errbuf[0] = 0;
+  if (validate_input(in, errbuf, errlen)) return -1;
+  smax_phase_mark("validate", &tv);
+  if (minlen == 0) {
+    seterr(errbuf, errlen, "minlen must be >= 1");
+    return -1;
+  }
+  return run_call(in, minlen, num_gpus, lcp_lb_rb, count, errbuf, errlen);
+}
+
+extern "C" int gt_smax_hip_enumerate(const GtSmaxInput *in, unsigned int minlen, int num_gpus,
+                                     GtSmaxIntervalFunc cb, void *data, char *errbuf,
+                                     size_t errlen) {
+  uint64_t *trip = NULL, count = 0;
+  if (cb == NULL) {
+    seterr(errbuf, errlen, "no interval callback");
+    return -1;
+  }
+  if (gt_smax_hip_enumerate_to_buffer(in, minlen, num_gpus, &trip, &count, errbuf, errlen))
+    return -1;
+  for (uint64_t i = 0; i < count; i++) {
+    if (cb(data, trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]) != 0) {
+      seterr(errbuf, errlen, "interval callback failed at interval %lu", (unsigned long) i);
+      free(trip);
+      return -1;
+    }
+  }
+  free(trip);
+  return 0;
+}

@@ -6,7 +6,9 @@
  * (src/match/sfx-run.c:213-300): bwttab2file (:174-212), outlcpvalues
  * (src/match/sfx-lcpvalues.c:371-470) and the suffix sort.  Output tables are
  * byte-identical to suffixerator's (.suf values, .lcp bytes, .llv entries,
- * .bwt bytes).  Limited to n+1 < 2^32 suffixes (32-bit suffix array).
+ * .bwt bytes), plus the packed bit-plane BWT the smax scan streams
+ * (GT_SMAX_PK_GROUPS in gt_smax_hip.h), emitted with the BWT bytes.  Limited
+ * to n+1 < 2^32 suffixes (32-bit suffix array).
  */
 #ifndef GT_SMAX_ESA_H
 #define GT_SMAX_ESA_H
@@ -29,6 +31,7 @@ typedef struct {
   uint8_t *bwttab_dev;        /* totallength+1 bytes, GT_SMAX_PAD layout     */
   GtSmaxLlv *llvtab_dev;      /* numllv entries                              */
   uint32_t *suftab_dev;       /* totallength+1 entries, or NULL              */
+  uint64_t *bwtpk_dev;        /* packed BWT, GT_SMAX_PK_GROUPS(totallength+1) */
 } GtSmaxEsaDev;
 
 /* text: n encoded symbols on the host (0..3, 254 wildcard, 255 separator). */
@@ -40,6 +43,10 @@ int gt_smax_esa_build(int device, const uint8_t *text, uint64_t n,
 int gt_smax_esa_download(const GtSmaxEsaDev *esa, uint8_t *lcptab,
                          uint8_t *bwttab, GtSmaxLlv *llvtab, uint64_t *suftab,
                          char *errbuf, size_t errlen);
+
+/* Copies the packed BWT (GT_SMAX_PK_GROUPS(totallength+1) u64) to pk. */
+int gt_smax_esa_download_packed(const GtSmaxEsaDev *esa, uint64_t *pk,
+                                char *errbuf, size_t errlen);
 
 void gt_smax_esa_release(GtSmaxEsaDev *esa);
 

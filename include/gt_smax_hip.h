@@ -39,8 +39,8 @@
  * src/match/esa-maxpairs.c:443 returns haserr ? -1 : 0).  A non-zero return
  * from the interval callback stops the enumeration and is propagated as -1
  * (src/match/esa-bottomup.c:147-157).  Input pointers are borrowed for the
- * duration of the call only; every device and pinned buffer is owned and
- * freed by this layer.
+ * duration of the call only; every device and pinned buffer is owned by this
+ * layer (cached across calls, see gt_smax_release_cache).
  */
 #ifndef GT_SMAX_HIP_H
 #define GT_SMAX_HIP_H
@@ -92,6 +92,17 @@ int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in,
 
 void gt_smax_free(void *ptr);
 
+/* The host-table entry points keep device memory (a per-device cache of
+ * table and plan buffers) and pinned staging buffers for the process, so a
+ * second call does not pay multi-GB allocations again; this returns all of
+ * it (GT_SMAX_NO_CACHE=1 in the environment frees before every return).
+ * num_gpus > 1 splits the suffix rows into num_gpus shards over the visible
+ * devices (contiguous blocks of shards per device, one host thread each);
+ * the shards' boundary records are exchanged with one RCCL all-gather over
+ * those devices (communicators created by the library and cached), or by
+ * device-to-device copies when one device holds all shards. */
+void gt_smax_release_cache(void);
+
 /* Number of HIP devices visible (0 if the runtime has none). */
 int gt_smax_device_count(void);
 
@@ -110,16 +121,40 @@ int gt_smax_device_count(void);
 #define GT_SMAX_PAD_FRONT 256
 #define GT_SMAX_PAD_BACK 32768
 
+/*
+ * Packed BWT (DNA alphabets: symbols 0..3 plus the specials >= 254), the
+ * form the scan streams: 0.5 B per row instead of the .bwt file's 1 B.
+ * u64 group gi (0 <= gi < GT_SMAX_PK_GROUPS(local_len)) holds local rows
+ * r = 16*(gi-1) + q, q = 0..15: bit q = bit 0 and bit 16+q = bit 1 of the
+ * row's symbol, bit 32+q = the row holds a special symbol (>= 254: WILDCARD,
+ * SEPARATOR or the undefined BWT character; its code bits are 0); rows
+ * outside [0, local_len) are all-zero.  Group 0 is the front halo.
+ * Producers: the GPU ESA builder (gt_smax_esa_build), gt_smax_pack_bwt on the
+ * host (the host-table entry points pack while staging), or the plan itself
+ * from bwt_dev (a plan-time pass over the byte table).  Specials are unique
+ * for left diversity, so the packed form loses nothing the smax predicate
+ * reads (src/match/esa-maxpairs.c:24-31).
+ */
+#define GT_SMAX_PK_GROUPS(local_len) ((local_len) / 16 + 134)
+
 typedef struct {
   const uint8_t *lcp_dev;
-  const uint8_t *bwt_dev;
+  const uint8_t *bwt_dev;    /* byte BWT, or NULL when bwtpk_dev is given  */
   const GtSmaxLlv *llv_dev;
   uint64_t numllv;
   uint64_t base, local_len;
   uint64_t begin, end;
   uint64_t nonspecials;      /* global N: LCP[0] = LCP[N] = 0 */
   int device;                /* HIP device ordinal */
+  /* packed BWT (GT_SMAX_PK_GROUPS(local_len) u64, 16-byte aligned), or NULL:
+   * the plan then packs bwt_dev itself when its alphabet is DNA */
+  const uint64_t *bwtpk_dev;
 } GtSmaxDevShard;
+
+/* Host packing of a DNA BWT: writes GT_SMAX_PK_GROUPS(len) groups of
+ * bwt[0 .. len) to pk.  Returns 0, or 1 (pk incomplete) when a symbol in
+ * [4, 254) shows that the alphabet is not DNA. */
+int gt_smax_pack_bwt(const uint8_t *bwt, uint64_t len, uint64_t *pk);
 
 /* Diversity of a run of BWT rows: set of symbols < 254 seen, dup flag. */
 typedef struct {

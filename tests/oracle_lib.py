@@ -192,3 +192,26 @@ def smax_pairs(intervals, suftab):
             for b in range(a + 1, len(occ)):
                 out.append((int(length), occ[a], occ[b]))
     return out
+
+
+def pack_bwt_ref(bwt):
+    """numpy restatement of the packed-BWT layout (GT_SMAX_PK_GROUPS,
+    include/gt_smax_hip.h): group gi holds rows 16*(gi-1) .. +15; bit q / 16+q
+    the symbol's bits 0 / 1, bit 32+q a special (>= 254, code bits 0); rows
+    outside the table are zero.  Returns (groups, is_dna)."""
+    bwt = np.asarray(bwt, dtype=np.uint8)
+    n = len(bwt)
+    ng = n // 16 + 134
+    rows = np.zeros(ng * 16, dtype=np.uint8)
+    valid = np.zeros(ng * 16, dtype=bool)
+    rows[16: 16 + n] = bwt
+    valid[16: 16 + n] = True
+    sp = valid & (rows >= 254)
+    b0 = (valid & ~sp & ((rows & 1) != 0)).reshape(ng, 16)
+    b1 = (valid & ~sp & ((rows & 2) != 0)).reshape(ng, 16)
+    s = sp.reshape(ng, 16)
+    w = 1 << np.arange(16, dtype=np.uint64)
+    out = ((b0 * w).sum(1).astype(np.uint64) | ((b1 * w).sum(1).astype(np.uint64) << np.uint64(16))
+           | ((s * w).sum(1).astype(np.uint64) << np.uint64(32)))
+    is_dna = not np.any((bwt > 3) & (bwt < 254))
+    return out, is_dna

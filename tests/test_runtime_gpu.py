@@ -1,0 +1,91 @@
+"""GPU checks of the host runtime (csrc/smax_runtime.cpp) and of the packed
+BWT input form (GT_SMAX_PK_GROUPS, include/gt_smax_hip.h):
+
+  - the GPU ESA builder's packed BWT equals the numpy restatement of the
+    layout over its own byte BWT;
+  - a plan over the builder's packed BWT, a plan packing the byte BWT itself
+    and the CPU oracle give the same interval arrays;
+  - the host-table entry point (gt_smax_hip_enumerate_to_buffer) with the
+    BWT packed during staging, with the byte fallback, with shards > devices,
+    and through the RCCL all-gather (GT_SMAX_FORCE_RCCL: a one-rank
+    communicator on the single GPU) equals the oracle;
+  - repeated calls on the cached buffers, and after gt_smax_release_cache.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import genometools_smax_amd as G
+import oracle_lib as O
+from conftest import oracle_esa
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def human10():
+    text = G.synth_genome("human", 10_000_000, 7, threads=8)
+    esa = G.DeviceEsa(text, device=0)
+    host = esa.download()
+    yield esa, host
+    esa.release()
+
+
+def test_builder_packed_bwt_matches_layout(human10):
+    esa, host = human10
+    got = esa.packed_bwt()
+    want, dna = O.pack_bwt_ref(host["bwttab"])
+    assert dna
+    assert np.array_equal(got, want)
+
+
+def test_plan_packed_and_byte_bwt_agree(human10):
+    esa, host = human10
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    for packed in (True, False):
+        p = esa.plan(20, packed=packed)
+        p.run()
+        got = p.fetch_triples()
+        p.close()
+        assert np.array_equal(got, want), (packed, len(got), len(want))
+
+
+def _host_call(e, minlen, shards, **env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, minlen, shards)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("env", [{}, {"GT_SMAX_BYTE_BWT": 1}, {"GT_SMAX_FORCE_RCCL": 1}])
+def test_host_entry_variants(shards, env):
+    e = oracle_esa("at1MB")
+    want = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 20)
+    got = _host_call(e, 20, shards, **env)
+    assert np.array_equal(got, want), (shards, env, len(got), len(want))
+
+
+def test_more_shards_than_devices_through_rccl():
+    e = oracle_esa("at1MB")
+    want = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8)
+    got = _host_call(e, 8, 7, GT_SMAX_FORCE_RCCL=1)
+    assert np.array_equal(got, want)
+
+
+def test_repeated_calls_and_cache_release(human10):
+    esa, host = human10
+    args = (host["lcptab"], host["llvtab"], host["bwttab"], esa.totallength, esa.nonspecials, 20)
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    for _ in range(3):
+        assert np.array_equal(G.enumerate_smax(*args, 1), want)
+    G.release_cache()
+    assert np.array_equal(G.enumerate_smax(*args, 2), want)
+    G.release_cache()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase breakdown of the host-table entry point (gt_smax_hip_enumerate_to_buffer)
 on C3: validate / H2D / plan / run / D2H+triples (GT_SMAX_TIMING=1 prints them
-from the C-ABI layer), three calls in a row (the first pays one-time costs)."""
+from the C-ABI layer), several calls in a row (the first pays one-time costs: pinned ring, device cache)."""
 import os
 import sys
 import time
@@ -18,7 +18,7 @@ esa = G.DeviceEsa(text, device=0, keep_suftab=False)
 host = esa.download()
 n, N = esa.totallength, esa.nonspecials
 esa.release()
-for i in range(3):
+for i in range(int(os.environ.get("CALLS", "6"))):
     t0 = time.perf_counter()
     iv = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], n, N, 20, 1)
     print("call %d: %.1f ms, %d intervals" % (i, (time.perf_counter() - t0) * 1e3, len(iv)),
