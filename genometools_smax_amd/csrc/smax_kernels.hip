@@ -68,7 +68,8 @@
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
 #define SMAX_SLOT_WIDE 0x80000000u
-#define SMAX_LLV_CAP 112                              // .llv values staged in K1's LDS (u16)
+#define SMAX_LLV_CAP 512                              // .llv values staged in K1's LDS (u16):
+                                                      // one 16-byte DMA per lane
 #define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
                                                       // records are >= 2 rows apart)
 
@@ -374,7 +375,7 @@ __device__ static void compute_head(const SmaxScanArgs &a) {
 __host__ __device__ __forceinline__ bool static_deferred(const SmaxScanArgs &a, uint64_t g0,
                                                          uint32_t wnf) {
   return g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u) ||
-         wnf > SMAX_LLV_CAP;
+         wnf > SMAX_LLV_CAP - 7;   // staged from the 8-aligned index at or below the first
 }
 
 __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, uint32_t *list,
@@ -454,9 +455,9 @@ __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0
     glds16(a.lcp + l0 + SMAX_TILE, wl + SMAX_LH + SMAX_TILE);
   }
   // u16 copies of the values (plan-time array; K1 defers windows holding a
-  // value >= 65536): two per lane from the even index at or below lo
-  if (n != 0 && lane < SMAX_LLV_CAP / 2 && (uint32_t) (2 * lane) < n + 1)
-    glds4(a.llv16 + (lo & ~1u) + 2 * lane, wv);
+  // value >= 65536): eight per lane from the 8-aligned index at or below lo
+  if (n != 0 && (uint32_t) (8 * lane) < n + (lo & 7u))
+    glds16(a.llv16 + (lo & ~7u) + 8 * lane, wv);
 }
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                              uint32_t lo, uint32_t n) {
@@ -486,8 +487,9 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val16));
   const uint8_t *lb = a.lcp + l0 - SMAX_LH;
   const uint8_t *pb = reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16);
-  const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~1u));
-  const uint32_t nl = n == 0 ? 0u : ((n + 2) / 2 < SMAX_LLV_CAP / 2 ? (n + 2) / 2 : SMAX_LLV_CAP / 2);
+  const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u));
+  const uint32_t nl8 = (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
+  const uint32_t nl = n == 0 ? 0u : (nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8);
   const uint64_t vmask = nl == 0 ? 0ull : (nl >= 64 ? ~0ull : (1ull << nl) - 1);
   const uint64_t imask = ibase != nullptr ? 3ull : 0ull;
   const uint8_t *ib = ibase != nullptr ? reinterpret_cast<const uint8_t *>(ibase) : lb;
@@ -510,7 +512,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
       "s_mov_b64 exec, %11\n\t"
       "s_mov_b32 m0, %6\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %3, %10 offset:0\n\t"
+      "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
       "s_mov_b64 exec, %13\n\t"
       "s_mov_b32 m0, %7\n\t"
       "s_nop 0\n\t"
@@ -1106,8 +1108,8 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   t.rank = wn == 0 ? nullptr : rank;
   t.nval = -1;
   if (wn != 0) {
-    const uint32_t cap = SMAX_LLV_CAP - (wlo & 1u);   // staged from the even index below wlo
-    t.val16 += wlo & 1u;
+    const uint32_t cap = SMAX_LLV_CAP - (wlo & 7u);   // staged from the 8-aligned index below wlo
+    t.val16 += wlo & 7u;
     t.nval = (int) (wn < cap ? wn : cap);
   }
   return segpre_bits;
@@ -1755,6 +1757,7 @@ struct GtSmaxPlan {
   uint32_t *static_count;
   uint32_t n_static, static_grid;
   hipStream_t side;          // K1b over the static list runs here, concurrent with K1
+  int k1b_mode;              // placement of the static K1b (GT_SMAX_K1B_MODE)
   hipEvent_t fork, join;
   uint32_t *err;
   uint32_t dbg;
@@ -1935,8 +1938,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   {
     const uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
     const unsigned blocks = (unsigned) ((work + 255) / 256);
-    HIPCHK(dalloc(&p->llv16, sizeof (uint16_t) * (shard->numllv + 4)));
-    HIPCHK(hipMemset(p->llv16, 0, sizeof (uint16_t) * (shard->numllv + 4)));
+    HIPCHK(dalloc(&p->llv16, sizeof (uint16_t) * (shard->numllv + 16)));
+    HIPCHK(hipMemset(p->llv16, 0, sizeof (uint16_t) * (shard->numllv + 16)));
     if (shard->numllv)
       hipLaunchKernelGGL(smax_llv16_kernel, dim3((unsigned) ((shard->numllv + 255) / 256)),
                          dim3(256), 0, 0, shard->llv_dev, shard->numllv, p->llv16);
@@ -1967,7 +1970,19 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     p->static_grid = (need < p->static_grid ? need : p->static_grid) + 1;
   }
   smax_phase_mark(" static_k1b", &tpc);
-  HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  {
+    // placement of the static K1b list (GT_SMAX_K1B_MODE, measured in
+    // DESIGN.md §5): 0 side stream beside K1, 1 before K1 on the caller's
+    // stream, 2 after K1, 3 side stream of the highest priority, launched
+    // ahead of K1
+    const char *m = getenv("GT_SMAX_K1B_MODE");
+    p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 0;
+    int lo = 0, hi = 0;
+    if (p->k1b_mode == 3 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      HIPCHK(hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, hi));
+    else
+      HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  }
   HIPCHK(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&p->join, hipEventDisableTiming));
   *planp = p;
@@ -2043,7 +2058,24 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     // fork point: after K0's resets (K1b over the static list then runs on
     // the side stream, concurrent with K1; disjoint tiles)
-    HIPCHK(hipEventRecord(p->fork, s));
+    SmaxScanArgs b = a;
+    b.defer_list = p->static_list;
+    b.defer_count = p->static_count;
+    b.k1b_head = 1;
+    const int mode = p->k1b_mode;
+    const bool side = mode == 0 || mode == 3;
+    if (mode == 1) {
+      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, s, b);
+      HIPCHK(hipGetLastError());
+    }
+    if (side) {
+      HIPCHK(hipEventRecord(p->fork, s));
+      HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
+    }
+    if (mode == 3) {   // ahead of K1 on the high-priority stream
+      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, p->side, b);
+      HIPCHK(hipGetLastError());
+    }
     const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
     {
@@ -2061,19 +2093,20 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     }
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
-    HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
-    {
-      SmaxScanArgs b = a;
-      b.defer_list = p->static_list;
-      b.defer_count = p->static_count;
-      b.k1b_head = 1;
+    if (mode == 0) {
       hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, p->side, b);
       HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(p->join, p->side));
-    // join (the static K1b finishes well inside K1), then K1b over K1's
-    // runtime list (exact-queue overflow)
-    HIPCHK(hipStreamWaitEvent(s, p->join, 0));
+    if (mode == 2) {
+      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, s, b);
+      HIPCHK(hipGetLastError());
+    }
+    if (side) {
+      // join (the static K1b finishes inside K1), then K1b over K1's
+      // runtime list (exact-queue overflow)
+      HIPCHK(hipEventRecord(p->join, p->side));
+      HIPCHK(hipStreamWaitEvent(s, p->join, 0));
+    }
     hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
