@@ -814,6 +814,91 @@ class DeviceEsa:
             pass
 
 
+class GtSmaxEsa64Dev(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("totallength", ctypes.c_uint64),
+        ("nonspecials", ctypes.c_uint64),
+        ("row_lo", ctypes.c_uint64),
+        ("row_hi", ctypes.c_uint64),
+        ("numllv", ctypes.c_uint64),
+        ("maxbranchdepth", ctypes.c_uint64),
+        ("averagelcp", ctypes.c_double),
+        ("sort_rounds", ctypes.c_int),
+        ("batches", ctypes.c_int),
+        ("lcptab_dev", ctypes.c_void_p),
+        ("bwttab_dev", ctypes.c_void_p),
+        ("bwtpk_dev", ctypes.c_void_p),
+        ("llvtab_dev", ctypes.c_void_p),
+        ("suftab_dev", ctypes.c_void_p),
+    ]
+
+
+def _esa64_lib():
+    L = _esa_lib()
+    if not getattr(L, "_esa64_ready", False):
+        vp, u64, ci, cs, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t
+        L.gt_smax_esa64_build.argtypes = [ci, vp, u64, u64, u64, ci, u64, ctypes.POINTER(GtSmaxEsa64Dev),
+                                          cs, sz]
+        L.gt_smax_esa64_download.argtypes = [ctypes.POINTER(GtSmaxEsa64Dev), vp, vp, vp, vp, vp, cs, sz]
+        L.gt_smax_esa64_release.argtypes = [ctypes.POINTER(GtSmaxEsa64Dev)]
+        L._esa64_ready = True
+    return L
+
+
+class DeviceEsa64:
+    """Rows [row_lo, row_hi) of a GPU-built ESA of any length
+    (gt_smax_esa64_build: 64-bit suffix array, bucketed, range-restricted)."""
+
+    def __init__(self, text, device=0, row_lo=0, row_hi=0, keep_suftab=False, batch_max=0):
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        self.esa = GtSmaxEsa64Dev()
+        eb = _errbuf()
+        _check(_esa64_lib().gt_smax_esa64_build(device, text.ctypes.data, len(text), int(row_lo),
+                                                int(row_hi), int(keep_suftab), int(batch_max),
+                                                ctypes.byref(self.esa), eb, len(eb)), eb)
+        self.device = device
+        self.totallength = self.esa.totallength
+        self.nonspecials = self.esa.nonspecials
+        self.numllv = self.esa.numllv
+        self.row_lo, self.row_hi = self.esa.row_lo, self.esa.row_hi
+
+    def download(self, suftab=False):
+        L = self.row_hi - self.row_lo
+        lcp = np.empty(L, dtype=np.uint8)
+        bwt = np.empty(L, dtype=np.uint8)
+        llv = np.empty((max(self.numllv, 1), 2), dtype=np.uint64)
+        pk = np.empty(pk_groups(L), dtype=np.uint64)
+        suf = np.empty(L, dtype=np.uint64) if suftab else None
+        eb = _errbuf()
+        _check(_esa64_lib().gt_smax_esa64_download(ctypes.byref(self.esa), lcp.ctypes.data,
+                                                   bwt.ctypes.data, llv.ctypes.data,
+                                                   suf.ctypes.data if suftab else None, pk.ctypes.data,
+                                                   eb, len(eb)), eb)
+        return {"lcptab": lcp, "bwttab": bwt, "llvtab": llv[: self.numllv], "suftab": suf,
+                "bwtpk": pk}
+
+    def plan(self, minlen, begin=None, end=None, capacity=0, packed=True):
+        """smax plan over rows [begin, end) (default: all the rows held may
+        own: the tables must hold LCP[begin-1 .. end])."""
+        N = self.nonspecials
+        begin = max(1, self.row_lo + 1) if begin is None else begin
+        end = min(N, self.row_hi - 1) if end is None else end
+        return SmaxPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
+                        self.row_lo, self.row_hi - self.row_lo, begin, end, N, minlen, self.device,
+                        capacity, bwtpk_ptr=self.esa.bwtpk_dev if packed else None)
+
+    def release(self):
+        if self.esa.lcptab_dev:
+            _esa64_lib().gt_smax_esa64_release(ctypes.byref(self.esa))
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
 SYNTH_KINDS = {"uniform": 0, "human": 1, "plant": 2}
 
 

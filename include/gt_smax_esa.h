@@ -50,6 +50,46 @@ int gt_smax_esa_download_packed(const GtSmaxEsaDev *esa, uint64_t *pk,
 
 void gt_smax_esa_release(GtSmaxEsaDev *esa);
 
+/*
+ * 64-bit, range-restricted builder (esa_build64.hip): the rows
+ * [row_lo, row_hi) of the suffix array of text[0 .. n) (n+1 suffixes,
+ * row_hi == 0 means n+1), for texts of any length -- BASELINE config C5
+ * (12 Gbp, > 2^32 suffixes, 8-byte suftab as the reference mandates there,
+ * src/match/sfx-suffixgetset.c:48-51) and the per-rank builds of a
+ * suffix-array range.  Tables are local: lcptab_dev[i] is
+ * LCP[row_lo + i] (GT_SMAX_PAD layout), likewise bwttab_dev/suftab_dev, the
+ * packed BWT covers the local rows (GT_SMAX_PK_GROUPS(row_hi - row_lo)),
+ * .llv positions are global rows in [row_lo, row_hi).  Byte-identical to
+ * gt_smax_esa_build on the rows both build.  batch_max caps the suffixes
+ * sorted together (0: as the free HBM allows).
+ */
+typedef struct {
+  int device;
+  uint64_t totallength, nonspecials;   /* of the whole text                  */
+  uint64_t row_lo, row_hi;             /* rows held                          */
+  uint64_t numllv, maxbranchdepth;     /* maxbranchdepth: max LCP of the rows */
+  double averagelcp;                   /* over the rows held                 */
+  int sort_rounds, batches;
+  uint8_t *lcptab_dev;
+  uint8_t *bwttab_dev;
+  uint64_t *bwtpk_dev;
+  GtSmaxLlv *llvtab_dev;
+  uint64_t *suftab_dev;                /* 8-byte suffixes, or NULL           */
+} GtSmaxEsa64Dev;
+
+int gt_smax_esa64_build(int device, const uint8_t *text, uint64_t n,
+                        uint64_t row_lo, uint64_t row_hi, int keep_suftab,
+                        uint64_t batch_max, GtSmaxEsa64Dev *out,
+                        char *errbuf, size_t errlen);
+
+/* Copies the held rows' tables to host buffers (any may be NULL). */
+int gt_smax_esa64_download(const GtSmaxEsa64Dev *esa, uint8_t *lcptab,
+                           uint8_t *bwttab, GtSmaxLlv *llvtab,
+                           uint64_t *suftab, uint64_t *bwtpk, char *errbuf,
+                           size_t errlen);
+
+void gt_smax_esa64_release(GtSmaxEsa64Dev *esa);
+
 #ifdef __cplusplus
 }
 #endif
