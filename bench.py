@@ -38,9 +38,11 @@ HBM_PEAK_GBS = 8000.0
 CONFIGS = {
     "c3": dict(kind="human", bases=3_000_000_000, seed=1, minlen=20,
                workload="3 Gbp synthetic human-like DNA (40% repeats), minlen=20"),
-    # C5's plant-like profile (80 % LTR-like families, nested insertions,
-    # minlen 50) at the largest size the GPU suffixerator builds (n+1 < 2^32);
-    # C5 itself (12 Gbp) needs the 64-bit builder
+    # configs[4]: 12 Gbp plant-like (80 % LTR-like families, nested
+    # insertions), minlen 50, > 2^32 suffixes: the 64-bit ESA builder
+    "c5": dict(kind="plant", bases=12_000_000_000, seed=2, minlen=50,
+               workload="12 Gbp synthetic plant-like DNA (80% LTR-like repeats), minlen=50"),
+    # C5's profile at 4.2 Gbp (round-1 proxy, kept for comparison)
     "c5p": dict(kind="plant", bases=4_200_000_000, seed=2, minlen=50,
                 workload="4.2 Gbp synthetic plant-like DNA (80% LTR-like repeats), minlen=50"),
     "c2": dict(kind="uniform", bases=100_000_000, seed=42, minlen=20,
@@ -87,6 +89,8 @@ def main():
                          "rehearsal on one GPU; the measured configuration is nccl = RCCL)")
     ap.add_argument("--one-gpu", action="store_true",
                     help="all ranks on cuda:0 (rehearsal only)")
+    ap.add_argument("--esa64", action="store_true",
+                    help="build with the 64-bit range builder even when the 32-bit one applies")
     ap.add_argument("--byte-bwt", action="store_true",
                     help="plan from the byte BWT (plan-time packing) instead of the builder's "
                          "packed BWT")
@@ -121,21 +125,32 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    # ---- setup (untimed): synthetic genome -> GPU ESA
+    # ---- setup (untimed): synthetic genome -> GPU ESA.  One GPU and
+    # n+1 < 2^32: the 32-bit builder over the whole text; otherwise the
+    # 64-bit builder, each rank building only the rows of its suffix-array
+    # range (LCP[begin-1 .. end])
     t0 = time.time()
     text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
     t_gen = time.time() - t0
     log("rank %d: generated %d symbols in %.1fs" % (rank, len(text), t_gen))
-    t0 = time.time()
-    esa = G.DeviceEsa(text, device=local, keep_suftab=False)
-    t_esa = time.time() - t0
-    n, N = esa.totallength, esa.nonspecials
-    log("rank %d: GPU ESA n=%d N=%d llv=%d rounds=%d in %.1fs"
-        % (rank, n, N, esa.numllv, esa.esa.sort_rounds, t_esa))
-
-    # ---- this rank's suffix-array range
+    n = len(text)
+    N = n - int(np.count_nonzero(text >= 254))
     begin = 1 + (N - 1) * rank // world
     end = 1 + (N - 1) * (rank + 1) // world
+    use64 = world > 1 or n + 1 >= 2 ** 32 or args.esa64
+    t0 = time.time()
+    if use64:
+        esa = G.DeviceEsa64(text, device=local, row_lo=begin - 1, row_hi=end + 1)
+        builder = "64-bit range builder, rows [%d, %d)" % (begin - 1, end + 1)
+    else:
+        esa = G.DeviceEsa(text, device=local, keep_suftab=False)
+        builder = "32-bit builder, whole text"
+    t_esa = time.time() - t0
+    assert (esa.totallength, esa.nonspecials) == (n, N)
+    log("rank %d: GPU ESA (%s) n=%d N=%d llv=%d rounds=%d in %.1fs"
+        % (rank, builder, n, N, esa.numllv, esa.esa.sort_rounds, t_esa))
+    if world > 1 or use64:
+        del text
     # the builder emits the packed bit-plane BWT the scan streams (0.5 B/row),
     # so creating the plan reads no BWT bytes: .llv index (u16 values, per-tile
     # windows), the static K1b list and the plan's buffers (--byte-bwt: the
@@ -205,9 +220,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = esa.download()
         llv_pos = host["llvtab"][:, 0] if len(host["llvtab"]) else np.zeros(0, np.uint64)
+        llv_here = int(np.count_nonzero((llv_pos >= begin - 1) & (llv_pos <= end)))
+        del llv_pos
+    elif use64:
+        llv_here = int(esa.numllv)        # the range build holds exactly these rows
     else:
         llv_pos = esa.download()["llvtab"][:, 0] if esa.numllv else np.zeros(0, np.uint64)
-    llv_here = int(np.count_nonzero((llv_pos >= begin - 1) & (llv_pos <= end)))
+        llv_here = int(np.count_nonzero((llv_pos >= begin - 1) & (llv_pos <= end)))
     rows = end - begin + 1
     # 2 B per suffix row (LCP + BWT byte) + 16 B per .llv entry
     # in range + 16 B per emitted interval record (K1's output)
@@ -241,40 +260,39 @@ def main():
     sample_full = False
     if host is not None:
         import oracle_lib  # noqa: E402  (tests/: the checker, CPU baseline leg only)
+        # parity: the all-core oracle scan (orc_linsmax_mt, row ranges per
+        # pthread, output identical to orc_linsmax) over ALL rows against the
+        # timed path's records, bit for bit
+        threads = max(1, min(len(os.sched_getaffinity(0)), args.cpu_threads))
+        log("parity: oracle linsmax over all %d rows (%d threads)" % (N, threads))
+        t0 = time.perf_counter()
+        res = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen,
+                                 threads=threads)
+        t_mt = time.perf_counter() - t0
+        sample_full = True
+        if not np.array_equal(gpu_trip, res):
+            log("FAIL: GPU (%d intervals) differs from the CPU oracle (%d)"
+                % (len(gpu_trip), len(res)))
+            parity_ok = False
+        else:
+            log("GPU interval array equals the CPU oracle's (%d intervals)" % len(res))
+        # the single-core baseline on a bounded sample of the same rows
         sample = min(N, args.cpu_sample)
-        sample_full = sample == N
         log("cpu baseline: oracle linsmax over %d rows (1 core)" % sample)
         t0 = time.perf_counter()
-        res = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample, minlen)
+        res1 = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample, minlen)
         t_cpu = time.perf_counter() - t0
-        if sample == N:
-            # bit-exact parity of the timed path's output (the plan's records)
-            if not np.array_equal(gpu_trip, res):
-                log("FAIL: GPU (%d intervals) differs from the CPU oracle (%d)"
-                    % (len(gpu_trip), len(res)))
-                parity_ok = False
-            else:
-                log("GPU interval array equals the CPU oracle's (%d intervals)" % len(res))
+        if sample == N and not np.array_equal(res1, res):
+            log("FAIL: single-core CPU scan (%d intervals) != all-core (%d)" % (len(res1), len(res)))
+            parity_ok = False
+        del res1
         cpu = {"value": sample / t_cpu, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
                "sample": "oracle orc_linsmax (single core, -O3) over suffix rows [0,%d) of the same "
                          "tables: %.2fs" % (sample, t_cpu)}
         cpu.update(host_cpu())
-        # all-core figure beside the single-core headline:
-        # orc_linsmax_mt, row ranges per pthread, same output
-        threads = min(len(os.sched_getaffinity(0)), args.cpu_threads)
         if threads > 1:
-            t0 = time.perf_counter()
-            res_mt = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], sample,
-                                        minlen, threads=threads)
-            t_mt = time.perf_counter() - t0
-            if not np.array_equal(res_mt, res):
-                log("FAIL: all-core CPU scan (%d intervals) != single-core (%d)"
-                    % (len(res_mt), len(res)))
-                parity_ok = False
-            cpu["all_cores"] = {"value": sample / t_mt, "cores": threads, "seconds": round(t_mt, 3),
-                                "sample": "orc_linsmax_mt (pthreads, equal row ranges) over the "
-                                          "same rows"}
-            del res_mt
+            cpu["all_cores"] = {"value": N / t_mt, "cores": threads, "seconds": round(t_mt, 3),
+                                "sample": "orc_linsmax_mt (pthreads, equal row ranges) over all rows"}
 
     # end-to-end through the drop-in boundary (host tables in memory -> H2D
     # -> plan -> K0..K3 -> D2H of the (lcp, lb, rb) list): reported beside
@@ -287,7 +305,7 @@ def main():
         t0 = time.perf_counter()
         iv = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], n, N, minlen, 1)
         t_e2e = time.perf_counter() - t0
-        if res is not None and sample == N and not np.array_equal(iv, res):
+        if res is not None and not np.array_equal(iv, res):
             log("FAIL: end-to-end result (%d intervals) differs from the CPU oracle (%d)"
                 % (len(iv), len(res)))
             parity_ok = False
@@ -337,7 +355,8 @@ def main():
                        if res is not None and sample_full else "not checked in this run"),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
-            "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2)},
+            "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2),
+                        "builder": builder},
             # plan creation over the resident tables, outside the timed steps
             "plan_ms": round(t_plan * 1e3, 3),
             "bwt_input": ("byte BWT, packed at plan time" if args.byte_bwt else

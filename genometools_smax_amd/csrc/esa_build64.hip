@@ -71,9 +71,13 @@ void seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
     }                                                                        \
   } while (0)
 
+// Launch sizes: a dispatch holds fewer than 2^32 work-items (the packet's
+// grid size is 32-bit), so every kernel that may see more elements than
+// that (positions of a > 4 Gbp text) is a grid-stride loop over a capped grid.
+constexpr uint64_t kMaxBlocks = (1ull << 32) / 256 - 1;
 inline unsigned blocks(uint64_t n, unsigned t = 256) {
   uint64_t b = (n + t - 1) / t;
-  return (unsigned) (b > 0x7fffffffull ? 0x7fffffffull : (b ? b : 1));
+  return (unsigned) (b > kMaxBlocks ? kMaxBlocks : (b ? b : 1));
 }
 
 // ------------------------------------------------------------ kernels
@@ -142,8 +146,9 @@ __device__ __forceinline__ bool bucket_special(uint32_t id) {
 
 __global__ void k_bucket_count(const uint64_t *P, const uint64_t *S, uint64_t m,
                                unsigned long long *cnt) {
-  const uint64_t p = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (p < m) atomicAdd(&cnt[bucket_of(P, S, p)], 1ull);
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t p = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; p < m; p += stride)
+    atomicAdd(&cnt[bucket_of(P, S, p)], 1ull);
 }
 
 struct InBuckets {
@@ -401,6 +406,16 @@ extern "C" int gt_smax_esa64_build(int device, const uint8_t *text, uint64_t n, 
   HIPCHK(hipGetLastError());
   cnt.resize(kNB);
   HIPCHK(hipMemcpy(cnt.data(), cnt_dev, sizeof (unsigned long long) * kNB, hipMemcpyDeviceToHost));
+  {
+    // every suffix counted once: the batches' buffers are sized from these
+    unsigned long long tot = 0;
+    for (unsigned long long c : cnt) tot += c;
+    if (tot != m) {
+      seterr(errbuf, errlen, "bucket histogram counts %llu suffixes, expected %lu", tot,
+             (unsigned long) m);
+      goto fail;
+    }
+  }
   (void) hipFree(cnt_dev);
   cnt_dev = NULL;
 
@@ -582,6 +597,9 @@ extern "C" int gt_smax_esa64_build(int device, const uint8_t *text, uint64_t n, 
         h += (uint64_t) ns;
       }
       rounds_max = std::max(rounds_max, rounds);
+      if (getenv("GT_SMAX_VERBOSE"))
+        fprintf(stderr, "gt_smax_esa64: batch %zu/%zu: %lu suffixes, %d rounds (depth %lu)\n",
+                bi + 1, bs.size() - 1, (unsigned long) got, rounds, (unsigned long) h);
       // 4. rows
       hipLaunchKernelGGL(k_emit64, dim3(blocks(got)), dim3(256), 0, s, P, S, SEP, SA, dep, got, prev, r0,
                          row_lo, row_hi, out->lcptab_dev, out->bwttab_dev, out->suftab_dev, big,
