@@ -140,8 +140,11 @@ def main():
     use64 = world > 1 or n + 1 >= 2 ** 32 or args.esa64
     t0 = time.time()
     if use64:
-        esa = G.DeviceEsa64(text, device=local, row_lo=begin - 1, row_hi=end + 1)
-        builder = "64-bit range builder, rows [%d, %d)" % (begin - 1, end + 1)
+        # one GPU: all n+1 rows (the host-table leg hands the whole tables
+        # to the drop-in entry point); ranks: LCP[begin-1 .. end] only
+        lo, hi = (0, n + 1) if world == 1 else (begin - 1, end + 1)
+        esa = G.DeviceEsa64(text, device=local, row_lo=lo, row_hi=hi)
+        builder = "64-bit range builder, rows [%d, %d)" % (lo, hi)
     else:
         esa = G.DeviceEsa(text, device=local, keep_suftab=False)
         builder = "32-bit builder, whole text"
