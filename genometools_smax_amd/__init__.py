@@ -22,7 +22,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgtsmax_hip.so")
+LIB_PATH = os.environ.get("GT_SMAX_LIB") or os.path.join(_HERE, "lib", "libgtsmax_hip.so")   # GT_SMAX_LIB: A/B diagnostics
 BIN_DIR = os.path.join(_HERE, "bin")
 
 PAD_FRONT = 256

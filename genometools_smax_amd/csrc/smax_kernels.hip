@@ -70,8 +70,10 @@
 #define SMAX_SLOT_WIDE 0x80000000u
 #define SMAX_LLV_CAP 512                              // .llv values staged in K1's LDS (u16):
                                                       // one 16-byte DMA per lane
-#define SMAX_WSLOT (SMAX_TILE / 2)                    // records per tile slot (starts of
-                                                      // records are >= 2 rows apart)
+#define SMAX_SSLOT 64                                 // packed records per K1 tile slot
+                                                      // (0.25 B per row; a tile with more
+                                                      // goes to K1b, whose 16-byte records
+                                                      // are allocated from the plan's pool)
 
 static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
               "back padding must cover a whole tile plus halo");
@@ -92,13 +94,19 @@ struct SmaxScanArgs {
   uint64_t tile_first;       // first local tile holding an owned row
   uint32_t minlen;
   uint32_t num_tiles;
-  GtSmaxRecord *slots;       // [tile][wave][SMAX_WSLOT] records, row order
+  uint64_t *slots;           // [tile][SMAX_SSLOT] K1's packed records, row order
+  GtSmaxRecord *pool;        // K1b's records, per tile a run allocated at tile_off
+  uint64_t pool_cap;         // records the pool holds
+  unsigned long long *pool_cursor;   // reset by K0
+  uint64_t *tile_off;        // per K1b tile: its first pool record (~0: pool full)
   uint32_t *tile_count;      // [tile][wave] record counts
   uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), zeroed by K0
   GtSmaxBoundary *bnd;
   uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
   uint32_t *defer_count;     // reset by K0
   uint32_t k1b_head;         // K1b: the last workgroup computes the boundary head
+  uint32_t wide_slot0;       // K1b: wide slot of list entry 0 (static list 0, runtime n_static)
+  uint32_t wide_cap;         // wide slots (SMAX_TILE / 2 records each) at the pool's start
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
 
@@ -395,6 +403,7 @@ __global__ void __launch_bounds__(256) smax_head_kernel(SmaxScanArgs a, int with
   if (i < nblock) a.block_sum[i] = 0;
   if (i != 0) return;
   a.bnd->pend_valid = 0;
+  *a.pool_cursor = (unsigned long long) a.wide_cap * (SMAX_TILE / 2);   // past the wide slots
   if (!(a.dbg & 16384u)) *a.defer_count = 0;   // diagnostic: K1b alone on K1's last list
   if (with_head) compute_head(a);
 }
@@ -1009,7 +1018,9 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     // K1b (16-byte records)
     if (__ballot(wide) != 0) return UINT32_MAX;
   }
-  // records in row order, written by the owning lanes
+  // records in row order, written by the owning lanes; a tile with more
+  // records than its slot holds goes to K1b (the writes past the slot land
+  // on its last entry; K1b redoes the tile)
   uint32_t wcount = 0;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -1038,12 +1049,12 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         width = res_w[i];
       }
       if (!(a.dbg & 4096u))
-        wdst[pos] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
+        wdst[min(pos, (uint32_t) SMAX_SSLOT - 1u)] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
       pos++;
     }
     wcount += tot;
   }
-  return wcount;
+  return wcount;   // > SMAX_SSLOT: the caller defers the tile
 }
 
 // next tile's window + the llv_win entry of the tile after it (ring slot iaddr)
@@ -1204,7 +1215,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
 
     // ---- detection, diversity, records (row order)
-    uint64_t *wdst = reinterpret_cast<uint64_t *>(a.slots + tile * (uint64_t) SMAX_WSLOT);
+    uint64_t *wdst = a.slots + tile * (uint64_t) SMAX_SSLOT;
     uint32_t wcount = 0;
     // shard-edge tiles and windows with more .llv values than K1 stages
     // belong to the static K1b list (plan time, smax_static_defer_kernel;
@@ -1214,7 +1225,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     bool defer = !stat && wave_pre && (a.dbg & 128u);
     if (!stat && !defer && wave_pre) {
       wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
-      defer = wcount == UINT32_MAX;   // exact-queue overflow: runtime K1b list
+      // exact-queue overflow (UINT32_MAX) or more records than the tile's
+      // slot holds: runtime K1b list
+      defer = wcount > SMAX_SSLOT;
     }
     if (lane == 0 && !stat) {
       if (defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
@@ -1480,37 +1493,63 @@ smax_defer_kernel(SmaxScanArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if ((a.dbg & 131072u)) tmark = __builtin_readcyclecounter();
-    GtSmaxRecord *wdst = a.slots + tile * (uint64_t) SMAX_WSLOT;
+    // the tile's records: list entry i owns wide slot wide_slot0 + i (a
+    // tile has at most SMAX_TILE / 2 records) -- one pass; beyond the wide
+    // slots, two passes over the starts (count, allocate a run from the
+    // pool's overflow part, write; eval_start_x is deterministic)
+    const uint32_t wslot = a.wide_slot0 + i;
+    const bool inwide = wslot < a.wide_cap;
+    GtSmaxRecord *wdst = nullptr;
     uint32_t wcount = 0;
-    for (uint32_t q0 = 0; q0 < SMAX_TILE; q0 += SMAX_XQ) {
-      // compact this round's starts (row order)
-      uint32_t ns = 0;
-      for (uint32_t s = q0 / 64; s < (q0 + SMAX_XQ) / 64; s++) {
-        const uint64_t m = W->st[s];
-        if ((m >> lane) & 1u) W->list[ns + (uint32_t) __popcll(m & ltm)] = (uint16_t) (s * 64 + lane);
-        ns += (uint32_t) __popcll(m);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
-        bool acc = false;
-        uint32_t cur = 0, b = 0;
-        uint64_t j = 0;
-        if (i0 + lane < ns) {
-          b = W->list[i0 + lane];
-          acc = eval_start_x(a, t, W, g0, b, &cur, &j);
+    const bool nowrite = (a.dbg & (4096u | 32768u)) != 0;
+    if (inwide && !nowrite) {
+      wdst = a.pool + (uint64_t) wslot * (SMAX_TILE / 2);
+      if (lane == 0) a.tile_off[tile] = (uint64_t) wslot * (SMAX_TILE / 2);
+    }
+    for (int pass = 0; pass < 2; pass++) {
+      if (pass == 1) {
+        if (inwide || wcount == 0 || nowrite) break;
+        uint64_t off = 0;
+        if (lane == 0) {
+          off = atomicAdd(a.pool_cursor, (unsigned long long) wcount);
+          if (off + wcount > a.pool_cap) off = ~0ull;   // pool full: the host re-plans
+          a.tile_off[tile] = off;
         }
-        const uint64_t am = __ballot(acc);
-        if (acc) {
-          GtSmaxRecord rec;
-          rec.lb = g0 + b - 1;
-          rec.lcp = cur;
-          rec.width = (uint32_t) (j - (g0 + b) + 2);
-          if (!(a.dbg & 4096u)) wdst[wcount + (uint32_t) __popcll(am & ltm)] = rec;
-        }
-        wcount += (uint32_t) __popcll(am);
+        off = __shfl(off, 0, 64);
+        if (off == ~0ull) break;
+        wdst = a.pool + off;
+        wcount = 0;
       }
-      __builtin_amdgcn_wave_barrier();   // list reused
+      for (uint32_t q0 = 0; q0 < SMAX_TILE; q0 += SMAX_XQ) {
+        // compact this round's starts (row order)
+        uint32_t ns = 0;
+        for (uint32_t s = q0 / 64; s < (q0 + SMAX_XQ) / 64; s++) {
+          const uint64_t m = W->st[s];
+          if ((m >> lane) & 1u) W->list[ns + (uint32_t) __popcll(m & ltm)] = (uint16_t) (s * 64 + lane);
+          ns += (uint32_t) __popcll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+          bool acc = false;
+          uint32_t cur = 0, b = 0;
+          uint64_t j = 0;
+          if (i0 + lane < ns) {
+            b = W->list[i0 + lane];
+            acc = eval_start_x(a, t, W, g0, b, &cur, &j);
+          }
+          const uint64_t am = __ballot(acc);
+          if (acc && wdst != nullptr) {
+            GtSmaxRecord rec;
+            rec.lb = g0 + b - 1;
+            rec.lcp = cur;
+            rec.width = (uint32_t) (j - (g0 + b) + 2);
+            wdst[wcount + (uint32_t) __popcll(am & ltm)] = rec;
+          }
+          wcount += (uint32_t) __popcll(am);
+        }
+        __builtin_amdgcn_wave_barrier();   // list reused
+      }
     }
     if (a.dbg & 32768u)   // diagnostic: per-tile cycles (/16), no counts
       wcount = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
@@ -1573,8 +1612,9 @@ smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, u
 // threads on consecutive output records -> ascending lb overall, coalesced.
 // Also publishes the total.
 __global__ void __launch_bounds__(256)
-smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
-                    const uint32_t *block_sum, uint64_t nslots, GtSmaxRecord *out,
+smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
+                    const uint32_t *block_sum, uint64_t nslots, const GtSmaxRecord *pool,
+                    uint64_t pool_cap, const uint64_t *tile_off, GtSmaxRecord *out,
                     uint64_t capacity, uint64_t *count, uint64_t g00) {
   __shared__ uint32_t sPre[SMAX_CPB + 1];
   __shared__ uint32_t sWave[4];
@@ -1617,10 +1657,12 @@ smax_compact_kernel(const GtSmaxRecord *slots, const uint32_t *slot_count,
     if (base + r >= capacity) continue;
     const uint64_t tile = s0 + lo;
     if (sWide[lo]) {
-      out[base + r] = slots[tile * (uint64_t) SMAX_WSLOT + (r - sPre[lo])];
+      // K1b tile: its run in the pool (absent if the pool was full, which
+      // only happens when the records exceed the capacity: re-planned)
+      const uint64_t off = tile_off[tile];
+      if (off <= pool_cap && off + (r - sPre[lo]) < pool_cap) out[base + r] = pool[off + (r - sPre[lo])];
     } else {
-      const uint64_t v =
-          reinterpret_cast<const uint64_t *>(slots + tile * (uint64_t) SMAX_WSLOT)[r - sPre[lo]];
+      const uint64_t v = slots[tile * (uint64_t) SMAX_SSLOT + (r - sPre[lo])];
       GtSmaxRecord rec;
       rec.lb = g00 + tile * (uint64_t) SMAX_TILE + (v & 0x7ffu) - 1;   // g00: global row of tile 0
       rec.width = (uint32_t) (v >> 11) & SMAX_PK_WMAX;
@@ -1742,7 +1784,11 @@ struct GtSmaxPlan {
   uint64_t tile_first;
   uint32_t grid, compact_grid, defer_grid;
   GtSmaxRecord *out;         // capacity records, ascending lb
-  GtSmaxRecord *slots;       // num_tiles * SMAX_WSLOT
+  uint64_t *slots;           // num_tiles * SMAX_SSLOT packed records (K1)
+  GtSmaxRecord *pool;        // wide_cap wide slots + capacity records (K1b tiles' runs)
+  uint32_t wide_cap;
+  unsigned long long *pool_cursor;
+  uint64_t *tile_off;        // num_tiles
   uint32_t *tile_count;      // num_tiles
   uint32_t *block_sum;       // compact_grid record sums (K1/K1b atomics, K3 offsets)
   uint64_t *count;
@@ -1911,7 +1957,13 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   smax_phase_mark(" occupancy", &tpc);
   HIPCHK(dalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
   smax_phase_mark(" out_alloc", &tpc);
-  HIPCHK(dalloc(&p->slots, sizeof (GtSmaxRecord) * SMAX_WSLOT * (uint64_t) p->num_tiles));
+  HIPCHK(dalloc(&p->slots, sizeof (uint64_t) * SMAX_SSLOT * (uint64_t) p->num_tiles));
+  // K1b's records: a wide slot per list entry for the static list and the
+  // first num_tiles/256 runtime deferrals, then a pool for the rest
+  p->wide_cap = 0;   // set once the static list is known (below)
+  p->pool = NULL;
+  HIPCHK(dalloc(&p->pool_cursor, sizeof (unsigned long long)));
+  HIPCHK(dalloc(&p->tile_off, sizeof (uint64_t) * (uint64_t) p->num_tiles));
   smax_phase_mark(" slot_alloc", &tpc);
   HIPCHK(dalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
 
@@ -1965,6 +2017,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                        a, p->static_list, p->static_count);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&p->n_static, p->static_count, sizeof (uint32_t), hipMemcpyDeviceToHost));
+    p->wide_cap = p->n_static + std::max<uint32_t>(256u, p->num_tiles / 256u);
+    HIPCHK(dalloc(&p->pool, sizeof (GtSmaxRecord) *
+                                ((uint64_t) p->wide_cap * (SMAX_TILE / 2) + capacity)));
     const uint32_t need = (p->n_static + 3) / 4;
     // + 1: the last workgroup computes the boundary head
     p->static_grid = (need < p->static_grid ? need : p->static_grid) + 1;
@@ -1996,7 +2051,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->tile_count, p->block_sum, p->count, p->bnd,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
@@ -2031,6 +2086,12 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.minlen = p->minlen;
   a.num_tiles = p->num_tiles;
   a.slots = p->slots;
+  a.pool = p->pool;
+  a.pool_cap = (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity;
+  a.wide_cap = p->wide_cap;
+  a.wide_slot0 = p->n_static;   // the runtime list (the static list sets 0)
+  a.pool_cursor = p->pool_cursor;
+  a.tile_off = p->tile_off;
   a.tile_count = p->tile_count;
   a.block_sum = p->block_sum;
   a.bnd = p->bnd;
@@ -2062,6 +2123,7 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     b.defer_list = p->static_list;
     b.defer_count = p->static_count;
     b.k1b_head = 1;
+    b.wide_slot0 = 0;
     const int mode = p->k1b_mode;
     const bool side = mode == 0 || mode == 3;
     if (mode == 1) {
@@ -2111,7 +2173,8 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->slots, p->tile_count, p->block_sum, (uint64_t) p->num_tiles,
-                       p->out, p->capacity, p->count,
+                       p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
+                       p->tile_off, p->out, p->capacity, p->count,
                        p->shard.base + p->tile_first * (uint64_t) SMAX_TILE);
     HIPCHK(hipGetLastError());
   }
