@@ -14,14 +14,16 @@
 // One pass = launches on one stream (plus a forked side stream), no host
 // synchronisation:
 //   K0  smax_head_kernel     per-run resets (pending-plateau slot, deferral
-//                            count, the 256-tile block sums)
+//                            count, K1b pool cursor)
 //   K1  smax_scan_kernel     the streaming kernel; K1b smax_defer_kernel over
 //                            the plan-time static list runs beside it on the
 //                            side stream (shard edges, dense-.llv windows) and
 //                            computes the boundary head
-//   K1b smax_defer_kernel    over K1's runtime list (exact-queue overflow)
+//   K1b smax_defer_kernel    over K1's runtime list (exact-queue overflow,
+//                            tiles with more records than a slot holds)
+//   K2  smax_block_sum_kernel  records per 256 tiles (K3's offsets)
 //   K3  smax_compact_kernel  ordered copy of the tiles' records -> ascending
-//                            lb, output offsets from the block sums
+//                            lb
 //
 // K1: every wave is an independent worker on 2048-row tiles (tile = wave id
 // + k * waves in grid; 8 generations of resident 4-wave workgroups), no
@@ -38,8 +40,10 @@
 //            maximum + left diversity from the bit planes); plateaus of
 //            >= 3 rows and 255 bytes (.llv values by rank) go to an exact
 //            queue, evaluated 64 starts at a time;
-//   output   owning lanes write packed 8-byte records in row order into the
-//            tile's slot; lane 0 adds the count to the 256-tile block sum.
+//   output   owning lanes put packed 8-byte records in row order into an
+//            LDS staging slot; lane r then holds record r, and the tile's
+//            slot store (one coalesced instruction) and count are issued at
+//            the start of the next tile, right after its window wait.
 // No MFMA: integer/byte work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -68,7 +72,7 @@
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
 #define SMAX_SLOT_WIDE 0x80000000u
-#define SMAX_LLV_CAP 512                              // .llv values staged in K1's LDS (u16):
+#define SMAX_LLV_CAP 496                              // .llv values staged in K1's LDS (u16):
                                                       // one 16-byte DMA per lane
 #define SMAX_SSLOT 64                                 // packed records per K1 tile slot
                                                       // (0.25 B per row; a tile with more
@@ -100,7 +104,7 @@ struct SmaxScanArgs {
   unsigned long long *pool_cursor;   // reset by K0
   uint64_t *tile_off;        // per K1b tile: its first pool record (~0: pool full)
   uint32_t *tile_count;      // [tile][wave] record counts
-  uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), zeroed by K0
+  uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), written by K2
   GtSmaxBoundary *bnd;
   uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
   uint32_t *defer_count;     // reset by K0
@@ -397,11 +401,8 @@ __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, 
 // K0: per-run resets ahead of K1 (the pending-plateau slot, which any K1 or
 // K1b wave may fill, and K1's deferral count); for an empty shard (begin ==
 // end) also the boundary head, otherwise computed by K1b.
-__global__ void __launch_bounds__(256) smax_head_kernel(SmaxScanArgs a, int with_head,
-                                                        uint32_t nblock) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nblock) a.block_sum[i] = 0;
-  if (i != 0) return;
+__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a, int with_head) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
   a.bnd->pend_valid = 0;
   *a.pool_cursor = (unsigned long long) a.wide_cap * (SMAX_TILE / 2);   // past the wide slots
   if (!(a.dbg & 16384u)) *a.defer_count = 0;   // diagnostic: K1b alone on K1's last list
@@ -915,7 +916,7 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
 template <int DL>
 __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &a, uint64_t g0,
                                               const uint8_t *sL, uint32_t *ent,
-                                              uint64_t *wdst, uint32_t segpre) {
+                                              uint64_t *stg, uint32_t segpre) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const bool all_exact = a.minlen > 128;
@@ -1048,8 +1049,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         lcp = res_lcp[i];
         width = res_w[i];
       }
-      if (!(a.dbg & 4096u))
-        wdst[min(pos, (uint32_t) SMAX_SSLOT - 1u)] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
+      if (!(a.dbg & (4096u | (1u << 21))))
+        stg[min(pos, (uint32_t) SMAX_SSLOT - 1u)] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
       pos++;
     }
     wcount += tot;
@@ -1126,6 +1127,18 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   return segpre_bits;
 }
 
+// A finished tile's records (lane r holds record r) to its slot with one
+// coalesced store, its count, and its share of the 256-tile block sum.
+__device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t tile, uint64_t rec,
+                                                uint32_t cnt) {
+  const int lane = threadIdx.x & 63;
+  if (a.dbg & 4096u) return;
+  if ((uint32_t) lane < cnt && !(a.dbg & (1u << 21))) a.slots[tile * (uint64_t) SMAX_SSLOT + lane] = rec;
+  if (lane == 0) {
+    if (!(a.dbg & (1u << 22))) a.tile_count[tile] = cnt;
+  }
+}
+
 // K1 body.  Interior tiles whose starts the direct path covers are finished
 // here; shard-edge tiles and tiles with more exact starts than the direct
 // path queues are deferred to K1b (their generic path is kept out of K1,
@@ -1140,6 +1153,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
   // per wave: wave_detect_direct's queue and results (3 x SMAX_DLIST u32),
   // compacted segment ids and accepted masks
   __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * SMAX_DLIST + 2 * 64 / 4 + 64];
+  // per wave: the tile's packed records in slot order (one slot's worth)
+  __shared__ __attribute__((aligned(16))) uint64_t sStage[SMAX_THREADS / 64][SMAX_SSLOT];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1168,6 +1183,13 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
                __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]));
 
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
+  // the previous tile's records (lane r holds record r) and count: stored
+  // one iteration late, right after the window wait, so that those stores
+  // (and the block-sum atomic) have a whole tile of work to complete before
+  // the next s_waitcnt vmcnt(0) -- issued at the end of their own tile they
+  // made that wait take their latency (measured 0.22 ms of K1 at C3)
+  uint64_t prec = 0, ptile = ~0ull;
+  uint32_t pcnt = 0;
   for (uint32_t it = 0;; it++) {
     const uint32_t cur = it & 1u;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
@@ -1182,6 +1204,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
+    if (ptile != ~0ull) {
+      smax_flush_tile(a, ptile, prec, pcnt);
+      ptile = ~0ull;
+    }
     // .llv window {lo, n | bit 31: a value >= 65536}
     const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][0]);
     const uint32_t wnf = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][1]);
@@ -1215,7 +1241,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
 
     // ---- detection, diversity, records (row order)
-    uint64_t *wdst = a.slots + tile * (uint64_t) SMAX_SSLOT;
     uint32_t wcount = 0;
     // shard-edge tiles and windows with more .llv values than K1 stages
     // belong to the static K1b list (plan time, smax_static_defer_kernel;
@@ -1224,22 +1249,26 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     const bool stat = static_deferred(a, g0, wnf);
     bool defer = !stat && wave_pre && (a.dbg & 128u);
     if (!stat && !defer && wave_pre) {
-      wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], wdst, segpre_bits);
+      wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], sStage[wave], segpre_bits);
       // exact-queue overflow (UINT32_MAX) or more records than the tile's
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
     }
-    if (lane == 0 && !stat) {
-      if (defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
-      else if (!(a.dbg & 4096u)) {
-        a.tile_count[tile] = wcount;
-        if (wcount) atomicAdd(&a.block_sum[tile / SMAX_CPB], wcount);
-      }
+    if (lane == 0 && defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
+    if (!stat && !defer) {
+      // the tile's records move from the LDS staging to one lane each; they
+      // are stored at the start of the next iteration (see above)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      prec = sStage[wave][lane];
+      ptile = tile;
+      pcnt = wcount;
     }
 
     tile = next;
     if (tile >= a.num_tiles) break;
   }
+  if (ptile != ~0ull) smax_flush_tile(a, ptile, prec, pcnt);
   glds_wait();
 }
 
@@ -1555,7 +1584,6 @@ smax_defer_kernel(SmaxScanArgs a) {
       wcount = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
     if (lane == 0 && !(a.dbg & 4096u)) {
       a.tile_count[tile] = wcount | ((a.dbg & 32768u) ? 0u : SMAX_SLOT_WIDE);   // 16-byte records
-      if (wcount && !(a.dbg & 32768u)) atomicAdd(&a.block_sum[tile / SMAX_CPB], wcount);
     }
     __builtin_amdgcn_wave_barrier();   // window reused by the next tile
   }
@@ -1602,6 +1630,25 @@ smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, u
   }
   pk[gi] = (uint64_t) code | ((uint64_t) sp << 32);
   if (other) atomicOr(flag, 1u);
+}
+
+// ------------------------------------------------------------ K2: block sums
+
+// The records of each SMAX_CPB consecutive tiles (one K3 workgroup's share),
+// from the per-tile counts K1 and K1b wrote.  A separate pass instead of
+// per-tile atomics in K1: the 256 tiles of one block are scanned at the same
+// time by 256 different waves, whose atomics to one address serialised and
+// held up each wave's next window wait.
+__global__ void __launch_bounds__(256)
+smax_block_sum_kernel(const uint32_t *tile_count, uint64_t ntiles, uint32_t *block_sum) {
+  __shared__ uint32_t sW[4];
+  const uint64_t t = blockIdx.x * (uint64_t) SMAX_CPB + threadIdx.x;
+  uint32_t c = t < ntiles ? (tile_count[t] & ~SMAX_SLOT_WIDE) : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0) sW[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = sW[0] + sW[1] + sW[2] + sW[3];
 }
 
 // ------------------------------------------------------------ K3: compact
@@ -1790,7 +1837,7 @@ struct GtSmaxPlan {
   unsigned long long *pool_cursor;
   uint64_t *tile_off;        // num_tiles
   uint32_t *tile_count;      // num_tiles
-  uint32_t *block_sum;       // compact_grid record sums (K1/K1b atomics, K3 offsets)
+  uint32_t *block_sum;       // compact_grid record sums (K2, K3's output offsets)
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
@@ -2110,8 +2157,7 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
   {
     SmaxScanArgs a = plan_args(p);
     const int empty = p->shard.begin >= p->shard.end;
-    hipLaunchKernelGGL(smax_head_kernel, dim3((p->compact_grid + 255) / 256 + 1), dim3(256), 0, s,
-                       a, empty, p->compact_grid);
+    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a, empty);
     HIPCHK(hipGetLastError());
     if (empty) {
       HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
@@ -2170,6 +2216,9 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       HIPCHK(hipStreamWaitEvent(s, p->join, 0));
     }
     hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
+                       p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->slots, p->tile_count, p->block_sum, (uint64_t) p->num_tiles,
