@@ -1143,8 +1143,12 @@ __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t 
 // here; shard-edge tiles and tiles with more exact starts than the direct
 // path queues are deferred to K1b (their generic path is kept out of K1,
 // whose register budget it would otherwise set).
-template <typename WinT>
-__device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
+template <typename WinT, bool DIAG>
+__device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
+  // the production kernel sees dbg == 0 as a constant: every diagnostic
+  // branch (GT_SMAX_DEBUG) folds away, a scalar test and branch each
+  SmaxScanArgs a = a_in;
+  if (!DIAG) a.dbg = 0;
   // every wave is an independent worker with its own double-buffered window:
   // no workgroup barrier anywhere in K1
   __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_THREADS / 64][2];
@@ -1218,7 +1222,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a) {
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
-    if (next < a.num_tiles) {
+    if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
       const uint64_t n2 = next + stride <= last ? next + stride : last;
       issue_next(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u], nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
@@ -1590,18 +1594,18 @@ smax_defer_kernel(SmaxScanArgs a) {
 }
 
 
-// K1 instantiations.  Packed DNA BWT (0.5 B/row of BWT traffic, 8.1 KB of LDS
-// per wave) at 4 waves/SIMD is the default; the 5-wave build (which the LDS
-// budget allows) currently spills VGPRs and is slower -- kept for A/B
-// (GT_SMAX_DEBUG=256).  Byte BWT (any alphabet): 4 waves/SIMD.
+// K1 instantiations.  Packed DNA BWT (0.5 B/row of BWT traffic) at 4
+// waves/SIMD is the production kernel; the _diag build keeps the
+// GT_SMAX_DEBUG ablation switches (used only when the variable is set).
+// Byte BWT (any alphabet): 3-4 waves/SIMD.
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk>(a);
+  smax_scan_body<SmaxWindowPk, false>(a);
 }
-__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_pk5(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk>(a);
+__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, true>(a);
 }
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindow>(a);
+  smax_scan_body<SmaxWindow, false>(a);
 }
 
 // ------------------------------------------------------------ BWT packing
@@ -1980,8 +1984,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       if (!p->pk) { smax_dev_free(p->bwtpk); p->bwtpk = NULL; }
     }
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, !p->pk ? smax_scan_kernel_bytes : (p->dbg & 256u) ? smax_scan_kernel_pk5
-                                                                   : smax_scan_kernel,
+        &per_cu, !p->pk ? smax_scan_kernel_bytes : p->dbg ? smax_scan_kernel_diag
+                                                          : smax_scan_kernel,
         SMAX_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
     // 8 generations of resident workgroups: the dispatcher hands a finished
@@ -2192,8 +2196,8 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       const unsigned lp = pad ? (unsigned) strtoul(pad, NULL, 0) : 0u;
       if ((p->dbg & 16384u) && p->runs > 0)
         ;   // diagnostic: re-run K1b on the first run's deferred tiles
-      else if (p->pk && (p->dbg & 256u))
-        hipLaunchKernelGGL(smax_scan_kernel_pk5, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+      else if (p->pk && p->dbg)
+        hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
       else if (p->pk)
         hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
       else
