@@ -267,8 +267,8 @@ __device__ __forceinline__ uint32_t pk_sym(uint64_t w, uint32_t q) {
 
 __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
-  if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(t.P[o >> 4], (uint32_t) (o & 15));
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
+  if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(t.P[o >> 4], (uint32_t) (o & 15));
   if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
   if (t.gpk != nullptr)
     return pk_sym(gld_u64(&t.gpk[(g - t.base) / 16 + 1]), (uint32_t) ((g - t.base) & 15));
@@ -637,7 +637,7 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
     const uint64_t LX = lds_bytes8(sL, co);
     // BWT symbols of rows c-1 .. c+6 as bytes (specials as 254)
     uint64_t BX;
-    if (t.P != nullptr) {
+    if (t.B == nullptr) {   // packed window (K1 sets B = nullptr: folds at compile time)
       const uint32_t o = co - 1, gi = o >> 4, q = o & 15u;
       const uint64_t w0 = t.P[gi], w1 = t.P[gi + 1];
       const uint32_t a0 = (uint32_t) w0, a1 = (uint32_t) w1;
@@ -748,7 +748,7 @@ __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0
 // unique), *div3 = {BWT[c-1], BWT[c], BWT[c+1]} pairwise distinct.
 __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t *div2,
                                             uint32_t *div3) {
-  if (t.P != nullptr) {
+  if (t.B == nullptr) {   // packed window
     const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1], nw = t.P[(so >> 4) + 1];
     // both code planes at once (low plane bits 0..15, high plane 16..31)
     const uint32_t c = (uint32_t) w, pc = (uint32_t) pw, nc = (uint32_t) nw;
@@ -1104,7 +1104,7 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   const uint4 v0 = *reinterpret_cast<const uint4 *>(&t.L[so]);
   const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
   uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
-  if (t.P != nullptr && !(a.dbg & 1u) &&
+  if (t.B == nullptr && !(a.dbg & 1u) &&
       __popcll(__ballot(segpre_bits & 1u)) + __popcll(__ballot(segpre_bits & 2u)) > 64) {
     // more active segments than one classification step holds (packed
     // windows): keep only segments where some row c can start a record --
