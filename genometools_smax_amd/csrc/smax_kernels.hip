@@ -489,20 +489,22 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
 // l0/16 .. l0/16+131 as 1 KiB + 32 B (2 lanes), the window's .llv values as
 // u16 pairs (vlanes lanes x 4 B), and, if ibase != 0, the llv_win entry at
 // ibase (2 lanes x 4 B) into LDS address iaddr.
-__device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
+// wl: LDS address of the target window (uniform, precomputed per buffer --
+// generic-to-LDS pointer casts carry null checks that cost scalar work per
+// tile); ibase: the llv_win entry to stage at iaddr.
+__device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
                                                 uint32_t lo, uint32_t n, const void *ibase,
                                                 uint32_t iaddr, uint32_t v16, uint32_t v4) {
-  const uint32_t wl = __builtin_amdgcn_readfirstlane(lds_addr(w->L));
-  const uint32_t wp = __builtin_amdgcn_readfirstlane(lds_addr(w->P));
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(lds_addr(w->val16));
+  const uint32_t wp = wl + (uint32_t) offsetof(SmaxWindowPk, P);
+  const uint32_t wv = wl + (uint32_t) offsetof(SmaxWindowPk, val16);
   const uint8_t *lb = a.lcp + l0 - SMAX_LH;
   const uint8_t *pb = reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16);
   const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u));
-  const uint32_t nl8 = (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
-  const uint32_t nl = n == 0 ? 0u : (nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8);
-  const uint64_t vmask = nl == 0 ? 0ull : (nl >= 64 ? ~0ull : (1ull << nl) - 1);
-  const uint64_t imask = ibase != nullptr ? 3ull : 0ull;
-  const uint8_t *ib = ibase != nullptr ? reinterpret_cast<const uint8_t *>(ibase) : lb;
+  const uint32_t nl8 = n == 0 ? 0u : (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
+  const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;   // < 64
+  const uint64_t vmask = (1ull << nl) - 1;
+  const uint64_t imask = 3ull;
+  const uint8_t *ib = reinterpret_cast<const uint8_t *>(ibase);
   uint32_t keep;
   uint64_t ex;
   asm volatile(
@@ -1060,13 +1062,13 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
 
 // next tile's window + the llv_win entry of the tile after it (ring slot iaddr)
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
-                                           uint32_t lo, uint32_t n, const uint2 *info, uint32_t iaddr,
-                                           uint32_t v16, uint32_t v4) {
-  issue_window_pk(a, l0, w, lo, n, info, iaddr, v16, v4);
+                                           uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
+  issue_window_pk(a, l0, wl, lo, n, info, iaddr, v16, v4);
 }
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
-                                           uint32_t lo, uint32_t n, const uint2 *info, uint32_t iaddr,
-                                           uint32_t v16, uint32_t v4) {
+                                           uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
   issue_window(a, l0, w, lo, n);
   if ((threadIdx.x & 63) < 2) glds4(reinterpret_cast<const uint32_t *>(info) + (threadIdx.x & 63), iaddr);
 }
@@ -1173,6 +1175,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   uint16_t *rank = sRank[wave];
 
   // prologue: .llv windows of the first two tiles, then the first window
+  const uint32_t wbase = __builtin_amdgcn_readfirstlane(lds_addr(&sWin[wave][0]));
   const uint32_t info0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
   const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
   if (lane < 2) {
@@ -1224,7 +1227,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // tile's work
     if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
       const uint64_t n2 = next + stride <= last ? next + stride : last;
-      issue_next(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u], nlo, nn,
+      issue_next(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
+                 wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
 
