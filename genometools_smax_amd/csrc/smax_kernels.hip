@@ -74,6 +74,11 @@
 #define SMAX_SLOT_WIDE 0x80000000u
 #define SMAX_LLV_CAP 496                              // .llv values staged in K1's LDS (u16):
                                                       // one 16-byte DMA per lane
+// llv_win[t].y: entries in the window (12 bits), of them in the left halo
+// (5 bits, <= 16), bit 31: K1 leaves the tile to the static K1b list
+#define SMAX_WIN_N(y) ((y) & 0xfffu)
+#define SMAX_WIN_HALO(y) (((y) >> 12) & 0x1fu)
+#define SMAX_WIN_STATIC 0x80000000u
 #define SMAX_SSLOT 64                                 // packed records per K1 tile slot
                                                       // (0.25 B per row; a tile with more
                                                       // goes to K1b, whose 16-byte records
@@ -206,6 +211,7 @@ struct Win {
   const uint32_t *val;        // LDS .llv values in rank order (nval of them), or
   const uint16_t *val16;      // the same as u16 (K1 windows: values < 65536)
   int nval;                   // -1: values not staged (read global by rank)
+  uint32_t halo_ff;           // 255 bytes in the window's left halo (K1)
   uint64_t g0;                // global row of the tile start
   uint64_t llv_base;          // first llv entry of the window
 };
@@ -214,7 +220,7 @@ __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.gpk = a.bwtpk; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
   t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr;
-  t.val16 = nullptr; t.nval = -1;
+  t.val16 = nullptr; t.nval = -1; t.halo_ff = 0;
   t.g0 = 0; t.llv_base = 0;
 }
 
@@ -382,12 +388,11 @@ __device__ static void compute_head(const SmaxScanArgs &a) {
 
 // The plan-time half of K1's deferral rule, shared by K1 and the static list
 // kernel: shard-edge tiles (row 0, begin, end, N: halos outside the shard)
-// and windows whose .llv entries K1 cannot stage (more than SMAX_LLV_CAP, or
-// a value >= 2^16: bit 31 of the llv_win count).
-__host__ __device__ __forceinline__ bool static_deferred(const SmaxScanArgs &a, uint64_t g0,
-                                                         uint32_t wnf) {
-  return g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > a.end || (a.dbg & 64u) ||
-         wnf > SMAX_LLV_CAP - 7;   // staged from the 8-aligned index at or below the first
+// and windows whose .llv entries K1 cannot stage (more than fit from the
+// 8-aligned index at or below the first, or a value >= 2^16) -- decided by
+// smax_llv_index_kernel into bit 31 of the tile's llv_win word.
+__host__ __device__ __forceinline__ bool static_deferred(const SmaxScanArgs &a, uint32_t wnf) {
+  return (wnf & SMAX_WIN_STATIC) != 0 || (a.dbg & 64u);
 }
 
 __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, uint32_t *list,
@@ -395,7 +400,8 @@ __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, 
   const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (t >= a.num_tiles) return;
   const uint64_t g0 = a.base + (a.tile_first + t) * (uint64_t) SMAX_TILE;
-  if (static_deferred(a, g0, a.llv_win[t].y)) list[atomicAdd(count, 1u)] = (uint32_t) t;
+  (void) g0;
+  if (static_deferred(a, a.llv_win[t].y)) list[atomicAdd(count, 1u)] = (uint32_t) t;
 }
 
 // K0: per-run resets ahead of K1 (the pending-plateau slot, which any K1 or
@@ -943,7 +949,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   // segments in row order (an inactive segment holds no byte >= 128)
   uint32_t fbase = 0;
   uint16_t *rank = const_cast<uint16_t *>(t.rank);
-  if (rank != nullptr) fbase = __builtin_amdgcn_readfirstlane(seg_ffcount(*reinterpret_cast<const uint4 *>(t.L)));
+  if (rank != nullptr) fbase = t.halo_ff;   // plan time (llv_win): the halo's 255 bytes
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
@@ -1218,9 +1224,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // .llv window {lo, n | bit 31: a value >= 65536}
     const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][0]);
     const uint32_t wnf = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][1]);
-    const uint32_t wn = wnf & 0x7fffffffu;
+    const uint32_t wn = SMAX_WIN_N(wnf);
     const uint32_t nlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][0]);
-    const uint32_t nn = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][1]) & 0x7fffffffu;
+    const uint32_t nn = SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][1]));
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
@@ -1232,6 +1238,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
 
+    t.halo_ff = SMAX_WIN_HALO(wnf);
     uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
     if (a.dbg & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
       if (a.dbg & (1u << 17)) {
@@ -1254,7 +1261,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // belong to the static K1b list (plan time, smax_static_defer_kernel;
     // run concurrently on the plan's side stream): K1 leaves them alone and
     // never waits on a global .llv read
-    const bool stat = static_deferred(a, g0, wnf);
+    const bool stat = static_deferred(a, wnf);
     bool defer = !stat && wave_pre && (a.dbg & 128u);
     if (!stat && !defer && wave_pre) {
       wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], sStage[wave], segpre_bits);
@@ -1311,7 +1318,7 @@ __device__ static void load_exact_window(const SmaxScanArgs &a, uint64_t l0, Sma
   const int lane = threadIdx.x & 63;
   const uint64_t g0 = a.base + l0;
   const uint2 info = a.llv_win[l0 / SMAX_TILE - a.tile_first];
-  const uint32_t lo = info.x, n = info.y & 0x7fffffffu;
+  const uint32_t lo = info.x, n = SMAX_WIN_N(info.y);
   const uint64_t wb = g0 - SMAX_LH;
   // every load of the window first (3 chunks of LCP and BWT per lane, the
   // first 4 .llv entries per lane), then the LDS writes
@@ -1738,7 +1745,7 @@ smax_llv16_kernel(const GtSmaxLlv *llv, uint64_t numllv, uint16_t *out) {
 }
 
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
-                                      uint64_t base, uint64_t tile_first,
+                                      uint64_t base, uint64_t tile_first, uint64_t end,
                                       uint32_t num_tiles, uint2 *win_out,
                                       uint32_t *err) {
   const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
@@ -1760,10 +1767,16 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
     const uint64_t mid = (lo2 + hi2) >> 1;
     if (llv[mid].position < key2) lo2 = mid + 1; else hi2 = mid;
   }
-  uint32_t wide = 0;                       // K1 stages values as u16
-  for (uint64_t k = lo; k < lo2; k++)
-    if (llv[k].value > 0xffffull) { wide = 0x80000000u; break; }
-  win_out[t] = make_uint2((uint32_t) lo, (uint32_t) (lo2 - lo) | wide);
+  bool wide = false;                       // K1 stages values as u16
+  uint32_t halo = 0;                       // entries in the left halo [g0 - LH, g0)
+  for (uint64_t k = lo; k < lo2; k++) {
+    if (llv[k].value > 0xffffull) wide = true;
+    if (llv[k].position < g0) halo++;
+  }
+  const uint32_t wn = (uint32_t) (lo2 - lo);   // <= SMAX_LDSB rows
+  const bool stat = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > end || wide ||
+                    wn + ((uint32_t) lo & 7u) > SMAX_LLV_CAP;
+  win_out[t] = make_uint2((uint32_t) lo, wn | (halo << 12) | (stat ? SMAX_WIN_STATIC : 0u));
 }
 
 // ------------------------------------------------------------ stitch
@@ -2051,7 +2064,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       hipLaunchKernelGGL(smax_llv16_kernel, dim3((unsigned) ((shard->numllv + 255) / 256)),
                          dim3(256), 0, 0, shard->llv_dev, shard->numllv, p->llv16);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
-                       shard->llv_dev, shard->numllv, shard->base, p->tile_first,
+                       shard->llv_dev, shard->numllv, shard->base, p->tile_first, shard->end,
                        p->num_tiles, p->llv_win, derr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
