@@ -212,6 +212,9 @@ struct Win {
   const uint16_t *val16;      // the same as u16 (K1 windows: values < 65536)
   int nval;                   // -1: values not staged (read global by rank)
   uint32_t halo_ff;           // 255 bytes in the window's left halo (K1)
+  bool staged_all;            // K1: every value of the window is staged (nval of
+                              // them; the static flag guarantees it) -- a constant
+                              // in K1, so the global fallback folds away
   uint64_t g0;                // global row of the tile start
   uint64_t llv_base;          // first llv entry of the window
 };
@@ -220,7 +223,7 @@ __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.gpk = a.bwtpk; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
   t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr;
-  t.val16 = nullptr; t.nval = -1; t.halo_ff = 0;
+  t.val16 = nullptr; t.nval = -1; t.halo_ff = 0; t.staged_all = false;
   t.g0 = 0; t.llv_base = 0;
 }
 
@@ -240,6 +243,7 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
     if (within < 8) cnt = __popcll(lo & ((1ull << (8 * within)) - 1));
     else cnt = __popcll(lo) + __popcll(hi & ((1ull << (8 * (within - 8))) - 1));
     const uint32_t r = t.rank[chunk] + (uint32_t) cnt;
+    if (t.staged_all) return t.val16[min((int) r, t.nval - 1)];
     if ((int) r < t.nval) return t.val16 != nullptr ? t.val16[r] : t.val[r];
     if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
     return llv_value(&t.llv[t.llv_base + r]);
@@ -472,7 +476,7 @@ __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0
   }
   // u16 copies of the values (plan-time array; K1 defers windows holding a
   // value >= 65536): eight per lane from the 8-aligned index at or below lo
-  if (n != 0 && (uint32_t) (8 * lane) < n + (lo & 7u))
+  if (n != 0 && lane < SMAX_LLV_CAP / 8 && (uint32_t) (8 * lane) < n + (lo & 7u))
     glds16(a.llv16 + (lo & ~7u) + 8 * lane, wv);
 }
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
@@ -587,6 +591,7 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 }
 
 __device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
+  if (t.staged_all) return t.val16[min((int) r, t.nval - 1)];
   if ((int) r < t.nval) return t.val16 != nullptr ? t.val16[r] : t.val[r];
   if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
   return llv_value(&t.llv[t.llv_base + r]);
@@ -1170,14 +1175,16 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t stride = (uint64_t) gridDim.x * (SMAX_THREADS / 64);
-  const uint64_t last = a.num_tiles - 1;
+  // tile indices are 32-bit (num_tiles < 2^32): one scalar op each
+  const uint32_t stride = gridDim.x * (SMAX_THREADS / 64);
+  const uint32_t last = a.num_tiles - 1;
 
-  uint64_t tile = (uint64_t) blockIdx.x * (SMAX_THREADS / 64) + wave;
+  uint32_t tile = blockIdx.x * (SMAX_THREADS / 64) + (uint32_t) wave;
   if (tile >= a.num_tiles) return;
 
   Win t;
   win_init(t, a);
+  t.staged_all = true;   // non-static tiles: all window values staged
   uint16_t *rank = sRank[wave];
 
   // prologue: .llv windows of the first two tiles, then the first window
@@ -1193,7 +1200,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   glds_wait();
   issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0],
                __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
-               __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]));
+               SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])));
 
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
   // the previous tile's records (lane r holds record r) and count: stored
@@ -1201,13 +1208,13 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // (and the block-sum atomic) have a whole tile of work to complete before
   // the next s_waitcnt vmcnt(0) -- issued at the end of their own tile they
   // made that wait take their latency (measured 0.22 ms of K1 at C3)
-  uint64_t prec = 0, ptile = ~0ull;
-  uint32_t pcnt = 0;
+  uint64_t prec = 0;
+  uint32_t ptile = ~0u, pcnt = 0;
   for (uint32_t it = 0;; it++) {
     const uint32_t cur = it & 1u;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
-    const uint64_t next = tile + stride;
+    const uint32_t next = tile + stride;
     WinT *W = &sWin[wave][cur];
     t.g0 = g0;
     t.L = W->L;
@@ -1217,22 +1224,24 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
-    if (ptile != ~0ull) {
+    if (ptile != ~0u) {
       smax_flush_tile(a, ptile, prec, pcnt);
-      ptile = ~0ull;
+      ptile = ~0u;
     }
-    // .llv window {lo, n | bit 31: a value >= 65536}
-    const uint32_t wlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][0]);
-    const uint32_t wnf = __builtin_amdgcn_readfirstlane(sInfo[wave][cur][1]);
+    // .llv windows of this tile and the next {lo, packed count word}: one
+    // 16-byte LDS read
+    const uint4 info = *reinterpret_cast<const uint4 *>(&sInfo[wave][0][0]);
+    const uint32_t wlo = __builtin_amdgcn_readfirstlane(cur ? info.z : info.x);
+    const uint32_t wnf = __builtin_amdgcn_readfirstlane(cur ? info.w : info.y);
     const uint32_t wn = SMAX_WIN_N(wnf);
-    const uint32_t nlo = __builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][0]);
-    const uint32_t nn = SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][cur ^ 1u][1]));
+    const uint32_t nlo = __builtin_amdgcn_readfirstlane(cur ? info.x : info.z);
+    const uint32_t nn = SMAX_WIN_N(__builtin_amdgcn_readfirstlane(cur ? info.y : info.w));
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
     if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
-      const uint64_t n2 = next + stride <= last ? next + stride : last;
+      const uint32_t n2 = next + stride <= last ? next + stride : last;
       issue_next(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
@@ -1283,7 +1292,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     tile = next;
     if (tile >= a.num_tiles) break;
   }
-  if (ptile != ~0ull) smax_flush_tile(a, ptile, prec, pcnt);
+  if (ptile != ~0u) smax_flush_tile(a, ptile, prec, pcnt);
   glds_wait();
 }
 
