@@ -140,6 +140,8 @@ def lib():
         L.gt_smax_free.argtypes = [vp]
         L.gt_smax_release_cache.argtypes = []
         L.gt_smax_pack_bwt.argtypes = [vp, u64, vp]
+        L.gt_smax_encode_fasta.argtypes = [ctypes.c_char_p, u64, vp, ctypes.POINTER(u64),
+                                           ctypes.POINTER(u64), cs, sz]
         L.gt_smax_device_count.restype = ci
         L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
         L.gt_smax_dev_free_table.argtypes = [ci, vp]
@@ -696,6 +698,18 @@ def pack_bwt(bwt):
     out = np.zeros(pk_groups(len(bwt)), dtype=np.uint64)
     rc = lib().gt_smax_pack_bwt(bwt.ctypes.data, len(bwt), out.ctypes.data)
     return out, rc == 0
+
+
+def encode_fasta(buf):
+    """FASTA bytes -> (encoded text, number of sequences): gt_smax_encode_fasta
+    (the GPU suffixerator's host-side reader; no GPU involved)."""
+    buf = bytes(buf)
+    out = np.empty(len(buf) + 1, dtype=np.uint8)
+    n, ns = ctypes.c_uint64(), ctypes.c_uint64()
+    eb = _errbuf()
+    _check(lib().gt_smax_encode_fasta(buf, len(buf), out.ctypes.data, ctypes.byref(n), ctypes.byref(ns),
+                                      eb, len(eb)), eb)
+    return out[: n.value].copy(), ns.value
 
 
 def release_cache():

@@ -90,6 +90,28 @@ int gt_smax_esa64_download(const GtSmaxEsa64Dev *esa, uint8_t *lcptab,
 
 void gt_smax_esa64_release(GtSmaxEsa64Dev *esa);
 
+/*
+ * The file side of the GPU suffixerator.
+ *
+ * gt_smax_encode_fasta: (multi-)FASTA bytes -> encoded DNA text (a/c/g/t/u
+ * -> 0..3, IUPAC wildcards -> 254, one SEPARATOR 255 between sequences), as
+ * GenomeTools' DNA alphabet and encseq produce it (src/core/alphabet.c:63,
+ * 440-465; src/core/chardef.h:34-40).  out holds >= len bytes.
+ *
+ * gt_smax_esa64_write: a whole-array build (rows [0, n+1), keep_suftab) ->
+ * indexname.{suf,lcp,llv,bwt,prj} as `gt suffixerator -dna -suf -lcp -bwt`
+ * writes them (src/match/sfx-run.c:174-300, src/match/sfx-outprj.c:39-120);
+ * suftab_bytes 8, or 4 (-suftabuint) when n+1 < 2^32.  dbfile / dbfile_bytes
+ * name the FASTA in the .prj's dbfile line.
+ */
+int gt_smax_encode_fasta(const char *buf, uint64_t len, uint8_t *out,
+                         uint64_t *n, uint64_t *numseq, char *errbuf,
+                         size_t errlen);
+int gt_smax_esa64_write(const GtSmaxEsa64Dev *esa, const uint8_t *text,
+                        uint64_t n, uint64_t numseq, const char *dbfile,
+                        uint64_t dbfile_bytes, const char *indexname,
+                        int suftab_bytes, char *errbuf, size_t errlen);
+
 #ifdef __cplusplus
 }
 #endif

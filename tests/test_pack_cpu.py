@@ -37,3 +37,20 @@ def test_pack_of_reference_fixture(golden):
     got, dna = G.pack_bwt(e.bwt)
     want, _ = O.pack_bwt_ref(e.bwt)
     assert dna and np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("fasta", ["Atinsert.fna", "at1MB", "Random.fna", "Random-Small.fna",
+                                   "TTT-small.fna"])
+def test_fasta_encoding_matches_oracle(golden, fasta):
+    import os
+    with open(os.path.join(golden, fasta), "rb") as fh:
+        buf = fh.read()
+    got, ns = G.encode_fasta(buf)
+    want, _ = O.encode_fasta(os.path.join(golden, fasta))
+    assert np.array_equal(got, want)
+    assert ns == buf.count(b">") or (ns == 1 and buf.count(b">") == 0)
+
+
+def test_fasta_encoding_rejects_non_dna():
+    with pytest.raises(G.SmaxError):
+        G.encode_fasta(b">x\nACGTQ\n")
