@@ -29,6 +29,7 @@
 // candidates, i.e. by the output size.  No MFMA.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_scan_by_key.hpp>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -64,7 +65,8 @@ __global__ void __launch_bounds__(256) mp_expand_kernel(const uint8_t *lcp, uint
                                                         uint32_t *X) {
   const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (k > N) return;
-  X[k] = (k == 0 || k == N) ? 0u : (uint32_t) lcp[k];
+  // 255 bytes are marked until their .llv value arrives (mp_llv_kernel)
+  X[k] = (k == 0 || k == N) ? 0u : (lcp[k] == 255 ? 0xffffffffu : (uint32_t) lcp[k]);
 }
 
 // .llv values over their 255 bytes; err bit 1: value >= 2^32, bit 2: a
@@ -76,9 +78,35 @@ __global__ void __launch_bounds__(256) mp_llv_kernel(const GtSmaxLlv *llv, uint6
   if (e >= numllv) return;
   const uint64_t pos = llv[e].position, v = llv[e].value;
   if (pos < 1 || pos >= N) return;
-  if (v > 0xffffffffull) atomicOr(err, 1u);
+  if (v >= 0xffffffffull) atomicOr(err, 1u);
   if (lcp[pos] != 255) atomicOr(err, 2u);
   X[pos] = (uint32_t) v;
+}
+
+// heads of the runs of equal BWT symbols (specials >= 254 are runs of one:
+// they differ from every symbol) for a max-scan to the run start
+__global__ void __launch_bounds__(256) mp_run_heads_kernel(const uint8_t *B, uint64_t N,
+                                                           uint64_t *hv) {
+  const uint64_t r = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (r > N) return;
+  const uint32_t b = B[r];
+  hv[r] = (r == 0 || b >= 254u || B[r - 1] != b) ? r : 0;
+}
+
+// RO[r] = r - (first row of r's run), from the scanned run starts
+__global__ void __launch_bounds__(256) mp_run_off_kernel(const uint64_t *rs, uint64_t N,
+                                                         uint32_t *RO) {
+  const uint64_t r = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (r > N) return;
+  const uint64_t d = r - rs[r];
+  RO[r] = d > 0xffffffffull ? 0xffffffffu : (uint32_t) d;
+}
+
+// a .lcp byte 255 whose row no .llv entry overwrote (X still holds the mark)
+__global__ void __launch_bounds__(256) mp_llv_check_kernel(const uint32_t *X, uint64_t N,
+                                                           uint32_t *err) {
+  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (k < N && X[k] == 0xffffffffu) atomicOr(err, 4u);
 }
 
 template <typename SufT>
@@ -88,9 +116,15 @@ __device__ __forceinline__ uint64_t suf_at(const void *S, uint64_t k) {
 
 // Walk of row j: counts (EMIT = false) or writes at out[o..] (EMIT = true)
 // the maximal pairs (i, j), i < j.  The early exit reads the LCP byte only
-// (exact below 255), so rows outside blocks cost one byte.
+// (exact below 255), so rows outside blocks cost one byte.  A run of >= 8
+// earlier rows sharing j's left symbol (no pairs with j) is skipped in one
+// step: RO[r] = rows between r and the first row of its run of equal BWT
+// symbols, RM[r] = min X over that run up to r -- so a walk costs its pairs
+// plus one step per run, not the rows of its block (a homopolymer block of
+// L rows with one left symbol: O(L) instead of O(L^2)).
 template <bool EMIT, typename SufT>
 __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *X, const uint8_t *B,
+                                            const uint32_t *RM, const uint32_t *RO,
                                             const void *S, uint64_t j, uint32_t minlen,
                                             uint64_t o, uint64_t *out, uint64_t capacity) {
   const uint32_t m8 = lcp[j];
@@ -113,6 +147,7 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
       bi[q] = r >= 0 ? (uint32_t) B[r] : 0u;
       si[q] = (EMIT && r >= 0) ? suf_at<SufT>(S, (uint64_t) r) : 0;
     }
+    int64_t inext = i - MP_STEP;
 #pragma unroll
     for (int q = 0; q < MP_STEP; q++) {
       if (!more) break;
@@ -125,11 +160,22 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
           w[2] = si[q] < sj ? sj : si[q];
         }
         c++;
+      } else if (i - q >= 0) {
+        const uint64_t r = (uint64_t) (i - q);
+        const uint32_t ro = RO[r];
+        if (ro >= MP_STEP) {               // long run of j's left symbol: jump over it
+          const uint32_t rm = RM[r];
+          m = rm < m ? rm : m;
+          if (m < minlen) more = false;
+          inext = (int64_t) (r - ro) - 1;
+          break;
+        }
       }
       m = xi[q] < m ? xi[q] : m;           // X[0] == 0 ends every walk
       if (m < minlen) more = false;
     }
-    i -= MP_STEP;
+    i = inext;
+    if (i < 0) more = false;
   }
   return c;
 }
@@ -205,23 +251,25 @@ mp_cand_write_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, const uint64_t
 // Pass C: pairs per candidate row.
 template <typename SufT>
 __global__ void __launch_bounds__(256)
-mp_count_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint64_t *list,
-                uint64_t ncand, uint32_t minlen, uint32_t *cnt) {
+mp_count_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint32_t *RM,
+                const uint32_t *RO, const uint64_t *list, uint64_t ncand, uint32_t minlen,
+                uint32_t *cnt) {
   const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (e >= ncand) return;
-  cnt[e] = mp_walk<false, SufT>(lcp, X, B, nullptr, list[e], minlen, 0, nullptr, 0);
+  cnt[e] = mp_walk<false, SufT>(lcp, X, B, RM, RO, nullptr, list[e], minlen, 0, nullptr, 0);
 }
 
 // Pass D: the pairs of every candidate row at its scanned offset,
 // (len, pos1 < pos2).
 template <typename SufT>
 __global__ void __launch_bounds__(256)
-mp_emit_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const void *S,
-               const uint64_t *list, uint64_t ncand, uint32_t minlen, const uint32_t *cnt,
-               const uint64_t *off, uint64_t *out, uint64_t capacity) {
+mp_emit_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint32_t *RM,
+               const uint32_t *RO, const void *S, const uint64_t *list, uint64_t ncand,
+               uint32_t minlen, const uint32_t *cnt, const uint64_t *off, uint64_t *out,
+               uint64_t capacity) {
   const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (e >= ncand || cnt[e] == 0) return;
-  (void) mp_walk<true, SufT>(lcp, X, B, S, list[e], minlen, off[e], out, capacity);
+  (void) mp_walk<true, SufT>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity);
 }
 
 __global__ void mp_total_kernel(const uint32_t *cnt, const uint64_t *off, uint64_t n,
@@ -259,6 +307,7 @@ struct GtMaxpairsPlan {
   GtMaxpairsDevInput in;
   unsigned int minlen;
   uint32_t *X;                   // N+1 exact LCP values
+  uint32_t *RM, *RO;             // N+1: runs of equal BWT symbols (mp_walk)
   uint64_t nwg;                  // candidate workgroups (MP_WG_ROWS rows)
   uint64_t *wg_cand, *wg_cand_off;
   uint64_t ncand;                // candidate rows (fixed by the tables and minlen)
@@ -276,8 +325,8 @@ static unsigned mp_blocks(uint64_t n) { return (unsigned) ((n + 255) / 256); }
 extern "C" void gt_maxpairs_plan_delete(GtMaxpairsPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
-  void *bufs[] = {p->X, p->wg_cand, p->wg_cand_off, p->list, p->cnt, p->off, p->total,
-                  p->scan_tmp};
+  void *bufs[] = {p->X, p->RM, p->RO, p->wg_cand, p->wg_cand_off, p->list, p->cnt, p->off,
+                  p->total, p->scan_tmp};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   free(p);
@@ -333,6 +382,40 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
                        in->numllv, in->lcp_dev, N, p->X, derr);
     MPCHK(hipGetLastError());
   }
+  hipLaunchKernelGGL(mp_llv_check_kernel, dim3(mp_blocks(N)), dim3(256), 0, 0, p->X, N, derr);
+  MPCHK(hipGetLastError());
+  // runs of equal BWT symbols: start offsets and running LCP minima
+  {
+    uint64_t *hv = NULL, *rs = NULL;
+    void *tmp = NULL;
+    size_t b1 = 0, b2 = 0;
+    hipError_t e = hipMalloc(&p->RM, sizeof (uint32_t) * (N + 1));
+    if (e == hipSuccess) e = hipMalloc(&p->RO, sizeof (uint32_t) * (N + 1));
+    if (e == hipSuccess) e = hipMalloc(&hv, sizeof (uint64_t) * (N + 1));
+    if (e == hipSuccess) e = hipMalloc(&rs, sizeof (uint64_t) * (N + 1));
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(mp_run_heads_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, 0,
+                         in->bwt_dev, N, hv);
+      e = rocprim::inclusive_scan(nullptr, b1, hv, rs, (size_t) (N + 1), rocprim::maximum<uint64_t>());
+    }
+    if (e == hipSuccess)
+      e = rocprim::inclusive_scan_by_key(nullptr, b2, rs, p->X, p->RM, (size_t) (N + 1),
+                                         rocprim::minimum<uint32_t>());
+    if (e == hipSuccess) e = hipMalloc(&tmp, b1 > b2 ? b1 : b2);
+    if (e == hipSuccess)
+      e = rocprim::inclusive_scan(tmp, b1, hv, rs, (size_t) (N + 1), rocprim::maximum<uint64_t>());
+    if (e == hipSuccess)
+      e = rocprim::inclusive_scan_by_key(tmp, b2, rs, p->X, p->RM, (size_t) (N + 1),
+                                         rocprim::minimum<uint32_t>());
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(mp_run_off_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, 0, rs, N, p->RO);
+      e = hipDeviceSynchronize();
+    }
+    if (hv) (void) hipFree(hv);
+    if (rs) (void) hipFree(rs);
+    if (tmp) (void) hipFree(tmp);
+    MPCHK(e);
+  }
   // candidate rows: their number sizes the per-candidate buffers (the tables
   // are immutable for the plan's life; every count pass rebuilds the list)
   if (N > 0) {
@@ -369,6 +452,7 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
   MPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   if (herr & 1u) { mp_seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
   if (herr & 2u) { mp_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
+  if (herr & 4u) { mp_seterr(errbuf, errlen, "inconsistent index: a .lcp byte 255 without its .llv entry"); goto fail; }
   (void) hipFree(derr);
   *planp = p;
   return 0;
@@ -398,7 +482,8 @@ extern "C" int gt_maxpairs_plan_count(GtMaxpairsPlan *p, void *stream) {
                        p->in.lcp_dev, N, mf, p->wg_cand_off, p->list);
     MPCHK(hipGetLastError());
     hipLaunchKernelGGL((mp_count_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
-                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->list, nc, p->minlen, p->cnt);
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->list, nc, p->minlen,
+                       p->cnt);
     MPCHK(hipGetLastError());
     bytes = p->scan_tmp_bytes;
     MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->cnt, p->off, (uint64_t) 0, (size_t) nc,
@@ -434,12 +519,12 @@ extern "C" int gt_maxpairs_plan_emit(GtMaxpairsPlan *p, uint64_t *out_dev, uint6
   if (nc == 0 || capacity == 0) return 0;
   if (p->in.suf_bytes == 8)
     hipLaunchKernelGGL((mp_emit_kernel<uint64_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
-                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->in.suf_dev, p->list, nc, p->minlen,
-                       p->cnt, p->off, out_dev, capacity);
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
+                       p->minlen, p->cnt, p->off, out_dev, capacity);
   else
     hipLaunchKernelGGL((mp_emit_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
-                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->in.suf_dev, p->list, nc, p->minlen,
-                       p->cnt, p->off, out_dev, capacity);
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
+                       p->minlen, p->cnt, p->off, out_dev, capacity);
   MPCHK(hipGetLastError());
   return 0;
 fail:

@@ -145,3 +145,45 @@ def test_errors_are_reported():
         G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab, e.n, e.n + 5, 8)
     with pytest.raises(G.SmaxError):
         G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab, e.n, e.nonspecials, 0)
+
+
+class _TablesEsa:
+    """Oracle view (exact LCP, suftab, text) of GPU-built tables."""
+
+    def __init__(self, text, d):
+        self.text = np.ascontiguousarray(text, dtype=np.uint8)
+        self.n = len(text)
+        self.nonspecials = int(self.n - np.count_nonzero(text >= 254))
+        self.lcp = d["lcptab"].astype(np.uint64)
+        if len(d["llvtab"]):
+            self.lcp[d["llvtab"][:, 0].astype(np.int64)] = d["llvtab"][:, 1]
+        self.suftab = d["suftab"].astype(np.uint64)
+
+
+@pytest.mark.parametrize("runlen", [100_000, 1_000_000])
+def test_homopolymer_block_costs_its_output(runlen):
+    # one block of ~runlen rows whose suffixes share their left symbol: the
+    # walk skips runs of j's left symbol (linear, not quadratic, in the block)
+    import time
+    rng = np.random.default_rng(runlen)
+    text = np.concatenate([rng.integers(0, 4, 200_000, dtype=np.uint8),
+                           np.zeros(runlen, dtype=np.uint8),
+                           rng.integers(0, 4, 200_000, dtype=np.uint8)])
+    esa = G.DeviceEsa(text, device=0, keep_suftab=True)
+    d = esa.download(suftab=True)
+    esa.release()
+    N = len(text)
+    t0 = time.perf_counter()
+    got = G.enumerate_maxpairs(d["lcptab"], d["llvtab"], d["bwttab"], d["suftab"], N, N, 20)
+    dt = time.perf_counter() - t0
+    want = O.maxpairs(_TablesEsa(text, d), 20)
+    assert len(want) > runlen // 2
+    assert np.array_equal(_norm(got), _norm(want))
+    assert dt < 20.0, dt
+
+
+def test_lcp_255_without_llv_is_an_error():
+    e = oracle_esa("at1MB")
+    llv = e.llv[1:]                      # drop one entry: its 255 byte is orphaned
+    with pytest.raises(G.SmaxError, match="255"):
+        G.enumerate_maxpairs(e.lcpbytes, llv, e.bwt, e.suftab, e.n, e.nonspecials, 20)
