@@ -180,6 +180,7 @@ def lib():
         L.gt_maxpairs_plan_count.argtypes = [vp, vp]
         L.gt_maxpairs_plan_total.argtypes = [vp, ctypes.POINTER(u64)]
         L.gt_maxpairs_plan_emit.argtypes = [vp, vp, u64, vp]
+        L.gt_maxpairs_plan_emit_ordered.argtypes = [vp, vp, u64, vp]
         L.gt_seqpos_map_dev.argtypes = [vp, u64, vp, u64, vp, ci, vp]
         L.gt_lcpitv_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput),
                                                         ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
@@ -369,9 +370,8 @@ class _OwnedTriples:
 
 def enumerate_maxpairs(lcptab, llvtab, bwttab, suftab, totallength, nonspecials, minlen):
     """All maximal pairs of length >= minlen as an (k,3) uint64 array of
-    (len, pos1, pos2), pos1 < pos2 (gt_maxpairs_hip_enumerate_to_buffer; the
-    pair set of `gt repfind -l minlen`, in row order rather than the
-    reference's traversal order)."""
+    (len, pos1, pos2), pos1 < pos2 (gt_maxpairs_hip_enumerate_to_buffer: the
+    pairs of `gt repfind -l minlen` in the reference's emission order)."""
     lcptab = np.ascontiguousarray(lcptab, dtype=np.uint8)
     bwttab = np.ascontiguousarray(bwttab, dtype=np.uint8)
     llvtab = np.ascontiguousarray(llvtab, dtype=np.uint64).reshape(-1, 2)
@@ -430,6 +430,11 @@ class MaxpairsPlan:
     def emit(self, out_ptr, capacity, stream=0):
         if lib().gt_maxpairs_plan_emit(self._p, out_ptr, int(capacity), stream) != 0:
             raise SmaxError("gt_maxpairs_plan_emit failed")
+
+    def emit_ordered(self, out_ptr, capacity, stream=0):
+        """Pairs in the reference's emission order (synchronises)."""
+        if lib().gt_maxpairs_plan_emit_ordered(self._p, out_ptr, int(capacity), stream) != 0:
+            raise SmaxError("gt_maxpairs_plan_emit_ordered failed")
 
     def close(self):
         if self._p:

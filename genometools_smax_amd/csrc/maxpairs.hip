@@ -27,7 +27,31 @@
 //
 // Integer/byte work; bound by the number of (row, earlier row in block)
 // candidates, i.e. by the output size.  No MFMA.
+//
+// Reference emission order (gt_maxpairs_plan_emit_ordered, the host entry
+// points): the traversal calls GtProcessmaxpairs at "events" -- a leaf
+// joining its interval (processleafedge, src/match/esa-maxpairs.c:181-240)
+// or a finished child interval merging into its father (processbranchingedge,
+// :242-360) -- in iteration order, and within an iteration the leaf first,
+// then the pops from the deepest.  A pair of rows x < y of depth L is
+// emitted at the event that brings y's unit (y itself, or the child of the
+// depth-L interval holding y) into that interval; its iteration is
+// t = min{k >= y : LCP[k+1] <= L}, and (t, -L) orders the events.  Inside an
+// event the cartesian loops order the pairs by left-symbol class (symbols,
+// then "unique" >= 254 last) and by row, since every per-symbol position
+// list is a contiguous slice filled in row order:
+//   leaf event (max(LCP[y], LCP[y+1]) == L):  (class x, x)
+//   branch event, x in the father, y in the child:
+//     class x, class y < 254:  (class x, class y, x, y)
+//     class x < 254, y unique: (class x, 254, y, x)
+//     x unique:                (254, x, class y, y)
+// The emission pass writes these keys beside the triples and three or four
+// stable LSD radix sorts give the permutation.  t comes from a 64-ary
+// minimum hierarchy over the exact LCP (one "next value <= L" search per
+// distinct depth of a walk).
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
 #include <stdarg.h>
@@ -114,6 +138,45 @@ __device__ __forceinline__ uint64_t suf_at(const void *S, uint64_t k) {
   return (uint64_t) reinterpret_cast<const SufT *>(S)[k];
 }
 
+// 64-ary minimum hierarchy over X[0..N]: lv[0] = X, lv[l][i] = min of
+// lv[l-1][64i .. 64i+63]; the top level has <= 64 entries.
+#define MP_HMAX 8
+struct MpHier {
+  const uint32_t *lv[MP_HMAX];
+  uint64_t n[MP_HMAX];
+  int levels;
+};
+
+// first k >= a with X[k] <= v (X[N] == 0: always found for a <= N)
+__device__ uint64_t mp_next_le(const MpHier &h, uint64_t a, uint32_t v) {
+  uint64_t idx = a;
+  int l = 0;
+  for (;;) {
+    const uint64_t g = ((idx >> 6) + 1) << 6;
+    const uint64_t end = g < h.n[l] ? g : h.n[l];
+    uint64_t k = idx;
+    while (k < end && h.lv[l][k] > v) k++;
+    if (k < end) { idx = k; break; }
+    if (l + 1 >= h.levels) return h.n[0] - 1;     // unreachable for valid tables
+    idx = (idx >> 6) + 1;
+    l++;
+  }
+  while (l > 0) {
+    l--;
+    uint64_t k = idx << 6;
+    while (h.lv[l][k] > v) k++;                    // a child holds the minimum
+    idx = k;
+  }
+  return idx;
+}
+
+// sort keys of the reference emission order (see the header), per pair
+struct MpKeys {
+  uint64_t *k1, *k2, *k3, *k4;   // r2 | (classes, r1) | event | t (split)
+  int rowbits, lbits;            // rows < 2^rowbits, depths < 2^lbits
+  int split;                     // rowbits + lbits > 64: t in k4, depth in k3
+};
+
 // Walk of row j: counts (EMIT = false) or writes at out[o..] (EMIT = true)
 // the maximal pairs (i, j), i < j.  The early exit reads the LCP byte only
 // (exact below 255), so rows outside blocks cost one byte.  A run of >= 8
@@ -122,11 +185,12 @@ __device__ __forceinline__ uint64_t suf_at(const void *S, uint64_t k) {
 // symbols, RM[r] = min X over that run up to r -- so a walk costs its pairs
 // plus one step per run, not the rows of its block (a homopolymer block of
 // L rows with one left symbol: O(L) instead of O(L^2)).
-template <bool EMIT, typename SufT>
+template <bool EMIT, typename SufT, bool ORD = false>
 __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *X, const uint8_t *B,
                                             const uint32_t *RM, const uint32_t *RO,
                                             const void *S, uint64_t j, uint32_t minlen,
-                                            uint64_t o, uint64_t *out, uint64_t capacity) {
+                                            uint64_t o, uint64_t *out, uint64_t capacity,
+                                            const MpHier *h = nullptr, const MpKeys *K = nullptr) {
   const uint32_t m8 = lcp[j];
   if (j == 0 || (m8 < 255u && m8 < minlen)) return 0;
   uint32_t m = X[j];                       // depth of the pair (j-1, j)
@@ -135,6 +199,12 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
   const uint32_t bj = B[j];
   const bool uj = bj >= 254u;              // unique left context
   const uint64_t sj = EMIT ? suf_at<SufT>(S, j) : 0;
+  // ORD: event of the current depth (recomputed when the depth drops)
+  const uint32_t xj = m, xj1 = ORD ? X[j + 1] : 0u;
+  const uint64_t cy = uj ? 254u : bj;
+  uint32_t ev_l = 0xffffffffu;
+  uint64_t ev_k = j + 1, ev_key3 = 0, ev_key4 = 0;
+  bool ev_leaf = false;
   int64_t i = (int64_t) j - 1;
   bool more = true;
   while (more) {
@@ -158,6 +228,29 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
           w[0] = m;
           w[1] = si[q] < sj ? si[q] : sj;
           w[2] = si[q] < sj ? sj : si[q];
+          if (ORD) {
+            if (m != ev_l) {
+              ev_l = m;
+              ev_k = mp_next_le(*h, ev_k, m);          // t = ev_k - 1
+              ev_leaf = (xj > xj1 ? xj : xj1) == m;
+              const uint64_t t = ev_k - 1;
+              const uint64_t ld = ((1ull << K->lbits) - 1) - m;   // deeper first
+              if (K->split) { ev_key3 = ld; ev_key4 = t; }
+              else { ev_key3 = (t << K->lbits) | ld; }
+            }
+            const uint64_t x = (uint64_t) (i - q), y = j, rb = (uint64_t) K->rowbits;
+            const uint64_t cx = bi[q] >= 254u ? 254u : bi[q];
+            uint64_t cls, r1, r2;
+            if (ev_leaf) { cls = cx << 8; r1 = x; r2 = 0; }
+            else if (cx < 254u && cy < 254u) { cls = (cx << 8) | cy; r1 = x; r2 = y; }
+            else if (cx < 254u) { cls = (cx << 8) | 254u; r1 = y; r2 = x; }
+            else { cls = 254u << 8; r1 = x; r2 = (cy << rb) | y; }
+            const uint64_t e = o + c;
+            K->k1[e] = r2;
+            K->k2[e] = (cls << rb) | r1;
+            K->k3[e] = ev_key3;
+            if (K->split) K->k4[e] = ev_key4;
+          }
         }
         c++;
       } else if (i - q >= 0) {
@@ -272,6 +365,46 @@ mp_emit_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const ui
   (void) mp_walk<true, SufT>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity);
 }
 
+// Pass D with the emission-order keys of every pair
+template <typename SufT>
+__global__ void __launch_bounds__(256)
+mp_emit_ord_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint32_t *RM,
+                   const uint32_t *RO, const void *S, const uint64_t *list, uint64_t ncand,
+                   uint32_t minlen, const uint32_t *cnt, const uint64_t *off, uint64_t *out,
+                   uint64_t capacity, MpHier h, MpKeys K) {
+  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (e >= ncand || cnt[e] == 0) return;
+  (void) mp_walk<true, SufT, true>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity,
+                                   &h, &K);
+}
+
+// one hierarchy level: dst[i] = min(src[64i .. 64i+63])
+__global__ void __launch_bounds__(256) mp_hier_kernel(const uint32_t *src, uint64_t nsrc,
+                                                      uint32_t *dst, uint64_t ndst) {
+  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (i >= ndst) return;
+  const uint64_t b = i << 6, e = b + 64 < nsrc ? b + 64 : nsrc;
+  uint32_t m = 0xffffffffu;
+  for (uint64_t k = b; k < e; k++) m = src[k] < m ? src[k] : m;
+  dst[i] = m;
+}
+
+__global__ void __launch_bounds__(256) mp_iota_kernel(uint64_t *p, uint64_t n) {
+  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (i < n) p[i] = i;
+}
+
+// dst[i] = src[perm[i]] (words per element: 1 for keys, 3 for triples)
+template <int W>
+__global__ void __launch_bounds__(256) mp_gather_kernel(const uint64_t *src, const uint64_t *perm,
+                                                        uint64_t n, uint64_t *dst) {
+  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t s = perm[i];
+#pragma unroll
+  for (int w = 0; w < W; w++) dst[W * i + w] = src[W * s + w];
+}
+
 __global__ void mp_total_kernel(const uint32_t *cnt, const uint64_t *off, uint64_t n,
                                 uint64_t *total) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *total = n == 0 ? 0 : off[n - 1] + cnt[n - 1];
@@ -318,6 +451,9 @@ struct GtMaxpairsPlan {
   void *scan_tmp;
   size_t scan_tmp_bytes;
   bool counted;
+  uint32_t *hier;                // levels >= 1 of the minimum hierarchy (ordered emission)
+  MpHier h;
+  uint32_t xmax;                 // largest exact LCP value
 };
 
 static unsigned mp_blocks(uint64_t n) { return (unsigned) ((n + 255) / 256); }
@@ -326,7 +462,7 @@ extern "C" void gt_maxpairs_plan_delete(GtMaxpairsPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
   void *bufs[] = {p->X, p->RM, p->RO, p->wg_cand, p->wg_cand_off, p->list, p->cnt, p->off,
-                  p->total, p->scan_tmp};
+                  p->total, p->scan_tmp, p->hier};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   free(p);
@@ -531,6 +667,133 @@ fail:
   return -1;
 }
 
+static int mp_bits(uint64_t v) { return v == 0 ? 1 : 64 - __builtin_clzll(v); }
+
+// the minimum hierarchy and the largest LCP value, once per plan
+static int mp_build_hier(GtMaxpairsPlan *p, hipStream_t s, char *errbuf, size_t errlen) {
+  const uint64_t N = p->in.nonspecials;
+  uint64_t n[MP_HMAX], off[MP_HMAX], tot = 0;
+  int L = 1;
+  uint32_t *dmax = NULL;
+  void *tmp = NULL;
+  size_t tb = 0;
+  if (p->hier != NULL || p->h.levels > 0) return 0;
+  n[0] = N + 1;
+  while (n[L - 1] > 64) {
+    if (L >= MP_HMAX) { mp_seterr(errbuf, errlen, "minimum hierarchy too deep"); return -1; }
+    n[L] = (n[L - 1] + 63) / 64;
+    off[L] = tot;
+    tot += n[L];
+    L++;
+  }
+  if (tot > 0) MPCHK(hipMalloc(&p->hier, sizeof (uint32_t) * tot));
+  p->h.lv[0] = p->X;
+  p->h.n[0] = n[0];
+  for (int l = 1; l < L; l++) {
+    p->h.lv[l] = p->hier + off[l];
+    p->h.n[l] = n[l];
+    hipLaunchKernelGGL(mp_hier_kernel, dim3(mp_blocks(n[l])), dim3(256), 0, s, p->h.lv[l - 1],
+                       n[l - 1], (uint32_t *) p->h.lv[l], n[l]);
+    MPCHK(hipGetLastError());
+  }
+  p->h.levels = L;
+  MPCHK(hipMalloc(&dmax, sizeof (uint32_t)));
+  MPCHK(rocprim::reduce(nullptr, tb, p->X, dmax, 0u, (size_t) (N + 1), rocprim::maximum<uint32_t>(), s));
+  MPCHK(hipMalloc(&tmp, tb ? tb : 16));
+  MPCHK(rocprim::reduce(tmp, tb, p->X, dmax, 0u, (size_t) (N + 1), rocprim::maximum<uint32_t>(), s));
+  MPCHK(hipMemcpyAsync(&p->xmax, dmax, sizeof (uint32_t), hipMemcpyDeviceToHost, s));
+  MPCHK(hipStreamSynchronize(s));
+  (void) hipFree(dmax);
+  (void) hipFree(tmp);
+  return 0;
+fail:
+  if (dmax) (void) hipFree(dmax);
+  if (tmp) (void) hipFree(tmp);
+  return -1;
+}
+
+extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_dev, uint64_t capacity,
+                                             void *stream) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  hipStream_t s = (hipStream_t) stream;
+  const uint64_t nc = p->ncand;
+  uint64_t T = 0;
+  uint64_t *tri = NULL, *keys = NULL, *ktmp = NULL, *pa = NULL, *pb = NULL;
+  void *st = NULL;
+  size_t sb = 0;
+  MpKeys K;
+  if (!p->counted) return -1;
+  MPCHK(hipSetDevice(p->in.device));
+  MPCHK(hipStreamSynchronize(s));
+  MPCHK(hipMemcpy(&T, p->total, sizeof (uint64_t), hipMemcpyDeviceToHost));
+  if (T == 0) return 0;
+  if (capacity < T) return -1;
+  if (mp_build_hier(p, s, errbuf, errlen) != 0) return -1;
+  K.rowbits = mp_bits(p->in.nonspecials);
+  K.lbits = mp_bits(p->xmax);
+  K.split = K.rowbits + K.lbits > 64;
+  if (K.rowbits > 48) return -1;
+  MPCHK(hipMalloc(&tri, sizeof (uint64_t) * 3 * T));
+  MPCHK(hipMalloc(&keys, sizeof (uint64_t) * (K.split ? 4 : 3) * T));
+  MPCHK(hipMalloc(&ktmp, sizeof (uint64_t) * T));
+  MPCHK(hipMalloc(&pa, sizeof (uint64_t) * T));
+  MPCHK(hipMalloc(&pb, sizeof (uint64_t) * T));
+  K.k1 = keys;
+  K.k2 = keys + T;
+  K.k3 = keys + 2 * T;
+  K.k4 = K.split ? keys + 3 * T : nullptr;
+  if (p->in.suf_bytes == 8)
+    hipLaunchKernelGGL((mp_emit_ord_kernel<uint64_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
+                       p->minlen, p->cnt, p->off, tri, T, p->h, K);
+  else
+    hipLaunchKernelGGL((mp_emit_ord_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
+                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
+                       p->minlen, p->cnt, p->off, tri, T, p->h, K);
+  MPCHK(hipGetLastError());
+  hipLaunchKernelGGL(mp_iota_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, pa, T);
+  MPCHK(hipGetLastError());
+  MPCHK(rocprim::radix_sort_pairs(nullptr, sb, ktmp, ktmp, pa, pb, (size_t) T, 0, 64, s));
+  MPCHK(hipMalloc(&st, sb ? sb : 16));
+  {
+    // stable LSD passes: r2, then (classes, r1), then the event [depth, then t]
+    const int nk = K.split ? 4 : 3;
+    const int bits[4] = {K.rowbits + 8, K.rowbits + 16, K.split ? K.lbits : K.rowbits + K.lbits,
+                         K.rowbits};
+    for (int k = 0; k < nk; k++) {
+      const uint64_t *src = keys + (uint64_t) k * T;
+      if (k == 0) {
+        MPCHK(hipMemcpyAsync(ktmp, src, sizeof (uint64_t) * T, hipMemcpyDeviceToDevice, s));
+      } else {
+        hipLaunchKernelGGL((mp_gather_kernel<1>), dim3(mp_blocks(T)), dim3(256), 0, s, src, pa, T,
+                           ktmp);
+        MPCHK(hipGetLastError());
+      }
+      // sorted keys land in k1's slot (no longer needed after the first pass)
+      size_t b = sb;
+      MPCHK(rocprim::radix_sort_pairs(st, b, ktmp, keys, pa, pb, (size_t) T, 0, bits[k], s));
+      uint64_t *t = pa; pa = pb; pb = t;
+    }
+  }
+  hipLaunchKernelGGL((mp_gather_kernel<3>), dim3(mp_blocks(T)), dim3(256), 0, s, tri, pa, T,
+                     out_dev);
+  MPCHK(hipGetLastError());
+  MPCHK(hipStreamSynchronize(s));
+  {
+    void *bufs[] = {tri, keys, ktmp, pa, pb, st};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) (void) hipFree(bufs[i]);
+  }
+  return 0;
+fail:
+  {
+    void *bufs[] = {tri, keys, ktmp, pa, pb, st};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
+      if (bufs[i]) (void) hipFree(bufs[i]);
+  }
+  return -1;
+}
+
 extern "C" int gt_seqpos_map_dev(const uint64_t *sep_dev, uint64_t nsep, const uint64_t *pairs_dev,
                                  uint64_t count, uint64_t *out_dev, int device, void *stream) {
   char *errbuf = NULL;
@@ -608,7 +871,7 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
       goto fail_quiet;
     }
     MPCHK(hipMalloc(&out, sizeof (uint64_t) * 3 * total));
-    if (gt_maxpairs_plan_emit(plan, out, total, NULL) != 0) {
+    if (gt_maxpairs_plan_emit_ordered(plan, out, total, NULL) != 0) {
       mp_seterr(errbuf, errlen, "maxpairs emission pass failed");
       goto fail_quiet;
     }

@@ -19,9 +19,8 @@
  * Output: one line per occurrence pair of every supermaximal repeat (or per
  * maximal pair), in the format of gt_simpleexactselfmatchoutput
  * (src/tools/gt_repfind.c:49-84, src/match/querymatch.c:130-190):
- * "len seqnum1 relpos1 F len seqnum2 relpos2".  Maximal pairs come in
- * suffix-array row order, not the reference's traversal order (same lines
- * after sorting).
+ * "len seqnum1 relpos1 F len seqnum2 relpos2".  Maximal pairs come in the
+ * reference's traversal order (the same lines in the same order).
  * Errors: "gt repfind: error: <msg>" on stderr, exit status 1 (gt_tool_run).
  */
 #include <stdint.h>

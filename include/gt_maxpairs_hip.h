@@ -17,12 +17,12 @@
  *                                 products of src/match/esa-maxpairs.c:181-360.
  *                                 The callback has the argument meaning of
  *                                 GtProcessmaxpairs (src/match/esa-maxpairs.h:38-43):
- *                                 (len, pos1, pos2), here with pos1 < pos2.
- *                                 Pair SET identical to the reference; the
- *                                 emission ORDER is by the later suffix-array
- *                                 row, then descending earlier row (the
- *                                 reference's is its traversal order), so
- *                                 outputs compare equal after sorting.
+ *                                 (len, pos1, pos2), here with pos1 < pos2
+ *                                 (the order gt_simpleexactselfmatchoutput
+ *                                 swaps them into, src/tools/gt_repfind.c:60-65).
+ *                                 Pairs AND their order are the reference's:
+ *                                 the callback sees them in the order the
+ *                                 traversal calls GtProcessmaxpairs.
  *  gt_maxpairs_hip_enumerate_to_buffer  same, malloc'd (len,pos1,pos2) triples.
  *
  * A maximal pair of length L >= minlen is a pair of suffix-array rows
@@ -86,10 +86,19 @@ int gt_maxpairs_plan_count(GtMaxpairsPlan *plan, void *stream);
 int gt_maxpairs_plan_total(GtMaxpairsPlan *plan, uint64_t *total);
 
 /* Enqueue the emission pass: out_dev receives 3*total uint64
- * (len, pos1 < pos2) triples; capacity is in triples (pairs beyond it are
+ * (len, pos1 < pos2) triples in suffix-array row order (by the later row,
+ * then descending earlier row); capacity is in triples (pairs beyond it are
  * dropped).  Requires a preceding count pass. */
 int gt_maxpairs_plan_emit(GtMaxpairsPlan *plan, uint64_t *out_dev, uint64_t capacity,
                           void *stream);
+
+/* The emission pass in the reference's order (the order of
+ * gt_maxpairs_hip_enumerate's callbacks): the pairs are written with their
+ * event/row sort keys and permuted by stable radix sorts.  Synchronises the
+ * stream (the pair count sizes its temporary buffers, ~80 bytes per pair);
+ * capacity must be >= the count, else -1.  Requires a preceding count pass. */
+int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *plan, uint64_t *out_dev, uint64_t capacity,
+                                  void *stream);
 
 /* F4: on-device sequence mapping of position pairs, the seqnum/relpos step
  * of gt_querymatch_fill / gt_encseq_seqnum (src/match/querymatch.c:47-67,

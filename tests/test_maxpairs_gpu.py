@@ -4,10 +4,12 @@ on-device seqnum/relpos mapping (F4), through the C-ABI.
 Pinned to the reference's own golden `testdata/repfind-8-Atinsert.txt`
 (`gt repfind -l 8` on Atinsert, 452 lines) after sorting, and to the
 oracle's restatement of the bottom-up maxpairs traversal
-(`orc_maxpairs`, src/match/esa-bottomup-maxpairs.inc:136-264) as a pair SET
-on fixtures and seeded texts with specials and .llv values.  The emission
-order differs from the reference's traversal order by design (row order),
-so every comparison is on sorted (len, pos1 < pos2) triples or sorted lines.
+(`orc_maxpairs`, src/match/esa-bottomup-maxpairs.inc:136-264) on fixtures and
+seeded texts with specials and .llv values.  The host entry points and
+`emit_ordered` emit in the reference's order: compared pair by pair, in
+order (each pair as (len, min pos, max pos), the swap
+gt_simpleexactselfmatchoutput makes); the row-order device pass
+(`plan.emit`) is compared as a set.
 """
 import os
 
@@ -29,6 +31,11 @@ def _norm(p):
     return q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]
 
 
+def _ordered(p):
+    p = np.asarray(p, dtype=np.uint64).reshape(-1, 3)
+    return np.stack([p[:, 0], np.minimum(p[:, 1], p[:, 2]), np.maximum(p[:, 1], p[:, 2])], axis=1)
+
+
 def _gpu(e, minlen, suf_dtype=np.uint64):
     return G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab.astype(suf_dtype), e.n,
                                 e.nonspecials, minlen)
@@ -41,7 +48,7 @@ def test_atinsert_matches_reference_golden():
     with open(os.path.join(GOLDEN, "repfind-8-Atinsert.txt")) as fh:
         want = [" ".join(ln.split()) for ln in fh if ln.strip()]
     assert len(lines) == 452
-    assert sorted(lines) == sorted(want)
+    assert lines == want                  # the reference's own order, line by line
 
 
 @pytest.mark.parametrize("minlen", [4, 8, 12, 20, 40])
@@ -49,21 +56,21 @@ def test_atinsert_pair_set(minlen):
     e = oracle_esa("Atinsert.fna")
     got = _gpu(e, minlen)
     assert np.all(got[:, 1] < got[:, 2])
-    assert np.array_equal(_norm(got), _norm(O.maxpairs(e, minlen)))
+    assert np.array_equal(got, _ordered(O.maxpairs(e, minlen)))
 
 
 @pytest.mark.parametrize("minlen", [20, 50, 255, 300])
 def test_at1mb_pair_set(minlen):
     e = oracle_esa("at1MB")
     got = _gpu(e, minlen)
-    assert np.array_equal(_norm(got), _norm(O.maxpairs(e, minlen)))
+    assert np.array_equal(got, _ordered(O.maxpairs(e, minlen)))
     if minlen == 20:
         assert len(O.format_pairs(got, e.separators)) == 4507
 
 
 def test_suftab_4_bytes():
     e = oracle_esa("at1MB")
-    assert np.array_equal(_norm(_gpu(e, 20, np.uint32)), _norm(_gpu(e, 20)))
+    assert np.array_equal(_gpu(e, 20, np.uint32), _gpu(e, 20))
 
 
 def _repetitive(rng, n, pspecial):
@@ -87,7 +94,7 @@ def test_random_repetitive(seed):
     t = _repetitive(rng, int(rng.integers(20000, 80000)), [0.0, 0.001, 0.01, 0.05][seed])
     e = O.Esa(t)
     for minlen in (12, 30, 256):
-        assert np.array_equal(_norm(_gpu(e, minlen)), _norm(O.maxpairs(e, minlen))), minlen
+        assert np.array_equal(_gpu(e, minlen), _ordered(O.maxpairs(e, minlen))), minlen
 
 
 def test_long_lcp_values():
@@ -99,7 +106,7 @@ def test_long_lcp_values():
     e = O.Esa(t)
     assert len(e.llv) > 0
     for minlen in (100, 255, 256, 1000, 1200, 1201):
-        assert np.array_equal(_norm(_gpu(e, minlen)), _norm(O.maxpairs(e, minlen))), minlen
+        assert np.array_equal(_gpu(e, minlen), _ordered(O.maxpairs(e, minlen))), minlen
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -112,7 +119,7 @@ def test_small_edge_texts(seed):
             t[rng.random(n) < 0.1] = 254
         e = O.Esa(t)
         for minlen in (1, 2, 5):
-            assert np.array_equal(_norm(_gpu(e, minlen)), _norm(O.maxpairs(e, minlen)))
+            assert np.array_equal(_gpu(e, minlen), _ordered(O.maxpairs(e, minlen)))
 
 
 def test_device_resident_plan_and_seqpos_map():
@@ -127,6 +134,10 @@ def test_device_resident_plan_and_seqpos_map():
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint64).reshape(-1, 3)
     assert np.array_equal(_norm(got), _norm(O.maxpairs(e, 20)))
+    ordered = torch.empty(3 * total, dtype=torch.int64, device="cuda")
+    p.emit_ordered(ordered.data_ptr(), total)
+    assert np.array_equal(ordered.cpu().numpy().view(np.uint64).reshape(-1, 3),
+                          _ordered(O.maxpairs(e, 20)))
     # F4: seqnum / relpos on the device == the oracle's formatter
     sep = torch.from_numpy(e.separators.view(np.int64)).cuda()
     mapped = torch.empty(5 * total, dtype=torch.int64, device="cuda")
@@ -178,7 +189,7 @@ def test_homopolymer_block_costs_its_output(runlen):
     dt = time.perf_counter() - t0
     want = O.maxpairs(_TablesEsa(text, d), 20)
     assert len(want) > runlen // 2
-    assert np.array_equal(_norm(got), _norm(want))
+    assert np.array_equal(got, _ordered(want))
     assert dt < 20.0, dt
 
 

@@ -4,7 +4,9 @@ minlen`) on the C2 workload (100 Mbp uniform ACGT, seed 42, minlen 20),
 tables (with the suffix array) resident in HBM.  A step is one count pass +
 scan + emission pass.  CPU baseline: the oracle's restatement of the
 reference's bottom-up maxpairs traversal (orc_maxpairs, single core) on the
-same tables.  Prints one JSON line."""
+same tables.  Also times the step with the emission in the reference's
+order (count + gt_maxpairs_plan_emit_ordered, which synchronises).  Prints
+one JSON line."""
 import argparse
 import json
 import os
@@ -51,6 +53,20 @@ def main():
         step()
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / args.steps
+    outo = torch.empty(max(3 * total, 3), dtype=torch.int64, device="cuda")
+
+    def step_ordered():
+        plan.count(s)
+        plan.emit_ordered(outo.data_ptr(), total, s)
+
+    for _ in range(args.warmup):
+        step_ordered()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_ordered()
+    torch.cuda.synchronize()
+    elo = (time.perf_counter() - t0) / args.steps
     cpu = None
     if not args.no_cpu_baseline:
         import oracle_lib as O
@@ -72,9 +88,14 @@ def main():
             q = np.stack([p[:, 0], np.minimum(p[:, 1], p[:, 2]), np.maximum(p[:, 1], p[:, 2])], 1)
             return q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]
         same = len(ref) == total and np.array_equal(norm(ref), norm(got))
+        goto = outo[: 3 * total].cpu().numpy().view(np.uint64).reshape(-1, 3)
+        refo = np.stack([ref[:, 0], np.minimum(ref[:, 1], ref[:, 2]),
+                         np.maximum(ref[:, 1], ref[:, 2])], 1) if len(ref) else ref
+        same_order = len(ref) == total and np.array_equal(refo, goto)
         cpu = {"value": N / tc, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
                "sample": "oracle orc_maxpairs (restated gt_esa_bottomup_maxpairs, 1 core) over all "
-                         "%d rows: %.2fs; pair set identical to the GPU's: %s" % (N, tc, same)}
+                         "%d rows: %.2fs; pair set identical to the GPU's: %s; reference emission order "
+                         "identical to the GPU's ordered pass: %s" % (N, tc, same, same_order)}
     print(json.dumps({
         "metric": "suffix-positions/s (maximal pairs, gt repfind -l %d)" % args.minlen,
         "value": N / el, "unit": "suffix-positions/s", "n_gpus": 1, "steps": args.steps,
@@ -83,6 +104,7 @@ def main():
         "config": {"workload": "%d bp synthetic %s DNA, minlen=%d" % (args.bases, args.kind, args.minlen),
                    "nonspecials": N},
         "maximal_pairs": total, "maximal_pairs_per_s": total / el,
+        "ms_per_step_reference_order": elo * 1e3,
         "cpu_baseline": cpu}), flush=True)
     plan.close()
     esa.release()
