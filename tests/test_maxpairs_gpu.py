@@ -2,7 +2,7 @@
 on-device seqnum/relpos mapping (F4), through the C-ABI.
 
 Pinned to the reference's own golden `testdata/repfind-8-Atinsert.txt`
-(`gt repfind -l 8` on Atinsert, 452 lines) after sorting, and to the
+(`gt repfind -l 8` on Atinsert, 452 lines) line for line, and to the
 oracle's restatement of the bottom-up maxpairs traversal
 (`orc_maxpairs`, src/match/esa-bottomup-maxpairs.inc:136-264) on fixtures and
 seeded texts with specials and .llv values.  The host entry points and
