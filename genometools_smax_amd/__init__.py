@@ -107,6 +107,9 @@ _ITV_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctype
                            ctypes.c_uint64)
 
 
+_TEXT_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+
+
 class GtLcpitvVisitor(ctypes.Structure):
     _fields_ = [("leaf_edge", _LEAF_CB), ("branching_edge", _BRANCH_CB), ("lcp_interval", _ITV_CB)]
 
@@ -182,6 +185,10 @@ def lib():
         L.gt_maxpairs_plan_emit.argtypes = [vp, vp, u64, vp]
         L.gt_maxpairs_plan_emit_ordered.argtypes = [vp, vp, u64, vp]
         L.gt_seqpos_map_dev.argtypes = [vp, u64, vp, u64, vp, ci, vp]
+        L.gt_repfind_pairs_lines_dev.argtypes = [vp, u64, vp, u64, ci, _TEXT_CB, vp, cs, sz]
+        L.gt_repfind_smax_lines.argtypes = [vp, u64, vp, u64, vp, u64, _TEXT_CB, vp, cs, sz]
+        L.gt_repfind_maxpairs_lines.argtypes = [ctypes.POINTER(GtSmaxInput), u32, vp, u64, _TEXT_CB,
+                                                vp, cs, sz]
         L.gt_lcpitv_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput),
                                                         ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
         L.gt_esa_bottomup_hip.argtypes = [ctypes.POINTER(GtSmaxInput), ctypes.POINTER(GtLcpitvVisitor),
@@ -402,6 +409,38 @@ def enumerate_maxpairs(lcptab, llvtab, bwttab, suftab, totallength, nonspecials,
     return np.asarray(_OwnedTriples(out.value, n))
 
 
+def _text_sink():
+    chunks = []
+
+    def cb(_data, text, nbytes):
+        chunks.append(ctypes.string_at(text, nbytes))
+        return 0
+    return chunks, _TEXT_CB(cb)
+
+
+def format_smax_lines(records, occpos, separators):
+    """`gt repfind -smax` pair lines formatted on the GPU
+    (gt_repfind_smax_lines): records is a RECORD_DTYPE array whose lb indexes
+    occpos (text positions); returns the text as bytes."""
+    rec = np.ascontiguousarray(records, dtype=RECORD_DTYPE)
+    occ = np.ascontiguousarray(occpos, dtype=np.uint64)
+    sep = np.ascontiguousarray(separators, dtype=np.uint64)
+    chunks, cb = _text_sink()
+    eb = _errbuf()
+    _check(lib().gt_repfind_smax_lines(rec.ctypes.data, len(rec), occ.ctypes.data, len(occ),
+                                       sep.ctypes.data, len(sep), cb, None, eb, len(eb)), eb)
+    return b"".join(chunks)
+
+
+def repfind_pairs_lines_dev(pairs_ptr, count, sep_ptr, nsep, device=0):
+    """Device (len, pos1, pos2) triples -> gt repfind lines (bytes)."""
+    chunks, cb = _text_sink()
+    eb = _errbuf()
+    _check(lib().gt_repfind_pairs_lines_dev(pairs_ptr, int(count), sep_ptr, int(nsep), int(device),
+                                            cb, None, eb, len(eb)), eb)
+    return b"".join(chunks)
+
+
 class MaxpairsPlan:
     """Device-resident maximal pairs over HBM tables (gt_maxpairs_plan_*)."""
 
@@ -537,21 +576,19 @@ def repfind_smax_lines(intervals, suftab, separators):
 
     Pairs are emitted per interval in occurrence order; each line orders
     pos1 < pos2 and maps both to (seqnum, relpos) as
-    gt_simpleexactselfmatchoutput does (src/tools/gt_repfind.c:49-84)."""
-    sep = np.asarray(separators, dtype=np.uint64)
-    starts = np.concatenate([[0], sep + 1]).astype(np.uint64)
-    lines = []
-    for length, lb, rb in np.asarray(intervals, dtype=np.uint64):
-        occ = [int(suftab[k]) for k in range(int(lb), int(rb) + 1)]
-        for a in range(len(occ)):
-            for b in range(a + 1, len(occ)):
-                p1, p2 = min(occ[a], occ[b]), max(occ[a], occ[b])
-                s1, s2 = int(_seqnum(sep, p1)), int(_seqnum(sep, p2))
-                r1, r2 = p1 - int(starts[s1]), p2 - int(starts[s2])
-                if s1 == s2 and r1 > r2:
-                    continue
-                lines.append("%d %d %d F %d %d %d" % (length, s1, r1, length, s2, r2))
-    return lines
+    gt_simpleexactselfmatchoutput does (src/tools/gt_repfind.c:49-84).  The
+    occurrence positions are gathered from suftab here; pairs and text are
+    generated on the GPU (format_smax_lines)."""
+    itv = np.asarray(intervals, dtype=np.uint64).reshape(-1, 3)
+    if len(itv) == 0:
+        return []
+    width = (itv[:, 2] - itv[:, 1] + 1).astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(width)[:-1]]).astype(np.int64)
+    rows = np.repeat(itv[:, 1].astype(np.int64) - starts, width) + np.arange(int(width.sum()))
+    occ = np.asarray(suftab)[rows].astype(np.uint64)
+    rec = np.empty(len(itv), dtype=RECORD_DTYPE)
+    rec["lb"], rec["lcp"], rec["width"] = starts, itv[:, 0], width
+    return format_smax_lines(rec, occ, separators).decode().splitlines()
 
 
 # ------------------------------------------------------- device-resident API

@@ -810,9 +810,15 @@ fail:
 
 // ------------------------------------------------------------ host boundary
 
-// Host tables -> HBM, count, emit, D2H.  *pairs is malloc'd (3 * *count).
+// Host tables -> HBM, count, emit in the reference's order, D2H.  *pairs is
+// malloc'd (3 * *count).  With lines != NULL the pairs stay in HBM and are
+// formatted there as gt repfind lines (F4) handed to lines(ldata, ...) in
+// chunks; sep[0..nsep) are the separator positions.
 static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pairs,
-                       uint64_t *count, char *errbuf, size_t errlen) {
+                       uint64_t *count, char *errbuf, size_t errlen,
+                       GtRepfindTextFunc lines = nullptr, void *ldata = nullptr,
+                       const uint64_t *sep = nullptr, uint64_t nsep = 0) {
+  uint64_t *dsep = NULL;
   uint8_t *lcp = NULL, *bwt = NULL;
   GtSmaxLlv *llv = NULL;
   void *suf = NULL;
@@ -865,8 +871,8 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
     goto fail_quiet;
   }
   if (total > 0) {
-    *pairs = (uint64_t *) malloc(sizeof (uint64_t) * 3 * total);
-    if (*pairs == NULL) {
+    if (lines == nullptr) *pairs = (uint64_t *) malloc(sizeof (uint64_t) * 3 * total);
+    if (lines == nullptr && *pairs == NULL) {
       mp_seterr(errbuf, errlen, "out of memory (%lu pairs)", (unsigned long) total);
       goto fail_quiet;
     }
@@ -875,12 +881,19 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
       mp_seterr(errbuf, errlen, "maxpairs emission pass failed");
       goto fail_quiet;
     }
-    MPCHK(hipMemcpy(*pairs, out, sizeof (uint64_t) * 3 * total, hipMemcpyDeviceToHost));
+    if (lines != nullptr) {
+      MPCHK(hipMalloc(&dsep, sizeof (uint64_t) * (nsep ? nsep : 1)));
+      if (nsep) MPCHK(hipMemcpy(dsep, sep, sizeof (uint64_t) * nsep, hipMemcpyHostToDevice));
+      if (gt_repfind_pairs_lines_dev(out, total, dsep, nsep, 0, lines, ldata, errbuf, errlen) != 0)
+        goto fail_quiet;
+    } else {
+      MPCHK(hipMemcpy(*pairs, out, sizeof (uint64_t) * 3 * total, hipMemcpyDeviceToHost));
+    }
   }
   *count = total;
   gt_maxpairs_plan_delete(plan);
   {
-    void *bufs[] = {lcp, bwt, suf, llv, out};
+    void *bufs[] = {lcp, bwt, suf, llv, out, dsep};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
       if (bufs[i]) (void) hipFree(bufs[i]);
   }
@@ -889,7 +902,7 @@ fail:
 fail_quiet:
   gt_maxpairs_plan_delete(plan);
   {
-    void *bufs[] = {lcp, bwt, suf, llv, out};
+    void *bufs[] = {lcp, bwt, suf, llv, out, dsep};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
       if (bufs[i]) (void) hipFree(bufs[i]);
   }
@@ -918,4 +931,15 @@ extern "C" int gt_maxpairs_hip_enumerate(const GtSmaxInput *in, unsigned int min
   }
   free(pairs);
   return 0;
+}
+
+extern "C" int gt_repfind_maxpairs_lines(const GtSmaxInput *in, unsigned int minlen,
+                                         const uint64_t *sep, uint64_t nsep, GtRepfindTextFunc cb,
+                                         void *data, char *errbuf, size_t errlen) {
+  uint64_t *pairs = NULL, count = 0;
+  if (cb == NULL) {
+    mp_seterr(errbuf, errlen, "no output function");
+    return -1;
+  }
+  return mp_host_run(in, minlen, &pairs, &count, errbuf, errlen, cb, data, sep, nsep);
 }

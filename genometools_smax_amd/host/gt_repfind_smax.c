@@ -19,7 +19,9 @@
  * Output: one line per occurrence pair of every supermaximal repeat (or per
  * maximal pair), in the format of gt_simpleexactselfmatchoutput
  * (src/tools/gt_repfind.c:49-84, src/match/querymatch.c:130-190):
- * "len seqnum1 relpos1 F len seqnum2 relpos2".  Maximal pairs come in the
+ * "len seqnum1 relpos1 F len seqnum2 relpos2", formatted on the GPU
+ * (gt_repfind_smax_lines / gt_repfind_maxpairs_lines, §8(f) F4) unless
+ * -hostformat asks for the host printf path.  Maximal pairs come in the
  * reference's traversal order (the same lines in the same order).
  * Errors: "gt repfind: error: <msg>" on stderr, exit status 1 (gt_tool_run).
  */
@@ -78,7 +80,52 @@ static int emit_maxpair(void *data, uint64_t len, uint64_t pos1, uint64_t pos2)
   return 0;
 }
 
-/* GtSmaxIntervalFunc: emits the pair lines of one interval */
+/* GtRepfindTextFunc: GPU-formatted lines (F4) to stdout */
+static int write_lines(void *data, const char *text, uint64_t bytes)
+{
+  OutState *st = data;
+  uint64_t k;
+  if (fwrite(text, 1, bytes, stdout) != bytes) return -1;
+  for (k = 0; k < bytes; k++) st->npairs += text[k] == '\n';
+  return 0;
+}
+
+/* -smax lines: intervals from the GPU, their occurrence positions gathered
+ * from the suffix array here, all pairs formatted on the GPU */
+static int smax_lines(OutState *st, const GtSmaxInput *in, unsigned int minlen, int gpus,
+                      char *errbuf, size_t errlen)
+{
+  uint64_t *trip = NULL, cnt = 0, nocc = 0, r, k;
+  GtSmaxRecord *rec = NULL;
+  uint64_t *occ = NULL;
+  int rc = -1;
+  if (gt_smax_hip_enumerate_to_buffer(in, minlen, gpus, &trip, &cnt, errbuf, errlen) != 0)
+    return -1;
+  st->nintervals = cnt;
+  for (r = 0; r < cnt; r++) nocc += trip[3 * r + 2] - trip[3 * r + 1] + 1;
+  rec = malloc(sizeof *rec * (cnt ? cnt : 1));
+  occ = malloc(sizeof *occ * (nocc ? nocc : 1));
+  if (rec == NULL || occ == NULL) {
+    snprintf(errbuf, errlen, "out of memory (%llu occurrences)", (unsigned long long) nocc);
+    goto done;
+  }
+  for (r = 0, nocc = 0; r < cnt; r++) {
+    const uint64_t lb = trip[3 * r + 1], rb = trip[3 * r + 2];
+    rec[r].lb = nocc;
+    rec[r].lcp = (uint32_t) trip[3 * r];
+    rec[r].width = (uint32_t) (rb - lb + 1);
+    for (k = lb; k <= rb; k++) occ[nocc++] = smax_esa_suffix(st->esa, k);
+  }
+  rc = gt_repfind_smax_lines(rec, cnt, occ, nocc, st->sep, st->nsep, write_lines, st, errbuf,
+                             errlen);
+done:
+  free(rec);
+  free(occ);
+  gt_smax_free(trip);
+  return rc;
+}
+
+/* GtSmaxIntervalFunc: emits the pair lines of one interval (host format) */
 static int emit_interval(void *data, uint64_t lcp, uint64_t lb, uint64_t rb)
 {
   OutState *st = data;
@@ -114,6 +161,7 @@ static void usage(FILE *fp)
               "-v         be verbose\n"
               "-gpus      number of GPUs (suffix-array shards)\n"
               "-intervals print lcp-intervals \"lcp lb rb\" instead of pairs\n"
+              "-hostformat format the pair lines on the host (default: on the GPU)\n"
               "-help      display help and exit\n");
 }
 
@@ -134,7 +182,7 @@ int main(int argc, char **argv)
 {
   const char *indexname = NULL;
   long minlen = 20;
-  int smax = 0, scan = 0, verbose = 0, gpus = 1, intervals = 0, i;
+  int smax = 0, scan = 0, verbose = 0, gpus = 1, intervals = 0, hostformat = 0, i;
   const char *excluded = NULL;
   char errbuf[1024], msg[1200];
   SmaxEsa esa;
@@ -149,6 +197,7 @@ int main(int argc, char **argv)
     else if (strcmp(a, "-scan") == 0) scan = 1;
     else if (strcmp(a, "-v") == 0) verbose = 1;
     else if (strcmp(a, "-intervals") == 0) intervals = 1;
+    else if (strcmp(a, "-hostformat") == 0) hostformat = 1;
     else if (strcmp(a, "-help") == 0) { usage(stdout); return 0; }
     else if (strcmp(a, "-l") == 0 || strcmp(a, "-ii") == 0 || strcmp(a, "-gpus") == 0) {
       char *end = NULL;
@@ -210,10 +259,14 @@ int main(int argc, char **argv)
            (unsigned long long) esa.totallength, (unsigned long long) esa.nonspecials,
            (unsigned long long) esa.numllv, gpus);
   }
-  if ((smax ? gt_smax_hip_enumerate(&in, (unsigned int) minlen, gpus, emit_interval, &st,
-                                    errbuf, sizeof errbuf)
-            : gt_maxpairs_hip_enumerate(&in, (unsigned int) minlen, emit_maxpair, &st,
-                                        errbuf, sizeof errbuf)) != 0) {
+  if (intervals || hostformat
+        ? (smax ? gt_smax_hip_enumerate(&in, (unsigned int) minlen, gpus, emit_interval, &st,
+                                        errbuf, sizeof errbuf)
+                : gt_maxpairs_hip_enumerate(&in, (unsigned int) minlen, emit_maxpair, &st,
+                                            errbuf, sizeof errbuf)) != 0
+        : (smax ? smax_lines(&st, &in, (unsigned int) minlen, gpus, errbuf, sizeof errbuf)
+                : gt_repfind_maxpairs_lines(&in, (unsigned int) minlen, st.sep, st.nsep,
+                                            write_lines, &st, errbuf, sizeof errbuf)) != 0) {
     fflush(stdout);
     free((void *) st.sep);
     free(st.occ);

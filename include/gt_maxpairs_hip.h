@@ -108,6 +108,36 @@ int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *plan, uint64_t *out_dev, uint6
 int gt_seqpos_map_dev(const uint64_t *sep_dev, uint64_t nsep, const uint64_t *pairs_dev,
                       uint64_t count, uint64_t *out_dev, int device, void *stream);
 
+/* F4: gt repfind output lines formatted on the GPU
+ * ("len seqnum1 relpos1 F len seqnum2 relpos2\n", gt_simpleexactselfmatchoutput
+ * + gt_querymatch_output, src/tools/gt_repfind.c:49-84,
+ * src/match/querymatch.c:130-190; pos1/pos2 swapped into ascending order,
+ * seqnum/relpos from the sorted separator positions).  The text arrives in
+ * chunks (whole lines, <= 2^22 pairs each) through the callback, in pair
+ * order; a non-zero return stops and yields -1. */
+typedef int (*GtRepfindTextFunc)(void *data, const char *text, uint64_t bytes);
+
+/* device (len, pos1, pos2) triples (e.g. gt_maxpairs_plan_emit_ordered's)
+ * and device separators -> lines */
+int gt_repfind_pairs_lines_dev(const uint64_t *pairs_dev, uint64_t count, const uint64_t *sep_dev,
+                               uint64_t nsep, int device, GtRepfindTextFunc cb, void *data,
+                               char *errbuf, size_t errlen);
+
+/* `gt repfind -l N` (maximal pairs) as lines: gt_maxpairs_hip_enumerate's
+ * pairs, in its (the reference's) order, formatted without leaving HBM. */
+int gt_repfind_maxpairs_lines(const GtSmaxInput *in, unsigned int minlen, const uint64_t *sep,
+                              uint64_t nsep, GtRepfindTextFunc cb, void *data, char *errbuf,
+                              size_t errlen);
+
+/* `gt repfind -smax` as lines: record r's occurrences are
+ * occpos[rec[r].lb .. rec[r].lb + rec[r].width) (text positions in
+ * suffix-array row order); every pair a < b of them, a outer, becomes one
+ * line of length rec[r].lcp -- the order bin/gt-repfind prints them in.
+ * The pairs are generated on the GPU from the records (none stored). */
+int gt_repfind_smax_lines(const GtSmaxRecord *rec, uint64_t nrec, const uint64_t *occpos,
+                          uint64_t nocc, const uint64_t *sep, uint64_t nsep,
+                          GtRepfindTextFunc cb, void *data, char *errbuf, size_t errlen);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,47 @@ def test_cli_at1mb_intervals_and_gpus(tmp_path):
         assert np.array_equal(got, want)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [["-smax", "-l", "20"], ["-smax", "-l", "20", "-gpus", "3"],
+                                  ["-l", "20"], ["-l", "30", "-scan"]])
+def test_cli_gpu_lines_equal_host_lines(tmp_path, args):
+    # F4: the GPU-formatted output is byte-identical to the host printf path
+    idx = _index(tmp_path, "at1MB")
+    gpu = subprocess.run([CLI, "-ii", idx] + args, check=True, capture_output=True).stdout
+    host = subprocess.run([CLI, "-ii", idx, "-hostformat"] + args, check=True,
+                          capture_output=True).stdout
+    assert len(gpu) > 10000 and gpu == host
+
+
+def _many_seqs_fasta(path, rng, nseq):
+    with open(path, "w") as fh:
+        for k in range(nseq):
+            n = int(rng.integers(1, 400))
+            s = "".join("ACGT"[c] for c in rng.integers(0, 4, n))
+            if k % 7 == 0:
+                s = "ACGTTGCAAGGCTTAACCGGTTA" * 3 + s     # shared repeat across sequences
+            fh.write(">s%d\n%s\n" % (k, s))
+
+
+@pytest.mark.gpu
+def test_cli_many_sequences_lines(tmp_path):
+    # thousands of sequences: multi-digit seqnums and relpos through the GPU
+    # formatter, against the oracle's restatement of the output function
+    fasta = str(tmp_path / "many.fna")
+    _many_seqs_fasta(fasta, np.random.default_rng(5), 3000)
+    idx = str(tmp_path / "many")
+    O.index_fasta(fasta, idx, 8)
+    e = O.Esa(G.encode_fasta(open(fasta, "rb").read())[0])
+    for args, want in ((["-smax", "-l", "12"],
+                        O.format_pairs(O.smax_pairs(O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials,
+                                                              12), e.suftab), e.separators)),
+                       (["-l", "12"], O.format_pairs(O.maxpairs(e, 12), e.separators))):
+        out = subprocess.run([CLI, "-ii", idx] + args, check=True, capture_output=True,
+                             text=True).stdout
+        assert len(want) > 1000
+        assert out.splitlines() == [w.rstrip("\n") for w in want]
+
+
 def test_cli_errors(tmp_path):
     r = subprocess.run([CLI, "-l", "8", "-ii", "x"], capture_output=True, text=True)
     assert r.returncode == 1 and "gt repfind: error:" in r.stderr

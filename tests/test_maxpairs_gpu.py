@@ -198,3 +198,60 @@ def test_lcp_255_without_llv_is_an_error():
     llv = e.llv[1:]                      # drop one entry: its 255 byte is orphaned
     with pytest.raises(G.SmaxError, match="255"):
         G.enumerate_maxpairs(e.lcpbytes, llv, e.bwt, e.suftab, e.n, e.nonspecials, 20)
+
+
+def test_smax_lines_edge_values_and_chunks():
+    # F4 formatter on its own: positions up to ~2^40, separators spread
+    # over them, a 2900-occurrence record (4.2 M pairs: more than one 2^22
+    # chunk), 0-length-digit edges; against the oracle's restatement of
+    # gt_querymatch_output line by line
+    rng = np.random.default_rng(77)
+    sep = np.unique(rng.integers(1, 1 << 40, 5000, dtype=np.uint64))
+    sep = np.concatenate([np.array([0, 9, 10, 99, 100], dtype=np.uint64), sep])
+    sep = np.unique(sep)
+    widths = [2900] + [int(w) for w in rng.integers(2, 6, 300)]
+    occ, recs, at = [], [], 0
+    for k, w in enumerate(widths):
+        pos = rng.integers(0, 1 << 40, w, dtype=np.uint64)
+        pos = pos[~np.isin(pos, sep)]
+        if len(pos) < 2:
+            continue
+        occ.append(pos)
+        recs.append((at, int(rng.integers(1, 1 << 31)), len(pos)))
+        at += len(pos)
+    occ = np.concatenate(occ)
+    rec = np.array(recs, dtype=G.RECORD_DTYPE)
+    text = G.format_smax_lines(rec, occ, sep)
+    small = [(int(r["lcp"]), int(a), int(b))
+             for r in rec[1:] for i, a in enumerate(occ[r["lb"]:r["lb"] + r["width"]])
+             for b in occ[r["lb"] + i + 1:r["lb"] + r["width"]]]
+    lines = text.decode().splitlines(keepends=True)
+    w0 = int(rec[0]["width"])
+    n0 = w0 * (w0 - 1) // 2
+    assert len(lines) == n0 + len(small)
+    assert lines[n0:] == O.format_pairs(small, sep)
+    # the big record: every 997th pair plus the chunk seam
+    o0 = occ[:w0]
+    pairs0 = [(a, b) for a in range(w0) for b in range(a + 1, w0)]
+    pick = sorted(set(list(range(0, n0, 997)) + [(1 << 22) - 1, 1 << 22, n0 - 1]))
+    want = O.format_pairs([(int(rec[0]["lcp"]), int(o0[pairs0[k][0]]), int(o0[pairs0[k][1]]))
+                           for k in pick], sep)
+    assert [lines[k] for k in pick] == want
+
+
+def test_maxpairs_lines_dev_equal_oracle_lines():
+    import torch
+    e = oracle_esa("at1MB")
+    got = _gpu(e, 20)
+    pairs = torch.from_numpy(got.view(np.int64).reshape(-1)).cuda()
+    sep = torch.from_numpy(np.ascontiguousarray(e.separators).view(np.int64)).cuda()
+    text = G.repfind_pairs_lines_dev(pairs.data_ptr(), len(got), sep.data_ptr(), len(e.separators))
+    assert text.decode().splitlines(keepends=True) == O.format_pairs(O.maxpairs(e, 20), e.separators)
+
+
+def test_python_repfind_smax_lines():
+    e = oracle_esa("Atinsert.fna")
+    itv = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8)
+    got = G.repfind_smax_lines(itv, e.suftab, e.separators)
+    want = [w.rstrip("\n") for w in O.format_pairs(O.smax_pairs(itv, e.suftab), e.separators)]
+    assert len(got) == 205 and got == want
