@@ -95,7 +95,18 @@ class GtMaxpairsDevInput(ctypes.Structure):
         ("suf_bytes", ctypes.c_int),
         ("nonspecials", ctypes.c_uint64),
         ("device", ctypes.c_int),
-        ("bwtpk_dev", ctypes.c_void_p),
+    ]
+
+
+class GtLcpitvDevInput(ctypes.Structure):
+    _fields_ = [
+        ("lcp_dev", ctypes.c_void_p),
+        ("llv_dev", ctypes.c_void_p),
+        ("numllv", ctypes.c_uint64),
+        ("suf_dev", ctypes.c_void_p),
+        ("suf_bytes", ctypes.c_int),
+        ("nonspecials", ctypes.c_uint64),
+        ("device", ctypes.c_int),
     ]
 
 
@@ -191,6 +202,13 @@ def lib():
                                                 vp, cs, sz]
         L.gt_lcpitv_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput),
                                                         ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
+        L.gt_lcpitv_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtLcpitvDevInput), cs, sz]
+        L.gt_lcpitv_plan_delete.argtypes = [vp]
+        L.gt_lcpitv_plan_intervals.argtypes = [vp, ctypes.POINTER(vp)]
+        L.gt_lcpitv_plan_intervals.restype = u64
+        L.gt_lcpitv_plan_num_events.argtypes = [vp]
+        L.gt_lcpitv_plan_num_events.restype = u64
+        L.gt_lcpitv_plan_events.argtypes = [vp, vp, vp]
         L.gt_esa_bottomup_hip.argtypes = [ctypes.POINTER(GtSmaxInput), ctypes.POINTER(GtLcpitvVisitor),
                                           vp, cs, sz]
         _lib = L
@@ -439,6 +457,45 @@ def repfind_pairs_lines_dev(pairs_ptr, count, sep_ptr, nsep, device=0):
     _check(lib().gt_repfind_pairs_lines_dev(pairs_ptr, int(count), sep_ptr, int(nsep), int(device),
                                             cb, None, eb, len(eb)), eb)
     return b"".join(chunks)
+
+
+class LcpitvPlan:
+    """Device-resident lcp-interval tree and visitor event stream
+    (gt_lcpitv_plan_*)."""
+
+    def __init__(self, lcp_ptr, llv_ptr, numllv, suf_ptr, suf_bytes, nonspecials, device=0):
+        inp = GtLcpitvDevInput()
+        inp.lcp_dev, inp.llv_dev, inp.numllv = lcp_ptr, llv_ptr, numllv
+        inp.suf_dev, inp.suf_bytes = suf_ptr, suf_bytes
+        inp.nonspecials, inp.device = nonspecials, device
+        self._p = ctypes.c_void_p()
+        eb = _errbuf()
+        _check(lib().gt_lcpitv_plan_create(ctypes.byref(self._p), ctypes.byref(inp), eb, len(eb)), eb)
+        self.device = device
+
+    def intervals(self):
+        """(count, device pointer) of the pop-ordered 5-word records."""
+        ptr = ctypes.c_void_p()
+        n = lib().gt_lcpitv_plan_intervals(self._p, ctypes.byref(ptr))
+        return n, ptr.value
+
+    def num_events(self):
+        return lib().gt_lcpitv_plan_num_events(self._p)
+
+    def events(self, out_ptr, stream=0):
+        if lib().gt_lcpitv_plan_events(self._p, out_ptr, stream) != 0:
+            raise SmaxError("gt_lcpitv_plan_events failed")
+
+    def close(self):
+        if self._p:
+            lib().gt_lcpitv_plan_delete(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class MaxpairsPlan:
@@ -858,6 +915,11 @@ class DeviceEsa:
             raise SmaxError("maxpairs needs the suffix array: build with keep_suftab=True")
         return MaxpairsPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
                             self.esa.suftab_dev, 4, self.nonspecials, minlen, self.device)
+
+    def lcpitv_plan(self):
+        """lcp-interval tree + visitor events over the device tables."""
+        return LcpitvPlan(self.esa.lcptab_dev, self.esa.llvtab_dev, self.numllv,
+                          self.esa.suftab_dev or None, 4, self.nonspecials, self.device)
 
     def release(self):
         if self.esa.lcptab_dev:

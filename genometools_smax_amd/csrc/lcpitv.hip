@@ -17,11 +17,17 @@
 //
 // Each search climbs a 64-ary min hierarchy over the exact LCP array (u32)
 // and descends again: at most 63 reads per level, 6 levels for 10^10 rows.
-// One thread per row; the intervals are compacted, radix-sorted into pop
-// order (rb ascending, depth descending) and the host replays the visitor
-// events in the reference's exact order from them (the replay is a merge,
-// no stack: which callback comes when is decided by LCP[idx], LCP[idx+1]
-// and whether a father shares its child's lb).
+// One thread per row; the intervals are compacted and radix-sorted into pop
+// order (rb ascending, depth descending).  The tree stays in HBM
+// (GtLcpitvPlan); the visitor's event stream is generated there too, every
+// event at its position in the reference's order, no stack and no replay
+// loop (li_events_*): per row idx (X = LCP[idx], Y = LCP[idx+1]) the
+// traversal emits exactly one leaf edge, then for every interval popped at
+// idx (pop order) its lcp-interval and branching-edge events, so with
+// P(idx) = #intervals with rb < idx the leaf of row idx sits at
+// idx + 2 P(idx) and popped interval r of row idx at idx + 2 P(idx) + 1 + 2r.
+// The host entry points download the events in chunks and call the
+// visitor.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -188,7 +194,7 @@ __global__ void __launch_bounds__(256) li_count_kernel(LiLevels L, uint64_t N, u
 // leftmost l-index, and the pop-order sort key rb << 32 | ~lcp
 __global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N,
                                                        const uint64_t *wg_off, uint64_t *rec,
-                                                       uint64_t *key, uint32_t *idx) {
+                                                       uint64_t *key, uint64_t *idx) {
   const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   uint64_t lb = 0;
   const bool open = li_leftmost(L, k, N, &lb);
@@ -208,11 +214,21 @@ __global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N,
   r[2] = q - 1;
   r[3] = fl;
   r[4] = flb;
-  key[pos] = ((q - 1) << 32) | (uint64_t) (0xffffffffu - v);
-  idx[pos] = (uint32_t) pos;
+  key[pos] = ((q - 1) << 32) | (uint64_t) (0xffffffffu - v);   // rb < 2^32 (else li_key_kernel)
+  idx[pos] = pos;
 }
 
-__global__ void __launch_bounds__(256) li_gather_kernel(const uint64_t *rec, const uint32_t *idx,
+// keys of the two-pass sort (rb >= 2^32): pass 0 ~lcp, pass 1 rb, of the
+// records in the current permutation
+__global__ void __launch_bounds__(256) li_key_kernel(const uint64_t *rec, const uint64_t *perm,
+                                                     uint64_t n, int pass, uint64_t *key) {
+  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t *r = rec + 5 * perm[i];
+  key[i] = pass == 0 ? (uint64_t) (0xffffffffu - (uint32_t) r[0]) : r[2];
+}
+
+__global__ void __launch_bounds__(256) li_gather_kernel(const uint64_t *rec, const uint64_t *idx,
                                                         uint64_t n, uint64_t *out) {
   const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -222,38 +238,306 @@ __global__ void __launch_bounds__(256) li_gather_kernel(const uint64_t *rec, con
   for (int f = 0; f < 5; f++) w[f] = r[f];
 }
 
-// father lb of leaf idx when it is attached in step 1 (LCP[idx+1] <= LCP[idx])
-__global__ void __launch_bounds__(256) li_leaf_kernel(LiLevels L, uint64_t N, uint64_t *leaf_lb) {
-  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  const uint32_t xi = L.lv[0][i], xn = L.lv[0][i + 1];
-  uint64_t lb = i;
-  if (xn <= xi) lb = xi == 0 ? 0 : li_prev(L, i, xi, true);
-  leaf_lb[i] = lb;
+// ------------------------------------------------------------ events
+
+// rows [lo, hi) of the sorted intervals: first index whose rb >= v
+__device__ __forceinline__ uint64_t li_lower_rb(const uint64_t *itv, uint64_t n, uint64_t v) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (itv[5 * mid + 2] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
 }
 
-// ------------------------------------------------------------ host
+// event positions of root edges that consume the reference's
+// firstedgefromroot flag (leaf edges to the root attached in step 1 and
+// branching edges to the root of pops); the first one in stream order gets
+// firstsucc = 1 (src/match/esa-bottomup.c:134-141)
+__global__ void __launch_bounds__(256) li_rootfirst_leaf_kernel(LiLevels L, uint64_t N,
+                                                                const uint64_t *itv, uint64_t nitv,
+                                                                unsigned long long *first) {
+  const uint64_t idx = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (idx >= N) return;
+  const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
+  if (X != 0 || Y > X) return;
+  const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
+  atomicMin(first, (unsigned long long) pos);
+}
+
+__global__ void __launch_bounds__(256) li_rootfirst_itv_kernel(const uint64_t *itv, uint64_t nitv,
+                                                               unsigned long long *first) {
+  const uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (j >= nitv) return;
+  const uint64_t *r = itv + 5 * j;
+  if (r[3] != 0) return;
+  const uint64_t g = li_lower_rb(itv, nitv, r[2]);
+  const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g) + 1;
+  atomicMin(first, (unsigned long long) pos);
+}
+
+// leaf edge of row idx: (0, firstsucc, fd, flb, leafnumber, 0, 0)
+template <typename SufT>
+__global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_t N,
+                                                             const uint64_t *itv, uint64_t nitv,
+                                                             const void *suf,
+                                                             const unsigned long long *first,
+                                                             uint64_t *ev) {
+  const uint64_t idx = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (idx >= N) return;
+  const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
+  const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
+  uint64_t *w = ev + 7 * pos;
+  w[0] = 0;
+  if (Y <= X) {            // attached to the interval of depth X holding idx
+    w[1] = (X == 0 && pos == *first) ? 1u : 0u;
+    w[2] = X;
+    w[3] = X == 0 ? 0 : li_prev(L, idx, X, true);
+  } else {                 // firstsucc leaf of the new interval (Y, idx)
+    w[1] = 1;
+    w[2] = Y;
+    w[3] = idx;
+  }
+  w[4] = suf == nullptr ? 0 : (uint64_t) reinterpret_cast<const SufT *>(suf)[idx];
+  w[5] = 0;
+  w[6] = 0;
+}
+
+// popped interval j: (2, 0, lcp, lb, rb, 0, 0) then its branching edge
+// (1, firstsucc, fd, flb, sd, slb, srb); a father that is new at rb (same
+// lb, pushed after the pops) gets the firstsucc edge with its own lb
+__global__ void __launch_bounds__(256) li_events_itv_kernel(const uint64_t *itv, uint64_t nitv,
+                                                            const unsigned long long *first,
+                                                            uint64_t *ev) {
+  const uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (j >= nitv) return;
+  const uint64_t *r = itv + 5 * j;
+  const uint64_t g = li_lower_rb(itv, nitv, r[2]);
+  const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g);
+  uint64_t *w = ev + 7 * pos;
+  w[0] = 2; w[1] = 0; w[2] = r[0]; w[3] = r[1]; w[4] = r[2]; w[5] = 0; w[6] = 0;
+  w += 7;
+  const bool newfather = r[3] > 0 && r[4] == r[1];
+  w[0] = 1;
+  w[1] = newfather ? 1u : ((r[3] == 0 && pos + 1 == *first) ? 1u : 0u);
+  w[2] = r[3];
+  w[3] = newfather ? r[1] : r[4];
+  w[4] = r[0]; w[5] = r[1]; w[6] = r[2];
+}
+
+// ------------------------------------------------------------ plan
 
 static unsigned li_blocks(uint64_t n) { return (unsigned) ((n + 255) / 256); }
 
-// Builds the tree on device 0: *itv (5 * *count, pop order) and, if
-// leaf_lb != NULL, the N step-1 leaf fathers.  Host buffers are malloc'd.
-static int li_build(const GtSmaxInput *in, uint64_t **itv, uint64_t *count, uint64_t **leaf_lb,
-                    char *errbuf, size_t errlen) {
-  uint8_t *lcp = NULL;
-  GtSmaxLlv *llv = NULL;
-  uint32_t *lev[LI_MAXLEV] = {NULL};
-  uint32_t *derr = NULL, herr = 0, *wg_cnt = NULL, *idx_in = NULL, *idx_out = NULL;
-  uint64_t *wg_off = NULL, *rec = NULL, *key_in = NULL, *key_out = NULL, *sorted = NULL,
-           *dleaf = NULL;
+struct GtLcpitvPlan {
+  GtLcpitvDevInput in;
+  uint32_t *lev[LI_MAXLEV];
+  LiLevels L;
+  uint64_t nitv;
+  uint64_t *itv;                 // 5 * nitv, pop order
+  unsigned long long *first;     // position of the first root edge
+};
+
+extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
+  if (p == NULL) return;
+  (void) hipSetDevice(p->in.device);
+  for (int l = 0; l < LI_MAXLEV; l++)
+    if (p->lev[l]) (void) hipFree(p->lev[l]);
+  if (p->itv) (void) hipFree(p->itv);
+  if (p->first) (void) hipFree(p->first);
+  free(p);
+}
+
+extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInput *in,
+                                     char *errbuf, size_t errlen) {
+  GtLcpitvPlan *p = NULL;
+  uint32_t *derr = NULL, herr = 0, *wg_cnt = NULL;
+  uint64_t *wg_off = NULL, *rec = NULL, *key_a = NULL, *key_b = NULL, *idx_a = NULL,
+           *idx_b = NULL;
   void *tmp = NULL;
   size_t tmp_bytes = 0;
-  LiLevels L;
-  uint64_t N, nwg, nitv = 0;
-  memset(&L, 0, sizeof L);
-  *itv = NULL;
-  *count = 0;
-  if (leaf_lb) *leaf_lb = NULL;
+  uint64_t N, nwg;
+  *planp = NULL;
+  if (in == NULL || in->lcp_dev == NULL) {
+    li_seterr(errbuf, errlen, "missing device lcptab");
+    return -1;
+  }
+  if (in->numllv > 0 && in->llv_dev == NULL) {
+    li_seterr(errbuf, errlen, "missing device llvtab");
+    return -1;
+  }
+  if (in->suf_dev != NULL && in->suf_bytes != 4 && in->suf_bytes != 8) {
+    li_seterr(errbuf, errlen, "suftab entries must be 4 or 8 bytes (got %d)", in->suf_bytes);
+    return -1;
+  }
+  p = (GtLcpitvPlan *) calloc(1, sizeof *p);
+  if (p == NULL) {
+    li_seterr(errbuf, errlen, "out of memory");
+    return -1;
+  }
+  p->in = *in;
+  N = in->nonspecials;
+  LICHK(hipSetDevice(in->device));
+  LICHK(hipMalloc(&derr, sizeof (uint32_t)));
+  LICHK(hipMemset(derr, 0, sizeof (uint32_t)));
+  LICHK(hipMalloc(&p->first, sizeof (unsigned long long)));
+  // level 0: exact LCP, then 64-ary mins until one entry remains
+  p->L.n[0] = N + 1;
+  LICHK(hipMalloc(&p->lev[0], sizeof (uint32_t) * p->L.n[0]));
+  hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, 0, in->lcp_dev, N,
+                     p->lev[0]);
+  LICHK(hipGetLastError());
+  if (in->numllv > 0) {
+    hipLaunchKernelGGL(li_llv_kernel, dim3(li_blocks(in->numllv)), dim3(256), 0, 0, in->llv_dev,
+                       in->numllv, in->lcp_dev, N, p->lev[0], derr);
+    LICHK(hipGetLastError());
+  }
+  p->L.nlev = 1;
+  while (p->L.n[p->L.nlev - 1] > 1 && p->L.nlev < LI_MAXLEV) {
+    const int l = p->L.nlev;
+    p->L.n[l] = (p->L.n[l - 1] + 63) / 64;
+    LICHK(hipMalloc(&p->lev[l], sizeof (uint32_t) * p->L.n[l]));
+    hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(p->L.n[l])), dim3(256), 0, 0, p->lev[l - 1],
+                       p->L.n[l - 1], p->lev[l], p->L.n[l]);
+    LICHK(hipGetLastError());
+    p->L.nlev++;
+  }
+  if (p->L.n[p->L.nlev - 1] > 1) {
+    li_seterr(errbuf, errlen, "too many suffixes for the minimum hierarchy");
+    goto fail;
+  }
+  for (int l = 0; l < p->L.nlev; l++) p->L.lv[l] = p->lev[l];
+  LICHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
+  if (herr & 1u) { li_seterr(errbuf, errlen, "lcp value >= 2^32-1 in .llv"); goto fail; }
+  if (herr & 2u) { li_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
+  // intervals: count per workgroup, scan, write, sort into pop order
+  nwg = (N + 255) / 256;
+  if (nwg > 0x7fffffffull) { li_seterr(errbuf, errlen, "too many suffixes"); goto fail; }
+  LICHK(hipMalloc(&wg_cnt, sizeof (uint32_t) * (nwg + 1)));
+  LICHK(hipMalloc(&wg_off, sizeof (uint64_t) * (nwg + 1)));
+  if (nwg > 0) {
+    hipLaunchKernelGGL(li_count_kernel, dim3((unsigned) nwg), dim3(256), 0, 0, p->L, N, wg_cnt);
+    LICHK(hipGetLastError());
+    LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
+                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
+    LICHK(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
+    LICHK(rocprim::exclusive_scan(tmp, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
+                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
+    uint64_t lo = 0;
+    uint32_t lc = 0;
+    LICHK(hipMemcpy(&lo, wg_off + nwg - 1, sizeof lo, hipMemcpyDeviceToHost));
+    LICHK(hipMemcpy(&lc, wg_cnt + nwg - 1, sizeof lc, hipMemcpyDeviceToHost));
+    p->nitv = lo + lc;
+  }
+  LICHK(hipMalloc(&p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
+  if (p->nitv > 0) {
+    const uint64_t n = p->nitv;
+    LICHK(hipMalloc(&rec, sizeof (uint64_t) * 5 * n));
+    LICHK(hipMalloc(&key_a, sizeof (uint64_t) * n));
+    LICHK(hipMalloc(&key_b, sizeof (uint64_t) * n));
+    LICHK(hipMalloc(&idx_a, sizeof (uint64_t) * n));
+    LICHK(hipMalloc(&idx_b, sizeof (uint64_t) * n));
+    hipLaunchKernelGGL(li_write_kernel, dim3((unsigned) nwg), dim3(256), 0, 0, p->L, N, wg_off, rec,
+                       key_a, idx_a);
+    LICHK(hipGetLastError());
+    LICHK(hipFree(tmp));
+    tmp = NULL;
+    tmp_bytes = 0;
+    LICHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0,
+                                    64, (hipStream_t) 0));
+    LICHK(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
+    if (N < 0xffffffffull) {
+      // key = rb << 32 | ~lcp: one pass
+      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 64,
+                                      (hipStream_t) 0));
+    } else {
+      // rb >= 2^32 possible: stable passes by ~lcp, then by rb
+      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_a, n, 0, key_a);
+      LICHK(hipGetLastError());
+      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 32,
+                                      (hipStream_t) 0));
+      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, 1, key_a);
+      LICHK(hipGetLastError());
+      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_b, idx_a, (size_t) n, 0, 64,
+                                      (hipStream_t) 0));
+      uint64_t *t = idx_a; idx_a = idx_b; idx_b = t;
+    }
+    hipLaunchKernelGGL(li_gather_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, p->itv);
+    LICHK(hipGetLastError());
+  }
+  LICHK(hipDeviceSynchronize());
+  {
+    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
+      if (bufs[i]) (void) hipFree(bufs[i]);
+  }
+  *planp = p;
+  return 0;
+fail:
+  {
+    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
+      if (bufs[i]) (void) hipFree(bufs[i]);
+  }
+  gt_lcpitv_plan_delete(p);
+  return -1;
+}
+
+extern "C" uint64_t gt_lcpitv_plan_intervals(const GtLcpitvPlan *p, const uint64_t **itv_dev) {
+  if (itv_dev) *itv_dev = p->itv;
+  return p->nitv;
+}
+
+extern "C" uint64_t gt_lcpitv_plan_num_events(const GtLcpitvPlan *p) {
+  return p->in.nonspecials + 2 * p->nitv;
+}
+
+extern "C" int gt_lcpitv_plan_events(GtLcpitvPlan *p, uint64_t *events_dev, void *stream) {
+  hipStream_t s = (hipStream_t) stream;
+  const uint64_t N = p->in.nonspecials, n = p->nitv;
+  const unsigned long long none = ~0ull;
+  if (hipSetDevice(p->in.device) != hipSuccess) return -1;
+  if (N == 0) return 0;
+  if (hipMemcpyAsync(p->first, &none, sizeof none, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+  hipLaunchKernelGGL(li_rootfirst_leaf_kernel, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N, p->itv,
+                     n, p->first);
+  if (n > 0)
+    hipLaunchKernelGGL(li_rootfirst_itv_kernel, dim3(li_blocks(n)), dim3(256), 0, s, p->itv, n,
+                       p->first);
+  if (p->in.suf_bytes == 4)
+    hipLaunchKernelGGL(li_events_leaf_kernel<uint32_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N,
+                       p->itv, n, p->in.suf_dev, p->first, events_dev);
+  else
+    hipLaunchKernelGGL(li_events_leaf_kernel<uint64_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N,
+                       p->itv, n, p->in.suf_dev, p->first, events_dev);
+  if (n > 0)
+    hipLaunchKernelGGL(li_events_itv_kernel, dim3(li_blocks(n)), dim3(256), 0, s, p->itv, n,
+                       p->first, events_dev);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------ host boundary
+
+// host tables -> HBM -> plan (device 0); *buf holds the device copies
+struct LiHostTables {
+  uint8_t *lcp;
+  GtSmaxLlv *llv;
+  void *suf;
+};
+
+static void li_host_free(LiHostTables *h) {
+  if (h->lcp) (void) hipFree(h->lcp);
+  if (h->llv) (void) hipFree(h->llv);
+  if (h->suf) (void) hipFree(h->suf);
+  memset(h, 0, sizeof *h);
+}
+
+static int li_host_plan(const GtSmaxInput *in, bool with_suf, LiHostTables *h, GtLcpitvPlan **plan,
+                        char *errbuf, size_t errlen) {
+  GtLcpitvDevInput din;
+  uint64_t N;
+  memset(h, 0, sizeof *h);
+  *plan = NULL;
   if (in == NULL || in->lcptab == NULL) {
     li_seterr(errbuf, errlen, "missing lcptab");
     return -1;
@@ -268,152 +552,74 @@ static int li_build(const GtSmaxInput *in, uint64_t **itv, uint64_t *count, uint
     return -1;
   }
   N = in->nonspecials;
-  if (N >= 0xffffffffull) {
-    li_seterr(errbuf, errlen, "lcp-interval enumeration supports < 2^32 suffixes");
-    return -1;
-  }
   LICHK(hipSetDevice(0));
-  LICHK(hipMalloc(&lcp, N + 1));
-  LICHK(hipMemcpy(lcp, in->lcptab, N + 1, hipMemcpyHostToDevice));
+  LICHK(hipMalloc(&h->lcp, N + 1));
+  LICHK(hipMemcpy(h->lcp, in->lcptab, N + 1, hipMemcpyHostToDevice));
   if (in->numllv > 0) {
-    LICHK(hipMalloc(&llv, sizeof (GtSmaxLlv) * in->numllv));
-    LICHK(hipMemcpy(llv, in->llvtab, sizeof (GtSmaxLlv) * in->numllv, hipMemcpyHostToDevice));
+    LICHK(hipMalloc(&h->llv, sizeof (GtSmaxLlv) * in->numllv));
+    LICHK(hipMemcpy(h->llv, in->llvtab, sizeof (GtSmaxLlv) * in->numllv, hipMemcpyHostToDevice));
   }
-  LICHK(hipMalloc(&derr, sizeof (uint32_t)));
-  LICHK(hipMemset(derr, 0, sizeof (uint32_t)));
-  // level 0: exact LCP, then 64-ary mins until one entry remains
-  L.n[0] = N + 1;
-  LICHK(hipMalloc(&lev[0], sizeof (uint32_t) * L.n[0]));
-  hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, 0, lcp, N, lev[0]);
-  LICHK(hipGetLastError());
-  if (in->numllv > 0) {
-    hipLaunchKernelGGL(li_llv_kernel, dim3(li_blocks(in->numllv)), dim3(256), 0, 0, llv,
-                       in->numllv, lcp, N, lev[0], derr);
-    LICHK(hipGetLastError());
+  if (with_suf && N > 0) {
+    LICHK(hipMalloc(&h->suf, (size_t) in->suftab_bytes * N));
+    LICHK(hipMemcpy(h->suf, in->suftab, (size_t) in->suftab_bytes * N, hipMemcpyHostToDevice));
   }
-  L.nlev = 1;
-  while (L.n[L.nlev - 1] > 1 && L.nlev < LI_MAXLEV) {
-    const int l = L.nlev;
-    L.n[l] = (L.n[l - 1] + 63) / 64;
-    LICHK(hipMalloc(&lev[l], sizeof (uint32_t) * L.n[l]));
-    hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(L.n[l])), dim3(256), 0, 0, lev[l - 1],
-                       L.n[l - 1], lev[l], L.n[l]);
-    LICHK(hipGetLastError());
-    L.nlev++;
-  }
-  for (int l = 0; l < L.nlev; l++) L.lv[l] = lev[l];
-  LICHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
-  if (herr & 1u) { li_seterr(errbuf, errlen, "lcp value >= 2^32-1 in .llv"); goto fail; }
-  if (herr & 2u) { li_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
-  // intervals: count per workgroup, scan, write, sort into pop order
-  nwg = (N + 255) / 256;
-  LICHK(hipMalloc(&wg_cnt, sizeof (uint32_t) * (nwg + 1)));
-  LICHK(hipMalloc(&wg_off, sizeof (uint64_t) * (nwg + 1)));
-  hipLaunchKernelGGL(li_count_kernel, dim3((unsigned) nwg), dim3(256), 0, 0, L, N, wg_cnt);
-  LICHK(hipGetLastError());
-  LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
-                                rocprim::plus<uint64_t>(), (hipStream_t) 0));
-  LICHK(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
-  LICHK(rocprim::exclusive_scan(tmp, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
-                                rocprim::plus<uint64_t>(), (hipStream_t) 0));
-  {
-    uint64_t lo = 0;
-    uint32_t lc = 0;
-    LICHK(hipMemcpy(&lo, wg_off + nwg - 1, sizeof lo, hipMemcpyDeviceToHost));
-    LICHK(hipMemcpy(&lc, wg_cnt + nwg - 1, sizeof lc, hipMemcpyDeviceToHost));
-    nitv = lo + lc;
-  }
-  if (nitv > 0) {
-    LICHK(hipMalloc(&rec, sizeof (uint64_t) * 5 * nitv));
-    LICHK(hipMalloc(&key_in, sizeof (uint64_t) * nitv));
-    LICHK(hipMalloc(&key_out, sizeof (uint64_t) * nitv));
-    LICHK(hipMalloc(&idx_in, sizeof (uint32_t) * nitv));
-    LICHK(hipMalloc(&idx_out, sizeof (uint32_t) * nitv));
-    LICHK(hipMalloc(&sorted, sizeof (uint64_t) * 5 * nitv));
-    hipLaunchKernelGGL(li_write_kernel, dim3((unsigned) nwg), dim3(256), 0, 0, L, N, wg_off, rec,
-                       key_in, idx_in);
-    LICHK(hipGetLastError());
-    LICHK(hipFree(tmp));
-    tmp = NULL;
-    tmp_bytes = 0;
-    LICHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key_in, key_out, idx_in, idx_out,
-                                    (size_t) nitv, 0, 64, (hipStream_t) 0));
-    LICHK(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
-    LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_in, key_out, idx_in, idx_out,
-                                    (size_t) nitv, 0, 64, (hipStream_t) 0));
-    hipLaunchKernelGGL(li_gather_kernel, dim3(li_blocks(nitv)), dim3(256), 0, 0, rec, idx_out,
-                       nitv, sorted);
-    LICHK(hipGetLastError());
-    *itv = (uint64_t *) malloc(sizeof (uint64_t) * 5 * nitv);
-    if (*itv == NULL) { li_seterr(errbuf, errlen, "out of memory"); goto fail; }
-    LICHK(hipMemcpy(*itv, sorted, sizeof (uint64_t) * 5 * nitv, hipMemcpyDeviceToHost));
-  }
-  if (leaf_lb != NULL && N > 0) {
-    LICHK(hipMalloc(&dleaf, sizeof (uint64_t) * N));
-    hipLaunchKernelGGL(li_leaf_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, L, N, dleaf);
-    LICHK(hipGetLastError());
-    *leaf_lb = (uint64_t *) malloc(sizeof (uint64_t) * N);
-    if (*leaf_lb == NULL) { li_seterr(errbuf, errlen, "out of memory"); goto fail; }
-    LICHK(hipMemcpy(*leaf_lb, dleaf, sizeof (uint64_t) * N, hipMemcpyDeviceToHost));
-  }
-  *count = nitv;
-  {
-    void *bufs[] = {lcp, llv, derr, wg_cnt, wg_off, rec, key_in, key_out, idx_in, idx_out,
-                    sorted, dleaf, tmp};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
-    for (int l = 0; l < LI_MAXLEV; l++)
-      if (lev[l]) (void) hipFree(lev[l]);
+  din.lcp_dev = h->lcp;
+  din.llv_dev = h->llv;
+  din.numllv = in->numllv;
+  din.suf_dev = h->suf;
+  din.suf_bytes = with_suf ? in->suftab_bytes : 8;
+  din.nonspecials = N;
+  din.device = 0;
+  if (gt_lcpitv_plan_create(plan, &din, errbuf, errlen) != 0) {
+    li_host_free(h);
+    return -1;
   }
   return 0;
 fail:
-  {
-    void *bufs[] = {lcp, llv, derr, wg_cnt, wg_off, rec, key_in, key_out, idx_in, idx_out,
-                    sorted, dleaf, tmp};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
-    for (int l = 0; l < LI_MAXLEV; l++)
-      if (lev[l]) (void) hipFree(lev[l]);
-  }
-  free(*itv);
-  *itv = NULL;
-  if (leaf_lb) { free(*leaf_lb); *leaf_lb = NULL; }
+  li_host_free(h);
   return -1;
 }
 
 extern "C" int gt_lcpitv_hip_enumerate_to_buffer(const GtSmaxInput *in, uint64_t **itv,
                                                  uint64_t *count, char *errbuf, size_t errlen) {
-  return li_build(in, itv, count, NULL, errbuf, errlen);
+  LiHostTables h;
+  GtLcpitvPlan *plan = NULL;
+  *itv = NULL;
+  *count = 0;
+  if (li_host_plan(in, false, &h, &plan, errbuf, errlen) != 0) return -1;
+  const uint64_t n = plan->nitv;
+  if (n > 0) {
+    *itv = (uint64_t *) malloc(sizeof (uint64_t) * 5 * n);
+    if (*itv == NULL) {
+      li_seterr(errbuf, errlen, "out of memory");
+    } else if (hipMemcpy(*itv, plan->itv, sizeof (uint64_t) * 5 * n, hipMemcpyDeviceToHost) !=
+               hipSuccess) {
+      li_seterr(errbuf, errlen, "device to host copy failed");
+      free(*itv);
+      *itv = NULL;
+    }
+    if (*itv == NULL) {
+      gt_lcpitv_plan_delete(plan);
+      li_host_free(&h);
+      return -1;
+    }
+  }
+  *count = n;
+  gt_lcpitv_plan_delete(plan);
+  li_host_free(&h);
+  return 0;
 }
 
-// exact LCP of row k from the host tables (A3 decoding; llv cursor advances)
-static inline uint64_t li_host_lcp(const GtSmaxInput *in, uint64_t k, uint64_t *cursor) {
-  if (k == 0 || k >= in->nonspecials) return 0;
-  const uint8_t b = in->lcptab[k];
-  if (b < 255) return b;
-  while (*cursor < in->numllv && in->llvtab[*cursor].position < k) (*cursor)++;
-  return *cursor < in->numllv && in->llvtab[*cursor].position == k ? in->llvtab[*cursor].value
-                                                                     : 255;
-}
+// gt_esa_bottomup's callback sequence from the device event stream, downloaded
+// in chunks of LI_EV_CHUNK events
+#define LI_EV_CHUNK (1ull << 20)
 
-static inline uint64_t li_suffix(const GtSmaxInput *in, uint64_t k) {
-  return in->suftab_bytes == 4 ? ((const uint32_t *) in->suftab)[k]
-                               : ((const uint64_t *) in->suftab)[k];
-}
-
-// Replays gt_esa_bottomup's callback sequence (src/match/esa-bottomup.c:
-// 131-271) from the tree: per row idx, with X = LCP[idx], Y = LCP[idx+1]:
-//   Y <= X: leaf edge to the interval of depth X holding idx (lb from the GPU)
-//   the intervals with rb == idx (pop order): lcp-interval callback, then
-//     the branching edge to the father -- unless the father is new at idx
-//     (same lb, depth Y), whose edge (firstsucc) comes after the pops
-//   Y > X: leaf edge (firstsucc) to the new interval (Y, idx)
-// firstsucc on an edge from the root: only the first such edge.
 extern "C" int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor *v, void *data,
                                    char *errbuf, size_t errlen) {
-  uint64_t *itv = NULL, *leaf_lb = NULL, count = 0, j = 0, cur2 = 0;
+  LiHostTables h;
+  GtLcpitvPlan *plan = NULL;
+  uint64_t *ev = NULL, *host = NULL, E;
   int rc = 0;
-  bool rootfirst = true;
   if (v == NULL) {
     li_seterr(errbuf, errlen, "missing visitor");
     return -1;
@@ -423,44 +629,44 @@ extern "C" int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor 
     li_seterr(errbuf, errlen, "leaf edges need suftab (4 or 8 bytes per entry)");
     return -1;
   }
-  if (li_build(in, &itv, &count, v->leaf_edge ? &leaf_lb : NULL, errbuf, errlen) != 0) return -1;
-  const uint64_t N = in->nonspecials;
-  uint64_t X = 0;
-  for (uint64_t idx = 0; idx < N && rc == 0; idx++) {
-    const uint64_t Y = li_host_lcp(in, idx + 1, &cur2);
-    if (Y <= X && v->leaf_edge) {
-      const bool first = X == 0 && rootfirst;
-      if (X == 0) rootfirst = false;
-      rc = v->leaf_edge(data, first, X, leaf_lb[idx], li_suffix(in, idx));
-    } else if (Y <= X && X == 0) {
-      rootfirst = false;
+  if (li_host_plan(in, v->leaf_edge != NULL, &h, &plan, errbuf, errlen) != 0) return -1;
+  E = gt_lcpitv_plan_num_events(plan);
+  if (E > 0) {
+    LICHK(hipMalloc(&ev, sizeof (uint64_t) * 7 * E));
+    if (gt_lcpitv_plan_events(plan, ev, NULL) != 0) {
+      li_seterr(errbuf, errlen, "event generation failed");
+      goto fail;
     }
-    const uint64_t *last = NULL;
-    while (rc == 0 && j < count && itv[5 * j + 2] == idx) {
-      const uint64_t *r = itv + 5 * j++;
-      if (v->lcp_interval) rc = v->lcp_interval(data, r[0], r[1], r[2]);
-      if (rc != 0) break;
-      if (r[3] > 0 && r[4] == r[1]) {
-        last = r;                        // father pushed after the pops
-      } else {
-        const bool first = r[3] == 0 && rootfirst;
-        if (r[3] == 0) rootfirst = false;
-        if (v->branching_edge) rc = v->branching_edge(data, first, r[3], r[4], r[0], r[1], r[2]);
+    LICHK(hipHostMalloc((void **) &host, sizeof (uint64_t) * 7 * (E < LI_EV_CHUNK ? E : LI_EV_CHUNK),
+                        hipHostMallocDefault));
+  }
+  for (uint64_t e0 = 0; e0 < E && rc == 0; e0 += LI_EV_CHUNK) {
+    const uint64_t n = E - e0 < LI_EV_CHUNK ? E - e0 : LI_EV_CHUNK;
+    LICHK(hipMemcpy(host, ev + 7 * e0, sizeof (uint64_t) * 7 * n, hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < n && rc == 0; k++) {
+      const uint64_t *r = host + 7 * k;
+      if (r[0] == 0) {
+        if (v->leaf_edge) rc = v->leaf_edge(data, (int) r[1], r[2], r[3], r[4]);
+      } else if (r[0] == 1) {
+        if (v->branching_edge) rc = v->branching_edge(data, (int) r[1], r[2], r[3], r[4], r[5], r[6]);
+      } else if (v->lcp_interval) {
+        rc = v->lcp_interval(data, r[2], r[3], r[4]);
       }
     }
-    if (rc == 0 && last != NULL) {
-      if (v->branching_edge) rc = v->branching_edge(data, true, last[3], last[1], last[0], last[1],
-                                                    last[2]);
-    } else if (rc == 0 && Y > X && v->leaf_edge) {
-      rc = v->leaf_edge(data, true, Y, idx, li_suffix(in, idx));
-    }
-    X = Y;
   }
-  free(itv);
-  free(leaf_lb);
+  if (ev) (void) hipFree(ev);
+  if (host) (void) hipHostFree(host);
+  gt_lcpitv_plan_delete(plan);
+  li_host_free(&h);
   if (rc != 0) {
     li_seterr(errbuf, errlen, "visitor callback returned non-zero");
     return -1;
   }
   return 0;
+fail:
+  if (ev) (void) hipFree(ev);
+  if (host) (void) hipHostFree(host);
+  gt_lcpitv_plan_delete(plan);
+  li_host_free(&h);
+  return -1;
 }

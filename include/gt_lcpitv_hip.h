@@ -27,7 +27,10 @@
  *
  * Device form: the tree comes from all-nearest-smaller-value searches over
  * the exact LCP array (a 64-ary min hierarchy), one thread per row; no
- * stack walk.
+ * stack walk.  The device-resident API (gt_lcpitv_plan_*) keeps the tree in
+ * HBM and writes the whole visitor event stream there, every event at its
+ * position in the reference's order; the host entry points above are built
+ * on it (events downloaded in chunks, callbacks on the calling thread).
  */
 #ifndef GT_LCPITV_HIP_H
 #define GT_LCPITV_HIP_H
@@ -61,6 +64,42 @@ int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor *v, void *d
  * descending).  malloc'd; free with gt_smax_free. */
 int gt_lcpitv_hip_enumerate_to_buffer(const GtSmaxInput *in, uint64_t **itv, uint64_t *count,
                                       char *errbuf, size_t errlen);
+
+/* -------------------------------------------------- device-resident API */
+
+/* Tables in HBM, global rows 0..N (as GtMaxpairsDevInput); suf_dev may be
+ * NULL (leaf numbers are then written as 0). */
+typedef struct {
+  const uint8_t *lcp_dev;
+  const GtSmaxLlv *llv_dev;
+  uint64_t numllv;
+  const void *suf_dev;
+  int suf_bytes;             /* 4 or 8 */
+  uint64_t nonspecials;      /* N */
+  int device;
+} GtLcpitvDevInput;
+
+typedef struct GtLcpitvPlan GtLcpitvPlan;
+
+/* Builds the lcp-interval tree in HBM (synchronous). */
+int gt_lcpitv_plan_create(GtLcpitvPlan **plan, const GtLcpitvDevInput *in, char *errbuf,
+                          size_t errlen);
+void gt_lcpitv_plan_delete(GtLcpitvPlan *plan);
+
+/* Number of lcp-intervals of depth > 0; *itv_dev = their device records,
+ * 5 uint64 each (lcp, lb, rb, fatherlcp, fatherlb), pop order. */
+uint64_t gt_lcpitv_plan_intervals(const GtLcpitvPlan *plan, const uint64_t **itv_dev);
+
+/* N + 2 * intervals: one leaf edge per row, an lcp-interval and a
+ * branching-edge event per interval. */
+uint64_t gt_lcpitv_plan_num_events(const GtLcpitvPlan *plan);
+
+/* Enqueues the event stream of gt_esa_bottomup (7 uint64 per event, in the
+ * reference's order) into events_dev (gt_lcpitv_plan_num_events entries):
+ *   (0, firstsucc, fd, flb, leafnumber, 0, 0)   visit_leaf_edge
+ *   (1, firstsucc, fd, flb, sd, slb, srb)       visit_branching_edge
+ *   (2, 0, lcp, lb, rb, 0, 0)                   visit_lcp_interval  */
+int gt_lcpitv_plan_events(GtLcpitvPlan *plan, uint64_t *events_dev, void *stream);
 
 #ifdef __cplusplus
 }

@@ -418,6 +418,100 @@ uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
   return n;
 }
 
+/* The other traversal gt dev sfxmap has: -enumlcpitvtree, the depth-first
+ * enumeration gt_depthfirstesa (src/match/esa-dfs.c:90-271) with the elcp
+ * callbacks of src/match/esa-lcpintervals.c:44-130.  Its L/B lines must
+ * equal those of -enumlcpitvtreeBU (gt_esa_bottomup + the lcpitvs visitor):
+ * the reference's own test diffs the two (testsuite/gt_suffixerator_include.rb:
+ * 597-603), which pins orc_bottomup_events, and through it the GPU event
+ * stream, to a second reference algorithm.  Records as orc_bottomup_events
+ * without the lcp-interval events and with srb = 0:
+ *   (0, firstsucc, fd, flb, leafnumber, 0, 0), (1, firstsucc, fd, flb, sd, slb, 0)
+ * Stack slots keep their node info when popped and are reused by the next
+ * push, as the reference's preallocated Dfsinfo slots are: a node pushed
+ * right after a pop starts with the popped child's leftmost leaf. */
+typedef struct {
+  uint64_t depth, left, offset;
+  int lastisleafedge;
+} DfsItv;
+
+uint64_t orc_dfs_events(const uint64_t *lcp, const uint64_t *suftab, uint64_t nonspecials,
+                        uint64_t **ev)
+{
+  DfsItv *stk = NULL;
+  uint64_t next = 0, alloc = 0, idx, n = 0, evalloc = 0, *e = NULL;
+  uint64_t lastoffset = 0, lastleft = 0;      /* Elcpstate.lastcompletenode */
+  int firstrootedge = 1;
+#define DFS_EV(T, F, A, B, C, D)                                             \
+  do {                                                                       \
+    if (n + 1 > evalloc) {                                                   \
+      evalloc = evalloc * 2 + 1024;                                          \
+      e = realloc(e, sizeof (uint64_t) * 7 * evalloc);                       \
+    }                                                                        \
+    uint64_t *r_ = e + 7 * n++;                                              \
+    r_[0] = (T); r_[1] = (F); r_[2] = (A); r_[3] = (B); r_[4] = (C);          \
+    r_[5] = (D); r_[6] = 0;                                                  \
+  } while (0)
+#define DFS_PUSH(D, B)                                                       \
+  do {                                                                       \
+    if (next >= alloc) {                                                     \
+      stk = realloc(stk, sizeof (DfsItv) * (alloc + 32));                    \
+      memset(stk + alloc, 0, sizeof (DfsItv) * 32);                          \
+      alloc += 32;                                                           \
+    }                                                                        \
+    stk[next].depth = (D); stk[next].lastisleafedge = (B);                   \
+    next++;                                                                  \
+  } while (0)
+#define TOPD (stk[next - 1])
+#define ABOVE (stk[next])
+#define BELOW (stk[next - 2])
+  DFS_PUSH(0, 1);
+  TOPD.left = 0;
+  for (idx = 0; idx < nonspecials; idx++) {
+    uint64_t cur = lcp[idx + 1], prev = suftab[idx];
+    while (cur < TOPD.depth) {
+      if (TOPD.lastisleafedge)
+        DFS_EV(0, 0, TOPD.depth, TOPD.left, prev, 0);
+      else
+        DFS_EV(1, 0, TOPD.depth, TOPD.left, ABOVE.offset, ABOVE.left);
+      /* assignrightmostleaf: right = idx (unused by the lines);
+         processcompletenode: offset = depth, lastcompletenode */
+      TOPD.offset = TOPD.depth;
+      lastoffset = TOPD.offset;
+      lastleft = TOPD.left;
+      next--;
+    }
+    if (cur == TOPD.depth) {
+      int firstedge = 0;
+      if (firstrootedge && TOPD.depth == 0) { firstedge = 1; firstrootedge = 0; }
+      if (TOPD.lastisleafedge) {
+        DFS_EV(0, firstedge, TOPD.depth, TOPD.left, prev, 0);
+      } else {
+        DFS_EV(1, firstedge, TOPD.depth, TOPD.left, ABOVE.offset, ABOVE.left);
+        TOPD.lastisleafedge = 1;
+      }
+    } else {
+      DFS_PUSH(cur, 1);
+      if (BELOW.lastisleafedge) {
+        TOPD.left = idx;
+        DFS_EV(0, 1, TOPD.depth, TOPD.left, prev, 0);
+        BELOW.lastisleafedge = 0;
+      } else {
+        /* son == NULL: the last complete node's offset and left */
+        DFS_EV(1, 1, TOPD.depth, TOPD.left, lastoffset, lastleft);
+      }
+    }
+  }
+  free(stk);
+#undef DFS_EV
+#undef DFS_PUSH
+#undef TOPD
+#undef ABOVE
+#undef BELOW
+  *ev = e;
+  return n;
+}
+
 /* --------------------------------------------------------- 3. brute force */
 
 static int is_spec(const uint8_t *t, uint64_t n, int64_t p)

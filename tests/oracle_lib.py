@@ -43,6 +43,8 @@ def lib():
         L.orc_maxpairs.restype = ctypes.c_uint64
         L.orc_bottomup_events.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_void_p]
         L.orc_bottomup_events.restype = ctypes.c_uint64
+        L.orc_dfs_events.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_void_p]
+        L.orc_dfs_events.restype = ctypes.c_uint64
         L.orc_format_pair.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _u64p,
                                       ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
         _lib = L
@@ -164,6 +166,19 @@ def bottomup_events(esa):
     pp = ctypes.c_void_p()
     cnt = lib().orc_bottomup_events(_p(esa.lcp, _u64p), _p(esa.suftab, _u64p), esa.nonspecials,
                                     ctypes.byref(pp))
+    if cnt == 0:
+        return np.zeros((0, 7), dtype=np.uint64)
+    buf = (ctypes.c_uint64 * (7 * cnt)).from_address(pp.value)
+    arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 7).copy()
+    lib().orc_free(pp)
+    return arr
+
+
+def dfs_events(esa):
+    """gt_depthfirstesa + elcp L/B lines (-enumlcpitvtree), orc_dfs_events."""
+    pp = ctypes.c_void_p()
+    cnt = lib().orc_dfs_events(_p(esa.lcp, _u64p), _p(esa.suftab, _u64p), esa.nonspecials,
+                               ctypes.byref(pp))
     if cnt == 0:
         return np.zeros((0, 7), dtype=np.uint64)
     buf = (ctypes.c_uint64 * (7 * cnt)).from_address(pp.value)

@@ -128,7 +128,7 @@ SFXMAP = os.path.join(G.BIN_DIR, "gt-sfxmap")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fasta", ["Atinsert.fna", "at1MB"])
+@pytest.mark.parametrize("fasta", ["Reads2.fna", "Atinsert.fna", "at1MB"])
 def test_sfxmap_enumlcpitvtree_bu(tmp_path, fasta):
     # `gt dev sfxmap -enumlcpitvtreeBU -esa IDX`: the lcpitvs visitor's
     # L/B lines (src/match/esa_lcpintervals_visitor.c:30-61), in the order of
@@ -144,6 +144,11 @@ def test_sfxmap_enumlcpitvtree_bu(tmp_path, fasta):
         elif r[0] == 1:
             want.append("B %d %d %d %d %d" % (r[1], r[2], r[3], r[4], r[5]))
     assert out == want
+    # the reference's check: the BU lines equal the depth-first traversal's
+    # (-enumlcpitvtree, gt_depthfirstesa), restated in the oracle
+    dfs = O.dfs_events(oracle_esa(fasta))
+    assert out == ["L %d %d %d %d" % tuple(r[1:5]) if r[0] == 0 else
+                   "B %d %d %d %d %d" % tuple(r[1:6]) for r in dfs]
 
 
 def test_sfxmap_errors():

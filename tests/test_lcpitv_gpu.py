@@ -3,10 +3,12 @@ lcp-interval tree computed on the GPU (ANSV searches) and replayed as
 GtESAVisitor events must equal, event for event and in order, the oracle's
 restatement of gt_esa_bottomup (src/match/esa-bottomup.c:116-273,
 orc_bottomup_events) -- leaf edges, branching edges, lcp-intervals, the
-firstsucc flags and every father/child field.  Parity rests on the oracle's
-restatement (itself pinned through the smax/maxpairs goldens); the
-reference's own lcp-interval test compares two gt traversals with each
-other and stores no output.
+firstsucc flags and every father/child field.  The reference's own
+lcp-interval test compares its two traversals with each other
+(`-enumlcpitvtreeBU` vs `-enumlcpitvtree` on Reads2.fna,
+testsuite/gt_suffixerator_include.rb:597-603) and stores no output; the
+oracle restates both (orc_bottomup_events, orc_dfs_events) and
+tests/test_oracle.py checks that they agree, on Reads2.fna among others.
 """
 import numpy as np
 import pytest
@@ -37,7 +39,8 @@ def _want_intervals(ev):
     return np.array(out, dtype=np.uint64).reshape(-1, 5)
 
 
-@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB", "Random.fna", "TTT-small.fna"])
+@pytest.mark.parametrize("name", ["Reads2.fna", "Atinsert.fna", "at1MB", "Random.fna",
+                                  "TTT-small.fna"])
 def test_fixture_event_stream(name):
     e = oracle_esa(name)
     want = O.bottomup_events(e)
@@ -84,3 +87,29 @@ def test_callback_stop_and_partial_visitor():
                    lcp_interval=lambda l, lb, rb: itv.append((l, lb, rb)))
     want = O.bottomup_events(e)
     assert np.array_equal(np.array(itv, dtype=np.uint64), want[want[:, 0] == 2][:, 2:5])
+
+
+def test_device_resident_tree_and_events():
+    # gt_lcpitv_plan_*: tree and event stream built and kept in HBM from a
+    # GPU-built index, equal to the oracle's traversal of the same tables
+    import torch
+    e = oracle_esa("at1MB")
+    d = G.DeviceEsa(e.text, keep_suftab=True)
+    p = d.lcpitv_plan()
+    want = O.bottomup_events(e)
+    n_ev = p.num_events()
+    assert n_ev == len(want)
+    ev = torch.empty(7 * n_ev, dtype=torch.int64, device="cuda")
+    p.events(ev.data_ptr())
+    torch.cuda.synchronize()
+    got = ev.cpu().numpy().view(np.uint64).reshape(-1, 7)
+    assert np.array_equal(got, want)
+    n, ptr = p.intervals()
+
+    class _View:       # the plan's device records as a torch view (no copy)
+        __cuda_array_interface__ = {"shape": (5 * n,), "typestr": "<i8", "data": (ptr, False),
+                                    "version": 2}
+    itv = torch.as_tensor(_View(), device="cuda").cpu().numpy().view(np.uint64).reshape(-1, 5)
+    assert np.array_equal(itv, _want_intervals(want))
+    p.close()
+    d.release()

@@ -218,3 +218,36 @@ def test_bottomup_event_stream_shape(name):
     sm = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8)
     allitv = set(map(tuple, itv[:, 2:5].tolist()))
     assert set(map(tuple, sm.tolist())) <= allitv
+
+
+def _lb_lines(ev):
+    """L/B records of an event stream as the lcpitvs visitor prints them
+    (srb and the lcp-interval events are not printed)."""
+    ev = ev[ev[:, 0] != 2].copy()
+    ev[:, 6] = 0
+    return ev
+
+
+@pytest.mark.parametrize("name", ["Reads2.fna", "Atinsert.fna", "Random.fna", "TTT-small.fna",
+                                  "at1MB"])
+def test_dfs_lines_equal_bottomup_lines(name):
+    # the reference's own lcp-interval test (testsuite/gt_suffixerator_include.rb:
+    # 597-603): `gt dev sfxmap -enumlcpitvtreeBU` == `-enumlcpitvtree` on
+    # Reads2.fna; here the restatements of both traversals (esa-bottomup.c,
+    # esa-dfs.c + esa-lcpintervals.c) on it and the other fixtures
+    e = oracle_esa(name)
+    dfs = O.dfs_events(e)
+    assert len(dfs) > 0
+    assert np.array_equal(dfs, _lb_lines(O.bottomup_events(e)))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_dfs_lines_equal_bottomup_lines_random(seed):
+    rng = np.random.default_rng(900 + seed)
+    for _ in range(30):
+        n = int(rng.integers(1, 3000))
+        t = rng.integers(0, int(rng.integers(1, 5)), n, dtype=np.uint8)
+        if seed % 2:
+            t[rng.random(n) < 0.02] = rng.choice(np.array([254, 255], np.uint8))
+        e = O.Esa(t)
+        assert np.array_equal(O.dfs_events(e), _lb_lines(O.bottomup_events(e)))
