@@ -945,9 +945,11 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   if (segpre & 2u) segl[n0 + __popcll(m1 & ltm)] = (uint8_t) (64 + lane);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones
-  uint32_t Dm0 = 0, Lm0 = 0, Dm1 = 0, Lm1 = 0, Lpre0 = 0, Lpre1 = 0, ro0 = 0, ro1 = 0;
-  uint32_t W30 = 0, W31 = 0, F0 = 0, F1 = 0, R0 = 0, R1 = 0;
+  // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones; set
+  // for every step k < nsteps and read only there (no zero-fill: each
+  // initialiser was a per-tile VALU move, and VALU issue bounds K1)
+  uint32_t Dm0, Lm0, Dm1, Lm1, Lpre0, Lpre1, ro0, ro1;
+  uint32_t W30, W31, F0, F1, R0, R1;
   uint32_t nL = 0;
   const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
   // 255-byte ranks: the left halo's count, then a prefix over the compacted
@@ -960,7 +962,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     if ((uint32_t) k >= nsteps) break;
     const uint32_t i = k * 64 + lane;
     uint32_t D = 0, D3 = 0, Lq = 0, ro = 0;
-    SegRel rel = {0, 0, 0, 0, 0, 0};
+    SegRel rel;                     // fields other than FF read only for i < nseg
+    rel.FF = 0;
     if (i < nseg) {
       const uint32_t sid = segl[i];
       ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
@@ -974,14 +977,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       fbase += ftot;
     }
     if (i < nseg) {
+      // every row is owned: tiles holding rows before `begin` are static K1b
       classify_fin(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq);
-      const uint64_t sg = g0 + ro;
-      if (sg < a.begin) {
-        const uint32_t m = sg + 16 <= a.begin ? 0u : (0xffffu << (a.begin - sg)) & 0xffffu;
-        D &= m;
-        D3 &= m;
-        Lq &= m;
-      }
     }
     const uint32_t F = rel.FF;
     uint32_t tot;
@@ -1230,12 +1227,17 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     }
     // .llv windows of this tile and the next {lo, packed count word}: one
     // 16-byte LDS read
+    // (wave-uniform: to scalars first, then scalar selects)
     const uint4 info = *reinterpret_cast<const uint4 *>(&sInfo[wave][0][0]);
-    const uint32_t wlo = __builtin_amdgcn_readfirstlane(cur ? info.z : info.x);
-    const uint32_t wnf = __builtin_amdgcn_readfirstlane(cur ? info.w : info.y);
+    const uint32_t ix = __builtin_amdgcn_readfirstlane(info.x);
+    const uint32_t iy = __builtin_amdgcn_readfirstlane(info.y);
+    const uint32_t iz = __builtin_amdgcn_readfirstlane(info.z);
+    const uint32_t iw = __builtin_amdgcn_readfirstlane(info.w);
+    const uint32_t wlo = cur ? iz : ix;
+    const uint32_t wnf = cur ? iw : iy;
     const uint32_t wn = SMAX_WIN_N(wnf);
-    const uint32_t nlo = __builtin_amdgcn_readfirstlane(cur ? info.x : info.z);
-    const uint32_t nn = SMAX_WIN_N(__builtin_amdgcn_readfirstlane(cur ? info.y : info.w));
+    const uint32_t nlo = cur ? ix : iz;
+    const uint32_t nn = SMAX_WIN_N(cur ? iy : iw);
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
@@ -1754,8 +1756,8 @@ smax_llv16_kernel(const GtSmaxLlv *llv, uint64_t numllv, uint16_t *out) {
 }
 
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
-                                      uint64_t base, uint64_t tile_first, uint64_t end,
-                                      uint32_t num_tiles, uint2 *win_out,
+                                      uint64_t base, uint64_t tile_first, uint64_t begin,
+                                      uint64_t end, uint32_t num_tiles, uint2 *win_out,
                                       uint32_t *err) {
   const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (t < numllv) {
@@ -1783,7 +1785,9 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
     if (llv[k].position < g0) halo++;
   }
   const uint32_t wn = (uint32_t) (lo2 - lo);   // <= SMAX_LDSB rows
-  const bool stat = g0 < SMAX_LH || g0 + SMAX_TILE + SMAX_RH > end || wide ||
+  // g0 < begin: the shard's first tile when begin is not tile-aligned (K1
+  // assumes every row of its tiles is owned)
+  const bool stat = g0 < SMAX_LH || g0 < begin || g0 + SMAX_TILE + SMAX_RH > end || wide ||
                     wn + ((uint32_t) lo & 7u) > SMAX_LLV_CAP;
   win_out[t] = make_uint2((uint32_t) lo, wn | (halo << 12) | (stat ? SMAX_WIN_STATIC : 0u));
 }
@@ -2073,8 +2077,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       hipLaunchKernelGGL(smax_llv16_kernel, dim3((unsigned) ((shard->numllv + 255) / 256)),
                          dim3(256), 0, 0, shard->llv_dev, shard->numllv, p->llv16);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
-                       shard->llv_dev, shard->numllv, shard->base, p->tile_first, shard->end,
-                       p->num_tiles, p->llv_win, derr);
+                       shard->llv_dev, shard->numllv, shard->base, p->tile_first, shard->begin,
+                       shard->end, p->num_tiles, p->llv_win, derr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   }
