@@ -115,6 +115,7 @@ struct SmaxScanArgs {
   uint32_t *defer_count;     // reset by K0
   uint32_t k1b_head;         // K1b: the last workgroup computes the boundary head
   uint32_t wide_slot0;       // K1b: wide slot of list entry 0 (static list 0, runtime n_static)
+  uint32_t defer_base;       // K0 resets *defer_count to this (combined list: n_static)
   uint32_t wide_cap;         // wide slots (SMAX_TILE / 2 records each) at the pool's start
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
@@ -415,7 +416,7 @@ __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a, int with_
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   a.bnd->pend_valid = 0;
   *a.pool_cursor = (unsigned long long) a.wide_cap * (SMAX_TILE / 2);   // past the wide slots
-  if (!(a.dbg & 16384u)) *a.defer_count = 0;   // diagnostic: K1b alone on K1's last list
+  if (!(a.dbg & 16384u)) *a.defer_count = a.defer_base;   // diagnostic: K1b alone on K1's last list
   if (with_head) compute_head(a);
 }
 
@@ -1885,6 +1886,7 @@ struct GtSmaxPlan {
   uint32_t n_static, static_grid;
   hipStream_t side;          // K1b over the static list runs here, concurrent with K1
   int k1b_mode;              // placement of the static K1b (GT_SMAX_K1B_MODE)
+  uint32_t comb_grid;        // mode 4: grid of the combined K1b launch (+1: head)
   hipEvent_t fork, join;
   uint32_t *err;
   uint32_t dbg;
@@ -2059,7 +2061,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(dalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
-  HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (uint64_t) p->num_tiles));
+  // K1's runtime list; in the combined placement (mode 4) the static list is
+  // copied to its front and K1 appends behind it
+  HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (2 * (uint64_t) p->num_tiles + 1)));
   HIPCHK(dalloc(&p->defer_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
   HIPCHK(dalloc(&derr, sizeof (uint32_t)));
@@ -2112,7 +2116,16 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     // stream, 2 after K1, 3 side stream of the highest priority, launched
     // ahead of K1
     const char *m = getenv("GT_SMAX_K1B_MODE");
-    p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 0;
+    p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 4;
+    if (p->k1b_mode == 4) {
+      // 4: one K1b launch after K1 over the static list followed by K1's
+      // deferrals (no second stream, no fork/join events: those cost
+      // ~25 us per step, measured on a 100 Mbp shard)
+      if (p->n_static)
+        HIPCHK(hipMemcpy(p->defer_list, p->static_list, sizeof (uint32_t) * p->n_static,
+                         hipMemcpyDeviceToDevice));
+      p->comb_grid = std::max(p->defer_grid, p->static_grid - 1) + 1;   // static_grid has its +1
+    }
     int lo = 0, hi = 0;
     if (p->k1b_mode == 3 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
       HIPCHK(hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, hi));
@@ -2171,6 +2184,11 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.pool_cap = (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity;
   a.wide_cap = p->wide_cap;
   a.wide_slot0 = p->n_static;   // the runtime list (the static list sets 0)
+  a.defer_base = 0;
+  if (p->k1b_mode == 4) {          // combined list: static entries at its front
+    a.wide_slot0 = 0;
+    a.defer_base = p->n_static;
+  }
   a.pool_cursor = p->pool_cursor;
   a.tile_off = p->tile_off;
   a.tile_count = p->tile_count;
@@ -2206,6 +2224,7 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     b.wide_slot0 = 0;
     const int mode = p->k1b_mode;
     const bool side = mode == 0 || mode == 3;
+    if (mode == 4) b.defer_base = p->n_static;
     if (mode == 1) {
       hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, s, b);
       HIPCHK(hipGetLastError());
@@ -2249,7 +2268,15 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       HIPCHK(hipEventRecord(p->join, p->side));
       HIPCHK(hipStreamWaitEvent(s, p->join, 0));
     }
-    hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
+    if (mode == 4) {
+      // static list + K1's deferrals in one launch; its last workgroup
+      // computes the boundary head
+      SmaxScanArgs c = a;
+      c.k1b_head = 1;
+      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->comb_grid), dim3(SMAX_THREADS), 0, s, c);
+    } else {
+      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
+    }
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
@@ -2379,7 +2406,7 @@ extern "C" uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *p) {
   if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;
   if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
     return 0xffffffffu;
-  return n;
+  return p->k1b_mode == 4 ? n - p->n_static : n;   // K1's deferrals only
 }
 
 extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_t *deferred,
@@ -2392,8 +2419,10 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
     for (uint64_t i = 0; i < p->num_tiles; i++) counts[i] &= ~SMAX_SLOT_WIDE;   // slot-format flag
   uint32_t n = 0;
   if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  const uint32_t base = p->k1b_mode == 4 ? p->n_static : 0;   // combined list: K1's part
+  n -= base;
   if (ndeferred) *ndeferred = n;
-  if (deferred && n && hipMemcpy(deferred, p->defer_list, sizeof (uint32_t) * n,
+  if (deferred && n && hipMemcpy(deferred, p->defer_list + base, sizeof (uint32_t) * n,
                                  hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return 0;

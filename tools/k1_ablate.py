@@ -13,6 +13,7 @@ import torch
 kind = sys.argv[1] if len(sys.argv) > 1 else "human"
 bases = int(float(sys.argv[2])) if len(sys.argv) > 2 else 300_000_000
 variants = [int(x, 0) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0, 1, 2, 4, 8, 15]
+minlen = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 text = G.synth_genome(kind, bases, 1 if kind != "uniform" else 42)
 esa = G.DeviceEsa(text)
 print("n=%d N=%d llv=%d" % (esa.totallength, esa.nonspecials, esa.numllv), flush=True)
@@ -20,7 +21,7 @@ res = {v: [] for v in variants}
 for rnd in range(3):
     for v in variants:
         os.environ["GT_SMAX_DEBUG"] = str(v)
-        p = esa.plan(20)
+        p = esa.plan(minlen)
         p.run(); torch.cuda.synchronize()
         if rnd == 0:
             print("dbg=%d: %d of %d tiles deferred to K1b" % (v, p.deferred_tiles(), p.num_tiles),

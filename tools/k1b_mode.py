@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: C3 step time (K0, K1, static K1b, runtime K1b, K3) for each
-placement of the static K1b list (GT_SMAX_K1B_MODE 0..3, see
+placement of the static K1b list (GT_SMAX_K1B_MODE 0..4, see
 gt_smax_plan_create), K1 time by HIP events, one ESA build."""
 import os
 import sys
@@ -19,7 +19,7 @@ del text
 s = torch.cuda.current_stream().cuda_stream
 ref = None
 for rep in range(2):
-    for mode in (0, 1, 2, 3):
+    for mode in (0, 2, 4):
         os.environ["GT_SMAX_K1B_MODE"] = str(mode)
         p = esa.plan(minlen)
         for _ in range(3):
