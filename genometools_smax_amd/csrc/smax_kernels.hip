@@ -11,17 +11,22 @@
 // BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
-// One pass = launches on one stream (plus a forked side stream), no host
-// synchronisation:
+// One pass = five launches on one stream, no host synchronisation
+// (DESIGN.md §4):
 //   K0  smax_head_kernel     per-run resets (pending-plateau slot, deferral
 //                            count, K1b pool cursor)
-//   K1  smax_scan_kernel     the streaming kernel; K1b smax_defer_kernel over
-//                            the plan-time static list runs beside it on the
-//                            side stream (shard edges, dense-.llv windows) and
-//                            computes the boundary head
-//   K1b smax_defer_kernel    over K1's runtime list (exact-queue overflow,
-//                            tiles with more records than a slot holds)
-//   K2  smax_block_sum_kernel  records per 256 tiles (K3's offsets)
+//   K1  smax_scan_kernel     the streaming kernel
+//   K1b smax_defer_kernel    the plan-time static list (shard edges,
+//                            dense-.llv windows) followed by K1's runtime
+//                            deferrals (exact-queue overflow, tiles with more
+//                            records than a slot holds); its last workgroup
+//                            computes the boundary head (GT_SMAX_K1B_MODE 0-3
+//                            keep the older placements of the static list:
+//                            side stream beside K1, before or after K1)
+//   K2  smax_block_sum_kernel  records per 256 tiles (K3's offsets; a
+//                            decoupled look-back inside K3 instead measured
+//                            1.3 -> 1.9 ms at C3: the prefix chain over 5663
+//                            workgroups serialises)
 //   K3  smax_compact_kernel  ordered copy of the tiles' records -> ascending
 //                            lb
 //
