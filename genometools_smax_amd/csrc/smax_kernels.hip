@@ -635,6 +635,16 @@ __device__ __forceinline__ bool diverse8(uint64_t X, uint32_t w) {
   return true;
 }
 
+// left diversity of the first w (2..8) rows of a packed-BWT window given as
+// 8-bit fields (bit k: row k): code low plane, code high plane, special mask;
+// non-special rows are pairwise distinct iff each of the 4 codes occurs at
+// most once (no 8-symbol byte expansion)
+__device__ __forceinline__ bool diverse_planes(uint32_t lo, uint32_t hi, uint32_t sp, uint32_t w) {
+  const uint32_t ns = ~sp & ((1u << w) - 1u);
+  const uint32_t c0 = ns & ~lo & ~hi, c1 = ns & lo & ~hi, c2 = ns & ~lo & hi, c3 = ns & lo & hi;
+  return ((c0 & (c0 - 1u)) | (c1 & (c1 - 1u)) | (c2 & (c2 - 1u)) | (c3 & (c3 - 1u))) == 0u;
+}
+
 // Exact evaluation of one plateau start (row offset `ro` inside the tile, its
 // .llv rank `rk` when its LCP byte is 255): *cur = LCP value, *j = last row of
 // the plateau; returns whether [c-1 .. j] is a supermaximal-repeat interval.
@@ -654,24 +664,22 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
   if (interior) {
     const uint32_t co = SMAX_LH + ro;
     const uint64_t LX = lds_bytes8(sL, co);
-    // BWT symbols of rows c-1 .. c+6 as bytes (specials as 254)
-    uint64_t BX;
+    // BWT symbols of rows c-1 .. c+6: bit planes (packed window) or bytes
+    uint64_t BX = 0;
+    uint32_t plo = 0, phi = 0, psp = 0;
     if (t.B == nullptr) {   // packed window (K1 sets B = nullptr: folds at compile time)
       const uint32_t o = co - 1, gi = o >> 4, q = o & 15u;
       const uint64_t w0 = t.P[gi], w1 = t.P[gi + 1];
       const uint32_t a0 = (uint32_t) w0, a1 = (uint32_t) w1;
-      const uint32_t lo = (((a0 & 0xffffu) | (a1 << 16)) >> q) & 0xffu;
-      const uint32_t hi = (((a0 >> 16) | (a1 & 0xffff0000u)) >> q) & 0xffu;
-      const uint32_t sp = (uint32_t) (((w0 >> 32) & 0xffffu) | (((w1 >> 32) & 0xffffu) << 16)) >> q;
-      BX = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint64_t sym = ((sp >> k) & 1u) ? 254u : ((lo >> k) & 1u) | (((hi >> k) & 1u) << 1);
-        BX |= sym << (8 * k);
-      }
+      plo = (((a0 & 0xffffu) | (a1 << 16)) >> q) & 0xffu;
+      phi = (((a0 >> 16) | (a1 & 0xffff0000u)) >> q) & 0xffu;
+      psp = ((uint32_t) (((w0 >> 32) & 0xffffu) | (((w1 >> 32) & 0xffffu) << 16)) >> q) & 0xffu;
     } else {
       BX = lds_bytes8(t.B, co - 1);
     }
+    auto div = [&](uint32_t w) {
+      return t.B == nullptr ? diverse_planes(plo, phi, psp, w) : diverse8(BX, w);
+    };
     const uint32_t cb = (uint32_t) LX & 0xffu;
     if (cb == 255) {
       // .llv start: exact values by rank; a run of equal values >= 255
@@ -695,7 +703,7 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
             slow = true;
           } else {
             j = cc + k;
-            if (rel < 0) acc = diverse8(BX, k + 2);
+            if (rel < 0) acc = div(k + 2);
           }
         }
       }
@@ -710,7 +718,7 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
         const uint32_t k = (uint32_t) __builtin_ctzll(ne) >> 3;
         const uint32_t nb = (uint32_t) (nx >> (8 * k)) & 0xffu;
         j = cc + k;
-        if (nb < cb) acc = diverse8(BX, k + 2);
+        if (nb < cb) acc = div(k + 2);
       }
     }
   }

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Diagnostic A/B with the two builds in ONE process on the same device
+tables: the in-tree library (A) and a second copy (B, path in argv[4]),
+plans created by each, runs alternated in rounds so that clock and
+thermal drift hit both alike.  Prints per-round and median step times.
+Args: kind bases minlen libB [rounds]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import genometools_smax_amd as G  # noqa: E402
+
+kind, bases, minlen, libb = sys.argv[1], int(float(sys.argv[2])), int(sys.argv[3]), sys.argv[4]
+rounds = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+LA = G.lib()
+pa_path = G.LIB_PATH
+G._lib, G.LIB_PATH = None, libb
+LB = G.lib()
+G._lib, G.LIB_PATH = LA, pa_path
+
+text = G.synth_genome(kind, bases, {"uniform": 42, "human": 1, "plant": 2}[kind])
+esa = G.DeviceEsa(text) if len(text) + 1 < 2 ** 32 else G.DeviceEsa64(text)
+del text
+plan_a = esa.plan(minlen)
+G._lib = LB
+plan_b = esa.plan(minlen)
+G._lib = LA
+s = torch.cuda.current_stream()
+sp = s.cuda_stream
+
+
+def timed(L, p, n=30):
+    for _ in range(3):
+        L.gt_smax_plan_run(p.plan, sp)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(n):
+        L.gt_smax_plan_run(p.plan, sp)
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+ta, tb = [], []
+for r in range(rounds):
+    a = timed(LA, plan_a)
+    b = timed(LB, plan_b)
+    ta.append(a)
+    tb.append(b)
+    print("round %d: A %.4f ms  B %.4f ms  B/A %.3f" % (r, a, b, b / a), flush=True)
+ta.sort()
+tb.sort()
+print("median step: A %.4f ms, B %.4f ms, B/A %.4f" % (ta[len(ta) // 2], tb[len(tb) // 2],
+                                                        tb[len(tb) // 2] / ta[len(ta) // 2]))
+G._lib = LB
+plan_b.close()
+G._lib = LA
+plan_a.close()
