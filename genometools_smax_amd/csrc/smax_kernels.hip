@@ -85,6 +85,7 @@
 #define SMAX_WIN_HALO(y) (((y) >> 12) & 0x1fu)
 #define SMAX_WIN_STATIC 0x80000000u
 #define SMAX_SSLOT 64                                 // packed records per K1 tile slot
+#define SMAX_FFPV_DENSITY 0.006                       // .llv entries per row: dense K1 above
                                                       // (0.25 B per row; a tile with more
                                                       // goes to K1b, whose 16-byte records
                                                       // are allocated from the plan's pool)
@@ -860,6 +861,71 @@ __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t
   r.pb = pb;
 }
 
+// UP/EQ of the rows q in FFP (255 bytes after 255 bytes) from the staged u16
+// .llv values: the values of ranks crank-2 .. crank+19 come in with 11 LDS
+// dword reads (realigned to rank crank-2 with one funnel shift each), all 18
+// "value(k) vs value(k-1)" relations are decided with packed u16 max/xor,
+// and rank index k maps back to row q: k = 255 bytes of the segment before
+// q -- a plain shift when the segment's 255 bytes are one run (dense .llv
+// regions), otherwise one register-only step per row.  Replaces a loop of
+// two dependent LDS reads per row (a quarter of K1 on the 12 Gbp plant
+// genome, whose long repeat families are dense in .llv values).
+typedef unsigned short smax_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t u16_nonzero(uint32_t x) {   // bit 15 / 31: lane != 0
+  return (((x & 0x7fff7fffu) + 0x7fff7fffu) | x) & 0x80008000u;
+}
+
+__device__ __forceinline__ void ffp_resolve(const Win &t, uint32_t F18, uint32_t FFP, uint32_t crank,
+                                            uint32_t *UP, uint32_t *EQ) {
+  // LDS byte address of rank crank - 2 (kept in the LDS address space: ds_read)
+  const uint32_t a0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) uint16_t *)
+                          t.val16 + 2u * crank - 4u;
+  typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+  lds_u32 *wp = (lds_u32 *) (uintptr_t) (a0 & ~3u);
+  const uint32_t sh = (a0 & 2u) * 8u;
+  uint32_t w[11];
+#pragma unroll
+  for (int i = 0; i < 11; i++) w[i] = wp[i];
+  uint32_t R[10];                                               // R[i]: ranks crank-2+2i, +1
+#pragma unroll
+  for (int i = 0; i < 10; i++) R[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
+  uint32_t gtm = 0, eqm = 0;                                    // bit k: rank crank+k vs crank+k-1
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t C = R[i + 1];                                // ranks crank+2i, crank+2i+1
+    const uint32_t P = __builtin_amdgcn_alignbit(R[i + 1], R[i], 16);   // crank+2i-1, crank+2i
+    smax_u16x2 cv, pv;
+    __builtin_memcpy(&cv, &C, 4);
+    __builtin_memcpy(&pv, &P, 4);
+    const smax_u16x2 mv = __builtin_elementwise_max(cv, pv);
+    uint32_t M;
+    __builtin_memcpy(&M, &mv, 4);
+    const uint32_t nzx = u16_nonzero(C ^ P), nzy = u16_nonzero(M ^ C);
+    const uint32_t gt = nzx & ~nzy, eq = ~nzx & 0x80008000u;   // C > P: max is C, C != P
+    gtm |= ((gt >> 15) & 1u) << (2 * i) | (gt >> 31) << (2 * i + 1);
+    eqm |= ((eq >> 15) & 1u) << (2 * i) | (eq >> 31) << (2 * i + 1);
+  }
+  uint32_t up = 0, eqr = 0;
+  const uint32_t low = F18 & (0u - F18);
+  if ((F18 & (F18 + low)) == 0) {                               // one run from row q0
+    const uint32_t q0 = (uint32_t) __builtin_ctz(F18);
+    up = gtm << q0;
+    eqr = eqm << q0;
+  } else {
+    uint32_t m = FFP;
+    while (m) {
+      const uint32_t q = (uint32_t) __builtin_ctz(m);
+      m &= m - 1;
+      const uint32_t k = (uint32_t) __popc(F18 & ((1u << q) - 1));
+      up |= ((gtm >> k) & 1u) << q;
+      eqr |= ((eqm >> k) & 1u) << q;
+    }
+  }
+  *UP = (*UP & ~FFP) | (up & FFP);
+  *EQ = (*EQ & ~FFP) | (eqr & FFP);
+}
+
 // Part 2, given the rank of the segment's first row among the window's 255
 // bytes (crank):
 //   *Dm  records [c-1 .. c] and [c-1 .. c+1] (D3 marks the latter): start,
@@ -872,6 +938,7 @@ __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t
 // predecessor (UP, EQ) for rows 0..17; successor relations are the same bits
 // shifted.  Byte compares are exact except between two 255 bytes: those
 // pairs (rare) are re-decided from the exact .llv values by rank.
+template <bool FFPV>
 __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r, uint32_t crank,
                                              bool all_exact, uint32_t *Dm, uint32_t *D3m,
                                              uint32_t *Lm) {
@@ -880,6 +947,8 @@ __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r
   bool unresolved = false;
   if (r.F18 != 0 && t.rank == nullptr) {
     unresolved = true;                      // no ranks (inconsistent index): exact queue
+  } else if (FFPV && FFP != 0 && t.staged_all) {
+    ffp_resolve(t, r.F18, FFP, crank, &UP, &EQ);
   } else {
     while (FFP) {
       const int q = __builtin_ctz(FFP);
@@ -940,7 +1009,7 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
 // classified: they are compacted (row order) so that each classification
 // step keeps all 64 lanes busy (about a third of the segments are active on
 // repeat-rich DNA, so one step usually covers the whole tile).
-template <int DL>
+template <int DL, bool FFPV>
 __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &a, uint64_t g0,
                                               const uint8_t *sL, uint32_t *ent,
                                               uint64_t *stg, uint32_t segpre) {
@@ -992,7 +1061,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     }
     if (i < nseg) {
       // every row is owned: tiles holding rows before `begin` are static K1b
-      classify_fin(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq);
+      classify_fin<FFPV>(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq);
     }
     const uint32_t F = rel.FF;
     uint32_t tot;
@@ -1167,7 +1236,7 @@ __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t 
 // here; shard-edge tiles and tiles with more exact starts than the direct
 // path queues are deferred to K1b (their generic path is kept out of K1,
 // whose register budget it would otherwise set).
-template <typename WinT, bool DIAG>
+template <typename WinT, bool DIAG, bool FFPV = false>
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // the production kernel sees dbg == 0 as a constant: every diagnostic
   // branch (GT_SMAX_DEBUG) folds away, a scalar test and branch each
@@ -1289,7 +1358,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const bool stat = static_deferred(a, wnf);
     bool defer = !stat && wave_pre && (a.dbg & 128u);
     if (!stat && !defer && wave_pre) {
-      wcount = wave_detect_direct<SMAX_DLIST>(t, a, g0, W->L, sQueue[wave], sStage[wave], segpre_bits);
+      wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave], sStage[wave],
+                                                    segpre_bits);
       // exact-queue overflow (UINT32_MAX) or more records than the tile's
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
@@ -1637,6 +1707,13 @@ smax_defer_kernel(SmaxScanArgs a) {
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false>(a);
 }
+// dense .llv shards (plan picks it above SMAX_FFPV_DENSITY entries per row):
+// the 255-after-255 relations of a segment are resolved vectorised
+// (ffp_resolve); measured C5 (12 Gbp plant, 0.94 % of rows) step 6.21 ->
+// 5.72 ms, C3 (human, 0.39 %) 1.253 -> 1.272 ms, hence the switch
+__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_dense(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, true>(a);
+}
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, true>(a);
 }
@@ -1900,6 +1977,7 @@ struct GtSmaxPlan {
   hipStream_t side;          // K1b over the static list runs here, concurrent with K1
   int k1b_mode;              // placement of the static K1b (GT_SMAX_K1B_MODE)
   uint32_t comb_grid;        // mode 4: grid of the combined K1b launch (+1: head)
+  bool dense;                // .llv entries per row above SMAX_FFPV_DENSITY: smax_scan_kernel_dense
   hipEvent_t fork, join;
   uint32_t *err;
   uint32_t dbg;
@@ -2128,6 +2206,12 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     // DESIGN.md §5): 0 side stream beside K1, 1 before K1 on the caller's
     // stream, 2 after K1, 3 side stream of the highest priority, launched
     // ahead of K1
+    {
+      const char *dv = getenv("GT_SMAX_DENSE");   // diagnostic override: 0 / 1
+      const uint64_t rows = shard->end > shard->begin ? shard->end - shard->begin : 1;
+      p->dense = dv ? strtol(dv, NULL, 0) != 0
+                    : (double) shard->numllv > SMAX_FFPV_DENSITY * (double) rows;
+    }
     const char *m = getenv("GT_SMAX_K1B_MODE");
     p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 4;
     if (p->k1b_mode == 4) {
@@ -2260,6 +2344,8 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
         ;   // diagnostic: re-run K1b on the first run's deferred tiles
       else if (p->pk && p->dbg)
         hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+      else if (p->pk && p->dense)
+        hipLaunchKernelGGL(smax_scan_kernel_dense, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
       else if (p->pk)
         hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
       else

@@ -212,3 +212,29 @@ def test_host_path_multi_chunk_output():
     assert len(iv) > (4 << 20)
     ref = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20, threads=8)
     assert np.array_equal(iv, ref)
+
+
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_dense_llv_kernel_variant(monkeypatch, dense):
+    # K1's dense-.llv variant (vectorised 255-after-255 relations, chosen by
+    # .llv density at plan time) and the default one, forced either way on
+    # texts with long repeats (runs of 255 bytes, equal and unequal .llv
+    # neighbours) and on at1MB at minlens around 255
+    monkeypatch.setenv("GT_SMAX_DENSE", dense)
+    rng = np.random.default_rng(77)
+    for k in range(3):
+        a = rng.integers(0, 4, int(rng.integers(600, 3000)), dtype=np.uint8)
+        b = a.copy()
+        b[len(b) // 2] = (b[len(b) // 2] + 1) % 4
+        parts = [rng.integers(0, 4, 20000, dtype=np.uint8)]
+        for _ in range(4 + k):
+            parts += [a, rng.integers(0, 4, 50, dtype=np.uint8), b,
+                      np.array([255], dtype=np.uint8)]
+        t = np.concatenate(parts)
+        e = O.Esa(t)
+        assert len(e.llv) > 100
+        for minlen in (20, 255, 400):
+            assert np.array_equal(_gpu(e, minlen), _cpu(e, minlen)), (k, minlen)
+    e = oracle_esa("at1MB")
+    for minlen in (20, 255, 300):
+        assert np.array_equal(_gpu(e, minlen), _cpu(e, minlen)), minlen

@@ -44,8 +44,12 @@ def timed(L, p, n=30):
 
 ta, tb = [], []
 for r in range(rounds):
-    a = timed(LA, plan_a)
-    b = timed(LB, plan_b)
+    if r % 2 == 0:                    # alternate which build goes first
+        a = timed(LA, plan_a)
+        b = timed(LB, plan_b)
+    else:
+        b = timed(LB, plan_b)
+        a = timed(LA, plan_a)
     ta.append(a)
     tb.append(b)
     print("round %d: A %.4f ms  B %.4f ms  B/A %.3f" % (r, a, b, b / a), flush=True)
