@@ -1707,6 +1707,142 @@ smax_defer_kernel(SmaxScanArgs a) {
 }
 
 
+// K1b, one workgroup per tile (the combined placement's kernel): a K1b
+// launch covers few tiles (the static list and K1's rare deferrals; about
+// 130 per shard of an 8-way C3 split), so its time is the slowest tile's,
+// and one wave per tile left three of every four waves idle.  Here wave 0
+// loads the exact window, the four waves share the ballot steps, and each
+// takes one 512-row round of starts: evaluated once into LDS (value, width,
+// accepted), the rounds' record counts are scanned across the waves and
+// the records written in row order.  Same results as smax_defer_kernel.
+struct SmaxDeferWG {
+  SmaxWindowX win;
+  uint16_t list[4][SMAX_XQ];        // per wave: its round's starts (row order)
+  uint32_t cur[4][SMAX_XQ];         // evaluated LCP value
+  uint32_t wid[4][SMAX_XQ];         // width; 0: not accepted
+  uint32_t cnt[4];
+  uint64_t off;                     // the tile's first record in the pool (~0: none)
+};
+
+__global__ void __launch_bounds__(SMAX_THREADS)
+smax_defer_wg_kernel(SmaxScanArgs a) {
+  __shared__ __attribute__((aligned(16))) SmaxDeferWG sD;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SmaxWindowX *W = &sD.win;
+  Win t;
+  win_init(t, a);
+  if (a.k1b_head && blockIdx.x == gridDim.x - 1) {
+    if (wave == 0) {
+      const uint64_t l0 = a.tile_first * (uint64_t) SMAX_TILE;
+      load_exact_window(a, l0, W);
+      head_from_window(a, W, a.base + l0);
+    }
+    return;
+  }
+  const uint32_t n = *a.defer_count;
+  const uint64_t ltm = lanemask_lt();
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x - a.k1b_head) {
+    const uint64_t tile = a.defer_list[i];
+    const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
+    const uint64_t g0 = a.base + l0;
+    if (wave == 0) load_exact_window(a, l0, W);
+    __syncthreads();
+    t.g0 = g0;
+    t.L = W->L;
+    t.B = W->B;
+    t.P = nullptr;
+    t.rank = nullptr;
+    t.val = nullptr;
+    t.val16 = nullptr;
+    t.nval = -1;
+    // ballots: the waves take every 4th 64-row step
+    for (uint32_t st = (uint32_t) wave; st < SMAX_XSTEPS; st += 4) {
+      const uint32_t b = st * 64 + lane, o = b + SMAX_LH;
+      bool ne = true, sm = false;
+      if (o + 1 < SMAX_LDSB) {
+        const uint32_t c = W->X[o], nx = W->X[o + 1], pv = W->X[o - 1];
+        const uint64_t g = g0 + b;
+        ne = nx != c;
+        sm = b < SMAX_TILE && c > pv && c >= a.minlen && g >= a.begin && g < a.end;
+      }
+      const uint64_t nem = __ballot(ne), stm = __ballot(sm);
+      if (lane == 0) {
+        W->ne[st] = nem;
+        if (st < SMAX_TILE / 64) W->st[st] = stm;
+      }
+    }
+    __syncthreads();
+    // wave w: the starts of rows [512 w, 512 w + 512), evaluated into LDS
+    const uint32_t q0 = (uint32_t) wave * SMAX_XQ;
+    uint32_t ns = 0;
+    for (uint32_t s2 = q0 / 64; s2 < (q0 + SMAX_XQ) / 64; s2++) {
+      const uint64_t m = W->st[s2];
+      if ((m >> lane) & 1u) sD.list[wave][ns + (uint32_t) __popcll(m & ltm)] = (uint16_t) (s2 * 64 + lane);
+      ns += (uint32_t) __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t wc = 0;
+    for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+      const uint32_t k = i0 + (uint32_t) lane;
+      bool acc = false;
+      if (k < ns) {
+        uint32_t cur = 0;
+        uint64_t j = 0;
+        const uint32_t b = sD.list[wave][k];
+        acc = eval_start_x(a, t, W, g0, b, &cur, &j);
+        sD.cur[wave][k] = cur;
+        sD.wid[wave][k] = acc ? (uint32_t) (j - (g0 + b) + 2) : 0u;
+      }
+      wc += (uint32_t) __popcll(__ballot(acc));
+    }
+    if (lane == 0) sD.cnt[wave] = wc;
+    __syncthreads();
+    const uint32_t c0 = sD.cnt[0], c1 = sD.cnt[1], c2 = sD.cnt[2], c3 = sD.cnt[3];
+    const uint32_t total = c0 + c1 + c2 + c3;
+    const uint32_t base = wave == 0 ? 0u : wave == 1 ? c0 : wave == 2 ? c0 + c1 : c0 + c1 + c2;
+    const bool nowrite = (a.dbg & (4096u | 32768u)) != 0;
+    if (threadIdx.x == 0) {
+      // the tile's records: list entry i owns wide slot wide_slot0 + i (a
+      // tile has at most SMAX_TILE / 2 records), else a run from the pool
+      uint64_t off = ~0ull;
+      const uint32_t wslot = a.wide_slot0 + i;
+      if (!nowrite) {
+        if (wslot < a.wide_cap) {
+          off = (uint64_t) wslot * (SMAX_TILE / 2);
+        } else if (total > 0) {
+          off = atomicAdd(a.pool_cursor, (unsigned long long) total);
+          if (off + total > a.pool_cap) off = ~0ull;   // pool full: the host re-plans
+        }
+        a.tile_off[tile] = off;
+      }
+      sD.off = off;
+      if (!(a.dbg & 4096u)) a.tile_count[tile] = total | SMAX_SLOT_WIDE;   // 16-byte records
+    }
+    __syncthreads();
+    const uint64_t off = sD.off;
+    if (off != ~0ull) {
+      GtSmaxRecord *wdst = a.pool + off + base;
+      uint32_t w = 0;
+      for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+        const uint32_t k = i0 + (uint32_t) lane;
+        const uint32_t wd = k < ns ? sD.wid[wave][k] : 0u;
+        const uint64_t am = __ballot(wd != 0);
+        if (wd != 0) {
+          GtSmaxRecord rec;
+          rec.lb = g0 + sD.list[wave][k] - 1;
+          rec.lcp = sD.cur[wave][k];
+          rec.width = wd;
+          wdst[w + (uint32_t) __popcll(am & ltm)] = rec;
+        }
+        w += (uint32_t) __popcll(am);
+      }
+    }
+    __syncthreads();   // window and lists reused by the next tile
+  }
+}
+
 // K1 instantiations.  Packed DNA BWT (0.5 B/row of BWT traffic) at 4
 // waves/SIMD is the production kernel; the _diag build keeps the
 // GT_SMAX_DEBUG ablation switches (used only when the variable is set).
@@ -1985,6 +2121,8 @@ struct GtSmaxPlan {
   int k1b_mode;              // placement of the static K1b (GT_SMAX_K1B_MODE)
   uint32_t comb_grid;        // mode 4: grid of the combined K1b launch (+1: head)
   bool dense;                // .llv entries per row above SMAX_FFPV_DENSITY: smax_scan_kernel_dense
+  bool k1b_wg;               // mode 4: one workgroup per K1b tile (GT_SMAX_K1B_WG=0: one wave)
+  uint32_t comb_grid_wg;     // its grid (+1: head)
   hipEvent_t fork, join;
   uint32_t *err;
   uint32_t dbg;
@@ -2229,6 +2367,16 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
         HIPCHK(hipMemcpy(p->defer_list, p->static_list, sizeof (uint32_t) * p->n_static,
                          hipMemcpyDeviceToDevice));
       p->comb_grid = std::max(p->defer_grid, p->static_grid - 1) + 1;   // static_grid has its +1
+      const char *wg = getenv("GT_SMAX_K1B_WG");
+      p->k1b_wg = wg ? strtol(wg, NULL, 0) != 0 : true;
+      // a workgroup per tile: the static list plus K1's deferrals (about one
+      // tile in 10^4) fit in one generation on all CUs
+      int ncu = 256;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, shard->device) !=
+              hipSuccess || ncu < 1)
+        ncu = 256;
+      p->comb_grid_wg = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u,
+                                           (uint32_t) ncu * 8u) + 1;
     }
     int lo = 0, hi = 0;
     if (p->k1b_mode == 3 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
@@ -2379,7 +2527,10 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       // computes the boundary head
       SmaxScanArgs c = a;
       c.k1b_head = 1;
-      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->comb_grid), dim3(SMAX_THREADS), 0, s, c);
+      if (p->k1b_wg)
+        hipLaunchKernelGGL(smax_defer_wg_kernel, dim3(p->comb_grid_wg), dim3(SMAX_THREADS), 0, s, c);
+      else
+        hipLaunchKernelGGL(smax_defer_kernel, dim3(p->comb_grid), dim3(SMAX_THREADS), 0, s, c);
     } else {
       hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
     }
