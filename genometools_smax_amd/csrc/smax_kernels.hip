@@ -1707,12 +1707,74 @@ smax_defer_kernel(SmaxScanArgs a) {
 }
 
 
+// load_exact_window for a whole workgroup (256 threads): one 16-row chunk
+// per thread and every .llv entry of the window (<= SMAX_LDSB) fetched in
+// one round of at most 9 per thread, instead of one wave doing 3 chunks per
+// lane and up to 4 dependent .llv rounds.  *nff is a workgroup counter the
+// caller zeroes.
+__device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, SmaxWindowX *W,
+                                            uint32_t *nff) {
+  const int tid = threadIdx.x;
+  const uint64_t g0 = a.base + l0;
+  const uint2 info = a.llv_win[l0 / SMAX_TILE - a.tile_first];
+  const uint32_t lo = info.x, n = SMAX_WIN_N(info.y);
+  const uint64_t wb = g0 - SMAX_LH;
+  constexpr int EPT = (SMAX_LDSB + 255) / 256;        // .llv entries per thread (9)
+  uint2 ep[EPT];
+  uint32_t ev[EPT];
+#pragma unroll
+  for (int r = 0; r < EPT; r++) {
+    const uint32_t e = (uint32_t) tid + 256u * r;
+    const uint32_t *rec = reinterpret_cast<const uint32_t *>(&a.llv[lo + (e < n ? e : 0)]);
+    ep[r] = e < n ? make_uint2(rec[0], rec[1]) : make_uint2(0xffffffffu, 0xffffffffu);
+    ev[r] = e < n ? rec[2] : 0u;
+  }
+  if (tid < SMAX_NCHUNK) {
+    const int i = tid;
+    const int64_t r0 = (int64_t) l0 - SMAX_LH + 16 * i;
+    const uint4 lv = *reinterpret_cast<const uint4 *>(a.lcp + r0);
+    const uint4 bv = a.bwtpk != nullptr ? pk_expand(a.bwtpk[l0 / 16 + i])
+                                        : *reinterpret_cast<const uint4 *>(a.bwt + r0);
+    *reinterpret_cast<uint4 *>(&W->L[16 * i]) = lv;
+    *reinterpret_cast<uint4 *>(&W->B[16 * i]) = bv;
+    const uint32_t f = seg_ffcount(lv);
+    if (f) atomicAdd(nff, f);
+    const int64_t gr = (int64_t) wb + 16 * i;
+    const uint32_t w[4] = {lv.x, lv.y, lv.z, lv.w};
+    const bool inner = gr >= 1 && gr + 16 <= (int64_t) a.N;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint4 x;
+      uint32_t *xe = &x.x;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int64_t g = gr + 4 * k + q;
+        const uint32_t byte = (w[k] >> (8 * q)) & 0xffu;
+        xe[q] = (inner || (g >= 1 && g < (int64_t) a.N)) ? byte : 0u;
+      }
+      *reinterpret_cast<uint4 *>(&W->X[16 * i + 4 * k]) = x;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < EPT; r++) {
+    const uint32_t e = (uint32_t) tid + 256u * r;
+    const uint64_t pos = ((uint64_t) ep[r].y << 32) | ep[r].x;
+    const uint64_t o = pos - wb;
+    if (e < n && o < SMAX_LDSB && pos < a.N) W->X[o] = ev[r];
+  }
+  __syncthreads();
+  // every 255 byte of [1, N) in the window has its entry
+  if (tid == 0 && *nff != n) atomicOr(a.err, SMAX_ERR_LLV);
+}
+
 // K1b, one workgroup per tile (the combined placement's kernel): a K1b
 // launch covers few tiles (the static list and K1's rare deferrals; about
 // 130 per shard of an 8-way C3 split), so its time is the slowest tile's,
-// and one wave per tile left three of every four waves idle.  Here wave 0
-// loads the exact window, the four waves share the ballot steps, and each
-// takes one 512-row round of starts: evaluated once into LDS (value, width,
+// and one wave per tile left three of every four waves idle.  Here the
+// whole workgroup loads the exact window (load_exact_window_wg), the four
+// waves share the ballot steps, and each takes one 512-row round of starts:
+// evaluated once into LDS (value, width,
 // accepted), the rounds' record counts are scanned across the waves and
 // the records written in row order.  Same results as smax_defer_kernel.
 struct SmaxDeferWG {
@@ -1721,6 +1783,7 @@ struct SmaxDeferWG {
   uint32_t cur[4][SMAX_XQ];         // evaluated LCP value
   uint32_t wid[4][SMAX_XQ];         // width; 0: not accepted
   uint32_t cnt[4];
+  uint32_t nff;                     // 255 bytes of the window (load_exact_window_wg)
   uint64_t off;                     // the tile's first record in the pool (~0: none)
 };
 
@@ -1746,8 +1809,9 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     const uint64_t tile = a.defer_list[i];
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
     const uint64_t g0 = a.base + l0;
-    if (wave == 0) load_exact_window(a, l0, W);
+    if (threadIdx.x == 0) sD.nff = 0;
     __syncthreads();
+    load_exact_window_wg(a, l0, W, &sD.nff);
     t.g0 = g0;
     t.L = W->L;
     t.B = W->B;
