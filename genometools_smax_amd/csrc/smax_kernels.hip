@@ -2019,26 +2019,49 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   const uint32_t total = sPre[SMAX_CPB];
   const uint64_t base = sRed[0] + sRed[1] + sRed[2] + sRed[3];
   if (tid == 0 && s0 + SMAX_CPB >= nslots) *count = base + total;
-  for (uint32_t r = tid; r < total; r += 256) {
-    uint32_t lo = 0, hi = SMAX_CPB;          // largest j with sPre[j] <= r
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (sPre[mid] <= r) lo = mid; else hi = mid;
+  // four records per thread per round: their slot searches and loads are
+  // independent, so their latencies overlap (one record at a time left the
+  // kernel latency-bound: 28 us for the 2.5 M records of an 8-way C3 shard)
+  constexpr int U = 4;
+  static_assert(SMAX_CPB == 256, "8 halvings find a slot among SMAX_CPB");
+  for (uint32_t r0 = tid; r0 < total; r0 += 256 * U) {
+    uint32_t los[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = r0 + 256u * u;
+      uint32_t lo = 0, hi = SMAX_CPB;        // largest j with sPre[j] <= r
+#pragma unroll
+      for (int st = 0; st < 8; st++) {       // SMAX_CPB = 256: 8 halvings
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sPre[mid] <= r) lo = mid; else hi = mid;
+      }
+      los[u] = lo;
     }
-    if (base + r >= capacity) continue;
-    const uint64_t tile = s0 + lo;
-    if (sWide[lo]) {
-      // K1b tile: its run in the pool (absent if the pool was full, which
-      // only happens when the records exceed the capacity: re-planned)
-      const uint64_t off = tile_off[tile];
-      if (off <= pool_cap && off + (r - sPre[lo]) < pool_cap) out[base + r] = pool[off + (r - sPre[lo])];
-    } else {
-      const uint64_t v = slots[tile * (uint64_t) SMAX_SSLOT + (r - sPre[lo])];
-      GtSmaxRecord rec;
-      rec.lb = g00 + tile * (uint64_t) SMAX_TILE + (v & 0x7ffu) - 1;   // g00: global row of tile 0
-      rec.width = (uint32_t) (v >> 11) & SMAX_PK_WMAX;
-      rec.lcp = (uint32_t) (v >> 32);
-      out[base + r] = rec;
+    uint64_t v[U];
+    bool wide[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = r0 + 256u * u, lo = los[u];
+      wide[u] = sWide[lo] != 0;
+      v[u] = (r < total && !wide[u]) ? slots[(s0 + lo) * (uint64_t) SMAX_SSLOT + (r - sPre[lo])] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t r = r0 + 256u * u, lo = los[u];
+      if (r >= total || base + r >= capacity) continue;
+      const uint64_t tile = s0 + lo;
+      if (wide[u]) {
+        // K1b tile: its run in the pool (absent if the pool was full, which
+        // only happens when the records exceed the capacity: re-planned)
+        const uint64_t off = tile_off[tile];
+        if (off <= pool_cap && off + (r - sPre[lo]) < pool_cap) out[base + r] = pool[off + (r - sPre[lo])];
+      } else {
+        GtSmaxRecord rec;
+        rec.lb = g00 + tile * (uint64_t) SMAX_TILE + (v[u] & 0x7ffu) - 1;   // g00: global row of tile 0
+        rec.width = (uint32_t) (v[u] >> 11) & SMAX_PK_WMAX;
+        rec.lcp = (uint32_t) (v[u] >> 32);
+        out[base + r] = rec;
+      }
     }
   }
 }
@@ -2416,10 +2439,19 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     // stream, 2 after K1, 3 side stream of the highest priority, launched
     // ahead of K1
     {
+      // density over the plan's own tiles (a shard plan over full tables
+      // sees every .llv entry): first entry of the first window to the end
+      // of the last one
       const char *dv = getenv("GT_SMAX_DENSE");   // diagnostic override: 0 / 1
-      const uint64_t rows = shard->end > shard->begin ? shard->end - shard->begin : 1;
+      uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
+      if (p->num_tiles > 0) {
+        HIPCHK(hipMemcpy(&w0, p->llv_win, sizeof w0, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&w1, p->llv_win + (p->num_tiles - 1), sizeof w1, hipMemcpyDeviceToHost));
+      }
+      const uint64_t inrange = (uint64_t) w1.x + SMAX_WIN_N(w1.y) - w0.x;
+      const uint64_t rows = (uint64_t) p->num_tiles * SMAX_TILE;
       p->dense = dv ? strtol(dv, NULL, 0) != 0
-                    : (double) shard->numllv > SMAX_FFPV_DENSITY * (double) rows;
+                    : rows > 0 && (double) inrange > SMAX_FFPV_DENSITY * (double) rows;
     }
     const char *m = getenv("GT_SMAX_K1B_MODE");
     p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 4;
