@@ -122,6 +122,7 @@ struct SmaxScanArgs {
   uint32_t k1b_head;         // K1b: the last workgroup computes the boundary head
   uint32_t wide_slot0;       // K1b: wide slot of list entry 0 (static list 0, runtime n_static)
   uint32_t defer_base;       // K0 resets *defer_count to this (combined list: n_static)
+  uint32_t k1_reset;         // combined placement without K0: K1 clears the pending slot
   uint32_t wide_cap;         // wide slots (SMAX_TILE / 2 records each) at the pool's start
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
 };
@@ -1260,6 +1261,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   const uint32_t last = a.num_tiles - 1;
 
   uint32_t tile = blockIdx.x * (SMAX_THREADS / 64) + (uint32_t) wave;
+  // no K0 (combined placement): K1 never fills the pending slot and K1b runs
+  // after it, so clearing the slot here is K0's only remaining reset (the
+  // deferral count and pool cursor are reset by the previous run's K3)
+  if (a.k1_reset && blockIdx.x == 0 && threadIdx.x == 0) a.bnd->pend_valid = 0;
   if (tile >= a.num_tiles) return;
 
   Win t;
@@ -1977,6 +1982,13 @@ smax_block_sum_kernel(const uint32_t *tile_count, uint64_t ntiles, uint32_t *blo
 
 // ------------------------------------------------------------ K3: compact
 
+struct SmaxNextRun {                  // K0's resets done by K3 (null: K0 runs)
+  uint32_t *defer_count, *defer_last;
+  unsigned long long *pool_cursor;
+  uint32_t defer_base;
+  unsigned long long pool_start;
+};
+
 // One workgroup per SMAX_CPB consecutive tile slots: the slots' counts are
 // scanned in LDS, then all 256 threads copy the slots' records to their final
 // positions (slot found by binary search in the LDS prefix), consecutive
@@ -1986,7 +1998,14 @@ __global__ void __launch_bounds__(256)
 smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
                     const uint32_t *block_sum, uint64_t nslots, const GtSmaxRecord *pool,
                     uint64_t pool_cap, const uint64_t *tile_off, GtSmaxRecord *out,
-                    uint64_t capacity, uint64_t *count, uint64_t g00) {
+                    uint64_t capacity, uint64_t *count, uint64_t g00, SmaxNextRun nr) {
+  // the next run's resets (combined placement: no K0): K1b, the last reader
+  // of the deferral count and pool cursor, has finished
+  if (nr.defer_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    *nr.defer_last = *nr.defer_count;
+    *nr.defer_count = nr.defer_base;
+    *nr.pool_cursor = nr.pool_start;
+  }
   __shared__ uint32_t sPre[SMAX_CPB + 1];
   __shared__ uint32_t sWave[4];
   __shared__ uint8_t sWide[SMAX_CPB];
@@ -2201,6 +2220,7 @@ struct GtSmaxPlan {
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
   uint32_t *defer_count;
+  uint32_t *defer_last;      // combined placement: K1's last count (K3 resets the live one)
   uint32_t *static_list;     // plan-time K1b list (edges, wide .llv windows) + count
   uint32_t *static_count;
   uint32_t n_static, static_grid;
@@ -2389,6 +2409,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (2 * (uint64_t) p->num_tiles + 1)));
   HIPCHK(dalloc(&p->defer_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
+  HIPCHK(dalloc(&p->defer_last, sizeof (uint32_t)));
+  HIPCHK(hipMemset(p->defer_last, 0, sizeof (uint32_t)));
   HIPCHK(dalloc(&derr, sizeof (uint32_t)));
   HIPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
   if (shard->numllv > 0xffffffffull) {
@@ -2473,6 +2495,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
         ncu = 256;
       p->comb_grid_wg = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u,
                                            (uint32_t) ncu * 8u) + 1;
+      // the first run's state (later runs: reset by the previous run's K3)
+      const unsigned long long pc = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
+      HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(p->pool_cursor, &pc, sizeof pc, hipMemcpyHostToDevice));
     }
     int lo = 0, hi = 0;
     if (p->k1b_mode == 3 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
@@ -2493,7 +2519,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
@@ -2545,6 +2571,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.defer_list = p->defer_list;
   a.defer_count = p->defer_count;
   a.k1b_head = 0;
+  a.k1_reset = 0;
   a.dbg = p->dbg;
   return a;
 }
@@ -2557,8 +2584,13 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
   {
     SmaxScanArgs a = plan_args(p);
     const int empty = p->shard.begin >= p->shard.end;
-    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a, empty);
-    HIPCHK(hipGetLastError());
+    // combined placement: no K0 (its resets: K1 and the previous run's K3)
+    const bool nok0 = p->k1b_mode == 4 && !empty && !(p->dbg & 16384u);
+    if (!nok0) {
+      hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a, empty);
+      HIPCHK(hipGetLastError());
+    }
+    a.k1_reset = nok0 ? 1u : 0u;
     if (empty) {
       HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
       return 0;
@@ -2634,11 +2666,19 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
     hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
     HIPCHK(hipGetLastError());
+    SmaxNextRun nr = {nullptr, nullptr, nullptr, 0u, 0ull};
+    if (nok0) {
+      nr.defer_count = p->defer_count;
+      nr.defer_last = p->defer_last;
+      nr.pool_cursor = p->pool_cursor;
+      nr.defer_base = p->n_static;
+      nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
+    }
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->slots, p->tile_count, p->block_sum, (uint64_t) p->num_tiles,
                        p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
                        p->tile_off, p->out, p->capacity, p->count,
-                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE);
+                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE, nr);
     HIPCHK(hipGetLastError());
   }
   p->runs++;
@@ -2757,7 +2797,9 @@ fail:
 extern "C" uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *p) {
   uint32_t n = 0;
   if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;
-  if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
+  // combined placement: K3 resets the live count; its last value is kept
+  if (hipMemcpy(&n, p->k1b_mode == 4 ? p->defer_last : p->defer_count, sizeof n,
+                hipMemcpyDeviceToHost) != hipSuccess)
     return 0xffffffffu;
   return p->k1b_mode == 4 ? n - p->n_static : n;   // K1's deferrals only
 }
@@ -2771,7 +2813,9 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
   if (counts && !(p->dbg & 32768u))
     for (uint64_t i = 0; i < p->num_tiles; i++) counts[i] &= ~SMAX_SLOT_WIDE;   // slot-format flag
   uint32_t n = 0;
-  if (hipMemcpy(&n, p->defer_count, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(&n, p->k1b_mode == 4 ? p->defer_last : p->defer_count, sizeof n,
+                hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
   const uint32_t base = p->k1b_mode == 4 ? p->n_static : 0;   // combined list: K1's part
   n -= base;
   if (ndeferred) *ndeferred = n;
