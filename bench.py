@@ -298,7 +298,7 @@ def main():
                                 "sample": "orc_linsmax_mt (pthreads, equal row ranges) over all rows"}
 
     # end-to-end through the drop-in boundary (host tables in memory -> H2D
-    # -> plan -> K0..K3 -> D2H of the (lcp, lb, rb) list): reported beside
+    # -> plan -> K1..K3 -> D2H of the (lcp, lb, rb) list): reported beside
     # `value`, never as it
     e2e = None
     if host is not None and not args.no_end_to_end:
@@ -315,7 +315,7 @@ def main():
         e2e = {"value": N / t_e2e, "unit": "suffix-positions/s", "seconds": round(t_e2e, 4),
                "path": "gt_smax_hip_enumerate_to_buffer: pageable host .lcp/.bwt/.llv -> H2D "
                        "(.bwt packed to bit planes during the staged fill) -> plan (llv index) -> "
-                       "K0..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
+                       "K1..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
                "vs_cpu_baseline": (N / t_e2e) / cpu["value"] if cpu else None}
         del iv
 
