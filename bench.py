@@ -3,7 +3,7 @@
 
 One "step" = one smax pass over the whole suffix array of the workload:
 the fused plateau-scan / left-diversity / ordered-compaction kernel K1
-(plus the one-wave head kernel) on every rank's suffix-array range and, with
+(plus K1b for deferred tiles, K2/K3 compaction) on every rank's suffix-array range and, with
 N > 1, the RCCL all-gather of the fixed-size boundary records and the stitch
 kernel.  The LCP/BWT/.llv tables are resident in HBM before timing starts
 (built on each GPU by the repo's GPU suffixerator replacement from a
@@ -91,6 +91,9 @@ def main():
                     help="all ranks on cuda:0 (rehearsal only)")
     ap.add_argument("--esa64", action="store_true",
                     help="build with the 64-bit range builder even when the 32-bit one applies")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip gathering every rank's records to rank 0 for the "
+                         "whole-table oracle check")
     ap.add_argument("--byte-bwt", action="store_true",
                     help="plan from the byte BWT (plan-time packing) instead of the builder's "
                          "packed BWT")
@@ -150,6 +153,7 @@ def main():
         builder = "32-bit builder, whole text"
     t_esa = time.time() - t0
     assert (esa.totallength, esa.nonspecials) == (n, N)
+    numllv = int(esa.numllv)
     log("rank %d: GPU ESA (%s) n=%d N=%d llv=%d rounds=%d in %.1fs"
         % (rank, builder, n, N, esa.numllv, esa.esa.sort_rounds, t_esa))
     if world > 1 or use64:
@@ -259,6 +263,54 @@ def main():
         traffic = pmc.get("hbm_bytes_per_launch")
         pmc_src = os.path.relpath(pmc_path, ROOT)
 
+    # N > 1 parity: every rank's stitched records gathered to rank 0 (padded
+    # all-gather over the same backend as the boundary exchange), compared
+    # bit for bit with the all-core oracle over the WHOLE table, which rank 0
+    # builds after the timed region (no rank holds it during the run)
+    dist_parity = None
+    if world > 1 and not args.no_parity:
+        mine = plan.fetch_triples().view(np.int64).reshape(-1)
+        plan.close()
+        plan = None
+        esa.release()
+        esa = None
+        dev = "cpu" if staged else "cuda"
+        cnts = torch.zeros(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(cnts, torch.tensor([len(mine)], dtype=torch.int64, device=dev))
+        kmax = max(int(cnts.max()), 1)
+        buf = torch.zeros(kmax, dtype=torch.int64, device=dev)
+        buf[:len(mine)] = torch.from_numpy(mine).to(dev)
+        gathered = torch.zeros(kmax * world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(gathered, buf)
+        del buf, mine
+        if rank == 0:
+            g = gathered.cpu().numpy()
+            got = np.concatenate([g[r * kmax: r * kmax + int(cnts[r])] for r in range(world)])
+            got = got.view(np.uint64).reshape(-1, 3)
+            del g
+            import oracle_lib  # noqa: E402  (tests/: the checker only)
+            t0 = time.time()
+            text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
+            if n + 1 >= 2 ** 32 or args.esa64:
+                full = G.DeviceEsa64(text, device=local, row_lo=0, row_hi=n + 1)
+            else:
+                full = G.DeviceEsa(text, device=local, keep_suftab=False)
+            del text
+            ht = full.download()
+            full.release()
+            threads = max(1, min(len(os.sched_getaffinity(0)), args.cpu_threads))
+            want = oracle_lib.linsmax(ht["lcptab"], ht["llvtab"], ht["bwttab"], N, minlen,
+                                      threads=threads)
+            del ht
+            dist_parity = bool(np.array_equal(got, want))
+            log("parity (%d ranks): %d gathered records %s the whole-table oracle's %d (%.1fs)"
+                % (world, len(got), "equal" if dist_parity else "DIFFER from", len(want),
+                   time.time() - t0))
+            if not dist_parity:
+                parity_ok = False
+            del got, want
+        del gathered
+
     cpu = None
     sample_full = False
     if host is not None:
@@ -337,7 +389,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": cfg["workload"], "minlen": minlen, "totallength": n,
-                       "nonspecials": N, "llv_entries": esa.numllv, "global_batch": N,
+                       "nonspecials": N, "llv_entries": numllv, "global_batch": N,
                        "parallelism": "sa-range-shard x%d + %s all-gather stitch"
                        % (world, "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)")
                        if world > 1 else "single GPU"},
@@ -355,7 +407,10 @@ def main():
                                              if traffic else None),
                          "traffic_source": pmc_src},
             "parity": ("bit-exact vs CPU oracle (plan records%s)" % (" + end-to-end" if e2e else "")
-                       if res is not None and sample_full else "not checked in this run"),
+                       if res is not None and sample_full else
+                       "bit-exact vs CPU oracle (all %d ranks' stitched records gathered to rank 0 "
+                       "vs the all-core oracle over the whole table)" % world
+                       if dist_parity else "not checked in this run"),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2),
@@ -368,7 +423,8 @@ def main():
         print(json.dumps(out), flush=True)
     if plan is not None:
         plan.close()
-    esa.release()
+    if esa is not None:
+        esa.release()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
