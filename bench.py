@@ -179,18 +179,27 @@ def main():
             hrecv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8)
 
     def step():
-        plan.run(sptr)
-        if world > 1:
-            # the one exchange step: all-gather of the fixed-size boundary
-            # records, then the stitch kernel resolves spanning plateaus
-            plan.copy_boundary(send.data_ptr(), sptr)
-            if staged:
-                hsend.copy_(send)
-                dist.all_gather_into_tensor(hrecv, hsend)
-                recv.copy_(hrecv)
-            else:
-                dist.all_gather_into_tensor(recv, send)
-            plan.stitch(recv.data_ptr(), world, rank, sptr)
+        if world == 1:
+            plan.run(sptr)
+            return
+        # the one exchange step: all-gather of the fixed-size boundary
+        # records, then the stitch kernel resolves spanning plateaus.  The
+        # boundary record is final after the scan (part 0), so the all-gather
+        # runs on RCCL's stream beside the compaction (part 1); the stitch
+        # waits for both
+        plan.run_part(0, sptr)
+        plan.copy_boundary(send.data_ptr(), sptr)
+        if staged:
+            hsend.copy_(send)
+            work = dist.all_gather_into_tensor(hrecv, hsend, async_op=True)
+            plan.run_part(1, sptr)
+            work.wait()
+            recv.copy_(hrecv)
+        else:
+            work = dist.all_gather_into_tensor(recv, send, async_op=True)
+            plan.run_part(1, sptr)
+            work.wait()
+        plan.stitch(recv.data_ptr(), world, rank, sptr)
 
     # first pass sizes the output exactly (re-plan on overflow)
     step()

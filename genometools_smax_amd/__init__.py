@@ -163,6 +163,7 @@ def lib():
                                           cs, sz]
         L.gt_smax_plan_delete.argtypes = [vp]
         L.gt_smax_plan_run.argtypes = [vp, vp]
+        L.gt_smax_plan_run_part.argtypes = [vp, ci, vp]
         L.gt_smax_plan_records.argtypes = [vp]
         L.gt_smax_plan_records.restype = vp
         L.gt_smax_plan_count_dev.argtypes = [vp]
@@ -697,6 +698,11 @@ class SmaxPlan:
     def run(self, stream=0):
         if lib().gt_smax_plan_run(self.plan, stream or None) != 0:
             raise SmaxError("gt_smax_plan_run failed")
+
+    def run_part(self, part, stream=0):
+        """Part 0: the scan (boundary record final); part 1: the compaction."""
+        if lib().gt_smax_plan_run_part(self.plan, int(part), stream or None) != 0:
+            raise SmaxError("gt_smax_plan_run_part(%d) failed" % part)
 
     def stitch(self, all_boundaries_ptr, nshards, shard_index, stream=0):
         if lib().gt_smax_plan_stitch(self.plan, all_boundaries_ptr, nshards, shard_index,

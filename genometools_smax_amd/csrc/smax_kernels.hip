@@ -1816,7 +1816,13 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     const uint64_t g0 = a.base + l0;
     if (threadIdx.x == 0) sD.nff = 0;
     __syncthreads();
+    // diagnostic (GT_SMAX_DEBUG 32768): the tile's cycles / 16 instead of its
+    // count; |65536 stops the clock after the window load, |131072 after the
+    // ballots, |262144 after the evaluation
+    const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
+    uint64_t tmark = 0;
     load_exact_window_wg(a, l0, W, &sD.nff);
+    if (a.dbg & 65536u) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
     t.L = W->L;
     t.B = W->B;
@@ -1842,6 +1848,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
       }
     }
     __syncthreads();
+    if ((a.dbg & 131072u) && tmark == 0) tmark = __builtin_readcyclecounter();
     // wave w: the starts of rows [512 w, 512 w + 512), evaluated into LDS
     const uint32_t q0 = (uint32_t) wave * SMAX_XQ;
     uint32_t ns = 0;
@@ -1868,6 +1875,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     }
     if (lane == 0) sD.cnt[wave] = wc;
     __syncthreads();
+    if ((a.dbg & 262144u) && tmark == 0) tmark = __builtin_readcyclecounter();
     const uint32_t c0 = sD.cnt[0], c1 = sD.cnt[1], c2 = sD.cnt[2], c3 = sD.cnt[3];
     const uint32_t total = c0 + c1 + c2 + c3;
     const uint32_t base = wave == 0 ? 0u : wave == 1 ? c0 : wave == 2 ? c0 + c1 : c0 + c1 + c2;
@@ -1887,7 +1895,10 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
         a.tile_off[tile] = off;
       }
       sD.off = off;
-      if (!(a.dbg & 4096u)) a.tile_count[tile] = total | SMAX_SLOT_WIDE;   // 16-byte records
+      if (a.dbg & 32768u)
+        a.tile_count[tile] = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
+      else if (!(a.dbg & 4096u))
+        a.tile_count[tile] = total | SMAX_SLOT_WIDE;   // 16-byte records
     }
     __syncthreads();
     const uint64_t off = sD.off;
@@ -2576,11 +2587,40 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   return a;
 }
 
-extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
+static int plan_run_scan(GtSmaxPlan *p, hipStream_t s);
+static int plan_run_compact(GtSmaxPlan *p, hipStream_t s);
+
+// parts: bit 0 = the scan (K1 and K1b; the boundary record is final after
+// it), bit 1 = the ordered compaction (K2 block sums, K3).  gt_smax_plan_run
+// enqueues both; a sharded caller can enqueue part 0, start the boundary
+// all-gather on its communication stream, then part 1 beside it.
+static int plan_run_parts(GtSmaxPlan *p, hipStream_t s, unsigned parts) {
   char *errbuf = NULL;
   size_t errlen = 0;
-  hipStream_t s = (hipStream_t) stream;
   HIPCHK(hipSetDevice(p->shard.device));
+  if (p->shard.begin >= p->shard.end) {
+    if (parts & 1u) return plan_run_scan(p, s);
+    return 0;
+  }
+  if ((parts & 1u) && plan_run_scan(p, s) != 0) return -1;
+  if ((parts & 2u) && plan_run_compact(p, s) != 0) return -1;
+  return 0;
+fail:
+  return -1;
+}
+
+extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
+  return plan_run_parts(p, (hipStream_t) stream, 3u);
+}
+
+extern "C" int gt_smax_plan_run_part(GtSmaxPlan *p, int part, void *stream) {
+  if (part != 0 && part != 1) return -1;
+  return plan_run_parts(p, (hipStream_t) stream, 1u << part);
+}
+
+static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
   {
     SmaxScanArgs a = plan_args(p);
     const int empty = p->shard.begin >= p->shard.end;
@@ -2663,6 +2703,17 @@ extern "C" int gt_smax_plan_run(GtSmaxPlan *p, void *stream) {
       hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
     }
     HIPCHK(hipGetLastError());
+  }
+  return 0;
+fail:
+  return -1;
+}
+
+static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
+  char *errbuf = NULL;
+  size_t errlen = 0;
+  {
+    const bool nok0 = p->k1b_mode == 4 && !(p->dbg & 16384u);
     hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
     HIPCHK(hipGetLastError());

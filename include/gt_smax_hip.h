@@ -195,6 +195,14 @@ void gt_smax_plan_delete(GtSmaxPlan *plan);
  * stream (a hipStream_t, NULL = default stream).  Asynchronous. */
 int gt_smax_plan_run(GtSmaxPlan *plan, void *stream);
 
+/* The same pass in two parts (plan_run == part 0 then part 1 on one stream):
+ * part 0 = the scan, after which the shard's boundary record is final
+ * (gt_smax_plan_copy_boundary may follow); part 1 = the ordered compaction
+ * into the record array.  A sharded caller enqueues part 0, the boundary
+ * copy and its all-gather (on the collective's stream), then part 1 beside
+ * the all-gather, and the stitch once both are done.  -1 for another part. */
+int gt_smax_plan_run_part(GtSmaxPlan *plan, int part, void *stream);
+
 /* Device pointers owned by the plan. */
 GtSmaxRecord *gt_smax_plan_records(GtSmaxPlan *plan);
 uint64_t *gt_smax_plan_count_dev(GtSmaxPlan *plan);   /* 1 x uint64 */

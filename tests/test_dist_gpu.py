@@ -3,8 +3,8 @@
 Each spawned rank (world_size 2 or 3, all on cuda:0, gloo process group)
 runs exactly the step bench.py runs per rank:
 
-    plan.run -> plan.copy_boundary -> all-gather of the boundary records
-             -> plan.stitch (smax_stitch_kernel) -> the rank's records
+    plan.run_part(0) -> plan.copy_boundary -> all-gather of the boundary
+    records -> plan.run_part(1) -> plan.stitch (smax_stitch_kernel)
 
 The boundary records are staged through host memory for gloo (bench.py's
 --dist-backend gloo rehearsal; the driver's 8-GPU run uses RCCL on device
@@ -41,13 +41,15 @@ def _padded(host, length):
 
 
 def _exchange(plan, world, rank):
-    """The rank's step: run, all-gather of boundary records, stitch."""
+    """The rank's step as bench.py runs it: scan (part 0), boundary copy and
+    all-gather, compaction (part 1), stitch."""
     stream = torch.cuda.current_stream().cuda_stream
-    plan.run(stream)
+    plan.run_part(0, stream)
     send = torch.zeros(G.BOUNDARY_BYTES, dtype=torch.uint8, device="cuda")
     plan.copy_boundary(send.data_ptr(), stream)
     hrecv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8)
     dist.all_gather_into_tensor(hrecv, send.cpu())
+    plan.run_part(1, stream)
     recv = hrecv.cuda()
     plan.stitch(recv.data_ptr(), world, rank, stream)
     torch.cuda.synchronize()

@@ -51,6 +51,40 @@ def test_plan_packed_and_byte_bwt_agree(human10):
         assert np.array_equal(got, want), (packed, len(got), len(want))
 
 
+def test_run_in_two_parts(human10):
+    """gt_smax_plan_run_part: scan then compaction equals plan_run, repeated
+    (each run's compaction resets the next run's deferral state); the
+    boundary record is final after part 0 (bench.py starts the all-gather
+    there, beside the compaction)."""
+    import torch
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+
+    def bnd(plan):
+        t = torch.zeros(G.BOUNDARY_BYTES, dtype=torch.uint8, device="cuda")
+        plan.copy_boundary(t.data_ptr())
+        torch.cuda.synchronize()
+        return t.cpu().numpy()
+
+    for begin, end in ((1, N), (1, N // 2), (N // 3, N)):
+        p = esa.plan(20, begin, end)
+        ref = esa.plan(20, begin, end)
+        ref.run()
+        ref_trip, ref_bnd = ref.fetch_triples(), bnd(ref)
+        if (begin, end) == (1, N):
+            assert np.array_equal(ref_trip, want)
+        for _ in range(3):
+            p.run_part(0)
+            assert np.array_equal(bnd(p), ref_bnd)
+            p.run_part(1)
+            assert np.array_equal(p.fetch_triples(), ref_trip)
+        with pytest.raises(G.SmaxError):
+            p.run_part(2)
+        p.close()
+        ref.close()
+
+
 def _host_call(e, minlen, shards, **env):
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})

@@ -1,0 +1,8 @@
+# Two-part plan run: runtime + multi-rank GPU tests, N=1 bench, 2-rank gloo rehearsal with parity.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/split
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_runtime_gpu.py tests/test_dist_gpu.py -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 300 python bench.py --no-end-to-end --no-cpu-baseline > $O/bench.json 2> $O/bench.err
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --one-gpu --dist-backend gloo --bases 300000000 --steps 10 --warmup 2 > $O/w2.json 2> $O/w2.err
