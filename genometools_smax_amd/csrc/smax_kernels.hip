@@ -19,7 +19,7 @@
 //   K1b smax_defer_kernel    the plan-time static list (shard edges,
 //                            dense-.llv windows) followed by K1's runtime
 //                            deferrals (exact-queue overflow, tiles with more
-//                            records than a slot holds); its last workgroup
+//                            records than a slot holds); one workgroup
 //                            computes the boundary head (GT_SMAX_K1B_MODE 0-3
 //                            keep the older placements of the static list:
 //                            side stream beside K1, before or after K1)
@@ -118,8 +118,10 @@ struct SmaxScanArgs {
   uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), written by K2
   GtSmaxBoundary *bnd;
   uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
+  uint2 *defer_info;         // beside each entry: the tile's llv_win word pair (K1b's
+                             // .llv loads need not wait for a load of llv_win[tile])
   uint32_t *defer_count;     // reset by K0
-  uint32_t k1b_head;         // K1b: the last workgroup computes the boundary head
+  uint32_t k1b_head;         // K1b: one workgroup computes the boundary head
   uint32_t wide_slot0;       // K1b: wide slot of list entry 0 (static list 0, runtime n_static)
   uint32_t defer_base;       // K0 resets *defer_count to this (combined list: n_static)
   uint32_t k1_reset;         // combined placement without K0: K1 clears the pending slot
@@ -405,6 +407,13 @@ __device__ static void compute_head(const SmaxScanArgs &a) {
 // smax_llv_index_kernel into bit 31 of the tile's llv_win word.
 __host__ __device__ __forceinline__ bool static_deferred(const SmaxScanArgs &a, uint32_t wnf) {
   return (wnf & SMAX_WIN_STATIC) != 0 || (a.dbg & 64u);
+}
+
+// the llv_win words of the combined list's static entries (plan time)
+__global__ void __launch_bounds__(256) smax_defer_info_kernel(const uint32_t *list, uint32_t n,
+                                                              const uint2 *llv_win, uint2 *info) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) info[k] = llv_win[list[k]];
 }
 
 __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, uint32_t *list,
@@ -1369,7 +1378,11 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
     }
-    if (lane == 0 && defer) a.defer_list[atomicAdd(a.defer_count, 1u)] = (uint32_t) tile;
+    if (lane == 0 && defer) {
+      const uint32_t k = atomicAdd(a.defer_count, 1u);
+      a.defer_list[k] = (uint32_t) tile;
+      a.defer_info[k] = make_uint2(wlo, wnf);
+    }
     if (!stat && !defer) {
       // the tile's records move from the LDS staging to one lane each; they
       // are stored at the start of the next iteration (see above)
@@ -1717,11 +1730,10 @@ smax_defer_kernel(SmaxScanArgs a) {
 // one round of at most 9 per thread, instead of one wave doing 3 chunks per
 // lane and up to 4 dependent .llv rounds.  *nff is a workgroup counter the
 // caller zeroes.
-__device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, SmaxWindowX *W,
-                                            uint32_t *nff) {
+__device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, uint2 info,
+                                            SmaxWindowX *W, uint32_t *nff) {
   const int tid = threadIdx.x;
   const uint64_t g0 = a.base + l0;
-  const uint2 info = a.llv_win[l0 / SMAX_TILE - a.tile_first];
   const uint32_t lo = info.x, n = SMAX_WIN_N(info.y);
   const uint64_t wb = g0 - SMAX_LH;
   constexpr int EPT = (SMAX_LDSB + 255) / 256;        // .llv entries per thread (9)
@@ -1785,8 +1797,13 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
 struct SmaxDeferWG {
   SmaxWindowX win;
   uint16_t list[4][SMAX_XQ];        // per wave: its round's starts (row order)
-  uint32_t cur[4][SMAX_XQ];         // evaluated LCP value
-  uint32_t wid[4][SMAX_XQ];         // width; 0: not accepted
+  // per wave: its accepted records, compacted (a 512-row round holds at most
+  // 256: consecutive accepted starts are >= 2 rows apart) -- half the LDS of
+  // per-start results (28 KB per workgroup; registers, not LDS, hold the
+  // kernel at 4 workgroups per CU: forcing 5 spilled to scratch and measured
+  // slower, profiles/r02v_k1b_variants.txt)
+  uint2 rec[4][SMAX_XQ / 2];        // {LCP value, width}
+  uint16_t row[4][SMAX_XQ / 2];     // start row in the tile
   uint32_t cnt[4];
   uint32_t nff;                     // 255 bytes of the window (load_exact_window_wg)
   uint64_t off;                     // the tile's first record in the pool (~0: none)
@@ -1800,7 +1817,9 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
   SmaxWindowX *W = &sD.win;
   Win t;
   win_init(t, a);
-  if (a.k1b_head && blockIdx.x == gridDim.x - 1) {
+  // workgroup 0 computes the boundary head: dispatched first, so its window
+  // load overlaps the tiles' (as the last workgroup it waited for a free slot)
+  if (a.k1b_head && blockIdx.x == 0) {
     if (wave == 0) {
       const uint64_t l0 = a.tile_first * (uint64_t) SMAX_TILE;
       load_exact_window(a, l0, W);
@@ -1810,8 +1829,11 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
   }
   const uint32_t n = *a.defer_count;
   const uint64_t ltm = lanemask_lt();
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x - a.k1b_head) {
+  for (uint32_t i = blockIdx.x - a.k1b_head; i < n; i += gridDim.x - a.k1b_head) {
+    // the list entry and its llv_win words in one round (no dependent load
+    // of llv_win[tile] before the window's .llv loads)
     const uint64_t tile = a.defer_list[i];
+    const uint2 info = a.defer_info[i];
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
     const uint64_t g0 = a.base + l0;
     if (threadIdx.x == 0) sD.nff = 0;
@@ -1821,7 +1843,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     // ballots, |262144 after the evaluation
     const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
     uint64_t tmark = 0;
-    load_exact_window_wg(a, l0, W, &sD.nff);
+    load_exact_window_wg(a, l0, info, W, &sD.nff);
     if (a.dbg & 65536u) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
     t.L = W->L;
@@ -1849,7 +1871,8 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     }
     __syncthreads();
     if ((a.dbg & 131072u) && tmark == 0) tmark = __builtin_readcyclecounter();
-    // wave w: the starts of rows [512 w, 512 w + 512), evaluated into LDS
+    // wave w: the starts of rows [512 w, 512 w + 512), evaluated; accepted
+    // records compacted into LDS in row order
     const uint32_t q0 = (uint32_t) wave * SMAX_XQ;
     uint32_t ns = 0;
     for (uint32_t s2 = q0 / 64; s2 < (q0 + SMAX_XQ) / 64; s2++) {
@@ -1863,15 +1886,23 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
       const uint32_t k = i0 + (uint32_t) lane;
       bool acc = false;
+      uint32_t cur = 0, b = 0;
+      uint64_t j = 0;
       if (k < ns) {
-        uint32_t cur = 0;
-        uint64_t j = 0;
-        const uint32_t b = sD.list[wave][k];
+        b = sD.list[wave][k];
         acc = eval_start_x(a, t, W, g0, b, &cur, &j);
-        sD.cur[wave][k] = cur;
-        sD.wid[wave][k] = acc ? (uint32_t) (j - (g0 + b) + 2) : 0u;
       }
-      wc += (uint32_t) __popcll(__ballot(acc));
+      const uint64_t am = __ballot(acc);
+      const uint32_t w = wc + (uint32_t) __popcll(am & ltm);
+      if (acc && w < SMAX_XQ / 2) {
+        sD.rec[wave][w] = make_uint2(cur, (uint32_t) (j - (g0 + b) + 2));
+        sD.row[wave][w] = (uint16_t) b;
+      }
+      wc += (uint32_t) __popcll(am);
+    }
+    if (wc > SMAX_XQ / 2) {   // impossible in a consistent index (see SmaxDeferWG)
+      if (lane == 0) atomicOr(a.err, SMAX_ERR_LLV);
+      wc = SMAX_XQ / 2;
     }
     if (lane == 0) sD.cnt[wave] = wc;
     __syncthreads();
@@ -1904,19 +1935,13 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     const uint64_t off = sD.off;
     if (off != ~0ull) {
       GtSmaxRecord *wdst = a.pool + off + base;
-      uint32_t w = 0;
-      for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
-        const uint32_t k = i0 + (uint32_t) lane;
-        const uint32_t wd = k < ns ? sD.wid[wave][k] : 0u;
-        const uint64_t am = __ballot(wd != 0);
-        if (wd != 0) {
-          GtSmaxRecord rec;
-          rec.lb = g0 + sD.list[wave][k] - 1;
-          rec.lcp = sD.cur[wave][k];
-          rec.width = wd;
-          wdst[w + (uint32_t) __popcll(am & ltm)] = rec;
-        }
-        w += (uint32_t) __popcll(am);
+      for (uint32_t k = (uint32_t) lane; k < wc; k += 64) {
+        const uint2 r = sD.rec[wave][k];
+        GtSmaxRecord rec;
+        rec.lb = g0 + sD.row[wave][k] - 1;
+        rec.lcp = r.x;
+        rec.width = r.y;
+        wdst[k] = rec;
       }
     }
     __syncthreads();   // window and lists reused by the next tile
@@ -2230,6 +2255,7 @@ struct GtSmaxPlan {
   bool pk, pk_owned;          // packed windows; bwtpk allocated by the plan
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
+  uint2 *defer_info;         // beside each entry: the tile's llv_win words
   uint32_t *defer_count;
   uint32_t *defer_last;      // combined placement: K1's last count (K3 resets the live one)
   uint32_t *static_list;     // plan-time K1b list (edges, wide .llv windows) + count
@@ -2418,6 +2444,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   // K1's runtime list; in the combined placement (mode 4) the static list is
   // copied to its front and K1 appends behind it
   HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (2 * (uint64_t) p->num_tiles + 1)));
+  HIPCHK(dalloc(&p->defer_info, sizeof (uint2) * (2 * (uint64_t) p->num_tiles + 1)));
   HIPCHK(dalloc(&p->defer_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
   HIPCHK(dalloc(&p->defer_last, sizeof (uint32_t)));
@@ -2492,9 +2519,13 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       // 4: one K1b launch after K1 over the static list followed by K1's
       // deferrals (no second stream, no fork/join events: those cost
       // ~25 us per step, measured on a 100 Mbp shard)
-      if (p->n_static)
+      if (p->n_static) {
         HIPCHK(hipMemcpy(p->defer_list, p->static_list, sizeof (uint32_t) * p->n_static,
                          hipMemcpyDeviceToDevice));
+        hipLaunchKernelGGL(smax_defer_info_kernel, dim3((p->n_static + 255) / 256), dim3(256), 0, 0,
+                           p->defer_list, p->n_static, p->llv_win, p->defer_info);
+        HIPCHK(hipGetLastError());
+      }
       p->comb_grid = std::max(p->defer_grid, p->static_grid - 1) + 1;   // static_grid has its +1
       const char *wg = getenv("GT_SMAX_K1B_WG");
       p->k1b_wg = wg ? strtol(wg, NULL, 0) != 0 : true;
@@ -2531,7 +2562,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
   void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last,
-                  p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list,
+                  p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
     (void) hipStreamSynchronize(p->side);
@@ -2580,6 +2611,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.block_sum = p->block_sum;
   a.bnd = p->bnd;
   a.defer_list = p->defer_list;
+  a.defer_info = p->defer_info;
   a.defer_count = p->defer_count;
   a.k1b_head = 0;
   a.k1_reset = 0;
@@ -2691,7 +2723,7 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
       HIPCHK(hipStreamWaitEvent(s, p->join, 0));
     }
     if (mode == 4) {
-      // static list + K1's deferrals in one launch; its last workgroup
+      // static list + K1's deferrals in one launch; one workgroup
       // computes the boundary head
       SmaxScanArgs c = a;
       c.k1b_head = 1;

@@ -3,7 +3,7 @@
 tables: the in-tree library (A) and a second copy (B, path in argv[4]),
 plans created by each, runs alternated in rounds so that clock and
 thermal drift hit both alike.  Prints per-round and median step times.
-Args: kind bases minlen libB [rounds]"""
+Args: kind bases minlen libB [rounds] [shard/of: plans over one shard's rows]"""
 import os
 import sys
 
@@ -13,6 +13,8 @@ import genometools_smax_amd as G  # noqa: E402
 
 kind, bases, minlen, libb = sys.argv[1], int(float(sys.argv[2])), int(sys.argv[3]), sys.argv[4]
 rounds = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+shard = sys.argv[6] if len(sys.argv) > 6 else "0/1"
+si, sw = (int(x) for x in shard.split("/"))
 LA = G.lib()
 pa_path = G.LIB_PATH
 G._lib, G.LIB_PATH = None, libb
@@ -22,9 +24,12 @@ G._lib, G.LIB_PATH = LA, pa_path
 text = G.synth_genome(kind, bases, {"uniform": 42, "human": 1, "plant": 2}[kind])
 esa = G.DeviceEsa(text) if len(text) + 1 < 2 ** 32 else G.DeviceEsa64(text)
 del text
-plan_a = esa.plan(minlen)
+N = esa.nonspecials
+begin, end = 1 + (N - 1) * si // sw, 1 + (N - 1) * (si + 1) // sw
+print("rows [%d, %d) (shard %d/%d)" % (begin, end, si, sw), flush=True)
+plan_a = esa.plan(minlen, begin, end)
 G._lib = LB
-plan_b = esa.plan(minlen)
+plan_b = esa.plan(minlen, begin, end)
 G._lib = LA
 s = torch.cuda.current_stream()
 sp = s.cuda_stream
@@ -33,13 +38,21 @@ sp = s.cuda_stream
 def timed(L, p, n=30):
     for _ in range(3):
         L.gt_smax_plan_run(p.plan, sp)
+    L.gt_smax_plan_timing(p.plan, n)           # K1 events of the timed runs
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(n):
         L.gt_smax_plan_run(p.plan, sp)
     e1.record(s)
     torch.cuda.synchronize()
+    import ctypes
+    ms, k = ctypes.c_double(), ctypes.c_int()
+    L.gt_smax_plan_timing_read(p.plan, ctypes.byref(ms), ctypes.byref(k))
+    k1.setdefault(id(L), []).append(ms.value / max(k.value, 1))
     return e0.elapsed_time(e1) / n
+
+
+k1 = {}
 
 
 ta, tb = [], []
@@ -57,6 +70,10 @@ ta.sort()
 tb.sort()
 print("median step: A %.4f ms, B %.4f ms, B/A %.4f" % (ta[len(ta) // 2], tb[len(tb) // 2],
                                                         tb[len(tb) // 2] / ta[len(ta) // 2]))
+ka, kb = sorted(k1[id(LA)]), sorted(k1[id(LB)])
+print("median K1: A %.4f ms, B %.4f ms; rest of the step: A %.4f ms, B %.4f ms"
+      % (ka[len(ka) // 2], kb[len(kb) // 2], ta[len(ta) // 2] - ka[len(ka) // 2],
+         tb[len(tb) // 2] - kb[len(kb) // 2]))
 G._lib = LB
 plan_b.close()
 G._lib = LA
