@@ -1731,7 +1731,7 @@ smax_defer_kernel(SmaxScanArgs a) {
 // lane and up to 4 dependent .llv rounds.  *nff is a workgroup counter the
 // caller zeroes.
 __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, uint2 info,
-                                            SmaxWindowX *W, uint32_t *nff) {
+                                            SmaxWindowX *W, uint32_t *nff, uint64_t *tmark) {
   const int tid = threadIdx.x;
   const uint64_t g0 = a.base + l0;
   const uint32_t lo = info.x, n = SMAX_WIN_N(info.y);
@@ -1746,16 +1746,20 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
     ep[r] = e < n ? make_uint2(rec[0], rec[1]) : make_uint2(0xffffffffu, 0xffffffffu);
     ev[r] = e < n ? rec[2] : 0u;
   }
+  uint32_t f = 0;
   if (tid < SMAX_NCHUNK) {
     const int i = tid;
     const int64_t r0 = (int64_t) l0 - SMAX_LH + 16 * i;
     const uint4 lv = *reinterpret_cast<const uint4 *>(a.lcp + r0);
     const uint4 bv = a.bwtpk != nullptr ? pk_expand(a.bwtpk[l0 / 16 + i])
                                         : *reinterpret_cast<const uint4 *>(a.bwt + r0);
+    if (a.dbg & 524288u) {   // diagnostic stamp: every load of the thread has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (*tmark == 0) *tmark = __builtin_readcyclecounter();
+    }
     *reinterpret_cast<uint4 *>(&W->L[16 * i]) = lv;
     *reinterpret_cast<uint4 *>(&W->B[16 * i]) = bv;
-    const uint32_t f = seg_ffcount(lv);
-    if (f) atomicAdd(nff, f);
+    f = seg_ffcount(lv);
     const int64_t gr = (int64_t) wb + 16 * i;
     const uint32_t w[4] = {lv.x, lv.y, lv.z, lv.w};
     const bool inner = gr >= 1 && gr + 16 <= (int64_t) a.N;
@@ -1772,7 +1776,12 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
       *reinterpret_cast<uint4 *>(&W->X[16 * i + 4 * k]) = x;
     }
   }
+  // the window's 255 bytes: one LDS atomic per wave (not per chunk)
+  uint32_t ftot;
+  (void) wave_excl(f, &ftot);
+  if ((threadIdx.x & 63) == 0 && ftot) atomicAdd(nff, ftot);
   __syncthreads();
+  if ((a.dbg & 1048576u) && *tmark == 0) *tmark = __builtin_readcyclecounter();
 #pragma unroll
   for (int r = 0; r < EPT; r++) {
     const uint32_t e = (uint32_t) tid + 256u * r;
@@ -1840,10 +1849,11 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     __syncthreads();
     // diagnostic (GT_SMAX_DEBUG 32768): the tile's cycles / 16 instead of its
     // count; |65536 stops the clock after the window load, |131072 after the
-    // ballots, |262144 after the evaluation
+    // ballots, |262144 after the evaluation; inside the load: |524288 when the
+    // loads of thread 0 have landed, |1048576 after the LDS writes
     const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
     uint64_t tmark = 0;
-    load_exact_window_wg(a, l0, info, W, &sD.nff);
+    load_exact_window_wg(a, l0, info, W, &sD.nff, &tmark);
     if (a.dbg & 65536u) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
     t.L = W->L;

@@ -25,7 +25,8 @@ N = esa.nonspecials
 begin, end = 1 + (N - 1) * si // sw, 1 + (N - 1) * (si + 1) // sw
 print("shard %d/%d rows [%d, %d)" % (si, sw, begin, end), flush=True)
 for label, dbg in (("whole tile", 32768), ("window load", 32768 | 65536),
-                   ("load+ballots", 32768 | 131072), ("+evaluation", 32768 | 262144)):
+                   ("load+ballots", 32768 | 131072), ("+evaluation", 32768 | 262144),
+                   ("loads landed", 32768 | 524288), ("+LDS writes", 32768 | 1048576)):
     os.environ["GT_SMAX_DEBUG"] = str(dbg | extra)
     p = esa.plan(minlen, begin, end)
     p.run()
