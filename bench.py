@@ -18,7 +18,7 @@ by range (strong scaling): value = nonspecials / max-over-ranks step time.
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 "roofline" for K1 (algorithmic bytes = 2 B per suffix row + 16 B per .llv
 entry + 16 B per emitted record, SURVEY.md §8(d), over the average K1 duration from HIP events recorded
-on K1's stream during the timed region) and, at N = 1, "cpu_baseline": the
+on K1's stream around every 4th K1 launch of the timed region) and, at N = 1, "cpu_baseline": the
 oracle's single-core linear scan (oracle/smax_oracle.c orc_linsmax, the
 repo's CPU esa_linsmax restatement) timed on this host over the same tables.
 """
@@ -212,7 +212,11 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    plan.enable_timing(args.steps)
+    # K1's duration by HIP events around every 4th launch of the timed
+    # region: each timed launch pays two event records (measured ~1 % of a
+    # C3 step, ~3 % of an 8-way shard's, profiles/r02z_event_overhead.txt)
+    ev_stride = 4
+    plan.enable_timing((args.steps + ev_stride - 1) // ev_stride, ev_stride)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -407,6 +411,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "smax_scan_kernel", "kernel_avg_ms": k1_avg_ms,
+                         "kernel_timed_launches": "%d of %d (HIP events on every %dth)"
+                                                  % (k1_n, args.steps, ev_stride),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          # the same kernel priced by the HBM bytes it really moves
                          # (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH §HBM)

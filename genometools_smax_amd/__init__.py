@@ -180,6 +180,7 @@ def lib():
         L.gt_smax_plan_fetch_count.argtypes = [vp, ctypes.POINTER(u64)]
         L.gt_smax_plan_fetch_triples.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
         L.gt_smax_plan_timing.argtypes = [vp, ci]
+        L.gt_smax_plan_timing_stride.argtypes = [vp, ci]
         L.gt_smax_plan_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ci)]
         L.gt_smax_plan_copy_boundary.argtypes = [vp, vp, vp]
         L.gt_smax_plan_error_bits.argtypes = [vp]
@@ -729,10 +730,13 @@ class SmaxPlan:
     def num_tiles(self):
         return lib().gt_smax_plan_num_tiles(self.plan)
 
-    def enable_timing(self, nslots):
-        """Record hipEvents around the scan kernel of the next runs."""
+    def enable_timing(self, nslots, stride=1):
+        """Record hipEvents around the scan kernel of every stride-th of the
+        next runs (nslots of them)."""
         if lib().gt_smax_plan_timing(self.plan, int(nslots)) != 0:
             raise SmaxError("gt_smax_plan_timing failed")
+        if lib().gt_smax_plan_timing_stride(self.plan, int(stride)) != 0:
+            raise SmaxError("gt_smax_plan_timing_stride failed")
 
     def kernel_ms(self):
         """(sum of scan-kernel milliseconds, launches timed)."""

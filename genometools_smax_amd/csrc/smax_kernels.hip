@@ -2283,6 +2283,7 @@ struct GtSmaxPlan {
   // optional K1 timing: event pairs recorded around the scan kernel
   hipEvent_t *ev;
   int nslots;
+  int tstride;               // K1 events on every tstride-th run (gt_smax_plan_timing_stride)
   uint64_t runs;
 };
 
@@ -2699,7 +2700,9 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
       hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, p->side, b);
       HIPCHK(hipGetLastError());
     }
-    const int slot = p->nslots ? (int) (p->runs % (uint64_t) p->nslots) : -1;
+    const uint64_t ts = p->tstride > 1 ? (uint64_t) p->tstride : 1u;
+    const int slot = p->nslots && p->runs % ts == 0 ? (int) ((p->runs / ts) % (uint64_t) p->nslots)
+                                                    : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
     {
       // diagnostic: extra dynamic LDS lowers residency (occupancy sensitivity)
@@ -2806,6 +2809,13 @@ extern "C" int gt_smax_stitch_host(const GtSmaxBoundary *all, int nshards,
   return stitch_resolve(all, nshards, shard_index, minlen, rec);
 }
 
+extern "C" int gt_smax_plan_timing_stride(GtSmaxPlan *p, int stride) {
+  if (stride < 1) return -1;
+  p->tstride = stride;
+  p->runs = 0;
+  return 0;
+}
+
 extern "C" int gt_smax_plan_timing(GtSmaxPlan *p, int nslots) {
   char *errbuf = NULL;
   size_t errlen = 0;
@@ -2829,7 +2839,9 @@ extern "C" int gt_smax_plan_timing_read(GtSmaxPlan *p, double *sum_ms, int *nrea
   char *errbuf = NULL;
   size_t errlen = 0;
   double acc = 0.0;
-  const int n = (int) (p->runs < (uint64_t) p->nslots ? p->runs : (uint64_t) p->nslots);
+  const uint64_t ts = p->tstride > 1 ? (uint64_t) p->tstride : 1u;
+  const uint64_t timed = (p->runs + ts - 1) / ts;
+  const int n = (int) (timed < (uint64_t) p->nslots ? timed : (uint64_t) p->nslots);
   HIPCHK(hipSetDevice(p->shard.device));
   for (int i = 0; i < n; i++) {
     float ms = 0.0f;

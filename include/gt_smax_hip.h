@@ -228,6 +228,10 @@ int gt_smax_stitch_host(const GtSmaxBoundary *all, int nshards,
  * filled so far (synchronising on them). */
 int gt_smax_plan_timing(GtSmaxPlan *plan, int nslots);
 int gt_smax_plan_timing_read(GtSmaxPlan *plan, double *sum_ms, int *nread);
+/* Events on every stride-th run only (default 1; resets the run count): each
+ * timed run pays the two event records (~1 % of a C3 step, ~3 % of an
+ * 8-way shard's). */
+int gt_smax_plan_timing_stride(GtSmaxPlan *plan, int stride);
 
 /* Copies this shard's boundary record to dst_dev (device memory) on stream,
  * e.g. into the send buffer of an all-gather. */

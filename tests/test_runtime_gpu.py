@@ -123,3 +123,18 @@ def test_repeated_calls_and_cache_release(human10):
     G.release_cache()
     assert np.array_equal(G.enumerate_smax(*args, 2), want)
     G.release_cache()
+
+
+def test_timing_stride(human10):
+    """gt_smax_plan_timing_stride: K1 events around every stride-th run only;
+    the read covers exactly those runs."""
+    esa, _ = human10
+    p = esa.plan(20)
+    for stride, runs, want in ((1, 5, 5), (4, 10, 3), (4, 12, 3), (3, 1, 1)):
+        p.enable_timing(16, stride)
+        for _ in range(runs):
+            p.run()
+        ms, n = p.kernel_ms()
+        assert n == want, (stride, runs, n)
+        assert ms > 0.0
+    p.close()
