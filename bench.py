@@ -186,21 +186,35 @@ def main():
         # records, then the stitch kernel resolves spanning plateaus.  The
         # boundary record is final after the scan (part 0), so the all-gather
         # runs on RCCL's stream beside the compaction (part 1); the stitch
-        # waits for both
+        # waits for both.  The send buffer is the plan's own boundary record
+        # (zero-copy tensor), so no copy launch sits between scan and collective
         plan.run_part(0, sptr)
-        plan.copy_boundary(send.data_ptr(), sptr)
+        src = bsend[0]
+        if src is None:
+            plan.copy_boundary(send.data_ptr(), sptr)
+            src = send
         if staged:
-            hsend.copy_(send)
+            hsend.copy_(src)
             work = dist.all_gather_into_tensor(hrecv, hsend, async_op=True)
             plan.run_part(1, sptr)
             work.wait()
             recv.copy_(hrecv)
         else:
-            work = dist.all_gather_into_tensor(recv, send, async_op=True)
+            work = dist.all_gather_into_tensor(recv, src, async_op=True)
             plan.run_part(1, sptr)
             work.wait()
         plan.stitch(recv.data_ptr(), world, rank, sptr)
 
+    def boundary_send():
+        # the plan's boundary record as the all-gather's send tensor; None:
+        # this torch cannot wrap device memory (then copy_boundary each step)
+        try:
+            return plan.boundary_tensor()
+        except Exception as e:  # noqa: BLE001
+            log("rank %d: zero-copy boundary send unavailable (%s); copying per step" % (rank, e))
+            return None
+
+    bsend = [boundary_send() if world > 1 else None]
     # first pass sizes the output exactly (re-plan on overflow)
     step()
     torch.cuda.synchronize()
@@ -209,6 +223,7 @@ def main():
         log("rank %d: %d intervals > capacity %d, re-planning" % (rank, cnt, plan.capacity))
         plan.close()
         plan = esa.plan(minlen, begin, end, capacity=cnt + 16, packed=not args.byte_bwt)
+        bsend[0] = boundary_send() if world > 1 else None
 
     for _ in range(args.warmup):
         step()

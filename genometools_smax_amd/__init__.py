@@ -746,6 +746,22 @@ class SmaxPlan:
             raise SmaxError("gt_smax_plan_timing_read failed")
         return ms.value, n.value
 
+    def boundary_tensor(self):
+        """The plan's device boundary record (GtSmaxBoundary, BOUNDARY_BYTES)
+        as a zero-copy torch uint8 tensor: final after run_part(0), so it can
+        be a collective's send buffer directly (no copy_boundary launch)."""
+        import torch
+
+        class _Dev:
+            pass
+        d = _Dev()
+        d.__cuda_array_interface__ = {"shape": (BOUNDARY_BYTES,), "typestr": "|u1",
+                                      "data": (int(self.boundary_ptr), False), "version": 3}
+        t = torch.as_tensor(d, device="cuda")
+        if t.data_ptr() != int(self.boundary_ptr):
+            raise SmaxError("boundary_tensor: torch copied the boundary record")
+        return t
+
     def copy_boundary(self, dst_ptr, stream=0):
         if lib().gt_smax_plan_copy_boundary(self.plan, dst_ptr, stream or None) != 0:
             raise SmaxError("gt_smax_plan_copy_boundary failed")

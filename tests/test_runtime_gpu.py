@@ -74,9 +74,13 @@ def test_run_in_two_parts(human10):
         ref_trip, ref_bnd = ref.fetch_triples(), bnd(ref)
         if (begin, end) == (1, N):
             assert np.array_equal(ref_trip, want)
+        bt = p.boundary_tensor()           # zero-copy view (bench.py's send buffer)
+        assert bt.data_ptr() == p.boundary_ptr and bt.numel() == G.BOUNDARY_BYTES
         for _ in range(3):
             p.run_part(0)
             assert np.array_equal(bnd(p), ref_bnd)
+            torch.cuda.synchronize()
+            assert np.array_equal(bt.cpu().numpy(), ref_bnd)
             p.run_part(1)
             assert np.array_equal(p.fetch_triples(), ref_trip)
         with pytest.raises(G.SmaxError):
