@@ -519,6 +519,13 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
 // wl: LDS address of the target window (uniform, precomputed per buffer --
 // generic-to-LDS pointer casts carry null checks that cost scalar work per
 // tile); ibase: the llv_win entry to stage at iaddr.
+// NT: the window stream (LCP bytes, packed BWT: read once per pass) as
+// non-temporal LDS-DMA loads.  Measured (profiles/r02zz_nt_policy.txt): on
+// shards whose stream exceeds the 256 MB MALL but whose per-tile state stays
+// small (the 4- and 8-way C3 splits) the step is 2-6 % shorter; on the whole
+// C3 table 6 % longer, on a table the MALL holds (C2) 4 % longer -- so the
+// plan picks it by shard size (GtSmaxPlan::nt).
+template <bool NT>
 __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
                                                 uint32_t lo, uint32_t n, const void *ibase,
                                                 uint32_t iaddr, uint32_t v16, uint32_t v4) {
@@ -534,34 +541,65 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   const uint8_t *ib = reinterpret_cast<const uint8_t *>(ibase);
   uint32_t keep;
   uint64_t ex;
+  if constexpr (NT) {
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %4\n\t"
-      "s_mov_b64 %1, exec\n\t"
-      "global_load_lds_dwordx4 %2, %8 offset:0\n\t"
-      "global_load_lds_dwordx4 %2, %8 offset:1024\n\t"
-      "s_mov_b32 m0, %5\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
-      "s_mov_b64 exec, 3\n\t"
-      "global_load_lds_dwordx4 %2, %9 offset:1024\n\t"
-      "s_mov_b32 m0, %4\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, %8 offset:2048\n\t"
-      "s_mov_b64 exec, %11\n\t"
-      "s_mov_b32 m0, %6\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
-      "s_mov_b64 exec, %13\n\t"
-      "s_mov_b32 m0, %7\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dword %3, %12 offset:0\n\t"
-      "s_mov_b64 exec, %1\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep), "=&s"(ex)
-      : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-        "s"(vmask), "s"(ib), "s"(imask)
-      : "memory");
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:0 nt\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:1024 nt\n\t"
+        "s_mov_b32 m0, %5\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:0 nt\n\t"
+        "s_mov_b64 exec, 3\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:1024 nt\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:2048 nt\n\t"
+        "s_mov_b64 exec, %11\n\t"
+        "s_mov_b32 m0, %6\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
+        "s_mov_b64 exec, %13\n\t"
+        "s_mov_b32 m0, %7\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, %12 offset:0\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(ex)
+        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask)
+        : "memory");
+  } else {
+  asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:1024\n\t"
+        "s_mov_b32 m0, %5\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
+        "s_mov_b64 exec, 3\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:1024\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:2048\n\t"
+        "s_mov_b64 exec, %11\n\t"
+        "s_mov_b32 m0, %6\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
+        "s_mov_b64 exec, %13\n\t"
+        "s_mov_b32 m0, %7\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, %12 offset:0\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(ex)
+        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask)
+        : "memory");
+  }
 }
 
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
@@ -1162,11 +1200,13 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
 }
 
 // next tile's window + the llv_win entry of the tile after it (ring slot iaddr)
+template <bool NT>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
                                            uint32_t iaddr, uint32_t v16, uint32_t v4) {
-  issue_window_pk(a, l0, wl, lo, n, info, iaddr, v16, v4);
+  issue_window_pk<NT>(a, l0, wl, lo, n, info, iaddr, v16, v4);
 }
+template <bool NT>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
                                            uint32_t iaddr, uint32_t v16, uint32_t v4) {
@@ -1246,7 +1286,7 @@ __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t 
 // here; shard-edge tiles and tiles with more exact starts than the direct
 // path queues are deferred to K1b (their generic path is kept out of K1,
 // whose register budget it would otherwise set).
-template <typename WinT, bool DIAG, bool FFPV = false>
+template <typename WinT, bool DIAG, bool FFPV = false, bool NT = false>
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // the production kernel sees dbg == 0 as a constant: every diagnostic
   // branch (GT_SMAX_DEBUG) folds away, a scalar test and branch each
@@ -1341,7 +1381,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // tile's work
     if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
       const uint32_t n2 = next + stride <= last ? next + stride : last;
-      issue_next(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
+      issue_next<NT>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
@@ -1972,6 +2012,13 @@ __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel(SmaxScanArgs
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_dense(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true>(a);
 }
+// non-temporal window stream (GtSmaxPlan::nt)
+__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_nt(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, false, true>(a);
+}
+__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, true, true>(a);
+}
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, true>(a);
 }
@@ -2275,6 +2322,7 @@ struct GtSmaxPlan {
   int k1b_mode;              // placement of the static K1b (GT_SMAX_K1B_MODE)
   uint32_t comb_grid;        // mode 4: grid of the combined K1b launch (+1: head)
   bool dense;                // .llv entries per row above SMAX_FFPV_DENSITY: smax_scan_kernel_dense
+  bool nt;                   // window stream with the non-temporal policy (smax_scan_kernel*_nt)
   bool k1b_wg;               // mode 4: one workgroup per K1b tile (GT_SMAX_K1B_WG=0: one wave)
   uint32_t comb_grid_wg;     // its grid (+1: head)
   hipEvent_t fork, join;
@@ -2524,6 +2572,17 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       p->dense = dv ? strtol(dv, NULL, 0) != 0
                     : rows > 0 && (double) inrange > SMAX_FFPV_DENSITY * (double) rows;
     }
+    {
+      // non-temporal window stream where it measured faster: the shard's
+      // stream (1.5 B per row) larger than the 256 MB MALL -- a smaller one
+      // is served from it on repeated passes, which nt gives up -- and at
+      // most 2^19 tiles (the 4- and 8-way C3 splits; the whole 3 Gbp table
+      // measured slower).  GT_SMAX_NT=0/1 overrides.
+      const char *ntv = getenv("GT_SMAX_NT");
+      const uint64_t stream_bytes = (uint64_t) p->num_tiles * SMAX_TILE * 3 / 2;
+      p->nt = ntv ? strtol(ntv, NULL, 0) != 0
+                  : stream_bytes > (256ull << 20) && p->num_tiles <= (1u << 19);
+    }
     const char *m = getenv("GT_SMAX_K1B_MODE");
     p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 4;
     if (p->k1b_mode == 4) {
@@ -2713,9 +2772,11 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
       else if (p->pk && p->dbg)
         hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
       else if (p->pk && p->dense)
-        hipLaunchKernelGGL(smax_scan_kernel_dense, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_dense_nt : smax_scan_kernel_dense, dim3(p->grid),
+                           dim3(SMAX_THREADS), lp, s, a);
       else if (p->pk)
-        hipLaunchKernelGGL(smax_scan_kernel, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_nt : smax_scan_kernel, dim3(p->grid),
+                           dim3(SMAX_THREADS), lp, s, a);
       else
         hipLaunchKernelGGL(smax_scan_kernel_bytes, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
     }

@@ -142,3 +142,33 @@ def test_timing_stride(human10):
         assert n == want, (stride, runs, n)
         assert ms > 0.0
     p.close()
+
+
+@pytest.mark.parametrize("nt", ["0", "1"])
+@pytest.mark.parametrize("dense", ["0", "1"])
+def test_window_stream_policy(human10, nt, dense):
+    """Both window-stream policies of K1 (GT_SMAX_NT; the plan picks nt by
+    shard size) and both K1 variants give the oracle's records, whole table
+    and a middle shard's plan run (against the plain-policy plan)."""
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    old = {k: os.environ.get(k) for k in ("GT_SMAX_NT", "GT_SMAX_DENSE")}
+    os.environ.update(GT_SMAX_NT=nt, GT_SMAX_DENSE=dense)
+    try:
+        p = esa.plan(20)
+        q = esa.plan(20, N // 3, 2 * N // 3)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    p.run()
+    assert np.array_equal(p.fetch_triples(), want)
+    r = esa.plan(20, N // 3, 2 * N // 3)
+    q.run()
+    r.run()
+    assert np.array_equal(q.fetch_triples(), r.fetch_triples())
+    for x in (p, q, r):
+        x.close()
