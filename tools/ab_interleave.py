@@ -27,7 +27,16 @@ del text
 N = esa.nonspecials
 begin, end = 1 + (N - 1) * si // sw, 1 + (N - 1) * (si + 1) // sw
 print("rows [%d, %d) (shard %d/%d)" % (begin, end, si, sw), flush=True)
+# AB_ENV_A="K=V,...": environment for creating plan A only (plan-time switches)
+env_a = dict(kv.split("=", 1) for kv in os.environ.get("AB_ENV_A", "").split(",") if kv)
+old_env = {k: os.environ.get(k) for k in env_a}
+os.environ.update(env_a)
 plan_a = esa.plan(minlen, begin, end)
+for k, v in old_env.items():
+    if v is None:
+        os.environ.pop(k, None)
+    else:
+        os.environ[k] = v
 G._lib = LB
 plan_b = esa.plan(minlen, begin, end)
 G._lib = LA
