@@ -1783,15 +1783,20 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
   for (int r = 0; r < EPT; r++) {
     const uint32_t e = (uint32_t) tid + 256u * r;
     const uint32_t *rec = reinterpret_cast<const uint32_t *>(&a.llv[lo + (e < n ? e : 0)]);
-    ep[r] = e < n ? make_uint2(rec[0], rec[1]) : make_uint2(0xffffffffu, 0xffffffffu);
-    ev[r] = e < n ? rec[2] : 0u;
+    const uint32_t r0 = __builtin_nontemporal_load(rec), r1 = __builtin_nontemporal_load(rec + 1);
+    const uint32_t r2 = __builtin_nontemporal_load(rec + 2);
+    ep[r] = e < n ? make_uint2(r0, r1) : make_uint2(0xffffffffu, 0xffffffffu);
+    ev[r] = e < n ? r2 : 0u;
   }
   uint32_t f = 0;
   if (tid < SMAX_NCHUNK) {
     const int i = tid;
     const int64_t r0 = (int64_t) l0 - SMAX_LH + 16 * i;
-    const uint4 lv = *reinterpret_cast<const uint4 *>(a.lcp + r0);
-    const uint4 bv = a.bwtpk != nullptr ? pk_expand(a.bwtpk[l0 / 16 + i])
+    // the window is read once (K1 skipped it): non-temporal loads
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 lq = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.lcp + r0));
+    const uint4 lv = make_uint4(lq.x, lq.y, lq.z, lq.w);
+    const uint4 bv = a.bwtpk != nullptr ? pk_expand(__builtin_nontemporal_load(&a.bwtpk[l0 / 16 + i]))
                                         : *reinterpret_cast<const uint4 *>(a.bwt + r0);
     if (a.dbg & 524288u) {   // diagnostic stamp: every load of the thread has landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
