@@ -65,6 +65,16 @@ def host_cpu():
             "affinity_cpus": len(os.sched_getaffinity(0))}
 
 
+def cgroup_cpus():
+    """CPUs the container's cgroup quota allows (cpu.max), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
@@ -81,7 +91,10 @@ def main():
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the host-tables (PCIe-inclusive) leg")
     ap.add_argument("--cpu-sample", type=int, default=4_300_000_000,
-                    help="max suffix rows timed on the CPU")
+                    help="max suffix rows timed on the CPU (single-core linear scan)")
+    ap.add_argument("--cpu-sample-bottomup", type=int, default=1_000_000_000,
+                    help="max suffix rows of the single-core reference-algorithm anchor "
+                         "(the bottom-up stack walk, about 20 s per 10^9 rows)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads for the all-core CPU figure (the GPU box's CPU share is 16)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -282,14 +295,28 @@ def main():
     value = N / (elapsed / args.steps)
     achieved = alg_bytes / (k1_avg_ms * 1e-3) / 1e9
 
+    # HBM traffic of K1 from the committed PMC profile of this config, used
+    # only when that profile was taken on this very build of the scan kernels
+    # (gt_smax_build_id stamped by tools/rocpd_summary.py) and config
     traffic = None
     pmc_src = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
-    if os.path.exists(pmc_path) and not args.bases:
+    if os.path.exists(pmc_path) and not args.bases and not args.minlen:
         with open(pmc_path) as fh:
             pmc = json.load(fh)
-        traffic = pmc.get("hbm_bytes_per_launch")
-        pmc_src = os.path.relpath(pmc_path, ROOT)
+        bid = G.build_id()
+        if pmc.get("build_id") == bid and pmc.get("config") == args.config:
+            traffic = pmc.get("hbm_bytes_per_launch")
+            pmc_src = "%s (build %s)" % (os.path.relpath(pmc_path, ROOT), bid)
+        else:
+            pmc_src = ("%s not used: taken on build %s / config %s, this run is build %s"
+                       % (os.path.relpath(pmc_path, ROOT), pmc.get("build_id"), pmc.get("config"),
+                          bid))
+    # a per-pass stream (1.5 B/row packed + .llv) that fits the 256 MiB
+    # Infinity Cache is re-read from it on every pass, not from HBM
+    # (MI355X_MICROARCH.md "Infinity Cache"): no HBM fraction is quoted then
+    stream_bytes = rows * 3 // 2 + 16 * llv_here
+    in_mall = world == 1 and stream_bytes < (256 << 20)
 
     # N > 1 parity: every rank's stitched records gathered to rank 0 (padded
     # all-gather over the same backend as the boundary exchange), compared
@@ -312,31 +339,36 @@ def main():
         dist.all_gather_into_tensor(gathered, buf)
         del buf, mine
         if rank == 0:
-            g = gathered.cpu().numpy()
-            got = np.concatenate([g[r * kmax: r * kmax + int(cnts[r])] for r in range(world)])
-            got = got.view(np.uint64).reshape(-1, 3)
-            del g
-            import oracle_lib  # noqa: E402  (tests/: the checker only)
-            t0 = time.time()
-            text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
-            if n + 1 >= 2 ** 32 or args.esa64:
-                full = G.DeviceEsa64(text, device=local, row_lo=0, row_hi=n + 1)
-            else:
-                full = G.DeviceEsa(text, device=local, keep_suftab=False)
-            del text
-            ht = full.download()
-            full.release()
-            threads = max(1, min(len(os.sched_getaffinity(0)), args.cpu_threads))
-            want = oracle_lib.linsmax(ht["lcptab"], ht["llvtab"], ht["bwttab"], N, minlen,
-                                      threads=threads)
-            del ht
-            dist_parity = bool(np.array_equal(got, want))
-            log("parity (%d ranks): %d gathered records %s the whole-table oracle's %d (%.1fs)"
-                % (world, len(got), "equal" if dist_parity else "DIFFER from", len(want),
-                   time.time() - t0))
-            if not dist_parity:
+            try:
+                g = gathered.cpu().numpy()
+                got = np.concatenate([g[r * kmax: r * kmax + int(cnts[r])] for r in range(world)])
+                got = got.view(np.uint64).reshape(-1, 3)
+                del g
+                import oracle_lib  # noqa: E402  (tests/: the checker only)
+                t0 = time.time()
+                text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
+                if n + 1 >= 2 ** 32 or args.esa64:
+                    full = G.DeviceEsa64(text, device=local, row_lo=0, row_hi=n + 1)
+                else:
+                    full = G.DeviceEsa(text, device=local, keep_suftab=False)
+                del text
+                ht = full.download()
+                full.release()
+                threads = max(1, min(len(os.sched_getaffinity(0)), args.cpu_threads))
+                want = oracle_lib.linsmax(ht["lcptab"], ht["llvtab"], ht["bwttab"], N, minlen,
+                                          threads=threads)
+                del ht
+                dist_parity = bool(np.array_equal(got, want))
+                log("parity (%d ranks): %d gathered records %s the whole-table oracle's %d (%.1fs)"
+                    % (world, len(got), "equal" if dist_parity else "DIFFER from", len(want),
+                       time.time() - t0))
+                if not dist_parity:
+                    parity_ok = False
+                del got, want
+            except Exception as ex:  # noqa: BLE001  (e.g. host memory for the whole table)
+                log("rank 0: whole-table parity check could not run: %r" % (ex,))
+                dist_parity = False
                 parity_ok = False
-            del got, want
         del gathered
 
     cpu = None
@@ -346,7 +378,8 @@ def main():
         # parity: the all-core oracle scan (orc_linsmax_mt, row ranges per
         # pthread, output identical to orc_linsmax) over ALL rows against the
         # timed path's records, bit for bit
-        threads = max(1, min(len(os.sched_getaffinity(0)), args.cpu_threads))
+        aff = len(os.sched_getaffinity(0))
+        threads = max(1, min(aff, args.cpu_threads))
         log("parity: oracle linsmax over all %d rows (%d threads)" % (N, threads))
         t0 = time.perf_counter()
         res = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen,
@@ -373,9 +406,42 @@ def main():
                "sample": "oracle orc_linsmax (single core, -O3) over suffix rows [0,%d) of the same "
                          "tables: %.2fs" % (sample, t_cpu)}
         cpu.update(host_cpu())
-        if threads > 1:
-            cpu["all_cores"] = {"value": N / t_mt, "cores": threads, "seconds": round(t_mt, 3),
-                                "sample": "orc_linsmax_mt (pthreads, equal row ranges) over all rows"}
+        # the reference's own algorithm, single core: the bottom-up stack walk
+        # of src/match/esa-bottomup.c:116-273 with a smax visitor, reading the
+        # tables as the sequential reader hands them out (orc_bottomup_smax_
+        # tables) -- the traversal the GPU path replaces -- on a bounded
+        # prefix of the rows
+        sb = min(N, args.cpu_sample_bottomup)
+        log("cpu anchor: bottom-up stack walk over %d rows (1 core)" % sb)
+        t0 = time.perf_counter()
+        rb = oracle_lib.bottomup_smax_tables(host["lcptab"], host["llvtab"], host["bwttab"], sb,
+                                             minlen, cap=max(16, len(res) + 16))
+        t_bu = time.perf_counter() - t0
+        if sb == N and not np.array_equal(rb, res):
+            log("FAIL: bottom-up CPU walk (%d intervals) != linear scan (%d)" % (len(rb), len(res)))
+            parity_ok = False
+        del rb
+        cpu["reference_algorithm_1core"] = {
+            "value": sb / t_bu, "cores": 1, "seconds": round(t_bu, 3),
+            "sample": "oracle orc_bottomup_smax_tables (the esa-bottomup.c:116-273 stack walk with "
+                      "a smax visitor, single core) over suffix rows [0,%d)" % sb}
+        cpu["all_cores"] = {"value": N / t_mt, "cores": threads, "seconds": round(t_mt, 3),
+                            "sample": "orc_linsmax_mt (pthreads, equal row ranges) over all rows"}
+        if aff > threads:
+            # every CPU of the affinity mask (the container's quota may be
+            # lower: cgroup_cpus); same output as the 16-thread scan
+            t0 = time.perf_counter()
+            ra = oracle_lib.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen,
+                                    threads=aff)
+            t_aff = time.perf_counter() - t0
+            if not np.array_equal(ra, res):
+                log("FAIL: %d-thread CPU scan differs" % aff)
+                parity_ok = False
+            del ra
+            cpu["all_affinity_cores"] = {
+                "value": N / t_aff, "cores": aff, "seconds": round(t_aff, 3),
+                "sample": "orc_linsmax_mt over all rows, one thread per CPU of the affinity mask"}
+        cpu["cgroup_cpus"] = cgroup_cpus()
 
     # end-to-end through the drop-in boundary (host tables in memory -> H2D
     # -> plan -> K1..K3 -> D2H of the (lcp, lb, rb) list): reported beside
@@ -397,10 +463,30 @@ def main():
                        "(.bwt packed to bit planes during the staged fill) -> plan (llv index) -> "
                        "K1..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
                "vs_cpu_baseline": (N / t_e2e) / cpu["value"] if cpu else None}
+        if cpu:
+            e2e["vs_cpu"] = {k: (N / t_e2e) / cpu[k]["value"] for k in
+                             ("reference_algorithm_1core", "all_cores", "all_affinity_cores")
+                             if k in cpu}
+            e2e["vs_cpu"]["linsmax_1core"] = e2e["vs_cpu_baseline"]
         del iv
 
-    if rank == 0 and not parity_ok:
-        log("parity failure: no bench line")
+    if dist:
+        # every rank learns rank 0's verdict, so all of them leave through the
+        # barrier and the teardown below instead of waiting in a collective
+        flag = torch.tensor([1 if parity_ok else 0], dtype=torch.int64,
+                            device="cpu" if staged else "cuda")
+        dist.broadcast(flag, 0)
+        parity_ok = bool(int(flag.item()))
+    if not parity_ok:
+        if rank == 0:
+            log("parity failure: no bench line")
+        if plan is not None:
+            plan.close()
+        if esa is not None:
+            esa.release()
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
         sys.exit(1)
     if rank == 0:
         out = {
@@ -423,8 +509,13 @@ def main():
                        if world > 1 else "single GPU"},
             "smax_intervals": count,
             "supermax_repeats_per_s": count / (elapsed / args.steps),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "roofline": {"bound": "mall" if in_mall else "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         # a stream resident in the Infinity Cache is not an
+                         # HBM utilisation: no fraction is quoted for it
+                         "frac": None if in_mall else achieved / HBM_PEAK_GBS,
+                         "stream_bytes_per_pass": stream_bytes,
+                         "traffic": traffic,
                          "kernel": "smax_scan_kernel", "kernel_avg_ms": k1_avg_ms,
                          "kernel_timed_launches": "%d of %d (HIP events on every %dth)"
                                                   % (k1_n, args.steps, ev_stride),
@@ -434,7 +525,7 @@ def main():
                          "achieved_by_traffic": (traffic / (k1_avg_ms * 1e-3) / 1e9
                                                  if traffic else None),
                          "frac_by_traffic": (traffic / (k1_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                                             if traffic else None),
+                                             if traffic and not in_mall else None),
                          "traffic_source": pmc_src},
             "parity": ("bit-exact vs CPU oracle (plan records%s)" % (" + end-to-end" if e2e else "")
                        if res is not None and sample_full else

@@ -157,6 +157,7 @@ def lib():
         L.gt_smax_encode_fasta.argtypes = [ctypes.c_char_p, u64, vp, ctypes.POINTER(u64),
                                            ctypes.POINTER(u64), cs, sz]
         L.gt_smax_device_count.restype = ci
+        L.gt_smax_build_id.restype = ctypes.c_char_p
         L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
         L.gt_smax_dev_free_table.argtypes = [ci, vp]
         L.gt_smax_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtSmaxDevShard), u32, u64,
@@ -854,6 +855,11 @@ def stitch_host(boundaries, shard_index, minlen):
 
 def device_count():
     return lib().gt_smax_device_count()
+
+
+def build_id():
+    """Hash of the scan kernels' sources and flags (gt_smax_build_id)."""
+    return lib().gt_smax_build_id().decode()
 
 
 # ------------------------------------------------------- ESA construction (F1)

@@ -2,8 +2,11 @@
 // FASTA -> GenomeTools' encoded DNA text, and a GPU-built ESA -> the
 // .suf/.lcp/.llv/.bwt/.prj files `gt suffixerator -dna -suf -lcp -bwt`
 // writes (src/match/sfx-run.c:174-300 tables, src/match/sfx-outprj.c:39-120
-// project file), so that the rest of the tool chain -- this repo's
-// bin/gt-repfind, or the reference's own readers -- runs on a GPU-built index.
+// project file, including `longest=`, the row of suffix 0, that esa-map.c:384-387
+// requires with SARR_SUFTAB).  No encoded-sequence files (.esq/.ssp/.des/.sds)
+// are written, so such an index is read by this repo's bin/gt-repfind (and
+// anything else that maps only .suf/.lcp/.llv/.bwt/.prj), not by the
+// reference's readers, which also ask for SARR_ESQTAB.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -111,7 +114,7 @@ extern "C" int gt_smax_esa64_write(const GtSmaxEsa64Dev *e, const uint8_t *text,
   std::vector<char> buf(64u << 20);
   std::string base(indexname);
   FILE *fp = NULL;
-  uint64_t sp[4], wc[4];
+  uint64_t sp[4], wc[4], longest = UINT64_MAX;
   if (errbuf && errlen) errbuf[0] = 0;
   if (e->row_lo != 0 || e->row_hi != m || e->totallength != n) {
     seterr(errbuf, errlen, "index files need the whole suffix array (rows [0, %lu))",
@@ -138,10 +141,10 @@ extern "C" int gt_smax_esa64_write(const GtSmaxEsa64Dev *e, const uint8_t *text,
   };
   // .suf: 8-byte suffixes (GtUword), or 4 with -suftabuint
   // (src/match/sfx-suffixgetset.c:467-481)
+  // longest: the row holding suffix 0 (gt_suffixsortspace_setdirect,
+  // src/match/sfx-suffixgetset.c:246-250), found while the rows stream out
   if (!open(".suf", "wb")) return -1;
-  if (suftab_bytes == 8) {
-    if (!dev_to_file(fp, e->suftab_dev, sizeof (uint64_t) * m, buf)) goto ioerr;
-  } else {
+  {
     std::vector<uint64_t> s(8u << 20);
     std::vector<uint32_t> s32(s.size());
     for (uint64_t off = 0; off < m; off += s.size()) {
@@ -149,8 +152,14 @@ extern "C" int gt_smax_esa64_write(const GtSmaxEsa64Dev *e, const uint8_t *text,
       if (hipMemcpy(s.data(), e->suftab_dev + off, sizeof (uint64_t) * k, hipMemcpyDeviceToHost) !=
           hipSuccess)
         goto ioerr;
-      for (uint64_t i = 0; i < k; i++) s32[i] = (uint32_t) s[i];
-      if (fwrite(s32.data(), sizeof (uint32_t), k, fp) != k) goto ioerr;
+      for (uint64_t i = 0; i < k; i++)
+        if (s[i] == 0) longest = off + i;
+      if (suftab_bytes == 8) {
+        if (fwrite(s.data(), sizeof (uint64_t), k, fp) != k) goto ioerr;
+      } else {
+        for (uint64_t i = 0; i < k; i++) s32[i] = (uint32_t) s[i];
+        if (fwrite(s32.data(), sizeof (uint32_t), k, fp) != k) goto ioerr;
+      }
     }
   }
   if (fclose(fp) != 0) { fp = NULL; goto ioerr; }
@@ -182,6 +191,7 @@ extern "C" int gt_smax_esa64_write(const GtSmaxEsa64Dev *e, const uint8_t *text,
   fprintf(fp, "numofdbsequences=%lu\n", (unsigned long) numseq);
   fprintf(fp, "numofquerysequences=0\n");
   fprintf(fp, "numberofallsortedsuffixes=%lu\n", (unsigned long) m);
+  if (longest != UINT64_MAX) fprintf(fp, "longest=%lu\n", (unsigned long) longest);
   fprintf(fp, "prefixlength=0\n");
   fprintf(fp, "largelcpvalues=%lu\n", (unsigned long) e->numllv);
   fprintf(fp, "averagelcp=%.2f\n", e->averagelcp);

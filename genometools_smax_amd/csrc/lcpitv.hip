@@ -66,33 +66,37 @@ struct LiLevels {
 
 // ------------------------------------------------------------ kernels
 
+// grid-stride loop over [0, n) of a 1-D launch (li_blocks caps the grid)
+#define LI_FOR(i, n)                                                          \
+  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x,         \
+                i##_stride = (uint64_t) gridDim.x * blockDim.x;               \
+       i < (n); i += i##_stride)
+
 __global__ void __launch_bounds__(256) li_expand_kernel(const uint8_t *lcp, uint64_t N,
                                                         uint32_t *X) {
-  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (k > N) return;
-  X[k] = (k == 0 || k == N) ? 0u : (uint32_t) lcp[k];
+  LI_FOR(k, N + 1) X[k] = (k == 0 || k == N) ? 0u : (uint32_t) lcp[k];
 }
 
 __global__ void __launch_bounds__(256) li_llv_kernel(const GtSmaxLlv *llv, uint64_t numllv,
                                                      const uint8_t *lcp, uint64_t N, uint32_t *X,
                                                      uint32_t *err) {
-  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (e >= numllv) return;
-  const uint64_t pos = llv[e].position, v = llv[e].value;
-  if (pos < 1 || pos >= N) return;
-  if (v > 0xfffffffeull) atomicOr(err, 1u);
-  if (lcp[pos] != 255) atomicOr(err, 2u);
-  X[pos] = (uint32_t) v;
+  LI_FOR(e, numllv) {
+    const uint64_t pos = llv[e].position, v = llv[e].value;
+    if (pos < 1 || pos >= N) continue;
+    if (v > 0xfffffffeull) atomicOr(err, 1u);
+    if (lcp[pos] != 255) atomicOr(err, 2u);
+    X[pos] = (uint32_t) v;
+  }
 }
 
 __global__ void __launch_bounds__(256) li_min64_kernel(const uint32_t *in, uint64_t n_in,
                                                        uint32_t *out, uint64_t n_out) {
-  const uint64_t g = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (g >= n_out) return;
-  uint32_t m = 0xffffffffu;
-  const uint64_t b = g * 64, e = b + 64 < n_in ? b + 64 : n_in;
-  for (uint64_t i = b; i < e; i++) m = in[i] < m ? in[i] : m;
-  out[g] = m;
+  LI_FOR(g, n_out) {
+    uint32_t m = 0xffffffffu;
+    const uint64_t b = g * 64, e = b + 64 < n_in ? b + 64 : n_in;
+    for (uint64_t i = b; i < e; i++) m = in[i] < m ? in[i] : m;
+    out[g] = m;
+  }
 }
 
 __device__ __forceinline__ bool li_ok(uint32_t x, uint32_t v, bool strict) {
@@ -182,25 +186,23 @@ __device__ __forceinline__ bool li_leftmost(const LiLevels &L, uint64_t k, uint6
   return L.lv[0][p] < v;
 }
 
-__global__ void __launch_bounds__(256) li_count_kernel(LiLevels L, uint64_t N, uint32_t *wg_cnt) {
-  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  uint64_t lb;
-  uint32_t tot;
-  (void) li_block_excl(li_leftmost(L, k, N, &lb) ? 1u : 0u, &tot);
-  if (threadIdx.x == 0) wg_cnt[blockIdx.x] = tot;
+// groups of 256 rows, group-stride over a capped grid (every thread of a
+// workgroup runs the same number of groups: li_block_excl synchronises)
+__global__ void __launch_bounds__(256) li_count_kernel(LiLevels L, uint64_t N, uint64_t ngroups,
+                                                       uint32_t *wg_cnt) {
+  for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const uint64_t k = g * 256 + threadIdx.x;
+    uint64_t lb;
+    uint32_t tot;
+    (void) li_block_excl(li_leftmost(L, k, N, &lb) ? 1u : 0u, &tot);
+    if (threadIdx.x == 0) wg_cnt[g] = tot;
+    __syncthreads();                 // sW is reused by the next group
+  }
 }
 
-// records (lcp, lb, rb, fatherlcp, fatherlb) in row order of their
-// leftmost l-index, and the pop-order sort key rb << 32 | ~lcp
-__global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N,
-                                                       const uint64_t *wg_off, uint64_t *rec,
-                                                       uint64_t *key, uint64_t *idx) {
-  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  uint64_t lb = 0;
-  const bool open = li_leftmost(L, k, N, &lb);
-  uint32_t tot;
-  const uint64_t pos = wg_off[blockIdx.x] + li_block_excl(open ? 1u : 0u, &tot);
-  if (!open) return;
+__device__ __forceinline__ void li_write_one(const LiLevels &L, uint64_t k, uint64_t lb,
+                                             uint64_t pos, uint64_t *rec, uint64_t *key,
+                                             uint64_t *idx) {
   const uint32_t v = L.lv[0][k];
   const uint64_t q = li_next(L, k, v);
   const uint32_t xl = L.lv[0][lb], xq = L.lv[0][q];
@@ -218,24 +220,41 @@ __global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N,
   idx[pos] = pos;
 }
 
+// records (lcp, lb, rb, fatherlcp, fatherlb) in row order of their
+// leftmost l-index, and the pop-order sort key rb << 32 | ~lcp
+__global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N, uint64_t ngroups,
+                                                       const uint64_t *wg_off, uint64_t *rec,
+                                                       uint64_t *key, uint64_t *idx) {
+  for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const uint64_t k = g * 256 + threadIdx.x;
+    uint64_t lb = 0;
+    const bool open = li_leftmost(L, k, N, &lb);
+    uint32_t tot;
+    const uint64_t pos = wg_off[g] + li_block_excl(open ? 1u : 0u, &tot);
+    __syncthreads();                 // sW is reused by the next group
+    if (open) li_write_one(L, k, lb, pos, rec, key, idx);
+  }
+}
+
+
 // keys of the two-pass sort (rb >= 2^32): pass 0 ~lcp, pass 1 rb, of the
 // records in the current permutation
 __global__ void __launch_bounds__(256) li_key_kernel(const uint64_t *rec, const uint64_t *perm,
                                                      uint64_t n, int pass, uint64_t *key) {
-  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t *r = rec + 5 * perm[i];
-  key[i] = pass == 0 ? (uint64_t) (0xffffffffu - (uint32_t) r[0]) : r[2];
+  LI_FOR(i, n) {
+    const uint64_t *r = rec + 5 * perm[i];
+    key[i] = pass == 0 ? (uint64_t) (0xffffffffu - (uint32_t) r[0]) : r[2];
+  }
 }
 
 __global__ void __launch_bounds__(256) li_gather_kernel(const uint64_t *rec, const uint64_t *idx,
                                                         uint64_t n, uint64_t *out) {
-  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t *r = rec + 5 * (uint64_t) idx[i];
-  uint64_t *w = out + 5 * i;
+  LI_FOR(i, n) {
+    const uint64_t *r = rec + 5 * (uint64_t) idx[i];
+    uint64_t *w = out + 5 * i;
 #pragma unroll
-  for (int f = 0; f < 5; f++) w[f] = r[f];
+    for (int f = 0; f < 5; f++) w[f] = r[f];
+  }
 }
 
 // ------------------------------------------------------------ events
@@ -257,23 +276,23 @@ __device__ __forceinline__ uint64_t li_lower_rb(const uint64_t *itv, uint64_t n,
 __global__ void __launch_bounds__(256) li_rootfirst_leaf_kernel(LiLevels L, uint64_t N,
                                                                 const uint64_t *itv, uint64_t nitv,
                                                                 unsigned long long *first) {
-  const uint64_t idx = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (idx >= N) return;
-  const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
-  if (X != 0 || Y > X) return;
-  const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
-  atomicMin(first, (unsigned long long) pos);
+  LI_FOR(idx, N) {
+    const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
+    if (X != 0 || Y > X) continue;
+    const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
+    atomicMin(first, (unsigned long long) pos);
+  }
 }
 
 __global__ void __launch_bounds__(256) li_rootfirst_itv_kernel(const uint64_t *itv, uint64_t nitv,
                                                                unsigned long long *first) {
-  const uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (j >= nitv) return;
-  const uint64_t *r = itv + 5 * j;
-  if (r[3] != 0) return;
-  const uint64_t g = li_lower_rb(itv, nitv, r[2]);
-  const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g) + 1;
-  atomicMin(first, (unsigned long long) pos);
+  LI_FOR(j, nitv) {
+    const uint64_t *r = itv + 5 * j;
+    if (r[3] != 0) continue;
+    const uint64_t g = li_lower_rb(itv, nitv, r[2]);
+    const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g) + 1;
+    atomicMin(first, (unsigned long long) pos);
+  }
 }
 
 // leaf edge of row idx: (0, firstsucc, fd, flb, leafnumber, 0, 0)
@@ -283,24 +302,24 @@ __global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_
                                                              const void *suf,
                                                              const unsigned long long *first,
                                                              uint64_t *ev) {
-  const uint64_t idx = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (idx >= N) return;
-  const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
-  const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
-  uint64_t *w = ev + 7 * pos;
-  w[0] = 0;
-  if (Y <= X) {            // attached to the interval of depth X holding idx
-    w[1] = (X == 0 && pos == *first) ? 1u : 0u;
-    w[2] = X;
-    w[3] = X == 0 ? 0 : li_prev(L, idx, X, true);
-  } else {                 // firstsucc leaf of the new interval (Y, idx)
-    w[1] = 1;
-    w[2] = Y;
-    w[3] = idx;
+  LI_FOR(idx, N) {
+    const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
+    const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
+    uint64_t *w = ev + 7 * pos;
+    w[0] = 0;
+    if (Y <= X) {            // attached to the interval of depth X holding idx
+      w[1] = (X == 0 && pos == *first) ? 1u : 0u;
+      w[2] = X;
+      w[3] = X == 0 ? 0 : li_prev(L, idx, X, true);
+    } else {                 // firstsucc leaf of the new interval (Y, idx)
+      w[1] = 1;
+      w[2] = Y;
+      w[3] = idx;
+    }
+    w[4] = suf == nullptr ? 0 : (uint64_t) reinterpret_cast<const SufT *>(suf)[idx];
+    w[5] = 0;
+    w[6] = 0;
   }
-  w[4] = suf == nullptr ? 0 : (uint64_t) reinterpret_cast<const SufT *>(suf)[idx];
-  w[5] = 0;
-  w[6] = 0;
 }
 
 // popped interval j: (2, 0, lcp, lb, rb, 0, 0) then its branching edge
@@ -309,25 +328,32 @@ __global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_
 __global__ void __launch_bounds__(256) li_events_itv_kernel(const uint64_t *itv, uint64_t nitv,
                                                             const unsigned long long *first,
                                                             uint64_t *ev) {
-  const uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (j >= nitv) return;
-  const uint64_t *r = itv + 5 * j;
-  const uint64_t g = li_lower_rb(itv, nitv, r[2]);
-  const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g);
-  uint64_t *w = ev + 7 * pos;
-  w[0] = 2; w[1] = 0; w[2] = r[0]; w[3] = r[1]; w[4] = r[2]; w[5] = 0; w[6] = 0;
-  w += 7;
-  const bool newfather = r[3] > 0 && r[4] == r[1];
-  w[0] = 1;
-  w[1] = newfather ? 1u : ((r[3] == 0 && pos + 1 == *first) ? 1u : 0u);
-  w[2] = r[3];
-  w[3] = newfather ? r[1] : r[4];
-  w[4] = r[0]; w[5] = r[1]; w[6] = r[2];
+  LI_FOR(j, nitv) {
+    const uint64_t *r = itv + 5 * j;
+    const uint64_t g = li_lower_rb(itv, nitv, r[2]);
+    const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g);
+    uint64_t *w = ev + 7 * pos;
+    w[0] = 2; w[1] = 0; w[2] = r[0]; w[3] = r[1]; w[4] = r[2]; w[5] = 0; w[6] = 0;
+    w += 7;
+    const bool newfather = r[3] > 0 && r[4] == r[1];
+    w[0] = 1;
+    w[1] = newfather ? 1u : ((r[3] == 0 && pos + 1 == *first) ? 1u : 0u);
+    w[2] = r[3];
+    w[3] = newfather ? r[1] : r[4];
+    w[4] = r[0]; w[5] = r[1]; w[6] = r[2];
+  }
 }
 
 // ------------------------------------------------------------ plan
 
-static unsigned li_blocks(uint64_t n) { return (unsigned) ((n + 255) / 256); }
+// a dispatch holds fewer than 2^32 work-items and N + 1 rows exceed that past
+// 2^32 suffixes: per-row kernels are grid-stride loops (LI_FOR) over a
+// capped grid, the 256-row group kernels group-stride loops
+#define LI_MAX_BLOCKS (1ull << 22)
+static unsigned li_blocks(uint64_t n) {
+  const uint64_t b = (n + 255) / 256;
+  return (unsigned) (b > LI_MAX_BLOCKS ? LI_MAX_BLOCKS : (b ? b : 1));
+}
 
 struct GtLcpitvPlan {
   GtLcpitvDevInput in;
@@ -416,7 +442,7 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
   LICHK(hipMalloc(&wg_cnt, sizeof (uint32_t) * (nwg + 1)));
   LICHK(hipMalloc(&wg_off, sizeof (uint64_t) * (nwg + 1)));
   if (nwg > 0) {
-    hipLaunchKernelGGL(li_count_kernel, dim3((unsigned) nwg), dim3(256), 0, 0, p->L, N, wg_cnt);
+    hipLaunchKernelGGL(li_count_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, p->L, N, nwg, wg_cnt);
     LICHK(hipGetLastError());
     LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
                                   rocprim::plus<uint64_t>(), (hipStream_t) 0));
@@ -437,8 +463,8 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
     LICHK(hipMalloc(&key_b, sizeof (uint64_t) * n));
     LICHK(hipMalloc(&idx_a, sizeof (uint64_t) * n));
     LICHK(hipMalloc(&idx_b, sizeof (uint64_t) * n));
-    hipLaunchKernelGGL(li_write_kernel, dim3((unsigned) nwg), dim3(256), 0, 0, p->L, N, wg_off, rec,
-                       key_a, idx_a);
+    hipLaunchKernelGGL(li_write_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, p->L, N, nwg, wg_off,
+                       rec, key_a, idx_a);
     LICHK(hipGetLastError());
     LICHK(hipFree(tmp));
     tmp = NULL;

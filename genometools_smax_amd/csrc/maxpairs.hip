@@ -81,16 +81,22 @@ static void mp_seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
 
 #define MP_STEP 8     // rows per walk step
 
+// grid-stride loop over [0, n) of a 1-D launch (mp_blocks caps the grid)
+#define MP_FOR(i, n)                                                          \
+  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x,         \
+                i##_stride = (uint64_t) gridDim.x * blockDim.x;               \
+       i < (n); i += i##_stride)
+#define MP_MAX_BLOCKS (1ull << 22)   // 2^30 work-items: fills the chip many times
+
 // ------------------------------------------------------------ kernels
 
 // X[k] = exact LCP[k] for k in [0, N] (0 at k = 0 and k = N; the 255 bytes
 // are overwritten by mp_llv_kernel).  A3 decoding, src/match/esa-seqread.h:96-215.
 __global__ void __launch_bounds__(256) mp_expand_kernel(const uint8_t *lcp, uint64_t N,
                                                         uint32_t *X) {
-  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (k > N) return;
   // 255 bytes are marked until their .llv value arrives (mp_llv_kernel)
-  X[k] = (k == 0 || k == N) ? 0u : (lcp[k] == 255 ? 0xffffffffu : (uint32_t) lcp[k]);
+  MP_FOR(k, N + 1)
+    X[k] = (k == 0 || k == N) ? 0u : (lcp[k] == 255 ? 0xffffffffu : (uint32_t) lcp[k]);
 }
 
 // .llv values over their 255 bytes; err bit 1: value >= 2^32, bit 2: a
@@ -98,39 +104,39 @@ __global__ void __launch_bounds__(256) mp_expand_kernel(const uint8_t *lcp, uint
 __global__ void __launch_bounds__(256) mp_llv_kernel(const GtSmaxLlv *llv, uint64_t numllv,
                                                      const uint8_t *lcp, uint64_t N, uint32_t *X,
                                                      uint32_t *err) {
-  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (e >= numllv) return;
-  const uint64_t pos = llv[e].position, v = llv[e].value;
-  if (pos < 1 || pos >= N) return;
-  if (v >= 0xffffffffull) atomicOr(err, 1u);
-  if (lcp[pos] != 255) atomicOr(err, 2u);
-  X[pos] = (uint32_t) v;
+  MP_FOR(e, numllv) {
+    const uint64_t pos = llv[e].position, v = llv[e].value;
+    if (pos < 1 || pos >= N) continue;
+    if (v >= 0xffffffffull) atomicOr(err, 1u);
+    if (lcp[pos] != 255) atomicOr(err, 2u);
+    X[pos] = (uint32_t) v;
+  }
 }
 
 // heads of the runs of equal BWT symbols (specials >= 254 are runs of one:
 // they differ from every symbol) for a max-scan to the run start
 __global__ void __launch_bounds__(256) mp_run_heads_kernel(const uint8_t *B, uint64_t N,
                                                            uint64_t *hv) {
-  const uint64_t r = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (r > N) return;
-  const uint32_t b = B[r];
-  hv[r] = (r == 0 || b >= 254u || B[r - 1] != b) ? r : 0;
+  MP_FOR(r, N + 1) {
+    const uint32_t b = B[r];
+    hv[r] = (r == 0 || b >= 254u || B[r - 1] != b) ? r : 0;
+  }
 }
 
 // RO[r] = r - (first row of r's run), from the scanned run starts
 __global__ void __launch_bounds__(256) mp_run_off_kernel(const uint64_t *rs, uint64_t N,
                                                          uint32_t *RO) {
-  const uint64_t r = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (r > N) return;
-  const uint64_t d = r - rs[r];
-  RO[r] = d > 0xffffffffull ? 0xffffffffu : (uint32_t) d;
+  MP_FOR(r, N + 1) {
+    const uint64_t d = r - rs[r];
+    RO[r] = d > 0xffffffffull ? 0xffffffffu : (uint32_t) d;
+  }
 }
 
 // a .lcp byte 255 whose row no .llv entry overwrote (X still holds the mark)
 __global__ void __launch_bounds__(256) mp_llv_check_kernel(const uint32_t *X, uint64_t N,
                                                            uint32_t *err) {
-  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (k < N && X[k] == 0xffffffffu) atomicOr(err, 4u);
+  MP_FOR(k, N)
+    if (X[k] == 0xffffffffu) atomicOr(err, 4u);
 }
 
 template <typename SufT>
@@ -347,9 +353,8 @@ __global__ void __launch_bounds__(256)
 mp_count_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint32_t *RM,
                 const uint32_t *RO, const uint64_t *list, uint64_t ncand, uint32_t minlen,
                 uint32_t *cnt) {
-  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (e >= ncand) return;
-  cnt[e] = mp_walk<false, SufT>(lcp, X, B, RM, RO, nullptr, list[e], minlen, 0, nullptr, 0);
+  MP_FOR(e, ncand)
+    cnt[e] = mp_walk<false, SufT>(lcp, X, B, RM, RO, nullptr, list[e], minlen, 0, nullptr, 0);
 }
 
 // Pass D: the pairs of every candidate row at its scanned offset,
@@ -360,9 +365,10 @@ mp_emit_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const ui
                const uint32_t *RO, const void *S, const uint64_t *list, uint64_t ncand,
                uint32_t minlen, const uint32_t *cnt, const uint64_t *off, uint64_t *out,
                uint64_t capacity) {
-  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (e >= ncand || cnt[e] == 0) return;
-  (void) mp_walk<true, SufT>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity);
+  MP_FOR(e, ncand) {
+    if (cnt[e] == 0) continue;
+    (void) mp_walk<true, SufT>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity);
+  }
 }
 
 // Pass D with the emission-order keys of every pair
@@ -372,37 +378,37 @@ mp_emit_ord_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, cons
                    const uint32_t *RO, const void *S, const uint64_t *list, uint64_t ncand,
                    uint32_t minlen, const uint32_t *cnt, const uint64_t *off, uint64_t *out,
                    uint64_t capacity, MpHier h, MpKeys K) {
-  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (e >= ncand || cnt[e] == 0) return;
-  (void) mp_walk<true, SufT, true>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity,
-                                   &h, &K);
+  MP_FOR(e, ncand) {
+    if (cnt[e] == 0) continue;
+    (void) mp_walk<true, SufT, true>(lcp, X, B, RM, RO, S, list[e], minlen, off[e], out, capacity,
+                                     &h, &K);
+  }
 }
 
 // one hierarchy level: dst[i] = min(src[64i .. 64i+63])
 __global__ void __launch_bounds__(256) mp_hier_kernel(const uint32_t *src, uint64_t nsrc,
                                                       uint32_t *dst, uint64_t ndst) {
-  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (i >= ndst) return;
-  const uint64_t b = i << 6, e = b + 64 < nsrc ? b + 64 : nsrc;
-  uint32_t m = 0xffffffffu;
-  for (uint64_t k = b; k < e; k++) m = src[k] < m ? src[k] : m;
-  dst[i] = m;
+  MP_FOR(i, ndst) {
+    const uint64_t b = i << 6, e = b + 64 < nsrc ? b + 64 : nsrc;
+    uint32_t m = 0xffffffffu;
+    for (uint64_t k = b; k < e; k++) m = src[k] < m ? src[k] : m;
+    dst[i] = m;
+  }
 }
 
 __global__ void __launch_bounds__(256) mp_iota_kernel(uint64_t *p, uint64_t n) {
-  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (i < n) p[i] = i;
+  MP_FOR(i, n) p[i] = i;
 }
 
 // dst[i] = src[perm[i]] (words per element: 1 for keys, 3 for triples)
 template <int W>
 __global__ void __launch_bounds__(256) mp_gather_kernel(const uint64_t *src, const uint64_t *perm,
                                                         uint64_t n, uint64_t *dst) {
-  const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t s = perm[i];
+  MP_FOR(i, n) {
+    const uint64_t s = perm[i];
 #pragma unroll
-  for (int w = 0; w < W; w++) dst[W * i + w] = src[W * s + w];
+    for (int w = 0; w < W; w++) dst[W * i + w] = src[W * s + w];
+  }
 }
 
 __global__ void mp_total_kernel(const uint32_t *cnt, const uint64_t *off, uint64_t n,
@@ -417,20 +423,20 @@ __global__ void mp_total_kernel(const uint32_t *cnt, const uint64_t *off, uint64
 __global__ void __launch_bounds__(256) seqpos_map_kernel(const uint64_t *sep, uint64_t nsep,
                                                          const uint64_t *pairs, uint64_t count,
                                                          uint64_t *out) {
-  const uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (k >= count) return;
-  const uint64_t len = pairs[3 * k], p[2] = {pairs[3 * k + 1], pairs[3 * k + 2]};
-  uint64_t *w = out + 5 * k;
-  w[0] = len;
+  MP_FOR(k, count) {
+    const uint64_t len = pairs[3 * k], p[2] = {pairs[3 * k + 1], pairs[3 * k + 2]};
+    uint64_t *w = out + 5 * k;
+    w[0] = len;
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-    uint64_t lo = 0, hi = nsep;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (sep[mid] < p[h]) lo = mid + 1; else hi = mid;
+    for (int h = 0; h < 2; h++) {
+      uint64_t lo = 0, hi = nsep;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (sep[mid] < p[h]) lo = mid + 1; else hi = mid;
+      }
+      w[1 + 2 * h] = lo;
+      w[2 + 2 * h] = p[h] - (lo == 0 ? 0 : sep[lo - 1] + 1);
     }
-    w[1 + 2 * h] = lo;
-    w[2 + 2 * h] = p[h] - (lo == 0 ? 0 : sep[lo - 1] + 1);
   }
 }
 
@@ -456,7 +462,13 @@ struct GtMaxpairsPlan {
   uint32_t xmax;                 // largest exact LCP value
 };
 
-static unsigned mp_blocks(uint64_t n) { return (unsigned) ((n + 255) / 256); }
+// per-element kernels are grid-stride loops (MP_FOR) over a capped grid: a
+// dispatch holds fewer than 2^32 work-items, and N + 1 rows exceed that past
+// 2^32 suffixes (12 Gbp: 1.2e10 rows)
+static unsigned mp_blocks(uint64_t n) {
+  const uint64_t b = (n + 255) / 256;
+  return (unsigned) (b > MP_MAX_BLOCKS ? MP_MAX_BLOCKS : (b ? b : 1));
+}
 
 extern "C" void gt_maxpairs_plan_delete(GtMaxpairsPlan *p) {
   if (p == NULL) return;

@@ -238,13 +238,17 @@ extern "C" int gt_repfind_pairs_lines_dev(const uint64_t *pairs_dev, uint64_t co
                                           const uint64_t *sep_dev, uint64_t nsep, int device,
                                           GtRepfindTextFunc cb, void *data, char *errbuf,
                                           size_t errlen) {
+  int cur = -1;
+  (void) hipGetDevice(&cur);
   if (hipSetDevice(device) != hipSuccess) {
     rl_seterr(errbuf, errlen, "hipSetDevice(%d) failed", device);
     return -1;
   }
   RlPairs src{pairs_dev};
   RlSep s{sep_dev, nsep};
-  return rl_format(src, count, s, cb, data, errbuf, errlen);
+  const int rc = rl_format(src, count, s, cb, data, errbuf, errlen);
+  if (cur >= 0) (void) hipSetDevice(cur);   // the caller's device again
+  return rc;
 }
 
 extern "C" int gt_repfind_smax_lines(const GtSmaxRecord *rec, uint64_t nrec, const uint64_t *occpos,
@@ -265,7 +269,7 @@ extern "C" int gt_repfind_smax_lines(const GtSmaxRecord *rec, uint64_t nrec, con
       return -1;
     }
   if (nrec == 0) return 0;
-  RLCHK(hipSetDevice(0));
+  // formats on the caller's current device (hipSetDevice before the call)
   RLCHK(hipMalloc(&drec, sizeof (GtSmaxRecord) * nrec));
   RLCHK(hipMalloc(&docc, sizeof (uint64_t) * (nocc ? nocc : 1)));
   RLCHK(hipMalloc(&dsep, sizeof (uint64_t) * (nsep ? nsep : 1)));

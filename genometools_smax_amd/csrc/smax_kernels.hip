@@ -2330,6 +2330,7 @@ struct GtSmaxPlan {
   bool nt;                   // window stream with the non-temporal policy (smax_scan_kernel*_nt)
   bool k1b_wg;               // mode 4: one workgroup per K1b tile (GT_SMAX_K1B_WG=0: one wave)
   uint32_t comb_grid_wg;     // its grid (+1: head)
+  bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   hipEvent_t fork, join;
   uint32_t *err;
   uint32_t dbg;
@@ -2355,6 +2356,11 @@ extern "C" int gt_smax_device_count(void) {
 }
 
 extern "C" void gt_smax_free(void *ptr) { free(ptr); }
+
+#ifndef GT_SMAX_BUILD_ID
+#define GT_SMAX_BUILD_ID "unknown"
+#endif
+extern "C" const char *gt_smax_build_id(void) { return GT_SMAX_BUILD_ID; }
 
 extern "C" int gt_smax_dev_alloc_table(int device, uint64_t len,
                                        uint8_t **table, char *errbuf,
@@ -2705,12 +2711,26 @@ static int plan_run_parts(GtSmaxPlan *p, hipStream_t s, unsigned parts) {
   char *errbuf = NULL;
   size_t errlen = 0;
   HIPCHK(hipSetDevice(p->shard.device));
+  // K3 of part 1 resets the deferral list and pool cursor the next part 0's
+  // K1/K1b start from: a second part 0 before that part 1 would run on stale
+  // state (and part 1 without a part 0 would compact stale tiles)
+  if ((parts & 1u) && p->part1_pending) {
+    fprintf(stderr, "gt_smax: gt_smax_plan_run_part(0) called again before part 1\n");
+    return -1;
+  }
+  if (parts == 2u && !p->part1_pending) {
+    fprintf(stderr, "gt_smax: gt_smax_plan_run_part(1) without a pending part 0\n");
+    return -1;
+  }
   if (p->shard.begin >= p->shard.end) {
+    p->part1_pending = (parts == 1u);
     if (parts & 1u) return plan_run_scan(p, s);
     return 0;
   }
   if ((parts & 1u) && plan_run_scan(p, s) != 0) return -1;
+  p->part1_pending = true;
   if ((parts & 2u) && plan_run_compact(p, s) != 0) return -1;
+  if (parts & 2u) p->part1_pending = false;
   return 0;
 fail:
   return -1;

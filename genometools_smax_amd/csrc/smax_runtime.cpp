@@ -708,21 +708,31 @@ hipError_t smax_dev_alloc(void **ptr, size_t bytes) {
 void smax_dev_free(void *ptr) {
   if (ptr == nullptr) return;
   Pool &P = pool();
-  std::lock_guard<std::mutex> g(P.mu);
-  auto it = P.live.find(ptr);
-  if (it == P.live.end()) return;
-  const auto key = it->second;
-  P.live.erase(it);
+  std::pair<int, size_t> key;
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.live.find(ptr);
+    if (it == P.live.end()) return;
+    key = it->second;
+    P.live.erase(it);
+  }
   static const bool nocache = env_on("GT_SMAX_NO_CACHE");
+  int cur = -1;
+  (void) hipGetDevice(&cur);
+  (void) hipSetDevice(key.first);
   if (nocache) {
-    int cur = -1;
-    (void) hipGetDevice(&cur);
-    (void) hipSetDevice(key.first);
     (void) hipFree(ptr);
-    if (cur >= 0) (void) hipSetDevice(cur);
   } else {
+    // a block goes back to the cache only once every kernel that may still
+    // use it has finished (hipFree synchronised implicitly; a plan closed
+    // right after run() must not hand its buffers to the next allocation
+    // while K1..K3 still write them).  Outside the pool lock: other device
+    // threads keep allocating meanwhile.
+    (void) hipDeviceSynchronize();
+    std::lock_guard<std::mutex> g(P.mu);
     P.idle.insert({key, ptr});
   }
+  if (cur >= 0) (void) hipSetDevice(cur);
 }
 
 double smax_phase_clock() {

@@ -118,7 +118,8 @@ int gt_seqpos_map_dev(const uint64_t *sep_dev, uint64_t nsep, const uint64_t *pa
 typedef int (*GtRepfindTextFunc)(void *data, const char *text, uint64_t bytes);
 
 /* device (len, pos1, pos2) triples (e.g. gt_maxpairs_plan_emit_ordered's)
- * and device separators -> lines */
+ * and device separators -> lines, on `device` (the caller's current device is
+ * restored on return) */
 int gt_repfind_pairs_lines_dev(const uint64_t *pairs_dev, uint64_t count, const uint64_t *sep_dev,
                                uint64_t nsep, int device, GtRepfindTextFunc cb, void *data,
                                char *errbuf, size_t errlen);
@@ -133,7 +134,8 @@ int gt_repfind_maxpairs_lines(const GtSmaxInput *in, unsigned int minlen, const 
  * occpos[rec[r].lb .. rec[r].lb + rec[r].width) (text positions in
  * suffix-array row order); every pair a < b of them, a outer, becomes one
  * line of length rec[r].lcp -- the order bin/gt-repfind prints them in.
- * The pairs are generated on the GPU from the records (none stored). */
+ * The pairs are generated on the GPU from the records (none stored), on the
+ * caller's current HIP device (left current on return). */
 int gt_repfind_smax_lines(const GtSmaxRecord *rec, uint64_t nrec, const uint64_t *occpos,
                           uint64_t nocc, const uint64_t *sep, uint64_t nsep,
                           GtRepfindTextFunc cb, void *data, char *errbuf, size_t errlen);

@@ -106,6 +106,12 @@ void gt_smax_release_cache(void);
 /* Number of HIP devices visible (0 if the runtime has none). */
 int gt_smax_device_count(void);
 
+/* Identity of the scan kernels' build: a hash of the K1..K3 sources and the
+ * gfx950 compile flags (set by the Makefile).  Profiles of the kernels
+ * (profiles/pmc_*.json) carry it, so a measurement can be matched to the
+ * code object it was taken on.  Static string. */
+const char *gt_smax_build_id(void);
+
 /* -------------------------------------------------- device-resident API */
 
 /*
@@ -189,6 +195,9 @@ int gt_smax_dev_free_table(int device, uint8_t *table);
 int gt_smax_plan_create(GtSmaxPlan **plan, const GtSmaxDevShard *shard,
                         unsigned int minlen, uint64_t capacity,
                         char *errbuf, size_t errlen);
+/* Frees the plan; its device buffers return to the runtime's cache only
+ * after the device has finished the work already enqueued (safe right after
+ * an asynchronous gt_smax_plan_run). */
 void gt_smax_plan_delete(GtSmaxPlan *plan);
 
 /* Enqueue one smax pass (scan + ordered compaction + boundary record) on
@@ -200,7 +209,11 @@ int gt_smax_plan_run(GtSmaxPlan *plan, void *stream);
  * (gt_smax_plan_copy_boundary may follow); part 1 = the ordered compaction
  * into the record array.  A sharded caller enqueues part 0, the boundary
  * copy and its all-gather (on the collective's stream), then part 1 beside
- * the all-gather, and the stitch once both are done.  -1 for another part. */
+ * the all-gather, and the stitch once both are done.  -1 for another part.
+ * Order: part 1 must follow every part 0 before the next part 0 (its
+ * compaction resets the deferral state the next scan starts from); a second
+ * part 0, or a part 1 with no part 0 pending, returns -1 and enqueues
+ * nothing.  gt_smax_plan_run is refused likewise while a part 1 is pending. */
 int gt_smax_plan_run_part(GtSmaxPlan *plan, int part, void *stream);
 
 /* Device pointers owned by the plan. */

@@ -317,6 +317,13 @@ int orc_index_fasta(const char *fastapath, const char *indexname,
     fprintf(fp, "numofdbsequences=%lu\n", (unsigned long) numseq);
     fprintf(fp, "numofquerysequences=0\n");
     fprintf(fp, "numberofallsortedsuffixes=%lu\n", (unsigned long) (n + 1));
+    /* longest: the row of suffix 0 (src/match/sfx-outprj.c:70-73 writes it
+     * whenever .suf is written; src/match/sfx-suffixgetset.c:246-250) */
+    for (k = 0; k <= n; k++)
+      if (suftab[k] == 0) {
+        fprintf(fp, "longest=%lu\n", (unsigned long) k);
+        break;
+      }
     fprintf(fp, "prefixlength=0\n");
     fprintf(fp, "largelcpvalues=%lu\n", (unsigned long) numllv);
     fprintf(fp, "averagelcp=%.2f\n", prj.averagelcp);

@@ -284,17 +284,29 @@ static void smax_branch(BUItv *f, int firstsucc)
   f->has_branch = 1;
 }
 
-/* Traversal as in gt_esa_bottomup (src/match/esa-bottomup.c:116-273).
- * lcp: decoded, lcp[idx+1] read at step idx; suftab full; text encoded. */
-uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
-                           const uint8_t *text, uint64_t nonspecials,
-                           uint64_t minlen, uint64_t *out, uint64_t cap)
+/* Traversal as in gt_esa_bottomup (src/match/esa-bottomup.c:116-273), over
+ * either
+ *  - lcp: decoded (lcp[idx+1] read at step idx), left characters from the
+ *    text through the suffix array (suftab, text), or
+ *  - the mapped tables as the sequential reader hands them out
+ *    (SSAR_NEXTSEQUENTIALLCPTABVALUE, src/match/esa-seqread.h:104-157: a
+ *    255 byte takes the next .llv value), left characters from the .bwt
+ *    (text[suftab[idx]-1], 254 for suffix 0 -- the same symbols).
+ * The steps run over rows [0, rows) (rows = N: the whole index); the value
+ * after the last row is taken as 0 (LCP[N] == 0 on file-based indexes). */
+static uint64_t bu_smax_core(const uint64_t *lcp, const uint64_t *suftab,
+                             const uint8_t *text, const uint8_t *lcpbytes,
+                             const OrcLlv *llv, uint64_t numllv,
+                             const uint8_t *bwt, uint64_t rows,
+                             uint64_t minlen, uint64_t *out, uint64_t cap)
 {
   BUStack st = {NULL, 0, 0};
   BUItv *last = NULL;
   BUItv lastcopy;
-  uint64_t idx, found = 0;
+  uint64_t idx, found = 0, li = 0;
+  const uint64_t nonspecials = rows;
   int firstedgefromroot = 1;
+  if (lcpbytes != NULL && rows > 0 && lcpbytes[0] == 255) li = 1;
 #define EMIT(I)                                                              \
   do {                                                                       \
     if ((I)->lcp >= minlen && !(I)->has_branch && !(I)->dup) {               \
@@ -305,13 +317,22 @@ uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
   } while (0)
   bu_push(&st, 0, 0);
   for (idx = 0; idx < nonspecials; idx++) {
-    uint64_t lcpvalue = lcp[idx + 1];
-    uint64_t prevsuffix = suftab[idx];
+    uint64_t lcpvalue;
+    uint8_t lc;
     int firstedge;
+    if (lcp != NULL) {
+      lcpvalue = lcp[idx + 1];
+      lc = leftchar_of(text, suftab[idx]);
+    } else {
+      if (idx + 1 >= rows) lcpvalue = 0;
+      else if (lcpbytes[idx + 1] < 255) lcpvalue = lcpbytes[idx + 1];
+      else lcpvalue = li < numllv ? llv[li++].value : 0;
+      lc = bwt[idx];
+    }
     if (lcpvalue <= BU_TOP(&st).lcp) {
       if (BU_TOP(&st).lcp > 0 || !firstedgefromroot) firstedge = 0;
       else { firstedge = 1; firstedgefromroot = 0; }
-      smax_leaf(&BU_TOP(&st), firstedge, leftchar_of(text, prevsuffix));
+      smax_leaf(&BU_TOP(&st), firstedge, lc);
     }
     last = NULL;
     while (lcpvalue < BU_TOP(&st).lcp) {
@@ -334,7 +355,7 @@ uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
         last = NULL;
       } else {
         bu_push(&st, lcpvalue, idx);
-        smax_leaf(&BU_TOP(&st), 1, leftchar_of(text, prevsuffix));
+        smax_leaf(&BU_TOP(&st), 1, lc);
       }
     }
   }
@@ -346,6 +367,26 @@ uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
   free(st.space);
 #undef EMIT
   return found;
+}
+
+uint64_t orc_bottomup_smax(const uint64_t *lcp, const uint64_t *suftab,
+                           const uint8_t *text, uint64_t nonspecials,
+                           uint64_t minlen, uint64_t *out, uint64_t cap)
+{
+  return bu_smax_core(lcp, suftab, text, NULL, NULL, 0, NULL, nonspecials,
+                      minlen, out, cap);
+}
+
+/* The same traversal over the mapped .lcp/.llv/.bwt tables, rows [0, rows):
+ * bench.py's reference-algorithm CPU anchor (the stack walk the GPU path
+ * replaces) and, with rows = N, a fourth derivation of the smax list. */
+uint64_t orc_bottomup_smax_tables(const uint8_t *lcpbytes, const OrcLlv *llv,
+                                  uint64_t numllv, const uint8_t *bwt,
+                                  uint64_t rows, uint64_t minlen,
+                                  uint64_t *out, uint64_t cap)
+{
+  return bu_smax_core(NULL, NULL, NULL, lcpbytes, llv, numllv, bwt, rows,
+                      minlen, out, cap);
 }
 
 /* Full event stream of gt_esa_bottomup (src/match/esa-bottomup.c:116-273)
@@ -807,4 +848,114 @@ int orc_format_pair(uint64_t len, uint64_t pos1, uint64_t pos2,
                   (unsigned long) len, (unsigned long) s1,
                   (unsigned long) (pos1 - st1), (unsigned long) len,
                   (unsigned long) s2, (unsigned long) (pos2 - st2));
+}
+
+/* ------------------------------------------- checkers past 2^32 rows */
+
+/* exact L[k] of the mapped tables (255 -> .llv by binary search) */
+static uint64_t orc_lcp_at(const uint8_t *lcpbytes, const OrcLlv *llv,
+                           uint64_t numllv, uint64_t k)
+{
+  uint64_t i;
+  if (lcpbytes[k] < 255) return lcpbytes[k];
+  i = orc_llv_lower(llv, numllv, k);
+  return i < numllv && llv[i].position == k ? llv[i].value : 0;
+}
+
+/* Every lcp-interval of depth > 0 with its father, in the pop order of
+ * gt_esa_bottomup (src/match/esa-bottomup.c:116-273): at step
+ * idx the intervals deeper than L[idx+1] are popped (rb = idx); a popped
+ * interval's father is the stack top if L[idx+1] <= its depth, else the
+ * interval (L[idx+1], popped lb) pushed right after.  5 words per interval
+ * (lcp, lb, rb, father lcp, father lb); F3's gt_lcpitv list, for tables too
+ * large for orc_bottomup_events.  L[N] is taken as 0. */
+uint64_t orc_lcp_intervals(const uint8_t *lcpbytes, const OrcLlv *llv,
+                           uint64_t numllv, uint64_t nonspecials,
+                           uint64_t *out, uint64_t cap)
+{
+  uint64_t *sl = NULL, *sb = NULL, top = 0, alloc = 0, idx, found = 0, li = 0;
+  const uint64_t N = nonspecials;
+  if (N > 0 && lcpbytes[0] == 255) li = 1;
+  alloc = 1024;
+  sl = malloc(sizeof (uint64_t) * alloc);
+  sb = malloc(sizeof (uint64_t) * alloc);
+  sl[0] = 0; sb[0] = 0; top = 1;
+  for (idx = 0; idx < N; idx++) {
+    uint64_t v, lastlb = 0;
+    int popped = 0;
+    if (idx + 1 >= N) v = 0;
+    else if (lcpbytes[idx + 1] < 255) v = lcpbytes[idx + 1];
+    else v = li < numllv ? llv[li++].value : 0;
+    while (v < sl[top - 1]) {
+      uint64_t l = sl[top - 1], b = sb[top - 1], fl, fb;
+      top--;
+      if (v <= sl[top - 1]) { fl = sl[top - 1]; fb = sb[top - 1]; }
+      else { fl = v; fb = b; }
+      if (found < cap) {
+        uint64_t *w = out + 5 * found;
+        w[0] = l; w[1] = b; w[2] = idx; w[3] = fl; w[4] = fb;
+      }
+      found++;
+      lastlb = b;
+      popped = 1;
+    }
+    if (v > sl[top - 1]) {
+      if (top >= alloc) {
+        alloc *= 2;
+        sl = realloc(sl, sizeof (uint64_t) * alloc);
+        sb = realloc(sb, sizeof (uint64_t) * alloc);
+      }
+      sl[top] = v;
+      sb[top] = popped ? lastlb : idx;
+      top++;
+    }
+  }
+  free(sl);
+  free(sb);
+  return found;
+}
+
+/* Maximal pairs by their definition, block by block: rows i < j of one
+ * block (a maximal run of rows k with L[k] >= minlen, plus the row before
+ * it) form a pair of length min L[i+1..j] when their left symbols differ
+ * (symbols >= 254 unique, ISLEFTDIVERSE, src/match/esa-maxpairs.c:24-31);
+ * triples (len, min pos, max pos) in no particular order; with suftab NULL
+ * the rows (len, i, j) instead.  Quadratic in the block size: for sparse
+ * synthetic tables past 2^32 rows (F2 checker). */
+uint64_t orc_maxpairs_blocks(const uint8_t *lcpbytes, const OrcLlv *llv,
+                             uint64_t numllv, const uint8_t *bwt,
+                             const uint64_t *suftab, uint64_t nonspecials,
+                             uint64_t minlen, uint64_t *out, uint64_t cap)
+{
+  const uint64_t N = nonspecials;
+  const uint8_t mf = minlen < 255 ? (uint8_t) minlen : 255;
+  uint64_t k = 1, found = 0;
+  while (k < N) {
+    uint64_t a, b, j;
+    if (lcpbytes[k] < mf || orc_lcp_at(lcpbytes, llv, numllv, k) < minlen) { k++; continue; }
+    a = k;
+    b = k;
+    while (b + 1 < N && lcpbytes[b + 1] >= mf &&
+           orc_lcp_at(lcpbytes, llv, numllv, b + 1) >= minlen)
+      b++;
+    for (j = a; j <= b; j++) {
+      uint64_t m = UINT64_MAX, i = j;
+      while (i >= a) {
+        uint64_t x = orc_lcp_at(lcpbytes, llv, numllv, i);
+        m = x < m ? x : m;
+        i--;
+        if (bwt[i] >= 254 || bwt[j] >= 254 || bwt[i] != bwt[j]) {
+          if (found < cap) {
+            uint64_t p = suftab ? suftab[i] : i, q = suftab ? suftab[j] : j;
+            out[3 * found] = m;
+            out[3 * found + 1] = p < q ? p : q;
+            out[3 * found + 2] = p < q ? q : p;
+          }
+          found++;
+        }
+      }
+    }
+    k = b + 1;
+  }
+  return found;
 }

@@ -36,6 +36,16 @@ def lib():
         L.orc_bottomup_smax.argtypes = [_u64p, _u64p, _u8p, ctypes.c_uint64, ctypes.c_uint64,
                                         _u64p, ctypes.c_uint64]
         L.orc_bottomup_smax.restype = ctypes.c_uint64
+        L.orc_bottomup_smax_tables.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint64, _u8p,
+                                               ctypes.c_uint64, ctypes.c_uint64, _u64p,
+                                               ctypes.c_uint64]
+        L.orc_bottomup_smax_tables.restype = ctypes.c_uint64
+        L.orc_lcp_intervals.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                        _u64p, ctypes.c_uint64]
+        L.orc_lcp_intervals.restype = ctypes.c_uint64
+        L.orc_maxpairs_blocks.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_uint64, _u8p, _u64p,
+                                          ctypes.c_uint64, ctypes.c_uint64, _u64p, ctypes.c_uint64]
+        L.orc_maxpairs_blocks.restype = ctypes.c_uint64
         L.orc_brute_smax.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64, _u64p, ctypes.c_uint64,
                                      _u64p, ctypes.c_uint64]
         L.orc_brute_smax.restype = ctypes.c_uint64
@@ -130,6 +140,42 @@ def bottomup_smax(esa, minlen):
     found = lib().orc_bottomup_smax(_p(esa.lcp, _u64p), _p(esa.suftab, _u64p), _p(esa.text, _u8p),
                                     esa.nonspecials, minlen, _p(out, _u64p), cap)
     assert found <= cap
+    return _triples(out, found)
+
+
+def bottomup_smax_tables(lcpbytes, llv, bwt, rows, minlen, cap=None):
+    """orc_bottomup_smax_tables: the reference's stack traversal
+    (esa-bottomup.c:116-273) over the mapped tables, rows [0, rows)."""
+    llv = np.ascontiguousarray(llv, dtype=np.uint64).reshape(-1, 2)
+    cap = cap or max(16, rows // 2 + 1)
+    out = np.empty(3 * cap, dtype=np.uint64)
+    found = lib().orc_bottomup_smax_tables(_p(lcpbytes, _u8p), llv.ctypes.data_as(ctypes.c_void_p),
+                                           len(llv), _p(bwt, _u8p), rows, minlen, _p(out, _u64p),
+                                           cap)
+    assert found <= cap
+    return _triples(out, found)
+
+
+def lcp_intervals(lcpbytes, llv, nonspecials, cap):
+    """orc_lcp_intervals: (lcp, lb, rb, father lcp, father lb), pop order."""
+    llv = np.ascontiguousarray(llv, dtype=np.uint64).reshape(-1, 2)
+    out = np.empty(5 * cap, dtype=np.uint64)
+    found = lib().orc_lcp_intervals(_p(lcpbytes, _u8p), llv.ctypes.data_as(ctypes.c_void_p),
+                                    len(llv), nonspecials, _p(out, _u64p), cap)
+    assert found <= cap, (found, cap)
+    return out[: 5 * found].reshape(-1, 5).copy()
+
+
+def maxpairs_blocks(lcpbytes, llv, bwt, suftab, nonspecials, minlen, cap):
+    """orc_maxpairs_blocks: maximal pairs by definition per block, unordered
+    (suftab None: rows instead of positions)."""
+    llv = np.ascontiguousarray(llv, dtype=np.uint64).reshape(-1, 2)
+    out = np.empty(3 * cap, dtype=np.uint64)
+    found = lib().orc_maxpairs_blocks(_p(lcpbytes, _u8p), llv.ctypes.data_as(ctypes.c_void_p),
+                                      len(llv), _p(bwt, _u8p),
+                                      _p(suftab, _u64p) if suftab is not None else None, nonspecials,
+                                      minlen, _p(out, _u64p), cap)
+    assert found <= cap, (found, cap)
     return _triples(out, found)
 
 

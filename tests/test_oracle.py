@@ -251,3 +251,79 @@ def test_dfs_lines_equal_bottomup_lines_random(seed):
             t[rng.random(n) < 0.02] = rng.choice(np.array([254, 255], np.uint8))
         e = O.Esa(t)
         assert np.array_equal(O.dfs_events(e), _lb_lines(O.bottomup_events(e)))
+
+
+def test_prj_longest_is_row_of_suffix_0(tmp_path):
+    """longest= (src/match/sfx-outprj.c:70-73) is the row holding suffix 0;
+    esa-map.c:384-387 refuses a .suf load without it."""
+    idx = str(tmp_path / "at")
+    O.index_fasta(os.path.join(GOLDEN, "Atinsert.fna"), idx)
+    e = oracle_esa("Atinsert.fna")
+    assert int(_prj(idx + ".prj")["longest"]) == int(np.flatnonzero(e.suftab == 0)[0])
+
+
+def _bottomup_tables_cases():
+    for name, minlens in (("Atinsert.fna", (1, 8, 20)), ("at1MB", (10, 20, 255, 300, 517))):
+        yield name, minlens
+
+
+@pytest.mark.parametrize("name,minlens", list(_bottomup_tables_cases()))
+def test_bottomup_over_tables_equals_linsmax(name, minlens):
+    """orc_bottomup_smax_tables (the stack walk over .lcp/.llv/.bwt as the
+    sequential reader hands them out; bench.py's reference-algorithm CPU
+    anchor) == orc_linsmax over all rows."""
+    e = oracle_esa(name)
+    for minlen in minlens:
+        a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        b = O.bottomup_smax_tables(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        assert np.array_equal(a, b), (name, minlen)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_bottomup_over_tables_random(seed):
+    rng = np.random.default_rng(100 + seed)
+    t = _random_text(rng, int(rng.integers(2, 400)), int(rng.integers(1, 5)), 0.03)
+    if seed % 2:
+        t = np.tile(t[:5], 80)
+    e = O.Esa(t)
+    for minlen in (1, 2, 5, 300):
+        a = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        b = O.bottomup_smax_tables(e.lcpbytes, e.llv, e.bwt, e.nonspecials, minlen)
+        assert np.array_equal(a, b)
+
+
+def _intervals_from_events(ev):
+    """(lcp, lb, rb, fatherlcp, fatherlb) of every popped interval: each
+    visit_lcp_interval event is followed by its branching edge to the father."""
+    out = []
+    for k in np.flatnonzero(ev[:, 0] == 2):
+        l, lb, rb = ev[k, 2:5]
+        assert ev[k + 1, 0] == 1 and tuple(ev[k + 1, 4:7]) == (l, lb, rb)
+        out.append((l, lb, rb, ev[k + 1, 2], ev[k + 1, 3]))
+    return np.array(out, dtype=np.uint64).reshape(-1, 5)
+
+
+@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB", "Reads2.fna", "TTT-small.fna"])
+def test_lcp_intervals_equal_bottomup_events(name):
+    """orc_lcp_intervals (F3's checker past 2^32 rows: tables only, no
+    suffix array) == the intervals and fathers of orc_bottomup_events."""
+    e = oracle_esa(name)
+    want = _intervals_from_events(O.bottomup_events(e))
+    got = O.lcp_intervals(e.lcpbytes, e.llv, e.nonspecials, cap=e.nonspecials + 1)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("name,minlen", [("Atinsert.fna", 8), ("Atinsert.fna", 14),
+                                         ("at1MB", 20), ("at1MB", 300)])
+def test_maxpairs_blocks_equal_maxpairs(name, minlen):
+    """orc_maxpairs_blocks (maximal pairs by definition, per block; F2's
+    checker past 2^32 rows) == orc_maxpairs as a set."""
+    e = oracle_esa(name)
+    want = O.maxpairs(e, minlen)
+    got = O.maxpairs_blocks(e.lcpbytes, e.llv, e.bwt, e.suftab, e.nonspecials, minlen,
+                            cap=len(want) + 16)
+    def key(a):
+        a = np.column_stack([a[:, 0], np.sort(a[:, 1:], axis=1)])
+        return a[np.lexsort(a.T[::-1])]
+    assert len(want) > 0
+    assert np.array_equal(key(got), key(want))

@@ -172,3 +172,43 @@ def test_window_stream_policy(human10, nt, dense):
     assert np.array_equal(q.fetch_triples(), r.fetch_triples())
     for x in (p, q, r):
         x.close()
+
+
+def test_run_part_order_enforced(human10):
+    """Part 1's K3 resets the state the next part 0 starts from: a second
+    part 0 before part 1, or a part 1 with no part 0 pending, is refused
+    (include/gt_smax_hip.h, gt_smax_plan_run_part) and the plan stays usable."""
+    esa, host = human10
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    p = esa.plan(20)
+    with pytest.raises(G.SmaxError):
+        p.run_part(1)
+    p.run_part(0)
+    with pytest.raises(G.SmaxError):
+        p.run_part(0)
+    p.run_part(1)
+    assert np.array_equal(p.fetch_triples(), want)
+    p.run()
+    assert np.array_equal(p.fetch_triples(), want)
+    p.close()
+
+
+def test_close_in_flight_then_reuse(human10):
+    """A plan closed right after run() with no synchronisation hands its
+    buffers back to the caching pool only once its kernels have finished:
+    new plans and an ESA build that take the same blocks at once still give
+    the oracle's records."""
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    for _ in range(3):
+        p = esa.plan(20)
+        for _ in range(4):
+            p.run()
+        p.close()                       # K1..K3 may still be running
+        q = esa.plan(20)
+        small = G.DeviceEsa(G.synth_genome("uniform", 1_000_000, 3, threads=4), device=0)
+        q.run()
+        assert np.array_equal(q.fetch_triples(), want)
+        q.close()
+        small.release()

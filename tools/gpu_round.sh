@@ -1,0 +1,69 @@
+#!/bin/bash
+# The one GPU-box recipe (run through gpurun from the repo root):
+#
+#   bash tools/gpu_round.sh TAG STEP [STEP ...]
+#
+#   tests            pytest -m gpu (all), -v, per-test timeout
+#   tests:EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench:CONFIG     python bench.py --config CONFIG        -> bench_CONFIG.json
+#   pmc:CONFIG       K1 HBM bytes: rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE
+#                    (separate passes) over tools/k1_once.py CONFIG
+#                    -> pmc_CONFIG.json (config + build id stamped)
+#   sq:CONFIG        K1 SQ instruction / wait counters, one pass -> sq_CONFIG.json
+#   prof:CONFIG      rocprofv3 --kernel-trace --stats of a bench run
+#                    -> kernel_stats_CONFIG.csv + the bench line under it
+#   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
+#
+# Outputs go to gpurun_out/TAG/.  Every GPU step runs under its own timeout
+# and the script stops at the first failure (set -e).
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+TAG=$1
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
+for S in "$@"; do
+  echo "[gpu_round] $S $(date +%T)"
+  case $S in
+    tests)
+      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+        > "$O/gpu_tests.log" 2>&1 ;;
+    tests:*)
+      K=${S#tests:}
+      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+        -k "$K" > "$O/gpu_tests_sel.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    bench:*)
+      C=${S#bench:}
+      timeout -k 10 900 python -u bench.py --config "$C" > "$O/bench_$C.json" 2> "$O/bench_$C.err" ;;
+    pmc:*)
+      C=${S#pmc:}
+      for X in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $X --kernel-include-regex smax_scan_kernel \
+          -d "$O/pmc_${C}_$X" -o p -- python3 "$R/tools/k1_once.py" "$C" 5 > "$O/pmc_${C}_$X.log" 2>&1)
+      done
+      python3 tools/rocpd_summary.py pmc "$O/pmc_$C.json" smax_scan_kernel "$C" \
+        "$O/pmc_${C}_FETCH_SIZE/p_results.db" "$O/pmc_${C}_WRITE_SIZE/p_results.db" ;;
+    sq:*)
+      C=${S#sq:}
+      (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $SQ --kernel-include-regex smax_scan_kernel \
+        -d "$O/sq_$C" -o p -- python3 "$R/tools/k1_once.py" "$C" 5 > "$O/sq_$C.log" 2>&1)
+      python3 tools/rocpd_summary.py pmc "$O/sq_$C.json" smax_scan_kernel "$C" "$O/sq_$C/p_results.db" ;;
+    prof:*)
+      C=${S#prof:}
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_$C" -o p -- \
+        python3 "$R/bench.py" --config "$C" --steps 20 --warmup 3 --no-cpu-baseline --no-end-to-end \
+        > "$O/prof_bench_$C.json" 2> "$O/prof_bench_$C.err")
+      python3 tools/rocpd_summary.py stats "$O/prof_$C/p_results.db" "$O/kernel_stats_$C.csv" ;;
+    shards:*)
+      W=${S#shards:}
+      timeout -k 10 600 python -u tools/shard_step.py human 3e9 20 "$W" > "$O/shards_$W.txt" 2>&1 ;;
+    *)
+      echo "unknown step $S"; exit 2 ;;
+  esac
+done
+echo "[gpu_round] done $(date +%T)"

@@ -2,8 +2,14 @@
 """Turn rocprofv3 rocpd databases into the summaries committed under
 profiles/.
 
-  rocpd_summary.py stats  DB OUT.csv            kernel-trace --stats table
-  rocpd_summary.py pmc    OUT.json KERNEL DB... per-launch HBM bytes of KERNEL
+  rocpd_summary.py stats  DB OUT.csv                   kernel-trace --stats table
+  rocpd_summary.py pmc    OUT.json KERNEL CONFIG DB... per-launch counters of KERNEL
+
+`pmc` keeps every counter of the passes (per launch), the HBM bytes when
+FETCH_SIZE and WRITE_SIZE are among them, the bench config the passes ran
+(tools/k1_once.py CONFIG) and the build identity of the library they ran on
+(gt_smax_build_id): bench.py uses a profile's traffic only when both match
+the run it reports.
 
 For `pmc`, each DB is one `rocprofv3 --pmc <COUNTER>` pass (FETCH_SIZE and
 WRITE_SIZE do not fit one pass on gfx950).  FETCH_SIZE / WRITE_SIZE are in
@@ -36,8 +42,11 @@ def stats(db, out):
     print("wrote", out, len(rows), "kernels")
 
 
-def pmc(out, kernel, dbs):
-    res = {"kernel": kernel, "passes": {}}
+def pmc(out, kernel, config, dbs):
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import genometools_smax_amd as G
+    res = {"kernel": kernel, "config": config, "build_id": G.build_id(), "passes": {}}
     for db in dbs:
         con = sqlite3.connect(db)
         rows = con.execute("select counter_name, value, duration from counters_collection "
@@ -54,9 +63,10 @@ def pmc(out, kernel, dbs):
         res["write_bytes_per_launch"] = 1024 * res["write_kib_per_launch"]
     if fetch and write:
         res["hbm_bytes_per_launch"] = res["read_bytes_per_launch"] + res["write_bytes_per_launch"]
-    res["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
-                     "read = 2 x 1024 x FETCH_SIZE (gfx950 half-count correction), "
-                     "write = 1024 x WRITE_SIZE")
+        res["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                         "read = 2 x 1024 x FETCH_SIZE (gfx950 half-count correction), "
+                         "write = 1024 x WRITE_SIZE")
+    res["per_launch"] = {k: sum(v) / len(v) for k, v in res["passes"].items() if v}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "passes"}, indent=1))
@@ -66,4 +76,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     else:
-        pmc(sys.argv[2], sys.argv[3], sys.argv[4:])
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5:])
