@@ -109,7 +109,6 @@ def test_maxpairs_past_2_32(tables):
     suf_t = torch.arange(N, -1, -1, dtype=torch.int64, device="cuda")    # suftab[r] = N - r
     plan = G.MaxpairsPlan(lcp_t.data_ptr(), bwt_t.data_ptr(), llv_t.data_ptr(), len(llvtab),
                           suf_t.data_ptr(), 8, N, minlen, device=0)
-    del suf_t
     plan.count()
     T = plan.total()
     assert T == len(want), (T, len(want))
@@ -118,7 +117,7 @@ def test_maxpairs_past_2_32(tables):
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint64).reshape(-1, 3).copy()
     plan.close()
-    del lcp_t, llv_t, bwt_t, out
+    del lcp_t, llv_t, bwt_t, suf_t, out       # the plan borrowed them until here
     # positions -> rows (suftab[r] = N - r): pos1 < pos2 is row2 < row1
     rows = np.column_stack([got[:, 0], np.uint64(N) - got[:, 2], np.uint64(N) - got[:, 1]])
 

@@ -165,3 +165,57 @@ def test_full_tables_bench_split(world, kind, bases, seed):
     got, want = r["got"], r["want"]
     assert len(want) > 100
     assert np.array_equal(got, want), (len(got), len(want))
+
+
+# ---------------------------------------------------------------- > 1 device
+# The measured multi-GPU configuration: one process per device, the nccl
+# backend (RCCL over xGMI), boundary records all-gathered in device memory
+# from the plan's own zero-copy boundary tensor, exactly bench.py's step.
+# Needs as many visible devices as ranks; skipped on a one-GPU box.
+
+def _worker_nccl(rank, world, port, kind, bases, seed, minlen, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", rank))
+    try:
+        text = G.synth_genome(kind, bases, seed, threads=4)
+        n = len(text)
+        N = n - int(np.count_nonzero(text >= 254))
+        begin = 1 + (N - 1) * rank // world
+        end = 1 + (N - 1) * (rank + 1) // world
+        esa = G.DeviceEsa64(text, device=rank, row_lo=begin - 1, row_hi=end + 1)
+        plan = esa.plan(minlen, begin, end, capacity=(end - begin) // 2 + 16)
+        stream = torch.cuda.current_stream().cuda_stream
+        recv = torch.zeros(G.BOUNDARY_BYTES * world, dtype=torch.uint8, device="cuda")
+        send = plan.boundary_tensor()
+        for _ in range(3):                       # repeated steps, as the bench runs them
+            plan.run_part(0, stream)
+            work = dist.all_gather_into_tensor(recv, send, async_op=True)
+            plan.run_part(1, stream)
+            work.wait()
+            plan.stitch(recv.data_ptr(), world, rank, stream)
+        torch.cuda.synchronize()
+        trip = plan.fetch_triples()
+        plan.close()
+        esa.release()
+        parts = [None] * world
+        dist.all_gather_object(parts, trip)
+        if rank == 0:
+            full = G.DeviceEsa(text, device=0)
+            host = full.download()
+            full.release()
+            want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen, threads=4)
+            np.savez(out_path, got=np.concatenate(parts).reshape(-1, 3), want=want)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 visible GPUs")
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_nccl_ranks_one_per_device(world):
+    if torch.cuda.device_count() < world:
+        pytest.skip("needs %d visible GPUs" % world)
+    r = _spawn(_worker_nccl, world, "human", 30_000_000, 5, 20)
+    assert len(r["want"]) > 100
+    assert np.array_equal(r["got"], r["want"]), (len(r["got"]), len(r["want"]))

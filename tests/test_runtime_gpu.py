@@ -212,3 +212,15 @@ def test_close_in_flight_then_reuse(human10):
         assert np.array_equal(q.fetch_triples(), want)
         q.close()
         small.release()
+
+
+@pytest.mark.skipif(G.device_count() < 2, reason="needs >= 2 visible GPUs")
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_host_entry_across_devices(human10, shards):
+    """num_gpus > 1 with several devices visible: one host thread per device
+    and the in-library RCCL all-gather (ncclCommInitAll) between them."""
+    esa, host = human10
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    got = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], esa.totallength,
+                           esa.nonspecials, 20, shards)
+    assert np.array_equal(got, want)
