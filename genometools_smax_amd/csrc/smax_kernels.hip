@@ -11,24 +11,27 @@
 // BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
-// One pass = five launches on one stream, no host synchronisation
-// (DESIGN.md §4):
-//   K0  smax_head_kernel     per-run resets (pending-plateau slot, deferral
-//                            count, K1b pool cursor)
-//   K1  smax_scan_kernel     the streaming kernel
-//   K1b smax_defer_kernel    the plan-time static list (shard edges,
-//                            dense-.llv windows) followed by K1's runtime
+// One pass = four launches on one stream, no host synchronisation
+// (DESIGN.md §4); gt_smax_plan_run_part splits them into part 0 (scan: K1,
+// K1b; the boundary record is final after it) and part 1 (compaction: K2, K3):
+//   K1  smax_scan_kernel     the streaming kernel; its block 0 also clears
+//                            the pending-plateau slot of this run
+//   K1b smax_defer_wg_kernel one workgroup per deferred tile: the plan-time
+//                            static list (shard edges, windows with more
+//                            .llv values than K1 stages), then K1's runtime
 //                            deferrals (exact-queue overflow, tiles with more
-//                            records than a slot holds); one workgroup
-//                            computes the boundary head (GT_SMAX_K1B_MODE 0-3
-//                            keep the older placements of the static list:
-//                            side stream beside K1, before or after K1)
+//                            records than a slot holds); one extra workgroup
+//                            computes the boundary head
 //   K2  smax_block_sum_kernel  records per 256 tiles (K3's offsets; a
 //                            decoupled look-back inside K3 instead measured
 //                            1.3 -> 1.9 ms at C3: the prefix chain over 5663
 //                            workgroups serialises)
 //   K3  smax_compact_kernel  ordered copy of the tiles' records -> ascending
-//                            lb
+//                            lb; resets the deferral count and pool cursor
+//                            for the next run (their last reader, K1b, is done)
+// (smax_head_kernel -- "K0", the per-run resets -- and the older K1b
+// placements, GT_SMAX_K1B_MODE 0-3 with smax_defer_kernel, remain as
+// diagnostics.)
 //
 // K1: every wave is an independent worker on 2048-row tiles (tile = wave id
 // + k * waves in grid; 8 generations of resident 4-wave workgroups), no

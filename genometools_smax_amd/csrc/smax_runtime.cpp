@@ -11,8 +11,8 @@
 //      are packed to their bit planes during the fill (0.5 B/row over PCIe
 //      and in HBM instead of 1 B/row), so no pass over byte BWT is left for
 //      the device;
-//   2. creates and runs each shard's plan (K0, K1 || static K1b, K1b, K3) on
-//      the device's stream;
+//   2. creates and runs each shard's plan (K1 -> K1b -> K2 -> K3, see
+//      smax_kernels.hip) on the device's stream;
 //   3. exchanges the 152-byte boundary records: an RCCL all-gather over the
 //      used devices (ncclAllGather on a communicator the library creates
 //      with ncclCommInitAll, cached for the process), or device-to-device
@@ -25,7 +25,9 @@
 //
 // Device memory (tables, plan buffers) comes from a per-device caching
 // allocator and pinned staging buffers live for the process, so repeated
-// calls do not pay hipMalloc/hipHostMalloc of multi-GB buffers per call;
+// calls do not pay hipMalloc/hipHostMalloc of multi-GB buffers per call (a
+// freed block is reused only after its device has finished the work queued
+// before the free, smax_dev_free);
 // gt_smax_release_cache() returns everything (GT_SMAX_NO_CACHE=1: free
 // before return).
 #include <dlfcn.h>

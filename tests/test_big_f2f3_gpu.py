@@ -106,7 +106,14 @@ def test_maxpairs_past_2_32(tables):
     assert np.count_nonzero(want[:, 2] >= 2 ** 32) > 1000
     lcp_t, llv_t = _dev(lcp, llvtab)
     bwt_t = torch.from_numpy(bwt).to("cuda")
-    suf_t = torch.arange(N, -1, -1, dtype=torch.int64, device="cuda")    # suftab[r] = N - r
+    # suftab[r] = N - r, filled in chunks of 2^30 (one torch.arange over all
+    # N + 1 > 2^32 elements left the rows past 2^32 zero on the box)
+    suf_t = torch.empty(N + 1, dtype=torch.int64, device="cuda")
+    for c0 in range(0, N + 1, 1 << 30):
+        c1 = min(N + 1, c0 + (1 << 30))
+        suf_t[c0:c1] = torch.arange(N - c0, N - c1, -1, dtype=torch.int64, device="cuda")
+    probe = [0, 2 ** 32 - 1, 2 ** 32, 2 ** 32 + 12345, N]
+    assert [int(suf_t[r]) for r in probe] == [N - r for r in probe]
     plan = G.MaxpairsPlan(lcp_t.data_ptr(), bwt_t.data_ptr(), llv_t.data_ptr(), len(llvtab),
                           suf_t.data_ptr(), 8, N, minlen, device=0)
     plan.count()

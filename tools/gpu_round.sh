@@ -14,6 +14,7 @@
 #   prof:CONFIG      rocprofv3 --kernel-trace --stats of a bench run
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
+#   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #
 # Outputs go to gpurun_out/TAG/.  Every GPU step runs under its own timeout
 # and the script stops at the first failure (set -e).
@@ -59,6 +60,10 @@ for S in "$@"; do
         python3 "$R/bench.py" --config "$C" --steps 20 --warmup 3 --no-cpu-baseline --no-end-to-end \
         > "$O/prof_bench_$C.json" 2> "$O/prof_bench_$C.err")
       python3 tools/rocpd_summary.py stats "$O/prof_$C/p_results.db" "$O/kernel_stats_$C.csv" ;;
+    llvstats)
+      for C in c3 c5; do
+        timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1
+      done ;;
     shards:*)
       W=${S#shards:}
       timeout -k 10 600 python -u tools/shard_step.py human 3e9 20 "$W" > "$O/shards_$W.txt" 2>&1 ;;
