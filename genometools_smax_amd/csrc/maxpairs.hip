@@ -232,8 +232,10 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
         if (EMIT && o + c < capacity) {
           uint64_t *w = out + 3 * (o + c);
           w[0] = m;
-          w[1] = si[q] < sj ? si[q] : sj;
-          w[2] = si[q] < sj ? sj : si[q];
+          if (!ORD) {                      // row-order pass: (len, pos1 < pos2)
+            w[1] = si[q] < sj ? si[q] : sj;
+            w[2] = si[q] < sj ? sj : si[q];
+          }
           if (ORD) {
             if (m != ev_l) {
               ev_l = m;
@@ -251,6 +253,15 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
             else if (cx < 254u && cy < 254u) { cls = (cx << 8) | cy; r1 = x; r2 = y; }
             else if (cx < 254u) { cls = (cx << 8) | 254u; r1 = y; r2 = x; }
             else { cls = 254u << 8; r1 = x; r2 = (cy << rb) | y; }
+            // the argument order of the reference's GtProcessmaxpairs call:
+            // a leaf edge passes (new leaf, earlier position)
+            // (src/match/esa-maxpairs.c:128,261), a branching edge (father's
+            // position, son's) except when the son's position has a unique
+            // left symbol and the father's not (cartproduct1 with the son's
+            // position as the "leaf", :128 via :307-312)
+            const bool later_first = ev_leaf || (cx < 254u && cy >= 254u);
+            w[1] = later_first ? sj : si[q];
+            w[2] = later_first ? si[q] : sj;
             const uint64_t e = o + c;
             K->k1[e] = r2;
             K->k2[e] = (cls << rb) | r1;

@@ -80,8 +80,10 @@
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
 #define SMAX_SLOT_WIDE 0x80000000u
-#define SMAX_LLV_CAP 496                              // .llv values staged in K1's LDS (u16):
-                                                      // one 16-byte DMA per lane
+#define SMAX_LLV_CAP 240                              // .llv values staged in K1's LDS (u16):
+                                                      // one 16-byte DMA per lane; windows
+                                                      // with more go to the static K1b list
+                                                      // (the LDS budget of 5 workgroups/CU)
 // llv_win[t].y: entries in the window (12 bits), of them in the left halo
 // (5 bits, <= 16), bit 31: K1 leaves the tile to the static K1b list
 #define SMAX_WIN_N(y) ((y) & 0xfffu)
@@ -475,6 +477,9 @@ struct SmaxWindowPk {          // packed BWT (DNA): 0.5 B per row
   uint64_t P[SMAX_LDSB / 16 + 2];   // + 2: the tail DMA moves 2 lanes x 16 B
   uint16_t val16[SMAX_LLV_CAP];
 };
+// window_scratch: 64 staged records + 2 x 64 results in the BWT region
+static_assert(sizeof(((SmaxWindowPk *) 0)->P) >= 64 * 8 + 2 * 64 * 4, "packed window scratch");
+static_assert(SMAX_LDSB >= 64 * 8 + 2 * 64 * 4, "byte window scratch");
 
 // Issue the DMA of tile `l0` (local index) into the calling wave's window
 // w: 16 B per lane per instruction (1 KiB per wave instruction), the two
@@ -1067,10 +1072,14 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const bool all_exact = a.minlen > 128;
-  uint32_t *res_lcp = ent + DL, *res_w = ent + 2 * DL;
-  uint8_t *segl = reinterpret_cast<uint8_t *>(ent + 3 * DL);
+  // the exact starts' results and the staged records live in the window's
+  // BWT region, dead once the starts are evaluated (nothing after reads
+  // BWT symbols); the next DMA into this window is issued after the records
+  // have moved to registers (smax_scan_body)
+  uint32_t *res_lcp = reinterpret_cast<uint32_t *>(stg + SMAX_SSLOT), *res_w = res_lcp + DL;
+  uint8_t *segl = reinterpret_cast<uint8_t *>(ent + DL);
   // accepted exact starts, one 16-bit row mask per compacted segment
-  uint32_t *accw = ent + 3 * DL + 2 * 64 / 4;
+  uint32_t *accw = ent + DL + 2 * 64 / 4;
   // compact the active segments (id = round * 64 + lane, row order)
   const uint64_t ltm = lanemask_lt();
   const uint64_t m0 = __ballot(segpre & 1u), m1 = __ballot((segpre >> 1) & 1u);
@@ -1143,19 +1152,24 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     accw[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i0 = 0; i0 < nL; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      if (i < nL) {
-        const uint32_t e = ent[i];
-        const uint32_t ro = e & 0x7ffu, si = (e >> 11) & 0x7fu;
-        uint32_t cur;
-        uint64_t j;
-        const bool acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
-        res_lcp[i] = cur;
-        res_w[i] = (uint32_t) (j - (g0 + ro) + 2);
-        if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
-        wide |= acc && j - (g0 + ro) + 2 > SMAX_PK_WMAX;
-      }
+    static_assert(DL <= 64, "one exact start per lane");
+    const uint32_t i = lane;
+    uint32_t cur = 0, width = 0;
+    if (i < nL) {
+      const uint32_t e = ent[i];
+      const uint32_t ro = e & 0x7ffu, si = (e >> 11) & 0x7fu;
+      uint64_t j;
+      const bool acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
+      width = (uint32_t) (j - (g0 + ro) + 2);
+      if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
+      wide = acc && j - (g0 + ro) + 2 > SMAX_PK_WMAX;
+    }
+    // every lane's BWT reads are done: the results may now overwrite them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (i < nL) {
+      res_lcp[i] = cur;
+      res_w[i] = width;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1219,6 +1233,16 @@ __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, S
 
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = W->B; t.P = nullptr; }
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = W->P; t.B = nullptr; }
+
+// A window's BWT region once the tile's exact starts are evaluated: the
+// staged records (SMAX_SSLOT u64) and the starts' results (2 x SMAX_DLIST
+// u32); nothing of the tile reads BWT symbols after that point, and the
+// wave's next DMA into this window follows the move of the records to
+// registers.  Keeps K1 inside 32 KiB of LDS per workgroup (5 per CU).
+__device__ __forceinline__ uint64_t *window_scratch(SmaxWindow *W) {
+  return reinterpret_cast<uint64_t *>(W->B);
+}
+__device__ __forceinline__ uint64_t *window_scratch(SmaxWindowPk *W) { return W->P; }
 
 // Filter of a landed window (one wave): per-lane segment "any byte >=
 // min(minlen,128)" bits; the .llv values are staged with the window, their
@@ -1300,11 +1324,11 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_THREADS / 64][2];
   __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_THREADS / 64][2][2];
   __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
-  // per wave: wave_detect_direct's queue and results (3 x SMAX_DLIST u32),
-  // compacted segment ids and accepted masks
-  __shared__ uint32_t sQueue[SMAX_THREADS / 64][3 * SMAX_DLIST + 2 * 64 / 4 + 64];
-  // per wave: the tile's packed records in slot order (one slot's worth)
-  __shared__ __attribute__((aligned(16))) uint64_t sStage[SMAX_THREADS / 64][SMAX_SSLOT];
+  // per wave: wave_detect_direct's queue of exact starts, compacted segment
+  // ids and accepted masks (the starts' results and the tile's staged
+  // records go to the current window's BWT region once it is dead:
+  // window_scratch)
+  __shared__ uint32_t sQueue[SMAX_THREADS / 64][SMAX_DLIST + 2 * 64 / 4 + 64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1415,8 +1439,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const bool stat = static_deferred(a, wnf);
     bool defer = !stat && wave_pre && (a.dbg & 128u);
     if (!stat && !defer && wave_pre) {
-      wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave], sStage[wave],
-                                                    segpre_bits);
+      wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave],
+                                                    window_scratch(W), segpre_bits);
       // exact-queue overflow (UINT32_MAX) or more records than the tile's
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
@@ -1431,7 +1455,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       // are stored at the start of the next iteration (see above)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      prec = sStage[wave][lane];
+      prec = window_scratch(W)[lane];
       ptile = tile;
       pcnt = wcount;
     }
@@ -2010,21 +2034,21 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
 // waves/SIMD is the production kernel; the _diag build keeps the
 // GT_SMAX_DEBUG ablation switches (used only when the variable is set).
 // Byte BWT (any alphabet): 3-4 waves/SIMD.
-__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false>(a);
 }
 // dense .llv shards (plan picks it above SMAX_FFPV_DENSITY entries per row):
 // the 255-after-255 relations of a segment are resolved vectorised
 // (ffp_resolve); measured C5 (12 Gbp plant, 0.94 % of rows) step 6.21 ->
 // 5.72 ms, C3 (human, 0.39 %) 1.253 -> 1.272 ms, hence the switch
-__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_dense(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_dense(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true>(a);
 }
 // non-temporal window stream (GtSmaxPlan::nt)
-__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_nt(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, false, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true, true>(a);
 }
 __global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {

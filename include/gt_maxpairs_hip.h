@@ -17,12 +17,16 @@
  *                                 products of src/match/esa-maxpairs.c:181-360.
  *                                 The callback has the argument meaning of
  *                                 GtProcessmaxpairs (src/match/esa-maxpairs.h:38-43):
- *                                 (len, pos1, pos2), here with pos1 < pos2
- *                                 (the order gt_simpleexactselfmatchoutput
- *                                 swaps them into, src/tools/gt_repfind.c:60-65).
- *                                 Pairs AND their order are the reference's:
- *                                 the callback sees them in the order the
- *                                 traversal calls GtProcessmaxpairs.
+ *                                 (len, pos1, pos2).  Pairs, their order AND
+ *                                 the order of pos1/pos2 in each call are
+ *                                 the reference's: the callback sees exactly
+ *                                 the calls the traversal makes (a leaf edge
+ *                                 passes the new leaf first, a branching
+ *                                 edge the father's position first,
+ *                                 src/match/esa-maxpairs.c:127-157,259-261,
+ *                                 349-351); gt_simpleexactselfmatchoutput
+ *                                 swaps them into pos1 < pos2 itself
+ *                                 (src/tools/gt_repfind.c:60-65).
  *  gt_maxpairs_hip_enumerate_to_buffer  same, malloc'd (len,pos1,pos2) triples.
  *
  * A maximal pair of length L >= minlen is a pair of suffix-array rows
@@ -93,8 +97,9 @@ int gt_maxpairs_plan_emit(GtMaxpairsPlan *plan, uint64_t *out_dev, uint64_t capa
                           void *stream);
 
 /* The emission pass in the reference's order (the order of
- * gt_maxpairs_hip_enumerate's callbacks): the pairs are written with their
- * event/row sort keys and permuted by stable radix sorts.  Synchronises the
+ * gt_maxpairs_hip_enumerate's callbacks, with the reference's pos1/pos2
+ * argument order): the pairs are written with their event/row sort keys and
+ * permuted by stable radix sorts.  Synchronises the
  * stream (the pair count sizes its temporary buffers, ~80 bytes per pair);
  * capacity must be >= the count, else -1.  Requires a preceding count pass. */
 int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *plan, uint64_t *out_dev, uint64_t capacity,

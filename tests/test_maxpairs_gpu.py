@@ -6,8 +6,9 @@ Pinned to the reference's own golden `testdata/repfind-8-Atinsert.txt`
 oracle's restatement of the bottom-up maxpairs traversal
 (`orc_maxpairs`, src/match/esa-bottomup-maxpairs.inc:136-264) on fixtures and
 seeded texts with specials and .llv values.  The host entry points and
-`emit_ordered` emit in the reference's order: compared pair by pair, in
-order (each pair as (len, min pos, max pos), the swap
+`emit_ordered` emit in the reference's order, each call's (pos1, pos2) in
+the reference's argument order: compared pair by pair (exactly on the
+fixtures; elsewhere as (len, min pos, max pos), the swap
 gt_simpleexactselfmatchoutput makes); the row-order device pass
 (`plan.emit`) is compared as a set.
 """
@@ -55,8 +56,8 @@ def test_atinsert_matches_reference_golden():
 def test_atinsert_pair_set(minlen):
     e = oracle_esa("Atinsert.fna")
     got = _gpu(e, minlen)
-    assert np.all(got[:, 1] < got[:, 2])
-    assert np.array_equal(got, _ordered(O.maxpairs(e, minlen)))
+    # the reference's calls exactly: order and pos1/pos2 argument order
+    assert np.array_equal(got, O.maxpairs(e, minlen))
 
 
 @pytest.mark.parametrize("minlen", [20, 50, 255, 300])
