@@ -125,8 +125,10 @@ def test_maxpairs_past_2_32(tables):
     got = out.cpu().numpy().view(np.uint64).reshape(-1, 3).copy()
     plan.close()
     del lcp_t, llv_t, bwt_t, suf_t, out       # the plan borrowed them until here
-    # positions -> rows (suftab[r] = N - r): pos1 < pos2 is row2 < row1
-    rows = np.column_stack([got[:, 0], np.uint64(N) - got[:, 2], np.uint64(N) - got[:, 1]])
+    # positions -> rows (suftab[r] = N - r); each pair comes in the reference's
+    # argument order, compared here as (len, smaller row, larger row)
+    r1, r2 = np.uint64(N) - got[:, 1], np.uint64(N) - got[:, 2]
+    rows = np.column_stack([got[:, 0], np.minimum(r1, r2), np.maximum(r1, r2)])
 
     def key(a):
         return a[np.lexsort(a.T[::-1])]

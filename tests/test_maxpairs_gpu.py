@@ -32,11 +32,6 @@ def _norm(p):
     return q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]
 
 
-def _ordered(p):
-    p = np.asarray(p, dtype=np.uint64).reshape(-1, 3)
-    return np.stack([p[:, 0], np.minimum(p[:, 1], p[:, 2]), np.maximum(p[:, 1], p[:, 2])], axis=1)
-
-
 def _gpu(e, minlen, suf_dtype=np.uint64):
     return G.enumerate_maxpairs(e.lcpbytes, e.llv, e.bwt, e.suftab.astype(suf_dtype), e.n,
                                 e.nonspecials, minlen)
@@ -64,7 +59,7 @@ def test_atinsert_pair_set(minlen):
 def test_at1mb_pair_set(minlen):
     e = oracle_esa("at1MB")
     got = _gpu(e, minlen)
-    assert np.array_equal(got, _ordered(O.maxpairs(e, minlen)))
+    assert np.array_equal(got, O.maxpairs(e, minlen))
     if minlen == 20:
         assert len(O.format_pairs(got, e.separators)) == 4507
 
@@ -95,7 +90,7 @@ def test_random_repetitive(seed):
     t = _repetitive(rng, int(rng.integers(20000, 80000)), [0.0, 0.001, 0.01, 0.05][seed])
     e = O.Esa(t)
     for minlen in (12, 30, 256):
-        assert np.array_equal(_gpu(e, minlen), _ordered(O.maxpairs(e, minlen))), minlen
+        assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen)), minlen
 
 
 def test_long_lcp_values():
@@ -107,7 +102,7 @@ def test_long_lcp_values():
     e = O.Esa(t)
     assert len(e.llv) > 0
     for minlen in (100, 255, 256, 1000, 1200, 1201):
-        assert np.array_equal(_gpu(e, minlen), _ordered(O.maxpairs(e, minlen))), minlen
+        assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen)), minlen
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -120,7 +115,7 @@ def test_small_edge_texts(seed):
             t[rng.random(n) < 0.1] = 254
         e = O.Esa(t)
         for minlen in (1, 2, 5):
-            assert np.array_equal(_gpu(e, minlen), _ordered(O.maxpairs(e, minlen)))
+            assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen))
 
 
 def test_device_resident_plan_and_seqpos_map():
@@ -138,7 +133,7 @@ def test_device_resident_plan_and_seqpos_map():
     ordered = torch.empty(3 * total, dtype=torch.int64, device="cuda")
     p.emit_ordered(ordered.data_ptr(), total)
     assert np.array_equal(ordered.cpu().numpy().view(np.uint64).reshape(-1, 3),
-                          _ordered(O.maxpairs(e, 20)))
+                          O.maxpairs(e, 20))
     # F4: seqnum / relpos on the device == the oracle's formatter
     sep = torch.from_numpy(e.separators.view(np.int64)).cuda()
     mapped = torch.empty(5 * total, dtype=torch.int64, device="cuda")
@@ -190,7 +185,7 @@ def test_homopolymer_block_costs_its_output(runlen):
     dt = time.perf_counter() - t0
     want = O.maxpairs(_TablesEsa(text, d), 20)
     assert len(want) > runlen // 2
-    assert np.array_equal(got, _ordered(want))
+    assert np.array_equal(got, want)
     assert dt < 20.0, dt
 
 
