@@ -34,7 +34,7 @@
 // diagnostics.)
 //
 // K1: every wave is an independent worker on 2048-row tiles (tile = wave id
-// + k * waves in grid; 8 generations of resident 4-wave workgroups), no
+// + k * waves in grid; 8 generations of resident one-wave workgroups), no
 // workgroup barrier.  Per tile:
 //   window   LCP bytes (+16-row halos), packed BWT bit planes (DNA) or BWT
 //            bytes, and the window's .llv values (u16) go global -> LDS by
@@ -66,7 +66,12 @@
 #include "gt_smax_hip.h"
 #include "smax_internal.h"
 
-#define SMAX_THREADS 256                              // 4 independent waves per workgroup
+#define SMAX_THREADS 256                              // 4 waves per K1b / K2 / K3 workgroup
+// K1 workgroup: ONE wave.  K1's waves share nothing (no barrier, each its own
+// LDS windows), so a one-wave workgroup frees its LDS and wave slot as soon
+// as that wave is done -- with four waves per workgroup, a wave that ran out
+// of tiles early held its slot idle until the slowest of the four finished
+#define SMAX_K1_THREADS 64
 #define SMAX_SEGS 2                                   // 16-row segments per lane
 #define SMAX_WAVE_BYTES (SMAX_SEGS * 64 * 16)         // 2048 rows per wave tile
 #define SMAX_TILE SMAX_WAVE_BYTES                     // a tile is one wave's work
@@ -1321,22 +1326,22 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   if (!DIAG) a.dbg = 0;
   // every wave is an independent worker with its own double-buffered window:
   // no workgroup barrier anywhere in K1
-  __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_THREADS / 64][2];
-  __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_THREADS / 64][2][2];
-  __shared__ uint16_t sRank[SMAX_THREADS / 64][SMAX_NCHUNK];
+  __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_K1_THREADS / 64][2];
+  __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_K1_THREADS / 64][2][2];
+  __shared__ uint16_t sRank[SMAX_K1_THREADS / 64][SMAX_NCHUNK];
   // per wave: wave_detect_direct's queue of exact starts, compacted segment
   // ids and accepted masks (the starts' results and the tile's staged
   // records go to the current window's BWT region once it is dead:
   // window_scratch)
-  __shared__ uint32_t sQueue[SMAX_THREADS / 64][SMAX_DLIST + 2 * 64 / 4 + 64];
+  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_DLIST + 2 * 64 / 4 + 64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // tile indices are 32-bit (num_tiles < 2^32): one scalar op each
-  const uint32_t stride = gridDim.x * (SMAX_THREADS / 64);
+  const uint32_t stride = gridDim.x * (SMAX_K1_THREADS / 64);
   const uint32_t last = a.num_tiles - 1;
 
-  uint32_t tile = blockIdx.x * (SMAX_THREADS / 64) + (uint32_t) wave;
+  uint32_t tile = blockIdx.x * (SMAX_K1_THREADS / 64) + (uint32_t) wave;
   // no K0 (combined placement): K1 never fills the pending slot and K1b runs
   // after it, so clearing the slot here is K0's only remaining reset (the
   // deferral count and pool cursor are reset by the previous run's K3)
@@ -2034,27 +2039,27 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
 // waves/SIMD is the production kernel; the _diag build keeps the
 // GT_SMAX_DEBUG ablation switches (used only when the variable is set).
 // Byte BWT (any alphabet): 3-4 waves/SIMD.
-__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false>(a);
 }
 // dense .llv shards (plan picks it above SMAX_FFPV_DENSITY entries per row):
 // the 255-after-255 relations of a segment are resolved vectorised
 // (ffp_resolve); measured C5 (12 Gbp plant, 0.94 % of rows) step 6.21 ->
 // 5.72 ms, C3 (human, 0.39 %) 1.253 -> 1.272 ms, hence the switch
-__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_dense(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true>(a);
 }
 // non-temporal window stream (GtSmaxPlan::nt)
-__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_nt(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, false, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_THREADS, 5) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
   smax_scan_body<SmaxWindow, false>(a);
 }
 
@@ -2495,7 +2500,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, !p->pk ? smax_scan_kernel_bytes : p->dbg ? smax_scan_kernel_diag
                                                           : smax_scan_kernel,
-        SMAX_THREADS, 0));
+        SMAX_K1_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
     // 8 generations of resident workgroups: the dispatcher hands a finished
     // slot the next workgroup, which balances tiles of uneven cost (measured
@@ -2503,7 +2508,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     uint64_t g = (uint64_t) dev_cus * (uint64_t) per_cu * 8;
     const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
     if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
-    const uint64_t wg = ((uint64_t) p->num_tiles + 3) / 4;   // workgroups with a tile per wave
+    const uint64_t wg = ((uint64_t) p->num_tiles + SMAX_K1_THREADS / 64 - 1) /
+                        (SMAX_K1_THREADS / 64);                // workgroups with a tile per wave
     p->grid = (uint32_t) (g < wg ? g : wg);
     if (getenv("GT_SMAX_VERBOSE"))
       fprintf(stderr, "gt_smax: K1 %s BWT, %d CUs x %d blocks/CU -> grid %u, %u tiles\n",
@@ -2822,15 +2828,15 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
       if ((p->dbg & 16384u) && p->runs > 0)
         ;   // diagnostic: re-run K1b on the first run's deferred tiles
       else if (p->pk && p->dbg)
-        hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+        hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
       else if (p->pk && p->dense)
         hipLaunchKernelGGL(p->nt ? smax_scan_kernel_dense_nt : smax_scan_kernel_dense, dim3(p->grid),
-                           dim3(SMAX_THREADS), lp, s, a);
+                           dim3(SMAX_K1_THREADS), lp, s, a);
       else if (p->pk)
         hipLaunchKernelGGL(p->nt ? smax_scan_kernel_nt : smax_scan_kernel, dim3(p->grid),
-                           dim3(SMAX_THREADS), lp, s, a);
+                           dim3(SMAX_K1_THREADS), lp, s, a);
       else
-        hipLaunchKernelGGL(smax_scan_kernel_bytes, dim3(p->grid), dim3(SMAX_THREADS), lp, s, a);
+        hipLaunchKernelGGL(smax_scan_kernel_bytes, dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
     }
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));

@@ -15,6 +15,8 @@
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
+#   ab:LIB:KIND:BASES:MINLEN:SHARD   A/B of the in-tree library against LIB
+#                    (tools/ab_interleave.py, 8 interleaved rounds)
 #
 # Outputs go to gpurun_out/TAG/.  Every GPU step runs under its own timeout
 # and the script stops at the first failure (set -e).
@@ -60,6 +62,12 @@ for S in "$@"; do
         python3 "$R/bench.py" --config "$C" --steps 20 --warmup 3 --no-cpu-baseline --no-end-to-end \
         > "$O/prof_bench_$C.json" 2> "$O/prof_bench_$C.err")
       python3 tools/rocpd_summary.py stats "$O/prof_$C/p_results.db" "$O/kernel_stats_$C.csv" ;;
+    ab:*)
+      # ab:LIBB:CONFIGKIND:BASES:MINLEN:SHARD -- tools/ab_interleave.py, in-tree
+      # library (A) against LIBB (B) in one process, interleaved rounds
+      IFS=: read -r _ LIBB KIND BASES MINLEN SHARD <<< "$S"
+      timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" "$LIBB" 8 "$SHARD" \
+        > "$O/ab_${KIND}_${SHARD//\//of}.txt" 2>&1 ;;
     llvstats)
       for C in c3 c5; do
         timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1
