@@ -2056,7 +2056,7 @@ __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_nt(SmaxSc
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_diag(SmaxScanArgs a) {
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_diag(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, true>(a);
 }
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {

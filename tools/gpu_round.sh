@@ -68,6 +68,9 @@ for S in "$@"; do
       IFS=: read -r _ LIBB KIND BASES MINLEN SHARD <<< "$S"
       timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" "$LIBB" 8 "$SHARD" \
         > "$O/ab_${KIND}_${SHARD//\//of}.txt" 2>&1 ;;
+    ablate:*)
+      # ablate:V1,V2,...  K1 time under GT_SMAX_DEBUG ablation bits at C3 (diag build)
+      timeout -k 10 600 python -u tools/k1_ablate.py human 3e9 "${S#ablate:}" > "$O/ablate.txt" 2>&1 ;;
     llvstats)
       for C in c3 c5; do
         timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1
