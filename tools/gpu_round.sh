@@ -71,6 +71,12 @@ for S in "$@"; do
     ablate:*)
       # ablate:V1,V2,...  K1 time under GT_SMAX_DEBUG ablation bits at C3 (diag build)
       timeout -k 10 600 python -u tools/k1_ablate.py human 3e9 "${S#ablate:}" > "$O/ablate.txt" 2>&1 ;;
+    abenv:*)
+      # abenv:K=V[;K=V]:KIND:BASES:MINLEN:SHARD -- plan A created under the
+      # environment K=V (plan-time switches), B without; same library
+      IFS=: read -r _ ENVA KIND BASES MINLEN SHARD <<< "$S"
+      AB_ENV_A="${ENVA//;/,}" timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" \
+        genometools_smax_amd/lib/libgtsmax_hip.so 8 "$SHARD" > "$O/abenv_${ENVA//[=;]/_}_${SHARD//\//of}.txt" 2>&1 ;;
     llvstats)
       for C in c3 c5; do
         timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1
