@@ -81,6 +81,11 @@ for S in "$@"; do
       for C in c3 c5; do
         timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1
       done ;;
+    profshards:*)
+      W=${S#profshards:}
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/profshards_$W" -o p -- \
+        python3 "$R/tools/shard_step.py" human 3e9 20 "$W" > "$O/profshards_$W.txt" 2>&1)
+      python3 tools/rocpd_summary.py stats "$O/profshards_$W/p_results.db" "$O/kernel_stats_shards_$W.csv" ;;
     shards:*)
       W=${S#shards:}
       timeout -k 10 600 python -u tools/shard_step.py human 3e9 20 "$W" > "$O/shards_$W.txt" 2>&1 ;;
