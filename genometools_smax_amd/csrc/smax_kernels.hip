@@ -2110,36 +2110,6 @@ smax_block_sum_kernel(const uint32_t *tile_count, uint64_t ntiles, uint32_t *blo
   if (threadIdx.x == 0) block_sum[blockIdx.x] = sW[0] + sW[1] + sW[2] + sW[3];
 }
 
-// K2b: exclusive prefix of the block sums (one workgroup of 1024 threads,
-// each over a contiguous run of blocks), so that a K3 workgroup reads its
-// output offset instead of summing every earlier block's count itself
-// (block b read b counts: O(blocks^2) reads over the grid, the tail
-// workgroups' loads in a dependent loop)
-#define SMAX_K2B_THREADS 1024
-__global__ void __launch_bounds__(SMAX_K2B_THREADS)
-smax_block_prefix_kernel(const uint32_t *block_sum, uint32_t nblocks, uint64_t *block_pre) {
-  __shared__ uint64_t sW[SMAX_K2B_THREADS / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t per = (nblocks + SMAX_K2B_THREADS - 1) / SMAX_K2B_THREADS;
-  const uint32_t b0 = tid * per, b1 = min(nblocks, b0 + per);
-  uint64_t sum = 0;
-  for (uint32_t b = b0; b < b1; b++) sum += block_sum[b];
-  uint64_t incl = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(incl, d, 64);
-    if ((int) lane >= d) incl += o;
-  }
-  if (lane == 63) sW[wave] = incl;
-  __syncthreads();
-  uint64_t run = incl - sum;
-  for (uint32_t w = 0; w < wave; w++) run += sW[w];
-  for (uint32_t b = b0; b < b1; b++) {
-    block_pre[b] = run;
-    run += block_sum[b];
-  }
-}
-
 // ------------------------------------------------------------ K3: compact
 
 struct SmaxNextRun {                  // K0's resets done by K3 (null: K0 runs)
@@ -2156,8 +2126,7 @@ struct SmaxNextRun {                  // K0's resets done by K3 (null: K0 runs)
 // Also publishes the total.
 __global__ void __launch_bounds__(256)
 smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
-                    const uint32_t *block_sum, const uint64_t *block_pre, uint64_t nslots,
-                    const GtSmaxRecord *pool,
+                    const uint32_t *block_sum, uint64_t nslots, const GtSmaxRecord *pool,
                     uint64_t pool_cap, const uint64_t *tile_off, GtSmaxRecord *out,
                     uint64_t capacity, uint64_t *count, uint64_t g00, SmaxNextRun nr) {
   // the next run's resets (combined placement: no K0): K1b, the last reader
@@ -2175,15 +2144,14 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   const uint64_t s0 = blockIdx.x * (uint64_t) SMAX_CPB;
   // this workgroup's output offset: the record counts of all earlier
   // workgroups (summed per SMAX_CPB tiles by K1 / K1b)
-  if (block_pre != nullptr) {          // K2b's prefix
-    if (tid < 4) sRed[tid] = tid == 0 ? block_pre[blockIdx.x] : 0;
-  } else {
-    uint64_t bs = 0;
-    for (uint32_t b = tid; b < blockIdx.x; b += 256) bs += block_sum[b];
+  // (a separate one-workgroup prefix kernel over the block sums instead
+  // measured 0.5 % longer at C3 and 2 % longer on an 8-way shard: the extra
+  // launch costs more than these loads, profiles/r03j_k2b_ab.txt)
+  uint64_t bs = 0;
+  for (uint32_t b = tid; b < blockIdx.x; b += 256) bs += block_sum[b];
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
-    if (lane == 0) sRed[wave] = bs;
-  }
+  for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
+  if (lane == 0) sRed[wave] = bs;
   const uint32_t cw = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
   const uint32_t c = cw & ~SMAX_SLOT_WIDE;
   sWide[tid] = (cw & SMAX_SLOT_WIDE) ? 1 : 0;
@@ -2377,7 +2345,6 @@ struct GtSmaxPlan {
   uint64_t *tile_off;        // num_tiles
   uint32_t *tile_count;      // num_tiles
   uint32_t *block_sum;       // compact_grid record sums (K2, K3's output offsets)
-  uint64_t *block_pre;       // their exclusive prefix (K2b), or null: K3 sums itself
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
@@ -2577,11 +2544,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
 
   HIPCHK(dalloc(&p->block_sum, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
   HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
-  {
-    const char *kb = getenv("GT_SMAX_K2B");      // A/B switch: 0 = K3 sums the block counts
-    if (!kb || strtol(kb, NULL, 0) != 0)
-      HIPCHK(dalloc(&p->block_pre, sizeof (uint64_t) * ((uint64_t) p->compact_grid + 1)));
-  }
+
   HIPCHK(dalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
   HIPCHK(dalloc(&p->bnd, sizeof (GtSmaxBoundary)));
@@ -2722,7 +2685,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->block_pre, p->count, p->bnd, p->defer_last,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
@@ -2927,9 +2890,6 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
     const bool nok0 = p->k1b_mode == 4 && !(p->dbg & 16384u);
     hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                        p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
-    if (p->block_pre != nullptr)
-      hipLaunchKernelGGL(smax_block_prefix_kernel, dim3(1), dim3(SMAX_K2B_THREADS), 0, s,
-                         p->block_sum, p->compact_grid, p->block_pre);
     HIPCHK(hipGetLastError());
     SmaxNextRun nr = {nullptr, nullptr, nullptr, 0u, 0ull};
     if (nok0) {
@@ -2940,7 +2900,7 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
       nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
     }
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->slots, p->tile_count, p->block_sum, p->block_pre, (uint64_t) p->num_tiles,
+                       p->slots, p->tile_count, p->block_sum, (uint64_t) p->num_tiles,
                        p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
                        p->tile_off, p->out, p->capacity, p->count,
                        p->shard.base + p->tile_first * (uint64_t) SMAX_TILE, nr);
