@@ -469,12 +469,6 @@ __device__ __forceinline__ void glds4(const void *g, uint32_t lds_base) {
                : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
 }
 __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// all but the newest N vector-memory operations done (loads return in order)
-template <int N>
-__device__ __forceinline__ void glds_wait_but() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
-}
 
 // One tile's LDS window: LCP and BWT bytes of rows [g0 - LH, g0 + TILE + RH)
 // and the window's .llv values (rank order, first SMAX_LLV_CAP of them).
@@ -555,10 +549,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u));
   const uint32_t nl8 = n == 0 ? 0u : (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
   const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;   // < 64
-  // at least one lane: every window is exactly SMAX_PK_DMA_OPS loads, which
-  // K1's wait counts on (llv16 holds 16 entries past numllv: lane 0 of an
-  // empty window reads inside it)
-  const uint64_t vmask = nl ? (1ull << nl) - 1 : 1ull;
+  const uint64_t vmask = (1ull << nl) - 1;
   const uint64_t imask = 3ull;
   const uint8_t *ib = reinterpret_cast<const uint8_t *>(ibase);
   uint32_t keep;
@@ -623,12 +614,6 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         : "memory");
   }
 }
-
-// VMEM instructions of one issue_window_pk (LCP 3, packed BWT 2, .llv
-// values 1, llv_win entry 1), each with at least one active lane
-#define SMAX_PK_DMA_OPS 7
-template <typename WinT> struct WinDma { static constexpr int ops = 0; };   // 0: wait for all
-template <> struct WinDma<SmaxWindowPk> { static constexpr int ops = SMAX_PK_DMA_OPS; };
 
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                              uint32_t lo, uint32_t n) {
@@ -1342,7 +1327,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // every wave is an independent worker with its own double-buffered window:
   // no workgroup barrier anywhere in K1
   __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_K1_THREADS / 64][2];
-  __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_K1_THREADS / 64][3][2];
+  __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_K1_THREADS / 64][2][2];
   __shared__ uint16_t sRank[SMAX_K1_THREADS / 64][SMAX_NCHUNK];
   // per wave: wave_detect_direct's queue of exact starts, compacted segment
   // ids and accepted masks (the starts' results and the tile's staged
@@ -1368,38 +1353,27 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   t.staged_all = true;   // non-static tiles: all window values staged
   uint16_t *rank = sRank[wave];
 
-  // .llv window words {lo, packed count} of the wave's tiles k, k+1, k+2 in
-  // a three-slot ring (SGPR addresses rotate each iteration): tile k's
-  // window DMA carries the words of tile k+2, so that the words of tile k+1
-  // are in LDS before tile k's window has landed -- the next window is
-  // issued BEFORE the wait for the current one (two windows in flight while
-  // a wave waits; one before round 3)
+  // prologue: .llv windows of the first two tiles, then the first window
   const uint32_t wbase = __builtin_amdgcn_readfirstlane(lds_addr(&sWin[wave][0]));
-  uint32_t s0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
-  uint32_t s1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
-  uint32_t s2 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][2][0]));
-  auto clamp_tile = [&](uint32_t x) { return x <= last ? x : last; };
-  typedef const __attribute__((address_space(3))) uint32_t lds_u32;
-  auto info_at = [](uint32_t addr, uint32_t k) {
-    return __builtin_amdgcn_readfirstlane(((lds_u32 *) (uintptr_t) addr)[k]);
-  };
-  // prologue: words of tiles 0 and 1, tile 0's window, tile 2's words
+  const uint32_t info0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
+  const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
   if (lane < 2) {
-    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, s0);
-    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + clamp_tile(tile + stride)) + lane, s1);
+    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
+    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + (tile + stride <= last ? tile + stride
+                                                                                : last)) + lane,
+          info1);
   }
   glds_wait();
-  issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], info_at(s0, 0),
-               SMAX_WIN_N(info_at(s0, 1)));
-  if (lane < 2)
-    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + clamp_tile(tile + 2 * stride)) + lane, s2);
+  issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0],
+               __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
+               SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])));
 
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
   // the previous tile's records (lane r holds record r) and count: stored
   // one iteration late, right after the window wait, so that those stores
   // (and the block-sum atomic) have a whole tile of work to complete before
-  // the next wait -- issued at the end of their own tile they made that wait
-  // take their latency (measured 0.22 ms of K1 at C3)
+  // the next s_waitcnt vmcnt(0) -- issued at the end of their own tile they
+  // made that wait take their latency (measured 0.22 ms of K1 at C3)
   uint64_t prec = 0;
   uint32_t ptile = ~0u, pcnt = 0;
   for (uint32_t it = 0;; it++) {
@@ -1414,35 +1388,34 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     t.val = nullptr;
     t.val16 = W->val16;
 
-    // .llv words of this tile (slot s0) and the next (s1): both landed with
-    // the windows of two and one tiles ago (scalar reads)
-    const uint32_t wlo = info_at(s0, 0);
-    const uint32_t wnf = info_at(s0, 1);
-    const uint32_t wn = SMAX_WIN_N(wnf);
-    const uint32_t nlo = info_at(s1, 0);
-    const uint32_t nn = SMAX_WIN_N(info_at(s1, 1));
-
-    // ---- DMA of the next tile's window (into the buffer of the tile before
-    // this one, done) with the words of the tile after it (into slot s0, just
-    // read), issued before this tile's wait
-    const bool issued = next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0);   // diag: compute only
-    if (issued)
-      issue_next<NT>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
-                     wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
-                     a.llv_win + clamp_tile(next + 2 * stride), s0, v16, v4);
-    // ---- this tile's window has landed (the wave's own DMA: no barrier):
-    // every vector-memory operation but the next window's
-    if (issued) glds_wait_but<WinDma<WinT>::ops>();
-    else glds_wait();
+    // ---- this tile's window has landed (the wave's own DMA: no barrier)
+    glds_wait();
     if (ptile != ~0u) {
       smax_flush_tile(a, ptile, prec, pcnt);
       ptile = ~0u;
     }
-    {
-      const uint32_t r = s0;    // ring: (k, k+1, k+2) -> (k+1, k+2, k+3)
-      s0 = s1;
-      s1 = s2;
-      s2 = r;
+    // .llv windows of this tile and the next {lo, packed count word}: one
+    // 16-byte LDS read
+    // (wave-uniform: to scalars first, then scalar selects)
+    const uint4 info = *reinterpret_cast<const uint4 *>(&sInfo[wave][0][0]);
+    const uint32_t ix = __builtin_amdgcn_readfirstlane(info.x);
+    const uint32_t iy = __builtin_amdgcn_readfirstlane(info.y);
+    const uint32_t iz = __builtin_amdgcn_readfirstlane(info.z);
+    const uint32_t iw = __builtin_amdgcn_readfirstlane(info.w);
+    const uint32_t wlo = cur ? iz : ix;
+    const uint32_t wnf = cur ? iw : iy;
+    const uint32_t wn = SMAX_WIN_N(wnf);
+    const uint32_t nlo = cur ? ix : iz;
+    const uint32_t nn = SMAX_WIN_N(cur ? iy : iw);
+
+    // ---- DMA of the next tile's window (and the .llv window of the tile
+    // after it, into the ring slot just read): in flight during all of this
+    // tile's work
+    if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
+      const uint32_t n2 = next + stride <= last ? next + stride : last;
+      issue_next<NT>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
+                 wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
+                 a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
 
     t.halo_ff = SMAX_WIN_HALO(wnf);
