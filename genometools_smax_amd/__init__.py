@@ -125,6 +125,22 @@ class GtLcpitvVisitor(ctypes.Structure):
     _fields_ = [("leaf_edge", _LEAF_CB), ("branching_edge", _BRANCH_CB), ("lcp_interval", _ITV_CB)]
 
 
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_LEAF_INFO_CB = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int, _u64, _u64, _vp, _u64)
+_BRANCH_INFO_CB = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int, _u64, _u64, _vp, _u64, _u64,
+                                   _u64, _vp)
+_ITV_INFO_CB = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _u64, _u64, _u64, _vp)
+_INFO_NEW_CB = ctypes.CFUNCTYPE(_vp, _vp)
+_INFO_DEL_CB = ctypes.CFUNCTYPE(None, _vp, _vp)
+
+
+class GtLcpitvInfoVisitor(ctypes.Structure):
+    _fields_ = [("leaf_edge", _LEAF_INFO_CB), ("branching_edge", _BRANCH_INFO_CB),
+                ("lcp_interval", _ITV_INFO_CB), ("info_new", _INFO_NEW_CB),
+                ("info_delete", _INFO_DEL_CB)]
+
+
 class GtSmaxRecord(ctypes.Structure):
     _fields_ = [("lb", ctypes.c_uint64), ("lcp", ctypes.c_uint32), ("width", ctypes.c_uint32)]
 
@@ -214,6 +230,8 @@ def lib():
         L.gt_lcpitv_plan_events.argtypes = [vp, vp, vp]
         L.gt_esa_bottomup_hip.argtypes = [ctypes.POINTER(GtSmaxInput), ctypes.POINTER(GtLcpitvVisitor),
                                           vp, cs, sz]
+        L.gt_esa_bottomup_info_hip.argtypes = [ctypes.POINTER(GtSmaxInput),
+                                               ctypes.POINTER(GtLcpitvInfoVisitor), vp, cs, sz]
         _lib = L
     return _lib
 
@@ -618,6 +636,36 @@ def esa_bottomup(lcptab, llvtab, suftab, totallength, nonspecials, leaf_edge=Non
         v.lcp_interval = cbs[-1]
     eb = _errbuf()
     _check(lib().gt_esa_bottomup_hip(ctypes.byref(inp), ctypes.byref(v), None, eb, len(eb)), eb)
+
+
+def esa_bottomup_info(lcptab, llvtab, suftab, totallength, nonspecials, info_new,
+                      info_delete=None, leaf_edge=None, branching_edge=None, lcp_interval=None):
+    """gt_esa_bottomup with per-node visitor state (gt_esa_bottomup_info_hip):
+    info_new() -> a non-zero int handle (the GtESAVisitorInfo), info_delete(h);
+    leaf_edge(firstsucc, fd, flb, finfo, leafnumber), branching_edge(firstsucc,
+    fd, flb, finfo, sd, slb, srb, sinfo), lcp_interval(lcp, lb, rb, info), with
+    the handles (sinfo 0 for none); a truthy return stops."""
+    inp, keep = _input(lcptab, llvtab, None, suftab, totallength, nonspecials)
+    v = GtLcpitvInfoVisitor()
+    cbs = [_INFO_NEW_CB(lambda d: int(info_new()))]
+    v.info_new = cbs[-1]
+    if info_delete is not None:
+        cbs.append(_INFO_DEL_CB(lambda x, d: info_delete(x or 0)))
+        v.info_delete = cbs[-1]
+    if leaf_edge is not None:
+        cbs.append(_LEAF_INFO_CB(lambda d, f, fd, flb, fi, leaf:
+                                 int(bool(leaf_edge(f, fd, flb, fi or 0, leaf)))))
+        v.leaf_edge = cbs[-1]
+    if branching_edge is not None:
+        cbs.append(_BRANCH_INFO_CB(lambda d, f, fd, flb, fi, sd, slb, srb, si:
+                                   int(bool(branching_edge(f, fd, flb, fi or 0, sd, slb, srb,
+                                                           si or 0)))))
+        v.branching_edge = cbs[-1]
+    if lcp_interval is not None:
+        cbs.append(_ITV_INFO_CB(lambda d, lcp, lb, rb, i: int(bool(lcp_interval(lcp, lb, rb, i or 0)))))
+        v.lcp_interval = cbs[-1]
+    eb = _errbuf()
+    _check(lib().gt_esa_bottomup_info_hip(ctypes.byref(inp), ctypes.byref(v), None, eb, len(eb)), eb)
 
 
 def enumerate_index(index, minlen, num_gpus=1):

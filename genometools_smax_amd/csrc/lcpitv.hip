@@ -29,6 +29,7 @@
 // The host entry points download the events in chunks and call the
 // visitor.
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <stdarg.h>
@@ -640,22 +641,21 @@ extern "C" int gt_lcpitv_hip_enumerate_to_buffer(const GtSmaxInput *in, uint64_t
 // in chunks of LI_EV_CHUNK events
 #define LI_EV_CHUNK (1ull << 20)
 
-extern "C" int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor *v, void *data,
-                                   char *errbuf, size_t errlen) {
+// The tree's visitor event stream, built in HBM and handed to sink(r) in
+// chunks in the reference's order (r: one 7-word event record); a non-zero
+// sink return stops.  need_suf: leaf numbers from the suffix array.
+template <typename Sink>
+static int li_replay(const GtSmaxInput *in, bool need_suf, Sink sink, char *errbuf, size_t errlen) {
   LiHostTables h;
   GtLcpitvPlan *plan = NULL;
   uint64_t *ev = NULL, *host = NULL, E;
   int rc = 0;
-  if (v == NULL) {
-    li_seterr(errbuf, errlen, "missing visitor");
-    return -1;
-  }
-  if (v->leaf_edge != NULL && (in == NULL || in->suftab == NULL ||
-                               (in->suftab_bytes != 4 && in->suftab_bytes != 8))) {
+  if (need_suf && (in == NULL || in->suftab == NULL ||
+                   (in->suftab_bytes != 4 && in->suftab_bytes != 8))) {
     li_seterr(errbuf, errlen, "leaf edges need suftab (4 or 8 bytes per entry)");
     return -1;
   }
-  if (li_host_plan(in, v->leaf_edge != NULL, &h, &plan, errbuf, errlen) != 0) return -1;
+  if (li_host_plan(in, need_suf, &h, &plan, errbuf, errlen) != 0) return -1;
   E = gt_lcpitv_plan_num_events(plan);
   if (E > 0) {
     LICHK(hipMalloc(&ev, sizeof (uint64_t) * 7 * E));
@@ -669,16 +669,7 @@ extern "C" int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor 
   for (uint64_t e0 = 0; e0 < E && rc == 0; e0 += LI_EV_CHUNK) {
     const uint64_t n = E - e0 < LI_EV_CHUNK ? E - e0 : LI_EV_CHUNK;
     LICHK(hipMemcpy(host, ev + 7 * e0, sizeof (uint64_t) * 7 * n, hipMemcpyDeviceToHost));
-    for (uint64_t k = 0; k < n && rc == 0; k++) {
-      const uint64_t *r = host + 7 * k;
-      if (r[0] == 0) {
-        if (v->leaf_edge) rc = v->leaf_edge(data, (int) r[1], r[2], r[3], r[4]);
-      } else if (r[0] == 1) {
-        if (v->branching_edge) rc = v->branching_edge(data, (int) r[1], r[2], r[3], r[4], r[5], r[6]);
-      } else if (v->lcp_interval) {
-        rc = v->lcp_interval(data, r[2], r[3], r[4]);
-      }
-    }
+    for (uint64_t k = 0; k < n && rc == 0; k++) rc = sink(host + 7 * k);
   }
   if (ev) (void) hipFree(ev);
   if (host) (void) hipHostFree(host);
@@ -695,4 +686,67 @@ fail:
   gt_lcpitv_plan_delete(plan);
   li_host_free(&h);
   return -1;
+}
+
+extern "C" int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor *v, void *data,
+                                   char *errbuf, size_t errlen) {
+  if (v == NULL) {
+    li_seterr(errbuf, errlen, "missing visitor");
+    return -1;
+  }
+  return li_replay(in, v->leaf_edge != NULL, [&](const uint64_t *r) {
+    if (r[0] == 0) return v->leaf_edge ? v->leaf_edge(data, (int) r[1], r[2], r[3], r[4]) : 0;
+    if (r[0] == 1)
+      return v->branching_edge ? v->branching_edge(data, (int) r[1], r[2], r[3], r[4], r[5], r[6]) : 0;
+    return v->lcp_interval ? v->lcp_interval(data, r[2], r[3], r[4]) : 0;
+  }, errbuf, errlen);
+}
+
+// GtESAVisitorInfo emulation (src/match/esa-bottomup.c:20-110): the
+// reference binds one info object to each STACK SLOT, created with
+// info_new in chunks of 32 as the stack grows and deleted, slot by slot, at
+// the end; a pushed interval reuses its slot's object, and a father pushed
+// right after its first child popped takes that child's slot -- so its
+// branching edge sees soninfo NULL and fatherinfo == the child's info.  The
+// event stream carries everything needed to follow the stack: a push is a
+// firstsucc leaf edge or a firstsucc branching edge of father depth > 0, a
+// pop is an lcp-interval event (firstsucc edges of depth 0 are the root's).
+extern "C" int gt_esa_bottomup_info_hip(const GtSmaxInput *in, const GtLcpitvInfoVisitor *v,
+                                        void *data, char *errbuf, size_t errlen) {
+  if (v == NULL || v->info_new == NULL) {
+    li_seterr(errbuf, errlen, "missing visitor or info_new");
+    return -1;
+  }
+  std::vector<void *> slot;
+  uint64_t depth = 0, last = 0;
+  auto grow = [&]() {
+    for (int k = 0; k < 32; k++) slot.push_back(v->info_new(data));   // allocateBUstack
+  };
+  grow();
+  depth = 1;                                                           // PUSH(0, 0): the root
+  const int rc = li_replay(in, v->leaf_edge != NULL, [&](const uint64_t *r) -> int {
+    if (r[0] == 0) {                                                   // leaf edge
+      if (r[1] != 0 && r[2] > 0) {                                     // PUSH(lcpvalue, idx)
+        if (depth >= slot.size()) grow();
+        depth++;
+      }
+      return v->leaf_edge ? v->leaf_edge(data, (int) r[1], r[2], r[3], slot[depth - 1], r[4]) : 0;
+    }
+    if (r[0] == 2) {                                                   // POP
+      if (depth < 2) return -1;                                        // never the root
+      last = --depth;
+      return v->lcp_interval ? v->lcp_interval(data, r[2], r[3], r[4], slot[last]) : 0;
+    }
+    void *son = slot[last];
+    if (r[1] != 0 && r[2] > 0) {                                       // PUSH(lcpvalue, last.lb)
+      depth++;                                                         // = the popped child's slot
+      son = nullptr;
+    }
+    return v->branching_edge
+               ? v->branching_edge(data, (int) r[1], r[2], r[3], slot[depth - 1], r[4], r[5], r[6], son)
+               : 0;
+  }, errbuf, errlen);
+  if (v->info_delete)
+    for (void *x : slot) v->info_delete(x, data);                      // gt_GtArrayGtBUItvinfo_delete
+  return rc;
 }

@@ -18,9 +18,9 @@
  *                                 sequence -- order, firstsucc flags, father
  *                                 depth/lb, child depth/lb/rb, leaf numbers
  *                                 -- is the reference traversal's, exactly.
- *                                 The per-node GtESAVisitorInfo state is not
- *                                 modelled (visitors that need it keep their
- *                                 own, keyed by the father's lb).
+ *  gt_esa_bottomup_info_hip       the same with the per-node GtESAVisitorInfo
+ *                                 of every callback (info_new / info_delete
+ *                                 per stack slot, as the reference's stack).
  *  gt_lcpitv_hip_enumerate_to_buffer  every lcp-interval of depth > 0 with
  *                                 its father, in bottom-up (pop) order:
  *                                 (lcp, lb, rb, father lcp, father lb).
@@ -58,6 +58,33 @@ typedef struct {
 /* in->suftab is required when v->leaf_edge is set (leaf numbers). */
 int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor *v, void *data,
                         char *errbuf, size_t errlen);
+
+/* GtESAVisitor with its per-node state (src/match/esa_visitor_rep.h:25-67):
+ * every callback also receives the GtESAVisitorInfo of the interval(s) it
+ * concerns, created by info_new and released by info_delete exactly as
+ * gt_esa_bottomup does (src/match/esa-bottomup.c:20-110,116-273): one info
+ * per stack slot, allocated 32 at a time as the stack grows, reused by the
+ * intervals that occupy the slot, deleted slot by slot after the traversal;
+ * a father pushed right after its first child's pop occupies that child's
+ * slot, so its branching edge passes soninfo NULL with fatherinfo == the
+ * child's info (the reference's hand-over of the child's state).  The
+ * callbacks and their order are gt_esa_bottomup_hip's; info_new is required,
+ * the other callbacks may be NULL. */
+typedef struct {
+  int (*leaf_edge)(void *data, int firstsucc, uint64_t fd, uint64_t flb, void *finfo,
+                   uint64_t leafnumber);
+  int (*branching_edge)(void *data, int firstsucc, uint64_t fd, uint64_t flb, void *finfo,
+                        uint64_t sd, uint64_t slb, uint64_t srb, void *sinfo);
+  int (*lcp_interval)(void *data, uint64_t lcp, uint64_t lb, uint64_t rb, void *info);
+  void *(*info_new)(void *data);
+  void (*info_delete)(void *info, void *data);
+} GtLcpitvInfoVisitor;
+
+/* gt_esa_bottomup(ssar, visitor, err) for visitors with per-node state
+ * (esa-bottomup.h:31-33 with the GtESAVisitorInfo arguments of
+ * esa_visitor.h:30-51). */
+int gt_esa_bottomup_info_hip(const GtSmaxInput *in, const GtLcpitvInfoVisitor *v, void *data,
+                             char *errbuf, size_t errlen);
 
 /* *itv receives 5*count uint64: (lcp, lb, rb, fatherlcp, fatherlb) per
  * lcp-interval of depth > 0, bottom-up order (rb ascending, then lcp

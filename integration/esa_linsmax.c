@@ -31,6 +31,8 @@
 #include "match/esa-seqread.h"
 #include "match/sarr-def.h"
 #include "match/esa_linsmax.h"
+#include "match/esa_visitor.h"
+#include "gt_lcpitv_hip.h"
 #include "gt_maxpairs_hip.h"
 #include "gt_smax_hip.h"
 
@@ -317,4 +319,101 @@ int gt_callenummaxpairs_hip(const char *indexname,
 {
   return smax_shim_run(indexname, userdefinedleastlength, scanfile, 1, false,
                        processmaxpairs, processmaxpairsinfo, logger, err);
+}
+
+/* ------------------------------------------- gt_esa_bottomup on the GPU */
+
+typedef struct
+{
+  GtESAVisitor *ev;
+  GtError *err;
+} GtEsaBottomupGpu;
+
+static int gpu_bu_leaf(void *data, int firstsucc, uint64_t fd, uint64_t flb,
+                       void *finfo, uint64_t leafnumber)
+{
+  GtEsaBottomupGpu *st = data;
+  return gt_esa_visitor_visit_leaf_edge(st->ev, firstsucc != 0, (GtUword) fd,
+                                        (GtUword) flb, finfo,
+                                        (GtUword) leafnumber, st->err);
+}
+
+static int gpu_bu_branch(void *data, int firstsucc, uint64_t fd, uint64_t flb,
+                         void *finfo, uint64_t sd, uint64_t slb, uint64_t srb,
+                         void *sinfo)
+{
+  GtEsaBottomupGpu *st = data;
+  return gt_esa_visitor_visit_branching_edge(st->ev, firstsucc != 0,
+                                             (GtUword) fd, (GtUword) flb,
+                                             finfo, (GtUword) sd,
+                                             (GtUword) slb, (GtUword) srb,
+                                             sinfo, st->err);
+}
+
+static int gpu_bu_interval(void *data, uint64_t lcp, uint64_t lb, uint64_t rb,
+                           void *info)
+{
+  GtEsaBottomupGpu *st = data;
+  return gt_esa_visitor_visit_lcp_interval(st->ev, (GtUword) lcp,
+                                           (GtUword) lb, (GtUword) rb, info,
+                                           st->err);
+}
+
+static void *gpu_bu_info_new(void *data)
+{
+  GtEsaBottomupGpu *st = data;
+  return gt_esa_visitor_info_new(st->ev);
+}
+
+static void gpu_bu_info_delete(void *info, void *data)
+{
+  GtEsaBottomupGpu *st = data;
+  gt_esa_visitor_info_delete(info, st->ev);
+}
+
+int gt_esa_bottomup_gpu(Sequentialsuffixarrayreader *ssar, GtESAVisitor *ev,
+                        GtError *err)
+{
+  const Suffixarray *sa = gt_suffixarraySequentialsuffixarrayreader(ssar);
+  GtLcpitvInfoVisitor v;
+  GtEsaBottomupGpu st;
+  GtSmaxInput in;
+  char msg[1024];
+  GtUword totallength;
+
+  gt_error_check(err);
+  if (sa == NULL || sa->lcptab == NULL || sa->suftab == NULL)
+  {
+    gt_error_set(err, "gt_esa_bottomup_gpu needs the mapped lcp and suffix "
+                      "tables (a reader opened without scanfile)");
+    return -1;
+  }
+  totallength = gt_encseq_total_length(sa->encseq);
+  memset(&in, 0, sizeof in);
+  in.lcptab = sa->lcptab;
+  in.llvtab = (const GtSmaxLlv *) sa->llvtab;
+  in.numllv = (uint64_t) sa->numoflargelcpvalues.valueunsignedlong;
+  in.bwttab = sa->bwttab;
+  in.suftab = sa->suftab;
+  in.suftab_bytes = (int) sizeof (ESASuffixptr);
+  in.totallength = (uint64_t) totallength;
+  in.nonspecials = (uint64_t) (totallength -
+                               gt_encseq_specialcharacters(sa->encseq));
+  st.ev = ev;
+  st.err = err;
+  v.leaf_edge = gpu_bu_leaf;
+  v.branching_edge = gpu_bu_branch;
+  v.lcp_interval = gpu_bu_interval;
+  v.info_new = gpu_bu_info_new;
+  v.info_delete = gpu_bu_info_delete;
+  msg[0] = '\0';
+  if (gt_esa_bottomup_info_hip(&in, &v, &st, msg, sizeof msg) != 0)
+  {
+    if (!gt_error_is_set(err))
+    {
+      gt_error_set(err, "%s", msg);
+    }
+    return -1;
+  }
+  return 0;
 }

@@ -17,6 +17,8 @@
 #include "core/error_api.h"
 #include "core/logger_api.h"
 #include "match/esa-maxpairs.h"
+#include "match/esa-seqread.h"
+#include "match/esa_visitor.h"
 
 /* gt repfind -smax: every occurrence pair of every supermaximal repeat of
    length >= userdefinedleastlength, passed to processmaxpairs in ascending
@@ -39,5 +41,16 @@ int gt_callenummaxpairs_hip(const char *indexname,
                             void *processmaxpairsinfo,
                             GtLogger *logger,
                             GtError *err);
+
+/* gt_esa_bottomup (src/match/esa-bottomup.h:31-33) on the GPU: any
+   GtESAVisitor -- the reference's own visitors included -- receives its
+   leaf-edge, branching-edge and lcp-interval calls with their
+   GtESAVisitorInfo objects (created with gt_esa_visitor_info_new, one per
+   stack slot, and deleted after the traversal, as esa-bottomup.c:20-110) in
+   the reference's order, from the lcp-interval tree built on the GPU
+   (gt_esa_bottomup_info_hip).  Needs the mapped .lcp/.llv/.suf tables
+   (a reader opened without scanfile).  0 on success, -1 with err set. */
+int gt_esa_bottomup_gpu(Sequentialsuffixarrayreader *ssar, GtESAVisitor *ev,
+                        GtError *err);
 
 #endif

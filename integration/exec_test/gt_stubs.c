@@ -16,6 +16,11 @@
  *   gt_freeSequentialsuffixarrayreader
  *   gt_encseq_total_length, gt_encseq_specialcharacters  (from the .prj)
  *   gt_error_set / gt_error_is_set, gt_malloc_mem / gt_realloc_mem / gt_free_mem
+ *   gt_esa_visitor_visit_leaf_edge / _branching_edge / _lcp_interval,
+ *   gt_esa_visitor_info_new / _delete (src/match/esa_visitor.h:30-61): a
+ *   recording visitor -- every call printed with the ids of its
+ *   GtESAVisitorInfo objects (numbered in creation order), every deletion
+ *   printed, for gt_esa_bottomup_gpu's execution test
  *
  * The expected output of the execution test comes from the repo's oracle
  * (tests/test_shim_exec_gpu.py), never from these stubs.
@@ -29,6 +34,7 @@
 #include "core/ma_api.h"
 #include "match/esa-seqread.h"
 #include "match/sarr-def.h"
+#include "match/esa_visitor.h"
 
 struct GtEncseq {
   GtUword totallength, specialcharacters;
@@ -154,7 +160,7 @@ Sequentialsuffixarrayreader *gt_newSequentialsuffixarrayreaderfromfile(
         return NULL;
       }
     }
-    if (sa->lcptab == NULL || sa->bwttab == NULL) {
+    if (sa->lcptab == NULL || ((demand & SARR_BWTTAB) && sa->bwttab == NULL)) {
       gt_error_set(err, "stub reader: missing .lcp/.bwt of %s", indexname);
       return NULL;
     }
@@ -191,4 +197,73 @@ void gt_freeSequentialsuffixarrayreader(Sequentialsuffixarrayreader **ssar)
   free(sa);
   free(*ssar);
   *ssar = NULL;
+}
+
+/* ---------------------------------------------- recording GtESAVisitor */
+
+struct GtESAVisitor {
+  FILE *out;
+  GtUword next_id;
+};
+
+struct GtESAVisitorInfo {
+  GtUword id;
+};
+
+GtESAVisitor *stub_visitor_new(FILE *out)
+{
+  GtESAVisitor *ev = calloc(1, sizeof *ev);
+  ev->out = out;
+  return ev;
+}
+
+GtESAVisitorInfo *gt_esa_visitor_info_new(GtESAVisitor *ev)
+{
+  GtESAVisitorInfo *info = malloc(sizeof *info);
+  info->id = ++ev->next_id;
+  return info;
+}
+
+void gt_esa_visitor_info_delete(GtESAVisitorInfo *info, GtESAVisitor *ev)
+{
+  if (info == NULL) return;
+  fprintf(ev->out, "D %lu\n", (unsigned long) info->id);
+  free(info);
+}
+
+int gt_esa_visitor_visit_leaf_edge(GtESAVisitor *ev, bool firstsucc, GtUword fd,
+                                   GtUword flb, GtESAVisitorInfo *finfo,
+                                   GtUword leafnumber, GtError *err)
+{
+  (void) err;
+  fprintf(ev->out, "0 %d %lu %lu %lu 0 0 %lu 0\n", firstsucc ? 1 : 0,
+          (unsigned long) fd, (unsigned long) flb, (unsigned long) leafnumber,
+          (unsigned long) (finfo ? finfo->id : 0));
+  return 0;
+}
+
+int gt_esa_visitor_visit_branching_edge(GtESAVisitor *ev, bool firstsucc,
+                                        GtUword fd, GtUword flb,
+                                        GtESAVisitorInfo *finfo, GtUword sd,
+                                        GtUword slb, GtUword srb,
+                                        GtESAVisitorInfo *sinfo, GtError *err)
+{
+  (void) err;
+  fprintf(ev->out, "1 %d %lu %lu %lu %lu %lu %lu %lu\n", firstsucc ? 1 : 0,
+          (unsigned long) fd, (unsigned long) flb, (unsigned long) sd,
+          (unsigned long) slb, (unsigned long) srb,
+          (unsigned long) (finfo ? finfo->id : 0),
+          (unsigned long) (sinfo ? sinfo->id : 0));
+  return 0;
+}
+
+int gt_esa_visitor_visit_lcp_interval(GtESAVisitor *ev, GtUword lcp, GtUword lb,
+                                      GtUword rb, GtESAVisitorInfo *info,
+                                      GtError *err)
+{
+  (void) err;
+  fprintf(ev->out, "2 0 %lu %lu %lu 0 0 %lu 0\n", (unsigned long) lcp,
+          (unsigned long) lb, (unsigned long) rb,
+          (unsigned long) (info ? info->id : 0));
+  return 0;
 }

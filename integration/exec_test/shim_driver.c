@@ -6,9 +6,13 @@
  * (len, pos1, pos2) it receives, in order:
  *
  *   shim_exec INDEX MINLEN smax|maxpairs [-scan] [GPUS]
+ *   shim_exec INDEX 0 bottomup
  *
- * prints one "len pos1 pos2" line per call; exit 0, or 1 with the GtError
- * message on stderr.
+ * prints one "len pos1 pos2" line per call; with bottomup, the reference's
+ * gt_esa_bottomup entry point on the GPU (gt_esa_bottomup_gpu) drives a
+ * recording GtESAVisitor (gt_stubs.c) -- one line per visitor call with its
+ * GtESAVisitorInfo ids, one "D id" line per deleted info; exit 0, or 1 with
+ * the GtError message on stderr.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -16,6 +20,8 @@
 #include "core/error_api.h"
 #include "match/esa-maxpairs.h"
 #include "match/esa_linsmax.h"
+
+GtESAVisitor *stub_visitor_new(FILE *out);
 
 struct GtError {
   char msg[4096];
@@ -50,6 +56,20 @@ int main(int argc, char **argv)
     else gpus = atoi(argv[i]);
   }
   memset(&err, 0, sizeof err);
+  if (strcmp(argv[3], "bottomup") == 0) {
+    Sequentialsuffixarrayreader *ssar =
+      gt_newSequentialsuffixarrayreaderfromfile(argv[1], SARR_LCPTAB | SARR_SUFTAB | SARR_ESQTAB,
+                                                false, NULL, &err);
+    GtESAVisitor *ev = stub_visitor_new(stdout);
+    rc = ssar == NULL ? -1 : gt_esa_bottomup_gpu(ssar, ev, &err);
+    if (ssar != NULL) gt_freeSequentialsuffixarrayreader(&ssar);
+    free(ev);
+    if (rc != 0) {
+      fprintf(stderr, "shim error: %s\n", err.isset ? err.msg : "(no message)");
+      return 1;
+    }
+    return 0;
+  }
   rc = smax ? gt_callenumsupermaxrepeats(argv[1], (unsigned) atoi(argv[2]), scan, gpus,
                                          record_pair, stdout, NULL, &err)
             : gt_callenummaxpairs_hip(argv[1], (unsigned) atoi(argv[2]), scan,

@@ -395,24 +395,35 @@ uint64_t orc_bottomup_smax_tables(const uint8_t *lcpbytes, const OrcLlv *llv,
  *   (1, firstsucc, fd, flb, sd, slb, srb)           visit_branching_edge
  *   (2, 0, lcp, lb, rb, 0, 0)                       visit_lcp_interval
  * (F3 checker).  Returns the number of events; *ev is malloc'd. */
-uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
-                             uint64_t nonspecials, uint64_t **ev)
+/* With slots != NULL also the stack slot of each event's interval(s) -- the
+ * reference binds one GtESAVisitorInfo to each slot (esa-bottomup.c:20-110):
+ * per event (father slot, son slot) for edges, (popped slot, -) for
+ * lcp-intervals, NONE (UINT64_MAX) where there is no son info (a leaf, or a
+ * father pushed into its first child's slot); *nslots = slots allocated
+ * (32 at a time, as allocateBUstack). */
+static uint64_t bu_events(const uint64_t *lcp, const uint64_t *suftab,
+                          uint64_t nonspecials, uint64_t **ev, uint64_t **slots,
+                          uint64_t *nslots)
 {
   BUStack st = {NULL, 0, 0};
   BUItv *last = NULL;
   BUItv lastcopy;
-  uint64_t idx, n = 0, alloc = 0, *e = NULL;
+  uint64_t idx, n = 0, alloc = 0, *e = NULL, *sl = NULL, lastslot = 0;
+  const uint64_t NONE = UINT64_MAX;
   int firstedgefromroot = 1;
-#define EV(T, F, A, B, C, D, E)                                              \
+#define EVS(T, F, A, B, C, D, E, S0, S1)                                     \
   do {                                                                       \
     if (n + 1 > alloc) {                                                     \
       alloc = alloc * 2 + 1024;                                              \
       e = realloc(e, sizeof (uint64_t) * 7 * alloc);                         \
+      if (slots) sl = realloc(sl, sizeof (uint64_t) * 2 * alloc);            \
     }                                                                        \
+    if (slots) { sl[2 * n] = (S0); sl[2 * n + 1] = (S1); }                   \
     uint64_t *r_ = e + 7 * n++;                                              \
     r_[0] = (T); r_[1] = (F); r_[2] = (A); r_[3] = (B); r_[4] = (C);          \
     r_[5] = (D); r_[6] = (E);                                                \
   } while (0)
+#define EV(T, F, A, B, C, D, E) EVS(T, F, A, B, C, D, E, NONE, NONE)
 #define FIRSTEDGE(F)                                                         \
   do {                                                                       \
     if (BU_TOP(&st).lcp > 0 || !firstedgefromroot) (F) = 0;                  \
@@ -425,7 +436,7 @@ uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
     int firstedge;
     if (lcpvalue <= BU_TOP(&st).lcp) {
       FIRSTEDGE(firstedge);
-      EV(0, firstedge, BU_TOP(&st).lcp, BU_TOP(&st).lb, prevsuffix, 0, 0);
+      EVS(0, firstedge, BU_TOP(&st).lcp, BU_TOP(&st).lb, prevsuffix, 0, 0, st.next - 1, NONE);
     }
     last = NULL;
     while (lcpvalue < BU_TOP(&st).lcp) {
@@ -433,10 +444,12 @@ uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
       lastcopy = st.space[st.next];
       last = &lastcopy;
       last->rb = idx;
-      EV(2, 0, last->lcp, last->lb, last->rb, 0, 0);
+      lastslot = st.next;
+      EVS(2, 0, last->lcp, last->lb, last->rb, 0, 0, lastslot, NONE);
       if (lcpvalue <= BU_TOP(&st).lcp) {
         FIRSTEDGE(firstedge);
-        EV(1, firstedge, BU_TOP(&st).lcp, BU_TOP(&st).lb, last->lcp, last->lb, last->rb);
+        EVS(1, firstedge, BU_TOP(&st).lcp, BU_TOP(&st).lb, last->lcp, last->lb, last->rb,
+            st.next - 1, lastslot);
         last = NULL;
       }
     }
@@ -444,19 +457,38 @@ uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
       if (last != NULL) {
         uint64_t l = last->lcp, b = last->lb, r = last->rb;
         bu_push(&st, lcpvalue, b);
-        EV(1, 1, BU_TOP(&st).lcp, BU_TOP(&st).lb, l, b, r);
+        EVS(1, 1, BU_TOP(&st).lcp, BU_TOP(&st).lb, l, b, r, st.next - 1, NONE);
         last = NULL;
       } else {
         bu_push(&st, lcpvalue, idx);
-        EV(0, 1, BU_TOP(&st).lcp, BU_TOP(&st).lb, prevsuffix, 0, 0);
+        EVS(0, 1, BU_TOP(&st).lcp, BU_TOP(&st).lb, prevsuffix, 0, 0, st.next - 1, NONE);
       }
     }
   }
+  if (nslots) *nslots = st.alloc;
   free(st.space);
 #undef EV
+#undef EVS
 #undef FIRSTEDGE
   *ev = e;
+  if (slots) *slots = sl;
   return n;
+}
+
+uint64_t orc_bottomup_events(const uint64_t *lcp, const uint64_t *suftab,
+                             uint64_t nonspecials, uint64_t **ev)
+{
+  return bu_events(lcp, suftab, nonspecials, ev, NULL, NULL);
+}
+
+/* orc_bottomup_events plus the stack slot (GtESAVisitorInfo) of each event,
+ * 2 words per event in *slots (malloc'd), and the number of slots allocated
+ * (F3's info-visitor checker). */
+uint64_t orc_bottomup_events_slots(const uint64_t *lcp, const uint64_t *suftab,
+                                   uint64_t nonspecials, uint64_t **ev,
+                                   uint64_t **slots, uint64_t *nslots)
+{
+  return bu_events(lcp, suftab, nonspecials, ev, slots, nslots);
 }
 
 /* The other traversal gt dev sfxmap has: -enumlcpitvtree, the depth-first

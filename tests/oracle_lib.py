@@ -53,6 +53,9 @@ def lib():
         L.orc_maxpairs.restype = ctypes.c_uint64
         L.orc_bottomup_events.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_void_p]
         L.orc_bottomup_events.restype = ctypes.c_uint64
+        L.orc_bottomup_events_slots.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_void_p, _u64p]
+        L.orc_bottomup_events_slots.restype = ctypes.c_uint64
         L.orc_dfs_events.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_void_p]
         L.orc_dfs_events.restype = ctypes.c_uint64
         L.orc_format_pair.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _u64p,
@@ -218,6 +221,26 @@ def bottomup_events(esa):
     arr = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 7).copy()
     lib().orc_free(pp)
     return arr
+
+
+def bottomup_events_slots(esa):
+    """orc_bottomup_events plus each event's stack slots (father, son; NONE =
+    2^64-1) and the number of slots allocated -- the reference's
+    GtESAVisitorInfo objects (esa-bottomup.c:20-110)."""
+    pp, ps = ctypes.c_void_p(), ctypes.c_void_p()
+    ns = ctypes.c_uint64()
+    cnt = lib().orc_bottomup_events_slots(_p(esa.lcp, _u64p), _p(esa.suftab, _u64p),
+                                          esa.nonspecials, ctypes.byref(pp), ctypes.byref(ps),
+                                          ctypes.byref(ns))
+    if cnt == 0:
+        return np.zeros((0, 7), np.uint64), np.zeros((0, 2), np.uint64), ns.value
+    ev = np.frombuffer((ctypes.c_uint64 * (7 * cnt)).from_address(pp.value),
+                       dtype=np.uint64).reshape(-1, 7).copy()
+    sl = np.frombuffer((ctypes.c_uint64 * (2 * cnt)).from_address(ps.value),
+                       dtype=np.uint64).reshape(-1, 2).copy()
+    lib().orc_free(pp)
+    lib().orc_free(ps)
+    return ev, sl, ns.value
 
 
 def dfs_events(esa):

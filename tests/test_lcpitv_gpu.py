@@ -113,3 +113,82 @@ def test_device_resident_tree_and_events():
     assert np.array_equal(itv, _want_intervals(want))
     p.close()
     d.release()
+
+
+NONE = np.uint64(2 ** 64 - 1)
+
+
+def _run_info_visitor(e):
+    """gt_esa_bottomup_info_hip with integer handles: every callback recorded
+    as (event record, father handle, son handle), handles 1, 2, ... in
+    info_new order, and the handles info_delete received."""
+    made, deleted, out = [0], [], []
+
+    def new():
+        made[0] += 1
+        return made[0]
+
+    G.esa_bottomup_info(e.lcpbytes, e.llv, e.suftab, e.n, e.nonspecials, new, deleted.append,
+                        leaf_edge=lambda f, fd, flb, fi, leaf: out.append(((0, f, fd, flb, leaf, 0, 0),
+                                                                          fi, 0)),
+                        branching_edge=lambda f, fd, flb, fi, sd, slb, srb, si:
+                            out.append(((1, f, fd, flb, sd, slb, srb), fi, si)),
+                        lcp_interval=lambda lcp, lb, rb, i: out.append(((2, 0, lcp, lb, rb, 0, 0), i, 0)))
+    return out, made[0], deleted
+
+
+@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB", "Reads2.fna", "TTT-small.fna"])
+def test_info_visitor_matches_reference_stack(name):
+    """Per-node visitor state (GtESAVisitorInfo, esa_visitor_rep.h:25-67):
+    every callback gets the info object the reference's stack slot would
+    hand it (orc_bottomup_events_slots: handle = slot + 1, none = 0), the
+    objects are created 32 at a time as the stack grows and each is deleted
+    once, in slot order, after the traversal (esa-bottomup.c:20-110)."""
+    e = oracle_esa(name)
+    want_ev, want_sl, nslots = O.bottomup_events_slots(e)
+    got, made, deleted = _run_info_visitor(e)
+    assert np.array_equal(np.array([g[0] for g in got], dtype=np.uint64).reshape(-1, 7), want_ev)
+    handles = np.array([(g[1], g[2]) for g in got], dtype=np.uint64).reshape(-1, 2)
+    want_h = np.where(want_sl == NONE, np.uint64(0), want_sl + np.uint64(1))
+    want_h[want_ev[:, 0] != 1, 1] = 0          # son handles exist on branching edges only
+    assert np.array_equal(handles, want_h)
+    assert made == nslots and deleted == list(range(1, nslots + 1))
+
+
+def test_info_visitor_leaf_counts_deep_stack():
+    """A visitor that needs per-node state -- the leaves below each interval,
+    accumulated through the info objects (a father pushed into its first
+    child's slot inherits the child's count, as the reference hands the
+    child's state over) -- reports rb - lb + 1 for every interval; the text
+    nests more than 32 intervals (a second chunk of info objects)."""
+    rng = np.random.default_rng(17)
+    t = np.concatenate([rng.integers(0, 4, 3000, dtype=np.uint8), np.full(150, 3, np.uint8),
+                        np.zeros(1, np.uint8), rng.integers(0, 4, 3000, dtype=np.uint8)])
+    e = O.Esa(t)
+    state, bad, seen = {}, [], [0]
+
+    def leaf(f, fd, flb, fi, leafnumber):
+        state[fi] = 1 if f else state[fi] + 1
+
+    def branch(f, fd, flb, fi, sd, slb, srb, si):
+        if si == 0:
+            assert f == 1 and flb == slb
+        elif f:
+            state[fi] = state[si]
+        else:
+            state[fi] += state[si]
+
+    def itv(lcp, lb, rb, i):
+        seen[0] += 1
+        if state[i] != rb - lb + 1:
+            bad.append((lcp, lb, rb))
+
+    made = [0]
+
+    def new():
+        made[0] += 1
+        return made[0]
+
+    G.esa_bottomup_info(e.lcpbytes, e.llv, e.suftab, e.n, e.nonspecials, new, None, leaf, branch, itv)
+    assert made[0] > 32 and seen[0] > 1000
+    assert bad == []

@@ -327,3 +327,56 @@ def test_maxpairs_blocks_equal_maxpairs(name, minlen):
         return a[np.lexsort(a.T[::-1])]
     assert len(want) > 0
     assert np.array_equal(key(got), key(want))
+
+
+NONE = np.uint64(2 ** 64 - 1)
+
+
+def _leafcount_visit(ev, sl):
+    """A visitor with per-node state (the leaves below each interval), run
+    over an event stream with its stack slots the way gt_esa_bottomup hands
+    GtESAVisitorInfo objects to a visitor: returns the intervals whose count
+    is not rb - lb + 1 (none, if the slot model is the reference's)."""
+    state, bad = {}, []
+    for (t, f, a, b, c, d, e), (s0, s1) in zip(ev.tolist(), sl.tolist()):
+        if t == 0:
+            state[s0] = 1 if f else state[s0] + 1
+        elif t == 1:
+            if s1 == int(NONE):            # father pushed into its first child's slot
+                assert f == 1 and b == d   # same lb: the child's state carries over
+            elif f:
+                state[s0] = state[s1]
+            else:
+                state[s0] += state[s1]
+        elif state[s0] != c - b + 1:
+            bad.append((a, b, c))
+    return bad
+
+
+@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB", "Reads2.fna", "TTT-small.fna"])
+def test_event_slots_model_visitor_info(name):
+    """orc_bottomup_events_slots: same events as orc_bottomup_events, and the
+    stack slots (the reference's GtESAVisitorInfo, esa-bottomup.c:20-110)
+    carry a per-node leaf count correctly -- the model F3's info visitor
+    (gt_esa_bottomup_info_hip) is checked against."""
+    e = oracle_esa(name)
+    ev, sl, nslots = O.bottomup_events_slots(e)
+    assert np.array_equal(ev, O.bottomup_events(e))
+    assert nslots % 32 == 0 and nslots > 0
+    used = sl[sl != NONE]
+    assert used.max() < nslots
+    assert _leafcount_visit(ev, sl) == []
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_event_slots_random(seed):
+    rng = np.random.default_rng(700 + seed)
+    t = _random_text(rng, int(rng.integers(2, 3000)), int(rng.integers(1, 5)), 0.02)
+    if seed % 2:                           # a run of the largest symbol before a smaller
+        run = np.full(int(rng.integers(40, 200)), 3, np.uint8)   # one: LCPs rise row by row,
+        t = np.concatenate([t[:50], run, np.zeros(1, np.uint8), t[50:100]])   # > 32 slots
+    e = O.Esa(t)
+    ev, sl, nslots = O.bottomup_events_slots(e)
+    assert _leafcount_visit(ev, sl) == []
+    if seed % 2:
+        assert nslots > 32

@@ -80,3 +80,36 @@ def test_maxpairs_through_the_shim(indexes, name, minlen, mode, width):
     got = _run(indexes[(name, width)], minlen, "maxpairs", *extra)
     assert len(want) > 0
     assert np.array_equal(got, want), (len(got), len(want))
+
+
+@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB"])
+def test_esa_bottomup_gpu_drives_a_gt_visitor(tmp_path, name):
+    """gt_esa_bottomup_gpu (the shim's replacement of gt_esa_bottomup,
+    src/match/esa-bottomup.h:31-33) drives a GtESAVisitor through the
+    reference's gt_esa_visitor_* calls (a recording double): every call,
+    its GtESAVisitorInfo objects (stack-slot identity, creation order) and
+    their deletion equal the reference traversal's
+    (orc_bottomup_events_slots, esa-bottomup.c:20-273)."""
+    if not os.path.isfile(SHIM_EXEC):
+        pytest.fail("integration/exec_test/_build/shim_exec missing")
+    idx = str(tmp_path / "idx")
+    O.index_fasta(os.path.join(GOLDEN, name), idx)
+    r = subprocess.run([SHIM_EXEC, idx, "0", "bottomup"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    calls, deleted = [], []
+    for line in r.stdout.splitlines():
+        f = line.split()
+        if f[0] == "D":
+            deleted.append(int(f[1]))
+        else:
+            calls.append([int(x) for x in f])
+    got = np.array(calls, dtype=np.uint64).reshape(-1, 9)
+    e = oracle_esa(name)
+    ev, sl, nslots = O.bottomup_events_slots(e)
+    none = np.uint64(2 ** 64 - 1)
+    ids = np.where(sl == none, np.uint64(0), sl + np.uint64(1))
+    ids[ev[:, 0] != 1, 1] = 0
+    assert np.array_equal(got[:, :7], ev)
+    assert np.array_equal(got[:, 7:], ids)
+    assert deleted == list(range(1, nslots + 1))
