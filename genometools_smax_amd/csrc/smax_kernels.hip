@@ -137,7 +137,24 @@ struct SmaxScanArgs {
   uint32_t k1_reset;         // combined placement without K0: K1 clears the pending slot
   uint32_t wide_cap;         // wide slots (SMAX_TILE / 2 records each) at the pool's start
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
+  unsigned long long *stamps; // diagnostic (GT_SMAX_STAMPS, diag build only): per-section
+                              // s_memtime cycles of K1 summed over waves, [7] = tiles
 };
+
+// K1 section stamps (diagnostic build): cycles since the previous stamp
+// into acc[k]; the production build compiles them away
+struct SmaxStamps {
+  unsigned long long acc[8];
+  unsigned long long prev;
+};
+#define SMAX_STAMP(ST, K)                                                    \
+  do {                                                                       \
+    if ((ST) != nullptr) {                                                   \
+      const unsigned long long tn_ = __builtin_amdgcn_s_memtime();           \
+      (ST)->acc[K] += tn_ - (ST)->prev;                                      \
+      (ST)->prev = tn_;                                                      \
+    }                                                                        \
+  } while (0)
 
 // ------------------------------------------------------------ helpers
 
@@ -1073,7 +1090,8 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
 template <int DL, bool FFPV>
 __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &a, uint64_t g0,
                                               const uint8_t *sL, uint32_t *ent,
-                                              uint64_t *stg, uint32_t segpre) {
+                                              uint64_t *stg, uint32_t segpre,
+                                              SmaxStamps *st = nullptr) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const bool all_exact = a.minlen > 128;
@@ -1148,6 +1166,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     rank[0] = 0;
     rank[1 + SMAX_TILE / 16] = (uint16_t) fbase;
   }
+  SMAX_STAMP(st, 3);
   if (nL > DL) return UINT32_MAX;
   if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
   // exact evaluation of the queued starts (one per lane); accepted ones set
@@ -1182,6 +1201,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     // K1b (16-byte records)
     if (__ballot(wide) != 0) return UINT32_MAX;
   }
+  SMAX_STAMP(st, 4);
   // records in row order, written by the owning lanes; a tile with more
   // records than its slot holds goes to K1b (the writes past the slot land
   // on its last entry; K1b redoes the tile)
@@ -1218,6 +1238,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     }
     wcount += tot;
   }
+  SMAX_STAMP(st, 5);
   return wcount;   // > SMAX_SSLOT: the caller defers the tile
 }
 
@@ -1376,6 +1397,15 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // made that wait take their latency (measured 0.22 ms of K1 at C3)
   uint64_t prec = 0;
   uint32_t ptile = ~0u, pcnt = 0;
+  SmaxStamps stv;
+  SmaxStamps *st = nullptr;
+  if constexpr (DIAG) {
+    if (a.stamps != nullptr) {
+      st = &stv;
+      for (int k = 0; k < 8; k++) stv.acc[k] = 0;
+      stv.prev = __builtin_amdgcn_s_memtime();
+    }
+  }
   for (uint32_t it = 0;; it++) {
     const uint32_t cur = it & 1u;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
@@ -1390,6 +1420,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
+    if constexpr (DIAG) SMAX_STAMP(st, 0);
     if (ptile != ~0u) {
       smax_flush_tile(a, ptile, prec, pcnt);
       ptile = ~0u;
@@ -1418,8 +1449,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
 
+    if constexpr (DIAG) SMAX_STAMP(st, 1);
     t.halo_ff = SMAX_WIN_HALO(wnf);
     uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
+    if constexpr (DIAG) SMAX_STAMP(st, 2);
     if (a.dbg & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
       if (a.dbg & (1u << 17)) {
         uint32_t x = segpre_bits;
@@ -1445,7 +1478,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     bool defer = !stat && wave_pre && (a.dbg & 128u);
     if (!stat && !defer && wave_pre) {
       wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave],
-                                                    window_scratch(W), segpre_bits);
+                                                    window_scratch(W), segpre_bits,
+                                                    DIAG ? st : nullptr);
       // exact-queue overflow (UINT32_MAX) or more records than the tile's
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
@@ -1464,12 +1498,20 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       ptile = tile;
       pcnt = wcount;
     }
+    if constexpr (DIAG) {
+      SMAX_STAMP(st, 6);
+      if (st != nullptr) st->acc[7]++;
+    }
 
     tile = next;
     if (tile >= a.num_tiles) break;
   }
   if (ptile != ~0u) smax_flush_tile(a, ptile, prec, pcnt);
   glds_wait();
+  if constexpr (DIAG) {
+    if (st != nullptr && lane == 0)
+      for (int k = 0; k < 8; k++) atomicAdd(&a.stamps[k], st->acc[k]);
+  }
 }
 
 // K1b: the tiles K1 defers -- shard edges (row 0, begin, end, N), windows
@@ -2371,6 +2413,7 @@ struct GtSmaxPlan {
   uint32_t dbg;
   // optional K1 timing: event pairs recorded around the scan kernel
   hipEvent_t *ev;
+  unsigned long long *stamps;    // GT_SMAX_STAMPS: K1 section cycles (diag build)
   int nslots;
   int tstride;               // K1 events on every tstride-th run (gt_smax_plan_timing_stride)
   uint64_t runs;
@@ -2467,6 +2510,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   {
     const char *d = getenv("GT_SMAX_DEBUG");
     p->dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
+    // section stamps need the diagnostic build (a no-op ablation bit selects it)
+    if (getenv("GT_SMAX_STAMPS")) p->dbg |= 1u << 30;
   }
   double tpc = smax_phase_clock();
   HIPCHK(hipSetDevice(shard->device));
@@ -2554,6 +2599,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(dalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
+  if (getenv("GT_SMAX_STAMPS")) {
+    HIPCHK(dalloc(&p->stamps, sizeof (unsigned long long) * 8));
+    HIPCHK(hipMemset(p->stamps, 0, sizeof (unsigned long long) * 8));
+  }
   // K1's runtime list; in the combined placement (mode 4) the static list is
   // copied to its front and K1 appends behind it
   HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (2 * (uint64_t) p->num_tiles + 1)));
@@ -2685,7 +2734,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
@@ -2740,6 +2789,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.k1b_head = 0;
   a.k1_reset = 0;
   a.dbg = p->dbg;
+  a.stamps = p->stamps;
   return a;
 }
 
@@ -3057,6 +3107,16 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
                                  hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return 0;
+}
+
+// diagnostic: K1's per-section cycle sums (GT_SMAX_STAMPS plans; 8 values:
+// wait, flush+issue, filter, classify+queue, exact starts, output, staging,
+// tiles); -1 if the plan has none
+extern "C" int gt_smax_plan_stamps(GtSmaxPlan *p, unsigned long long *out8) {
+  if (p->stamps == nullptr) return -1;
+  if (hipSetDevice(p->shard.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpy(out8, p->stamps, sizeof (unsigned long long) * 8, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? 0 : -1;
 }
 
 extern "C" uint32_t gt_smax_plan_error_bits(GtSmaxPlan *p) {

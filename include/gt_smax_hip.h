@@ -265,6 +265,13 @@ int gt_smax_plan_fetch_triples(GtSmaxPlan *plan, uint64_t *lcp_lb_rb,
  * 2 = a table read outside the shard's rows. */
 uint32_t gt_smax_plan_error_bits(GtSmaxPlan *plan);
 
+/* Diagnostic: with GT_SMAX_STAMPS set when the plan was created, K1 runs its
+ * diagnostic build and sums s_memtime cycles per section over all waves:
+ * out8 = {window wait, flush + next DMA issue, segment filter,
+ * classification + exact queue, exact starts, record output, staging, tiles}
+ * accumulated over the plan's runs.  -1 for a plan without stamps. */
+int gt_smax_plan_stamps(GtSmaxPlan *plan, unsigned long long *out8);
+
 /* Diagnostic: tiles the last run handed from K1 to the generic kernel K1b
  * (shard edges and tiles with more exact-evaluation starts than K1 queues). */
 uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *plan);
