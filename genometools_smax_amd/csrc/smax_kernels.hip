@@ -109,6 +109,8 @@ struct SmaxScanArgs {
   const uint8_t *lcp;        // local tables: index i <-> global base+i
   const uint8_t *bwt;
   const uint64_t *bwtpk;     // packed BWT, 16 rows per u64 (index local_row/16 + 1), or null
+  const uint32_t *bwt2;      // its two code planes alone, 16 rows per u32 (same index), or
+                             // null: K1's window stream when no window holds a special
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
   const uint16_t *llv16;     // their values as u16 (plan time; windows with larger ones defer)
   uint64_t numllv;
@@ -244,6 +246,7 @@ struct Win {
   const uint8_t *L;           // LDS window: index o = g - g0 + LH
   const uint8_t *B;           // BWT bytes of the window (byte kernel), or
   const uint64_t *P;          // packed BWT of the window, 16 rows per word
+  bool p2;                    // P holds u32 words (code planes only, no specials)
   const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
   const uint32_t *val;        // LDS .llv values in rank order (nval of them), or
   const uint16_t *val16;      // the same as u16 (K1 windows: values < 65536)
@@ -259,13 +262,19 @@ struct Win {
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.glcp = a.lcp; t.gbwt = a.bwt; t.gpk = a.bwtpk; t.llv = a.llv; t.numllv = a.numllv;
   t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
-  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.rank = nullptr; t.val = nullptr;
+  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.p2 = false; t.rank = nullptr; t.val = nullptr;
   t.val16 = nullptr; t.nval = -1; t.halo_ff = 0; t.staged_all = false;
   t.g0 = 0; t.llv_base = 0;
 }
 
 __device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
   return (int64_t) (g - t.g0) + SMAX_LH;
+}
+
+// packed BWT group gi of the window as a u64 word (the 2-plane form reads
+// as the u64 form with no special bits)
+__device__ __forceinline__ uint64_t pk_word(const Win &t, uint32_t gi) {
+  return t.p2 ? (uint64_t) reinterpret_cast<const uint32_t *>(t.P)[gi] : t.P[gi];
 }
 
 // exact LCP of a row whose byte is 255
@@ -315,7 +324,7 @@ __device__ __forceinline__ uint32_t pk_sym(uint64_t w, uint32_t q) {
 __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
-  if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(t.P[o >> 4], (uint32_t) (o & 15));
+  if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(pk_word(t, (uint32_t) (o >> 4)), (uint32_t) (o & 15));
   if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
   if (t.gpk != nullptr)
     return pk_sym(gld_u64(&t.gpk[(g - t.base) / 16 + 1]), (uint32_t) ((g - t.base) & 15));
@@ -526,6 +535,7 @@ __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0
   if (n != 0 && lane < SMAX_LLV_CAP / 8 && (uint32_t) (8 * lane) < n + (lo & 7u))
     glds16(a.llv16 + (lo & ~7u) + 8 * lane, wv);
 }
+template <bool BW2 = false>   // byte windows: no 2-plane form
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
@@ -555,14 +565,15 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
 // small (the 4- and 8-way C3 splits) the step is 2-6 % shorter; on the whole
 // C3 table 6 % longer, on a table the MALL holds (C2) 4 % longer -- so the
 // plan picks it by shard size (GtSmaxPlan::nt).
-template <bool NT>
+template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
                                                 uint32_t lo, uint32_t n, const void *ibase,
                                                 uint32_t iaddr, uint32_t v16, uint32_t v4) {
   const uint32_t wp = wl + (uint32_t) offsetof(SmaxWindowPk, P);
   const uint32_t wv = wl + (uint32_t) offsetof(SmaxWindowPk, val16);
   const uint8_t *lb = a.lcp + l0 - SMAX_LH;
-  const uint8_t *pb = reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16);
+  const uint8_t *pb = BW2 ? reinterpret_cast<const uint8_t *>(a.bwt2 + l0 / 16)
+                          : reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16);
   const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u));
   const uint32_t nl8 = n == 0 ? 0u : (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
   const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;   // < 64
@@ -571,7 +582,66 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   const uint8_t *ib = reinterpret_cast<const uint8_t *>(ibase);
   uint32_t keep;
   uint64_t ex;
-  if constexpr (NT) {
+  // 2-plane form: groups l0/16 .. l0/16+131 are 132 u32 = 33 lanes x 16 B
+  const uint64_t p2mask = (1ull << 33) - 1;
+  (void) p2mask;
+  if constexpr (BW2 && NT) {
+  asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:0 nt\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:1024 nt\n\t"
+        "s_mov_b32 m0, %5\n\t"
+        "s_mov_b64 exec, %14\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:0 nt\n\t"
+        "s_mov_b64 exec, 3\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:2048 nt\n\t"
+        "s_mov_b64 exec, %11\n\t"
+        "s_mov_b32 m0, %6\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
+        "s_mov_b64 exec, %13\n\t"
+        "s_mov_b32 m0, %7\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, %12 offset:0\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(ex)
+        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+        : "memory");
+  } else if constexpr (BW2) {
+  asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:1024\n\t"
+        "s_mov_b32 m0, %5\n\t"
+        "s_mov_b64 exec, %14\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
+        "s_mov_b64 exec, 3\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:2048\n\t"
+        "s_mov_b64 exec, %11\n\t"
+        "s_mov_b32 m0, %6\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
+        "s_mov_b64 exec, %13\n\t"
+        "s_mov_b32 m0, %7\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, %12 offset:0\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(ex)
+        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+        : "memory");
+  } else if constexpr (NT) {
   asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %4\n\t"
@@ -632,13 +702,18 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   }
 }
 
+template <bool BW2 = false>
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
   const uint32_t wp = __builtin_amdgcn_readfirstlane(lds_addr(w->P));
+  issue_lcp_llv(a, l0, w->L, w->val16, lo, n);
+  if (BW2) {   // 2-plane groups l0/16 .. l0/16 + 131 (u32 each): 33 lanes x 16 B
+    if (lane < 33) glds16(a.bwt2 + l0 / 16 + lane * 4, wp);
+    return;
+  }
   // groups l0/16 .. l0/16 + 129 of the packed array (index = local_row/16 + 1)
   const uint64_t *ps = a.bwtpk + l0 / 16;
-  issue_lcp_llv(a, l0, w->L, w->val16, lo, n);
   glds16(ps + lane * 2, wp);                             // groups 0 .. 127
   if (lane == 0) glds16(ps + 128, wp + 1024);            // groups 128, 129
 }
@@ -748,7 +823,7 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
     uint32_t plo = 0, phi = 0, psp = 0;
     if (t.B == nullptr) {   // packed window (K1 sets B = nullptr: folds at compile time)
       const uint32_t o = co - 1, gi = o >> 4, q = o & 15u;
-      const uint64_t w0 = t.P[gi], w1 = t.P[gi + 1];
+      const uint64_t w0 = pk_word(t, gi), w1 = pk_word(t, gi + 1);
       const uint32_t a0 = (uint32_t) w0, a1 = (uint32_t) w1;
       plo = (((a0 & 0xffffu) | (a1 << 16)) >> q) & 0xffu;
       phi = (((a0 >> 16) | (a1 & 0xffff0000u)) >> q) & 0xffu;
@@ -855,7 +930,7 @@ __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0
 __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t *div2,
                                             uint32_t *div3) {
   if (t.B == nullptr) {   // packed window
-    const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1], nw = t.P[(so >> 4) + 1];
+    const uint64_t w = pk_word(t, so >> 4), pw = pk_word(t, (so >> 4) - 1), nw = pk_word(t, (so >> 4) + 1);
     // both code planes at once (low plane bits 0..15, high plane 16..31)
     const uint32_t c = (uint32_t) w, pc = (uint32_t) pw, nc = (uint32_t) nw;
     const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
@@ -1243,13 +1318,13 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
 }
 
 // next tile's window + the llv_win entry of the tile after it (ring slot iaddr)
-template <bool NT>
+template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
                                            uint32_t iaddr, uint32_t v16, uint32_t v4) {
-  issue_window_pk<NT>(a, l0, wl, lo, n, info, iaddr, v16, v4);
+  issue_window_pk<NT, BW2>(a, l0, wl, lo, n, info, iaddr, v16, v4);
 }
-template <bool NT>
+template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
                                            uint32_t iaddr, uint32_t v16, uint32_t v4) {
@@ -1282,7 +1357,7 @@ __device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint3
   // any 0xff byte: a zero byte of ~w (exact as an any-test)
   const uint32_t ff = ((0xfefefefeu - v.x) & v.x) | ((0xfefefefeu - v.y) & v.y) |
                       ((0xfefefefeu - v.z) & v.z) | ((0xfefefefeu - v.w) & v.w);
-  const uint64_t w = t.P[so >> 4], pw = t.P[(so >> 4) - 1];
+  const uint64_t w = pk_word(t, so >> 4), pw = pk_word(t, (so >> 4) - 1);
   const uint32_t c = (uint32_t) w, pc = (uint32_t) pw;
   const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
   const uint32_t spm1 = ((sp << 1) | ((uint32_t) (pw >> 47) & 1u)) & 0xffffu;
@@ -1339,7 +1414,7 @@ __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t 
 // here; shard-edge tiles and tiles with more exact starts than the direct
 // path queues are deferred to K1b (their generic path is kept out of K1,
 // whose register budget it would otherwise set).
-template <typename WinT, bool DIAG, bool FFPV = false, bool NT = false>
+template <typename WinT, bool DIAG, bool FFPV = false, bool NT = false, bool BW2 = false>
 __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // the production kernel sees dbg == 0 as a constant: every diagnostic
   // branch (GT_SMAX_DEBUG) folds away, a scalar test and branch each
@@ -1385,7 +1460,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
           info1);
   }
   glds_wait();
-  issue_window(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0],
+  issue_window<BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0],
                __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
                SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])));
 
@@ -1415,6 +1490,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     t.g0 = g0;
     t.L = W->L;
     set_bwt_window(t, W);
+    t.p2 = BW2;
     t.val = nullptr;
     t.val16 = W->val16;
 
@@ -1444,7 +1520,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // tile's work
     if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
       const uint32_t n2 = next + stride <= last ? next + stride : last;
-      issue_next<NT>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
+      issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
@@ -2098,6 +2174,20 @@ __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_nt(SmaxSc
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true, true>(a);
 }
+// 2-plane BWT window stream (GtSmaxPlan::bw2: 0.25 B/row of BWT instead of
+// 0.5; windows holding a special BWT symbol go to the static K1b list)
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, false, false, true>(a);
+}
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_dense(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, true, false, true>(a);
+}
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_nt(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, false, true, true>(a);
+}
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_dense_nt(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowPk, false, true, true, true>(a);
+}
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_diag(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, true>(a);
 }
@@ -2262,6 +2352,28 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
 
 // ------------------------------------------------------------ llv index
 
+// K1's 2-plane window stream from the packed BWT: bwt2[g] = the code planes
+// of group g; a group with a special row flags every K1 window that reads it
+// (tile i's window: groups L/16 .. L/16 + 129, L = (tile_first + i) * TILE)
+// for the static K1b list
+__global__ void __launch_bounds__(256)
+smax_bwt2_kernel(const uint64_t *pk, uint64_t ngroups, uint32_t *bwt2, uint2 *llv_win,
+                 uint64_t tile_first, uint64_t num_tiles) {
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t g = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; g < ngroups; g += stride) {
+    const uint64_t w = pk[g];
+    bwt2[g] = (uint32_t) w;
+    if ((w >> 32) & 0xffffull) {
+      constexpr uint64_t GPT = SMAX_TILE / 16;                      // groups per tile
+      const uint64_t t_hi = g / GPT;                                 // L/16 <= g
+      const uint64_t t_lo = g >= 129 ? (g - 129 + GPT - 1) / GPT : 0; // g <= L/16 + 129
+      for (uint64_t t = t_lo; t <= t_hi; t++)
+        if (t >= tile_first && t - tile_first < num_tiles)
+          atomicOr(&llv_win[t - tile_first].y, SMAX_WIN_STATIC);
+    }
+  }
+}
+
 // u16 copies of the .llv values (larger values are flagged per tile by the
 // index kernel; those windows never read this array)
 __global__ void __launch_bounds__(256)
@@ -2392,6 +2504,8 @@ struct GtSmaxPlan {
   uint2 *llv_win;
   uint64_t *bwtpk;           // packed BWT (DNA shards), else null
   bool pk, pk_owned;          // packed windows; bwtpk allocated by the plan
+  uint32_t *bwt2;            // its code planes alone (K1's 2-plane window stream), or null
+  bool bw2;                  // K1 streams bwt2 (windows with a special BWT row: static K1b)
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
   uint2 *defer_info;         // beside each entry: the tile's llv_win words
@@ -2635,8 +2749,24 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   if (herr & 2u) { seterr(errbuf, errlen, ".llv positions not strictly increasing"); goto fail; }
   smax_dev_free(derr);
   derr = NULL;
-  // static K1b list (needs llv_win)
   smax_phase_mark(" llv_index", &tpc);
+  // K1's 2-plane window stream: the packed BWT without its special plane
+  // (0.25 B per row instead of 0.5); a window that holds a special BWT row
+  // goes to the static K1b list, which reads the full packed form
+  // (GT_SMAX_BW2=0: K1 streams the u64 groups)
+  {
+    const char *b2 = getenv("GT_SMAX_BW2");
+    p->bw2 = p->pk && !(b2 && strtol(b2, NULL, 0) == 0) && p->num_tiles > 0;
+    if (p->bw2) {
+      const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
+      HIPCHK(dalloc(&p->bwt2, sizeof (uint32_t) * ngroups));
+      hipLaunchKernelGGL(smax_bwt2_kernel, dim3((unsigned) std::min<uint64_t>((ngroups + 255) / 256, 1u << 20)),
+                         dim3(256), 0, 0, p->bwtpk, ngroups, p->bwt2, p->llv_win, p->tile_first,
+                         (uint64_t) p->num_tiles);
+      HIPCHK(hipGetLastError());
+    }
+  }
+  // static K1b list (needs llv_win)
   HIPCHK(dalloc(&p->static_list, sizeof (uint32_t) * ((uint64_t) p->num_tiles + 1)));
   HIPCHK(dalloc(&p->static_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->static_count, 0, sizeof (uint32_t)));
@@ -2734,7 +2864,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   if (p->side) {
@@ -2755,6 +2885,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.lcp = p->shard.lcp_dev;
   a.bwt = p->shard.bwt_dev;
   a.bwtpk = p->pk ? p->bwtpk : nullptr;
+  a.bwt2 = p->bw2 ? p->bwt2 : nullptr;
   a.llv16 = p->llv16;
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;
@@ -2889,6 +3020,12 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
         ;   // diagnostic: re-run K1b on the first run's deferred tiles
       else if (p->pk && p->dbg)
         hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
+      else if (p->bw2 && p->dense)
+        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_dense_nt : smax_scan_kernel_b2_dense,
+                           dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
+      else if (p->bw2)
+        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_nt : smax_scan_kernel_b2, dim3(p->grid),
+                           dim3(SMAX_K1_THREADS), lp, s, a);
       else if (p->pk && p->dense)
         hipLaunchKernelGGL(p->nt ? smax_scan_kernel_dense_nt : smax_scan_kernel_dense, dim3(p->grid),
                            dim3(SMAX_K1_THREADS), lp, s, a);

@@ -144,17 +144,20 @@ def test_timing_stride(human10):
     p.close()
 
 
+@pytest.mark.parametrize("bw2", ["0", "1"])
 @pytest.mark.parametrize("nt", ["0", "1"])
 @pytest.mark.parametrize("dense", ["0", "1"])
-def test_window_stream_policy(human10, nt, dense):
+def test_window_stream_policy(human10, nt, dense, bw2):
     """Both window-stream policies of K1 (GT_SMAX_NT; the plan picks nt by
-    shard size) and both K1 variants give the oracle's records, whole table
-    and a middle shard's plan run (against the plain-policy plan)."""
+    shard size), both K1 variants and both BWT window forms (GT_SMAX_BW2: the
+    2-plane stream, windows with a special BWT row left to K1b; or the u64
+    groups) give the oracle's records, whole table and a middle shard's plan
+    run (against the plain-policy plan)."""
     esa, host = human10
     N = esa.nonspecials
     want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
-    old = {k: os.environ.get(k) for k in ("GT_SMAX_NT", "GT_SMAX_DENSE")}
-    os.environ.update(GT_SMAX_NT=nt, GT_SMAX_DENSE=dense)
+    old = {k: os.environ.get(k) for k in ("GT_SMAX_NT", "GT_SMAX_DENSE", "GT_SMAX_BW2")}
+    os.environ.update(GT_SMAX_NT=nt, GT_SMAX_DENSE=dense, GT_SMAX_BW2=bw2)
     try:
         p = esa.plan(20)
         q = esa.plan(20, N // 3, 2 * N // 3)
