@@ -76,7 +76,7 @@ for S in "$@"; do
       # environment K=V (plan-time switches), B without; same library
       IFS=: read -r _ ENVA KIND BASES MINLEN SHARD <<< "$S"
       AB_ENV_A="${ENVA//;/,}" timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" \
-        genometools_smax_amd/lib/libgtsmax_hip.so 8 "$SHARD" > "$O/abenv_${ENVA//[=;]/_}_${SHARD//\//of}.txt" 2>&1 ;;
+        genometools_smax_amd/lib/libgtsmax_hip.so 8 "$SHARD" > "$O/abenv_${KIND}_${ENVA//[=;]/_}_${SHARD//\//of}.txt" 2>&1 ;;
     stamps:*)
       timeout -k 10 600 python -u tools/k1_stamps.py "${S#stamps:}" 5 > "$O/stamps_${S#stamps:}.txt" 2>&1 ;;
     llvstats)
