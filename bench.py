@@ -312,10 +312,12 @@ def main():
             pmc_src = ("%s not used: taken on build %s / config %s, this run is build %s"
                        % (os.path.relpath(pmc_path, ROOT), pmc.get("build_id"), pmc.get("config"),
                           bid))
-    # a per-pass stream (1.5 B/row packed + .llv) that fits the 256 MiB
-    # Infinity Cache is re-read from it on every pass, not from HBM
-    # (MI355X_MICROARCH.md "Infinity Cache"): no HBM fraction is quoted then
-    stream_bytes = rows * 3 // 2 + 16 * llv_here
+    # a per-pass stream (LCP byte + 2-plane BWT = 1.25 B/row, 1.5 B/row with
+    # GT_SMAX_BW2=0, + .llv) that fits the 256 MiB Infinity Cache is re-read
+    # from it on every pass, not from HBM (MI355X_MICROARCH.md "Infinity
+    # Cache"): no HBM fraction is quoted then
+    per_row4 = 6 if os.environ.get("GT_SMAX_BW2", "1") == "0" else 5
+    stream_bytes = rows * per_row4 // 4 + 16 * llv_here
     in_mall = world == 1 and stream_bytes < (256 << 20)
 
     # N > 1 parity: every rank's stitched records gathered to rank 0 (padded

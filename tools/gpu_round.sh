@@ -18,7 +18,8 @@
 #   ab:LIB:KIND:BASES:MINLEN:SHARD   A/B of the in-tree library against LIB
 #                    (tools/ab_interleave.py, 8 interleaved rounds)
 #
-# Outputs go to gpurun_out/TAG/.  Every GPU step runs under its own timeout
+# Outputs go to gpurun_out/TAG/ (profiler databases are summarised and then
+# removed: gpurun copies back at most 64 MiB).  Every GPU step runs under its own timeout
 # and the script stops at the first failure (set -e).
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -50,18 +51,21 @@ for S in "$@"; do
           -d "$O/pmc_${C}_$X" -o p -- python3 "$R/tools/k1_once.py" "$C" 5 > "$O/pmc_${C}_$X.log" 2>&1)
       done
       python3 tools/rocpd_summary.py pmc "$O/pmc_$C.json" smax_scan_kernel "$C" \
-        "$O/pmc_${C}_FETCH_SIZE/p_results.db" "$O/pmc_${C}_WRITE_SIZE/p_results.db" ;;
+        "$O/pmc_${C}_FETCH_SIZE/p_results.db" "$O/pmc_${C}_WRITE_SIZE/p_results.db"
+      rm -rf "$O/pmc_${C}_FETCH_SIZE" "$O/pmc_${C}_WRITE_SIZE" ;;
     sq:*)
       C=${S#sq:}
       (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $SQ --kernel-include-regex smax_scan_kernel \
         -d "$O/sq_$C" -o p -- python3 "$R/tools/k1_once.py" "$C" 5 > "$O/sq_$C.log" 2>&1)
-      python3 tools/rocpd_summary.py pmc "$O/sq_$C.json" smax_scan_kernel "$C" "$O/sq_$C/p_results.db" ;;
+      python3 tools/rocpd_summary.py pmc "$O/sq_$C.json" smax_scan_kernel "$C" "$O/sq_$C/p_results.db"
+      rm -rf "$O/sq_$C" ;;
     prof:*)
       C=${S#prof:}
       (cd /tmp && TMPDIR=/tmp timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_$C" -o p -- \
         python3 "$R/bench.py" --config "$C" --steps 20 --warmup 3 --no-cpu-baseline --no-end-to-end \
         > "$O/prof_bench_$C.json" 2> "$O/prof_bench_$C.err")
-      python3 tools/rocpd_summary.py stats "$O/prof_$C/p_results.db" "$O/kernel_stats_$C.csv" ;;
+      python3 tools/rocpd_summary.py stats "$O/prof_$C/p_results.db" "$O/kernel_stats_$C.csv"
+      rm -rf "$O/prof_$C" ;;
     ab:*)
       # ab:LIBB:CONFIGKIND:BASES:MINLEN:SHARD -- tools/ab_interleave.py, in-tree
       # library (A) against LIBB (B) in one process, interleaved rounds
@@ -87,7 +91,8 @@ for S in "$@"; do
       W=${S#profshards:}
       (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/profshards_$W" -o p -- \
         python3 "$R/tools/shard_step.py" human 3e9 20 "$W" > "$O/profshards_$W.txt" 2>&1)
-      python3 tools/rocpd_summary.py stats "$O/profshards_$W/p_results.db" "$O/kernel_stats_shards_$W.csv" ;;
+      python3 tools/rocpd_summary.py stats "$O/profshards_$W/p_results.db" "$O/kernel_stats_shards_$W.csv"
+      rm -rf "$O/profshards_$W" ;;
     shards:*)
       W=${S#shards:}
       timeout -k 10 600 python -u tools/shard_step.py human 3e9 20 "$W" > "$O/shards_$W.txt" 2>&1 ;;
