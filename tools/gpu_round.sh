@@ -15,6 +15,7 @@
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
+#   tilestats:CONFIG tools/tile_stats.py (active segments and records per K1 tile)
 #   ab:LIB:KIND:BASES:MINLEN:SHARD   A/B of the in-tree library against LIB
 #                    (tools/ab_interleave.py, 8 interleaved rounds)
 #
@@ -83,6 +84,8 @@ for S in "$@"; do
         genometools_smax_amd/lib/libgtsmax_hip.so 8 "$SHARD" > "$O/abenv_${KIND}_${ENVA//[=;]/_}_${SHARD//\//of}.txt" 2>&1 ;;
     stamps:*)
       timeout -k 10 600 python -u tools/k1_stamps.py "${S#stamps:}" 5 > "$O/stamps_${S#stamps:}.txt" 2>&1 ;;
+    tilestats:*)
+      timeout -k 10 600 python -u tools/tile_stats.py "${S#tilestats:}" > "$O/tilestats_${S#tilestats:}.txt" 2>&1 ;;
     llvstats)
       for C in c3 c5; do
         timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1

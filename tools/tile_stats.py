@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Diagnostic: per K1 tile (2048 rows) of one bench config, how many of its
+128 16-row segments pass the filter (some LCP byte >= min(minlen, 128)) and
+how many smax records it holds -- the work K1 does beyond the window
+stream.
+
+  tile_stats.py CONFIG        (bench.py config: c2, c3, c5 ...)
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import genometools_smax_amd as G  # noqa: E402
+
+TILE, SEG = 2048, 16
+cfg = bench.CONFIGS[sys.argv[1]]
+minlen = cfg["minlen"]
+text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
+n = len(text)
+esa = G.DeviceEsa64(text, device=0) if n + 1 >= 2 ** 32 else G.DeviceEsa(text, device=0)
+del text
+N = esa.nonspecials
+plan = esa.plan(minlen)
+plan.run()
+trip = plan.fetch_triples()
+plan.close()
+lcp = esa.download()["lcptab"]
+esa.release()
+ntiles = (N + TILE - 1) // TILE
+mf = min(minlen, 128)
+act = np.zeros(ntiles, dtype=np.int32)
+CH = 1 << 16                      # tiles per chunk
+for t0 in range(0, ntiles, CH):
+    t1 = min(ntiles, t0 + CH)
+    seg = lcp[t0 * TILE: t1 * TILE]
+    pad = (t1 - t0) * TILE - len(seg)
+    if pad:
+        seg = np.concatenate([seg, np.zeros(pad, np.uint8)])
+    act[t0:t1] = (seg.reshape(t1 - t0, TILE // SEG, SEG) >= mf).any(axis=2).sum(axis=1)
+rec = np.bincount((trip[:, 1] // TILE).astype(np.int64), minlength=ntiles)[:ntiles]
+print("%s: N=%d, %d tiles, %d records (%.2f per tile)" % (sys.argv[1], N, ntiles, len(trip),
+                                                          len(trip) / ntiles))
+print("active segments per tile (of 128): mean %.1f" % act.mean())
+for lo, hi in ((0, 0), (1, 16), (17, 32), (33, 64), (65, 96), (97, 128)):
+    m = (act >= lo) & (act <= hi)
+    print("  %3d-%3d: %6.2f %% of tiles" % (lo, hi, 100.0 * m.mean()))
+print("records per tile: max %d" % rec.max())
+for lo, hi in ((0, 0), (1, 8), (9, 16), (17, 32), (33, 64), (65, 1 << 30)):
+    m = (rec >= lo) & (rec <= hi)
+    print("  %3d-%s: %6.2f %% of tiles" % (lo, hi if hi < 1 << 30 else "", 100.0 * m.mean()))
