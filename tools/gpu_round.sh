@@ -11,10 +11,13 @@
 #                    (separate passes) over tools/k1_once.py CONFIG
 #                    -> pmc_CONFIG.json (config + build id stamped)
 #   sq:CONFIG        K1 SQ instruction / wait counters, one pass -> sq_CONFIG.json
+#   sq2:CONFIG       K1 SQ active-per-pipe / waitcnt counters -> sq2_CONFIG.json
 #   prof:CONFIG      rocprofv3 --kernel-trace --stats of a bench run
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
+#   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
+#   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
 #   tilestats:CONFIG tools/tile_stats.py (active segments and records per K1 tile)
 #   ab:LIB:KIND:BASES:MINLEN:SHARD   A/B of the in-tree library against LIB
 #                    (tools/ab_interleave.py, 8 interleaved rounds)
@@ -30,6 +33,7 @@ shift
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
+SQ2="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS"
 for S in "$@"; do
   echo "[gpu_round] $S $(date +%T)"
   case $S in
@@ -54,6 +58,13 @@ for S in "$@"; do
       python3 tools/rocpd_summary.py pmc "$O/pmc_$C.json" smax_scan_kernel "$C" \
         "$O/pmc_${C}_FETCH_SIZE/p_results.db" "$O/pmc_${C}_WRITE_SIZE/p_results.db"
       rm -rf "$O/pmc_${C}_FETCH_SIZE" "$O/pmc_${C}_WRITE_SIZE" ;;
+    sq2:*)
+      # where the waves' cycles go: parked in s_waitcnt, issuing per pipe
+      C=${S#sq2:}
+      (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $SQ2 --kernel-include-regex smax_scan_kernel \
+        -d "$O/sq2_$C" -o p -- python3 "$R/tools/k1_once.py" "$C" 5 > "$O/sq2_$C.log" 2>&1)
+      python3 tools/rocpd_summary.py pmc "$O/sq2_$C.json" smax_scan_kernel "$C" "$O/sq2_$C/p_results.db"
+      rm -rf "$O/sq2_$C" ;;
     sq:*)
       C=${S#sq:}
       (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $SQ --kernel-include-regex smax_scan_kernel \
@@ -84,6 +95,24 @@ for S in "$@"; do
         genometools_smax_amd/lib/libgtsmax_hip.so 8 "$SHARD" > "$O/abenv_${KIND}_${ENVA//[=;]/_}_${SHARD//\//of}.txt" 2>&1 ;;
     stamps:*)
       timeout -k 10 600 python -u tools/k1_stamps.py "${S#stamps:}" 5 > "$O/stamps_${S#stamps:}.txt" 2>&1 ;;
+    rehearse:*)
+      # rehearse:W[:BASES] -- bench.py --gpus W as W torchrun ranks on this
+      # one GPU, boundary exchange staged through gloo (parity checked)
+      IFS=: read -r _ W BASES <<< "$S"
+      timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$W" \
+        --master-addr 127.0.0.1 --master-port $((29500 + W)) bench.py --gpus "$W" --one-gpu \
+        --dist-backend gloo ${BASES:+--bases $BASES} --steps 10 --warmup 2 \
+        > "$O/rehearse_w$W.json" 2> "$O/rehearse_w$W.err" ;;
+    pmcablate:*)
+      # pmcablate:V1,V2,... -- K1 SQ counters under GT_SMAX_DEBUG ablation bits (C3)
+      P="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM"
+      for V in $(echo "${S#pmcablate:}" | tr , ' '); do
+        (cd /tmp && GT_SMAX_DEBUG=$V TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc $P \
+          --kernel-include-regex smax_scan -d "$O/pmca_$V" -o p -- python3 "$R/tools/k1_once.py" c3 2 \
+          > "$O/pmca_$V.log" 2>&1)
+        python3 tools/rocpd_summary.py pmc "$O/pmca_$V.json" smax_scan "c3" "$O/pmca_$V/p_results.db"
+        rm -rf "$O/pmca_$V"
+      done ;;
     tilestats:*)
       timeout -k 10 600 python -u tools/tile_stats.py "${S#tilestats:}" > "$O/tilestats_${S#tilestats:}.txt" 2>&1 ;;
     llvstats)

@@ -33,6 +33,9 @@ esa.release()
 ntiles = (N + TILE - 1) // TILE
 mf = min(minlen, 128)
 act = np.zeros(ntiles, dtype=np.int32)
+# LCP chunks of 32 / 64 / 128 bytes with no byte >= mf (a zone map per 16
+# rows would let K1 skip their DMA), and runs of such chunks
+idle = {32: 0, 64: 0, 128: 0}
 CH = 1 << 16                      # tiles per chunk
 for t0 in range(0, ntiles, CH):
     t1 = min(ntiles, t0 + CH)
@@ -40,7 +43,10 @@ for t0 in range(0, ntiles, CH):
     pad = (t1 - t0) * TILE - len(seg)
     if pad:
         seg = np.concatenate([seg, np.zeros(pad, np.uint8)])
-    act[t0:t1] = (seg.reshape(t1 - t0, TILE // SEG, SEG) >= mf).any(axis=2).sum(axis=1)
+    a16 = (seg.reshape(t1 - t0, TILE // SEG, SEG) >= mf).any(axis=2)
+    act[t0:t1] = a16.sum(axis=1)
+    for w in idle:
+        idle[w] += int((~a16.reshape(t1 - t0, -1, w // SEG).any(axis=2)).sum())
 rec = np.bincount((trip[:, 1] // TILE).astype(np.int64), minlength=ntiles)[:ntiles]
 print("%s: N=%d, %d tiles, %d records (%.2f per tile)" % (sys.argv[1], N, ntiles, len(trip),
                                                           len(trip) / ntiles))
@@ -48,6 +54,9 @@ print("active segments per tile (of 128): mean %.1f" % act.mean())
 for lo, hi in ((0, 0), (1, 16), (17, 32), (33, 64), (65, 96), (97, 128)):
     m = (act >= lo) & (act <= hi)
     print("  %3d-%3d: %6.2f %% of tiles" % (lo, hi, 100.0 * m.mean()))
+for w in sorted(idle):
+    tot = ntiles * TILE // w
+    print("LCP chunks of %3d B with no byte >= %d: %6.2f %%" % (w, mf, 100.0 * idle[w] / tot))
 print("records per tile: max %d" % rec.max())
 for lo, hi in ((0, 0), (1, 8), (9, 16), (17, 32), (33, 64), (65, 1 << 30)):
     m = (rec >= lo) & (rec <= hi)
