@@ -258,6 +258,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     k1_ms, k1_n = plan.kernel_ms()
+    k1_name = plan.scan_kernel()
     count = plan.fetch_count()
     parity_ok = True
     res = None
@@ -518,7 +519,7 @@ def main():
                          "frac": None if in_mall else achieved / HBM_PEAK_GBS,
                          "stream_bytes_per_pass": stream_bytes,
                          "traffic": traffic,
-                         "kernel": "smax_scan_kernel", "kernel_avg_ms": k1_avg_ms,
+                         "kernel": k1_name, "kernel_avg_ms": k1_avg_ms,
                          "kernel_timed_launches": "%d of %d (HIP events on every %dth)"
                                                   % (k1_n, args.steps, ev_stride),
                          "algorithmic_bytes_per_launch": alg_bytes,

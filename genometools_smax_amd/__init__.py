@@ -174,6 +174,8 @@ def lib():
                                            ctypes.POINTER(u64), cs, sz]
         L.gt_smax_device_count.restype = ci
         L.gt_smax_build_id.restype = ctypes.c_char_p
+        L.gt_smax_plan_scan_kernel.restype = ctypes.c_char_p
+        L.gt_smax_plan_scan_kernel.argtypes = [vp]
         L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
         L.gt_smax_dev_free_table.argtypes = [ci, vp]
         L.gt_smax_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtSmaxDevShard), u32, u64,
@@ -817,6 +819,10 @@ class SmaxPlan:
 
     def error_bits(self):
         return lib().gt_smax_plan_error_bits(self.plan)
+
+    def scan_kernel(self):
+        """Name of the K1 variant this plan launches (gt_smax_plan_scan_kernel)."""
+        return lib().gt_smax_plan_scan_kernel(self.plan).decode()
 
     def deferred_tiles(self):
         return lib().gt_smax_plan_deferred_tiles(self.plan)

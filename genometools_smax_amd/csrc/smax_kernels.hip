@@ -3249,6 +3249,16 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
 // diagnostic: K1's per-section cycle sums (GT_SMAX_STAMPS plans; 8 values:
 // wait, flush+issue, filter, classify+queue, exact starts, output, staging,
 // tiles); -1 if the plan has none
+extern "C" const char *gt_smax_plan_scan_kernel(const GtSmaxPlan *p) {
+  // the selection of plan_run_scan
+  if (p->pk && p->dbg) return "smax_scan_kernel_diag";
+  if (p->bw2 && p->dense) return p->nt ? "smax_scan_kernel_b2_dense_nt" : "smax_scan_kernel_b2_dense";
+  if (p->bw2) return p->nt ? "smax_scan_kernel_b2_nt" : "smax_scan_kernel_b2";
+  if (p->pk && p->dense) return p->nt ? "smax_scan_kernel_dense_nt" : "smax_scan_kernel_dense";
+  if (p->pk) return p->nt ? "smax_scan_kernel_nt" : "smax_scan_kernel";
+  return "smax_scan_kernel_bytes";
+}
+
 extern "C" int gt_smax_plan_stamps(GtSmaxPlan *p, unsigned long long *out8) {
   if (p->stamps == nullptr) return -1;
   if (hipSetDevice(p->shard.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;

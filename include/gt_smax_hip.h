@@ -272,6 +272,12 @@ uint32_t gt_smax_plan_error_bits(GtSmaxPlan *plan);
  * accumulated over the plan's runs.  -1 for a plan without stamps. */
 int gt_smax_plan_stamps(GtSmaxPlan *plan, unsigned long long *out8);
 
+/* Name of the K1 variant the plan's runs launch (smax_scan_kernel,
+ * _b2 = 2-plane BWT window stream, _dense = vectorised 255-after-255
+ * relations, _nt = non-temporal window loads, _diag = GT_SMAX_DEBUG,
+ * _bytes = byte BWT windows); a static string. */
+const char *gt_smax_plan_scan_kernel(const GtSmaxPlan *plan);
+
 /* Diagnostic: tiles the last run handed from K1 to the generic kernel K1b
  * (shard edges and tiles with more exact-evaluation starts than K1 queues). */
 uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *plan);
