@@ -83,6 +83,16 @@ ka, kb = sorted(k1[id(LA)]), sorted(k1[id(LB)])
 print("median K1: A %.4f ms, B %.4f ms; rest of the step: A %.4f ms, B %.4f ms"
       % (ka[len(ka) // 2], kb[len(kb) // 2], ta[len(ta) // 2] - ka[len(ka) // 2],
          tb[len(tb) // 2] - kb[len(kb) // 2]))
+
+# both plans' last outputs must agree record for record
+na = plan_a.fetch_count()
+ra = plan_a.fetch_triples()
+G._lib = LB
+nb = plan_b.fetch_count()
+rb = plan_b.fetch_triples()
+G._lib = LA
+same = na == nb and bool((ra == rb).all())
+print("outputs A == B: %s (%d / %d records)" % (same, na, nb), flush=True)
 G._lib = LB
 plan_b.close()
 G._lib = LA
