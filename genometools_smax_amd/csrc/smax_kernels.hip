@@ -226,30 +226,54 @@ __device__ __forceinline__ uint64_t bytes_eq64(uint64_t x, uint64_t y) {
          bytes_eq((uint32_t) x, (uint32_t) y);
 }
 
+// LDS pointers held in Win are 32-bit local addresses (address space 3):
+// generic 64-bit pointers kept for their null tests cost an SGPR pair each
+// across K1's tile loop, and K1's loop was spilling SGPRs to VGPR lanes
+#define LDSP __attribute__((address_space(3)))
+template <typename T>
+__device__ __forceinline__ const LDSP T *to_lds(const T *p) { return (const LDSP T *) p; }
+__device__ __forceinline__ const LDSP uint8_t *to_lds_any(const uint8_t *p) { return to_lds(p); }
+__device__ __forceinline__ const LDSP uint8_t *to_lds_any(const LDSP uint8_t *p) { return p; }
+// 16 window bytes at an LDS address (16-byte aligned): one ds_read_b128
+__device__ __forceinline__ uint4 lds_ld16(const LDSP uint8_t *p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = *reinterpret_cast<const LDSP v4u *>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // 8 consecutive window bytes starting at LDS offset o (o + 11 inside the
 // window): three aligned dword reads, issued together
-__device__ __forceinline__ uint64_t lds_bytes8(const uint8_t *base, uint32_t o) {
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(base + (o & ~3u));
+template <typename P>
+__device__ __forceinline__ uint64_t lds_bytes8(P base, uint32_t o) {
+  const auto *w = reinterpret_cast<const LDSP uint32_t *>(to_lds_any(base) + (o & ~3u));
   const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
   const uint32_t sh = o & 3u;
   return ((uint64_t) __builtin_amdgcn_alignbyte(d2, d1, sh) << 32) |
          __builtin_amdgcn_alignbyte(d1, d0, sh);
 }
 
+// The launch's SmaxScanArgs in the kernarg segment: every kernel that builds
+// a Win takes them as its first parameter.  The global-fallback paths (rows
+// outside the LDS window, .llv values not staged) load the shard's table
+// pointers and bounds from there where they are used, through an opaque copy
+// of the segment pointer, so that none of them is held in SGPRs across K1's
+// tile loop (K1 spilled SGPRs to VGPR lanes, a VALU readlane per reload).
+typedef const __attribute__((address_space(4))) SmaxScanArgs *KArgs;
+__device__ __forceinline__ KArgs kargs() {
+  uint64_t p = (uint64_t) __builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (KArgs) p;
+}
+
 struct Win {
-  const uint8_t *glcp;        // global (local-indexed) tables
-  const uint8_t *gbwt;
-  const uint64_t *gpk;        // packed BWT groups (index local_row/16 + 1), or null
-  const GtSmaxLlv *llv;
-  uint64_t numllv, base, N, end, local_len;
-  uint32_t *err;
-  const uint8_t *L;           // LDS window: index o = g - g0 + LH
-  const uint8_t *B;           // BWT bytes of the window (byte kernel), or
-  const uint64_t *P;          // packed BWT of the window, 16 rows per word
+  uint64_t N, end;            // global row bounds (plateau scans)
+  const LDSP uint8_t *L;      // LDS window: index o = g - g0 + LH
+  const LDSP uint8_t *B;      // BWT bytes of the window (byte kernel), or
+  const LDSP uint64_t *P;     // packed BWT of the window, 16 rows per word
   bool p2;                    // P holds u32 words (code planes only, no specials)
-  const uint16_t *rank;       // per 16-byte chunk: 255 bytes before it
-  const uint32_t *val;        // LDS .llv values in rank order (nval of them), or
-  const uint16_t *val16;      // the same as u16 (K1 windows: values < 65536)
+  const LDSP uint16_t *rank;  // per 16-byte chunk: 255 bytes before it
+  const LDSP uint32_t *val;   // LDS .llv values in rank order (nval of them), or
+  const LDSP uint16_t *val16; // the same as u16 (K1 windows: values < 65536)
   int nval;                   // -1: values not staged (read global by rank)
   uint32_t halo_ff;           // 255 bytes in the window's left halo (K1)
   bool staged_all;            // K1: every value of the window is staged (nval of
@@ -260,8 +284,7 @@ struct Win {
 };
 
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
-  t.glcp = a.lcp; t.gbwt = a.bwt; t.gpk = a.bwtpk; t.llv = a.llv; t.numllv = a.numllv;
-  t.base = a.base; t.N = a.N; t.end = a.end; t.local_len = a.local_len; t.err = a.err;
+  t.N = a.N; t.end = a.end;
   t.L = nullptr; t.B = nullptr; t.P = nullptr; t.p2 = false; t.rank = nullptr; t.val = nullptr;
   t.val16 = nullptr; t.nval = -1; t.halo_ff = 0; t.staged_all = false;
   t.g0 = 0; t.llv_base = 0;
@@ -274,7 +297,7 @@ __device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
 // packed BWT group gi of the window as a u64 word (the 2-plane form reads
 // as the u64 form with no special bits)
 __device__ __forceinline__ uint64_t pk_word(const Win &t, uint32_t gi) {
-  return t.p2 ? (uint64_t) reinterpret_cast<const uint32_t *>(t.P)[gi] : t.P[gi];
+  return t.p2 ? (uint64_t) reinterpret_cast<const LDSP uint32_t *>(t.P)[gi] : t.P[gi];
 }
 
 // exact LCP of a row whose byte is 255
@@ -282,7 +305,7 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
   if (t.rank != nullptr && o >= 0 && o < SMAX_LDSB) {
     const int chunk = (int) (o >> 4), within = (int) (o & 15);
-    const uint4 v = *reinterpret_cast<const uint4 *>(&t.L[chunk * 16]);
+    const uint4 v = lds_ld16(&t.L[chunk * 16]);
     const uint64_t lo = (uint64_t) bytes_ff(v.x) | ((uint64_t) bytes_ff(v.y) << 32);
     const uint64_t hi = (uint64_t) bytes_ff(v.z) | ((uint64_t) bytes_ff(v.w) << 32);
     int cnt;
@@ -291,10 +314,12 @@ __device__ static uint32_t lcp_big(const Win &t, uint64_t g) {
     const uint32_t r = t.rank[chunk] + (uint32_t) cnt;
     if (t.staged_all) return t.val16[min((int) r, t.nval - 1)];
     if ((int) r < t.nval) return t.val16 != nullptr ? t.val16[r] : t.val[r];
-    if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
-    return llv_value(&t.llv[t.llv_base + r]);
+    const KArgs k = kargs();
+    if (t.llv_base + r >= k->numllv) { atomicOr(k->err, SMAX_ERR_LLV); return 255; }
+    return llv_value(&k->llv[t.llv_base + r]);
   }
-  return llv_search_global(t.llv, 0, t.numllv, g, t.err);
+  const KArgs k = kargs();
+  return llv_search_global(k->llv, 0, k->numllv, g, k->err);
 }
 
 // byte of LCP[g] (LCP[0] = LCP[N] = 0 are returned as 0)
@@ -302,8 +327,9 @@ __device__ __forceinline__ uint32_t lcp_byte(const Win &t, uint64_t g) {
   if (g == 0 || g >= t.N) return 0;
   const int64_t o = win_off(t, g);
   if (t.L != nullptr && o >= 0 && o < SMAX_LDSB) return t.L[o];
-  if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 0; }
-  return gld_u8(&t.glcp[g - t.base]);
+  const KArgs k = kargs();
+  if (g < k->base || g - k->base >= k->local_len) { atomicOr(k->err, SMAX_ERR_RANGE); return 0; }
+  return gld_u8(&k->lcp[g - k->base]);
 }
 
 __device__ __forceinline__ uint32_t lcp_exact(const Win &t, uint64_t g) {
@@ -325,10 +351,12 @@ __device__ __forceinline__ uint32_t bwt_at(const Win &t, uint64_t g) {
   const int64_t o = win_off(t, g);
   if (t.B != nullptr && o >= 0 && o < SMAX_LDSB) return t.B[o];
   if (t.P != nullptr && o >= 0 && o < SMAX_LDSB) return pk_sym(pk_word(t, (uint32_t) (o >> 4)), (uint32_t) (o & 15));
-  if (g < t.base || g - t.base >= t.local_len) { atomicOr(t.err, SMAX_ERR_RANGE); return 254; }
-  if (t.gpk != nullptr)
-    return pk_sym(gld_u64(&t.gpk[(g - t.base) / 16 + 1]), (uint32_t) ((g - t.base) & 15));
-  return gld_u8(&t.gbwt[g - t.base]);
+  const KArgs k = kargs();
+  const uint64_t base = k->base;
+  if (g < base || g - base >= k->local_len) { atomicOr(k->err, SMAX_ERR_RANGE); return 254; }
+  if (k->bwtpk != nullptr)
+    return pk_sym(gld_u64(&k->bwtpk[(g - base) / 16 + 1]), (uint32_t) ((g - base) & 15));
+  return gld_u8(&k->bwt[g - base]);
 }
 
 // the 16 rows of a packed group as BWT bytes (specials as 254)
@@ -753,14 +781,15 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 __device__ __forceinline__ uint32_t llv_by_rank(const Win &t, uint32_t r) {
   if (t.staged_all) return t.val16[min((int) r, t.nval - 1)];
   if ((int) r < t.nval) return t.val16 != nullptr ? t.val16[r] : t.val[r];
-  if (t.llv_base + r >= t.numllv) { atomicOr(t.err, SMAX_ERR_LLV); return 255; }
-  return llv_value(&t.llv[t.llv_base + r]);
+  const KArgs k = kargs();
+  if (t.llv_base + r >= k->numllv) { atomicOr(k->err, SMAX_ERR_LLV); return 255; }
+  return llv_value(&k->llv[t.llv_base + r]);
 }
 
 // rank of window offset o among the window's 255 bytes (t.rank staged)
 __device__ __forceinline__ uint32_t rank_at(const Win &t, uint32_t o) {
   const uint32_t chunk = o >> 4, within = o & 15;
-  const uint4 v = *reinterpret_cast<const uint4 *>(&t.L[chunk * 16]);
+  const uint4 v = lds_ld16(&t.L[chunk * 16]);
   const uint64_t lo = (uint64_t) bytes_ff(v.x) | ((uint64_t) bytes_ff(v.y) << 32);
   const uint64_t hi = (uint64_t) bytes_ff(v.z) | ((uint64_t) bytes_ff(v.w) << 32);
   const uint32_t cnt = within < 8 ? __popcll(lo & ((1ull << (8 * within)) - 1))
@@ -947,7 +976,7 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
     *div3 = d2 & (ne1n | sp | spp1) & (ne2 | spm1 | spp1);
     return;
   }
-  const uint4 bv = *reinterpret_cast<const uint4 *>(&t.B[so]);
+  const uint4 bv = lds_ld16(&t.B[so]);
   const uint32_t bp = t.B[so - 1], bn = t.B[so + 16];
   uint32_t r2 = 0, r3 = 0;
 #pragma unroll
@@ -987,8 +1016,8 @@ struct SegRel {
 // Part 1: the relations of rows 0..17 of segment `so` to their predecessors
 // (byte compares), the >= min(minlen,128) filter and the 255 bytes.
 __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t mf, SegRel &r) {
-  const uint8_t *L = t.L;
-  const uint4 v = *reinterpret_cast<const uint4 *>(&L[so]);
+  const LDSP uint8_t *L = t.L;
+  const uint4 v = lds_ld16(&L[so]);
   const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
   uint32_t up[4], eq[4], ge[4], ff[4];
@@ -1196,7 +1225,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   // 255-byte ranks: the left halo's count, then a prefix over the compacted
   // segments in row order (an inactive segment holds no byte >= 128)
   uint32_t fbase = 0;
-  uint16_t *rank = const_cast<uint16_t *>(t.rank);
+  LDSP uint16_t *rank = const_cast<LDSP uint16_t *>(t.rank);
   if (rank != nullptr) fbase = t.halo_ff;   // plan time (llv_win): the halo's 255 bytes
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -1332,8 +1361,8 @@ __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, S
   if ((threadIdx.x & 63) < 2) glds4(reinterpret_cast<const uint32_t *>(info) + (threadIdx.x & 63), iaddr);
 }
 
-__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = W->B; t.P = nullptr; }
-__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = W->P; t.B = nullptr; }
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = to_lds<uint8_t>(W->B); t.P = nullptr; }
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = to_lds<uint64_t>(W->P); t.B = nullptr; }
 
 // A window's BWT region once the tile's exact starts are evaluated: the
 // staged records (SMAX_SSLOT u64) and the starts' results (2 x SMAX_DLIST
@@ -1372,8 +1401,8 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint32_t so = SMAX_LH + lane * 16;
-  const uint4 v0 = *reinterpret_cast<const uint4 *>(&t.L[so]);
-  const uint4 v1 = *reinterpret_cast<const uint4 *>(&t.L[so + 1024]);
+  const uint4 v0 = lds_ld16(&t.L[so]);
+  const uint4 v1 = lds_ld16(&t.L[so + 1024]);
   uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
   if (t.B == nullptr && !(a.dbg & 1u) &&
       __popcll(__ballot(segpre_bits & 1u)) + __popcll(__ballot(segpre_bits & 2u)) > 64) {
@@ -1388,7 +1417,7 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   t.llv_base = wlo;
   // no .llv entry in the window: no 255 byte (in a consistent index; a
   // stray 255 still resolves exactly through the global .llv search)
-  t.rank = wn == 0 ? nullptr : rank;
+  t.rank = wn == 0 ? nullptr : to_lds<uint16_t>(rank);
   t.nval = -1;
   if (wn != 0) {
     const uint32_t cap = SMAX_LLV_CAP - (wlo & 7u);   // staged from the 8-aligned index below wlo
@@ -1488,11 +1517,11 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const uint32_t next = tile + stride;
     WinT *W = &sWin[wave][cur];
     t.g0 = g0;
-    t.L = W->L;
+    t.L = to_lds<uint8_t>(W->L);
     set_bwt_window(t, W);
     t.p2 = BW2;
     t.val = nullptr;
-    t.val16 = W->val16;
+    t.val16 = to_lds<uint16_t>(W->val16);
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
@@ -1820,8 +1849,8 @@ smax_defer_kernel(SmaxScanArgs a) {
     uint64_t tmark = 0;   // diagnostic phase stamp (GT_SMAX_DEBUG 32768|65536 / |131072)
     if ((a.dbg & 65536u)) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
-    t.L = W->L;
-    t.B = W->B;
+    t.L = to_lds<uint8_t>(W->L);
+    t.B = to_lds<uint8_t>(W->B);
     t.P = nullptr;
     t.rank = nullptr;     // 255 values beyond the window: global search
     t.val = nullptr;
@@ -2051,8 +2080,8 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     load_exact_window_wg(a, l0, info, W, &sD.nff, &tmark);
     if (a.dbg & 65536u) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
-    t.L = W->L;
-    t.B = W->B;
+    t.L = to_lds<uint8_t>(W->L);
+    t.B = to_lds<uint8_t>(W->B);
     t.P = nullptr;
     t.rank = nullptr;
     t.val = nullptr;
