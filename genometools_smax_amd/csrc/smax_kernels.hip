@@ -11,9 +11,9 @@
 // BWT[lb..rb] below 254 are pairwise distinct (ISLEFTDIVERSE semantics of
 // src/match/esa-maxpairs.c:24-31: WILDCARD/SEPARATOR/UNDEFBWTCHAR are unique).
 //
-// One pass = four launches on one stream, no host synchronisation
+// One pass = three launches on one stream, no host synchronisation
 // (DESIGN.md §4); gt_smax_plan_run_part splits them into part 0 (scan: K1,
-// K1b; the boundary record is final after it) and part 1 (compaction: K2, K3):
+// K1b; the boundary record is final after it) and part 1 (compaction: K3):
 //   K1  smax_scan_kernel     the streaming kernel; its block 0 also clears
 //                            the pending-plateau slot of this run
 //   K1b smax_defer_wg_kernel one workgroup per deferred tile: the plan-time
@@ -21,8 +21,11 @@
 //                            .llv values than K1 stages), then K1's runtime
 //                            deferrals (exact-queue overflow, tiles with more
 //                            records than a slot holds); one extra workgroup
-//                            computes the boundary head
-//   K2  smax_block_sum_kernel  records per 256 tiles (K3's offsets; a
+//                            computes the boundary head, and its last
+//                            workgroups add up the records per 256 tiles
+//                            (K3's offsets; K2's work without its launch)
+//   K2  smax_block_sum_kernel  the same block sums as a launch of its own
+//                            (diagnostic builds and GT_SMAX_FUSE_BS=0; a
 //                            decoupled look-back inside K3 instead measured
 //                            1.3 -> 1.9 ms at C3: the prefix chain over 5663
 //                            workgroups serialises)
@@ -84,6 +87,7 @@
 // K1b), K1b writes GtSmaxRecord (16 bytes) and flags its tile count
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
+#define SMAX_BSW 4                                    // block sums per K1b block-sum workgroup
 #define SMAX_SLOT_WIDE 0x80000000u
 #define SMAX_LLV_CAP 240                              // .llv values staged in K1's LDS (u16):
                                                       // one 16-byte DMA per lane; windows
@@ -139,6 +143,8 @@ struct SmaxScanArgs {
   uint32_t k1_reset;         // combined placement without K0: K1 clears the pending slot
   uint32_t wide_cap;         // wide slots (SMAX_TILE / 2 records each) at the pool's start
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
+  uint32_t bs_wgs;           // block-sum workgroups at the end of the K1b grid (0: K2 runs);
+                             // K1 then marks its deferred and static tiles' counts
   unsigned long long *stamps; // diagnostic (GT_SMAX_STAMPS, diag build only): per-section
                               // s_memtime cycles of K1 summed over waves, [7] = tiles
 };
@@ -1594,6 +1600,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       a.defer_list[k] = (uint32_t) tile;
       a.defer_info[k] = make_uint2(wlo, wnf);
     }
+    // K1b's tiles: their count words carry the wide bit (K1b writes
+    // count | wide), so the block sums in K1b's launch skip them and K1b adds
+    // their records itself
+    if (lane == 0 && (stat || defer) && a.bs_wgs) a.tile_count[tile] = SMAX_SLOT_WIDE;
     if (!stat && !defer) {
       // the tile's records move from the LDS staging to one lane each; they
       // are stored at the start of the next iteration (see above)
@@ -2050,6 +2060,29 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
   SmaxWindowX *W = &sD.win;
   Win t;
   win_init(t, a);
+  // the last bs_wgs workgroups: K3's block sums (K2's work, without its
+  // launch), SMAX_BSW blocks each, from the counts K1 wrote; tiles K1 left
+  // to K1b hold the wide bit and are added by their K1b workgroup below.
+  // Both add into the run's zeroed buffer (K3 clears the other one).
+  const uint32_t tile_wgs = gridDim.x - a.bs_wgs;
+  if (blockIdx.x >= tile_wgs) {
+    const uint32_t nb = (a.num_tiles + SMAX_CPB - 1) / SMAX_CPB;
+    const uint32_t b0 = (blockIdx.x - tile_wgs) * SMAX_BSW;
+    uint32_t v[SMAX_BSW];
+#pragma unroll
+    for (int u = 0; u < SMAX_BSW; u++) {
+      const uint32_t tt = (b0 + u) * SMAX_CPB + threadIdx.x;
+      v[u] = b0 + u < nb && tt < a.num_tiles ? a.tile_count[tt] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < SMAX_BSW; u++) {
+      uint32_t c = (v[u] & SMAX_SLOT_WIDE) ? 0u : v[u];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+      if (lane == 0 && c != 0 && b0 + u < nb) atomicAdd(&a.block_sum[b0 + u], c);
+    }
+    return;
+  }
   // workgroup 0 computes the boundary head: dispatched first, so its window
   // load overlaps the tiles' (as the last workgroup it waited for a free slot)
   if (a.k1b_head && blockIdx.x == 0) {
@@ -2062,7 +2095,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
   }
   const uint32_t n = *a.defer_count;
   const uint64_t ltm = lanemask_lt();
-  for (uint32_t i = blockIdx.x - a.k1b_head; i < n; i += gridDim.x - a.k1b_head) {
+  for (uint32_t i = blockIdx.x - a.k1b_head; i < n; i += tile_wgs - a.k1b_head) {
     // the list entry and its llv_win words in one round (no dependent load
     // of llv_win[tile] before the window's .llv loads)
     const uint64_t tile = a.defer_list[i];
@@ -2164,6 +2197,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
         a.tile_count[tile] = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
       else if (!(a.dbg & 4096u))
         a.tile_count[tile] = total | SMAX_SLOT_WIDE;   // 16-byte records
+      if (a.bs_wgs && total != 0) atomicAdd(&a.block_sum[tile / SMAX_CPB], total);
     }
     __syncthreads();
     const uint64_t off = sD.off;
@@ -2289,7 +2323,11 @@ __global__ void __launch_bounds__(256)
 smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
                     const uint32_t *block_sum, uint64_t nslots, const GtSmaxRecord *pool,
                     uint64_t pool_cap, const uint64_t *tile_off, GtSmaxRecord *out,
-                    uint64_t capacity, uint64_t *count, uint64_t g00, SmaxNextRun nr) {
+                    uint64_t capacity, uint64_t *count, uint64_t g00, SmaxNextRun nr,
+                    uint32_t *bs_clear) {
+  // block sums added up in K1b's launch: this block's entry of the next
+  // run's buffer starts at zero
+  if (bs_clear != nullptr && threadIdx.x == 0) bs_clear[blockIdx.x] = 0;
   // the next run's resets (combined placement: no K0): K1b, the last reader
   // of the deferral count and pool cursor, has finished
   if (nr.defer_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2550,6 +2588,7 @@ struct GtSmaxPlan {
   bool nt;                   // window stream with the non-temporal policy (smax_scan_kernel*_nt)
   bool k1b_wg;               // mode 4: one workgroup per K1b tile (GT_SMAX_K1B_WG=0: one wave)
   uint32_t comb_grid_wg;     // its grid (+1: head)
+  uint32_t bs_wgs;           // block-sum workgroups appended to it (0: K2 runs; GT_SMAX_FUSE_BS=0)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   hipEvent_t fork, join;
   uint32_t *err;
@@ -2730,8 +2769,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   smax_phase_mark(" slot_alloc", &tpc);
   HIPCHK(dalloc(&p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles));
 
-  HIPCHK(dalloc(&p->block_sum, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
-  HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * ((uint64_t) p->compact_grid + 1)));
+  // two buffers: with the block sums added up in K1b's launch, run r adds
+  // into buffer r % 2 and its K3 clears the other
+  HIPCHK(dalloc(&p->block_sum, sizeof (uint32_t) * (2 * (uint64_t) p->compact_grid + 1)));
+  HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * (2 * (uint64_t) p->compact_grid + 1)));
 
   HIPCHK(dalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
@@ -2869,6 +2910,12 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
         ncu = 256;
       p->comb_grid_wg = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u,
                                            (uint32_t) ncu * 8u) + 1;
+      // K3's block sums in the same launch (no K2): K1b's last workgroups
+      const char *fb = getenv("GT_SMAX_FUSE_BS");
+      // (measured against K2: C3 step -0.3 %, 3/8 shard -1.4 %, C2 -4.2 %,
+      // profiles/r03zb/fuse_bs_*.txt)
+      if ((fb ? strtol(fb, NULL, 0) != 0 : true) && p->k1b_wg && p->dbg == 0)
+        p->bs_wgs = (p->compact_grid + SMAX_BSW - 1) / SMAX_BSW;
       // the first run's state (later runs: reset by the previous run's K3)
       const unsigned long long pc = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
       HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
@@ -2941,7 +2988,8 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.pool_cursor = p->pool_cursor;
   a.tile_off = p->tile_off;
   a.tile_count = p->tile_count;
-  a.block_sum = p->block_sum;
+  a.block_sum = p->block_sum + (p->bs_wgs ? (p->runs & 1) * (uint64_t) p->compact_grid : 0);
+  a.bs_wgs = p->bs_wgs;
   a.bnd = p->bnd;
   a.defer_list = p->defer_list;
   a.defer_info = p->defer_info;
@@ -3086,7 +3134,8 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
       SmaxScanArgs c = a;
       c.k1b_head = 1;
       if (p->k1b_wg)
-        hipLaunchKernelGGL(smax_defer_wg_kernel, dim3(p->comb_grid_wg), dim3(SMAX_THREADS), 0, s, c);
+        hipLaunchKernelGGL(smax_defer_wg_kernel, dim3(p->comb_grid_wg + p->bs_wgs), dim3(SMAX_THREADS),
+                           0, s, c);
       else
         hipLaunchKernelGGL(smax_defer_kernel, dim3(p->comb_grid), dim3(SMAX_THREADS), 0, s, c);
     } else {
@@ -3104,9 +3153,15 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
   size_t errlen = 0;
   {
     const bool nok0 = p->k1b_mode == 4 && !(p->dbg & 16384u);
-    hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
-    HIPCHK(hipGetLastError());
+    uint32_t *bs = p->block_sum, *bs_clear = nullptr;
+    if (p->bs_wgs) {   // block sums added up in K1b's launch
+      bs = p->block_sum + (p->runs & 1) * (uint64_t) p->compact_grid;
+      bs_clear = p->block_sum + ((p->runs + 1) & 1) * (uint64_t) p->compact_grid;
+    } else {
+      hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
+                         p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
+      HIPCHK(hipGetLastError());
+    }
     SmaxNextRun nr = {nullptr, nullptr, nullptr, 0u, 0ull};
     if (nok0) {
       nr.defer_count = p->defer_count;
@@ -3116,10 +3171,10 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
       nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
     }
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                       p->slots, p->tile_count, p->block_sum, (uint64_t) p->num_tiles,
+                       p->slots, p->tile_count, bs, (uint64_t) p->num_tiles,
                        p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
                        p->tile_off, p->out, p->capacity, p->count,
-                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE, nr);
+                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE, nr, bs_clear);
     HIPCHK(hipGetLastError());
   }
   p->runs++;

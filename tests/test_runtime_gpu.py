@@ -177,6 +177,41 @@ def test_window_stream_policy(human10, nt, dense, bw2):
         x.close()
 
 
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_block_sums_in_k1b_launch(human10, fuse):
+    """K3's block sums added up by K1b's last workgroups (GT_SMAX_FUSE_BS=1,
+    no K2; two buffers alternate by run) or by K2: the oracle's records over
+    five consecutive runs (both buffers twice), split runs included, whole
+    table and a middle shard."""
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    old = os.environ.get("GT_SMAX_FUSE_BS")
+    os.environ["GT_SMAX_FUSE_BS"] = fuse
+    try:
+        p = esa.plan(20)
+        q = esa.plan(20, N // 3, 2 * N // 3)
+    finally:
+        if old is None:
+            os.environ.pop("GT_SMAX_FUSE_BS", None)
+        else:
+            os.environ["GT_SMAX_FUSE_BS"] = old
+    r = esa.plan(20, N // 3, 2 * N // 3)
+    r.run()
+    ref = r.fetch_triples()
+    for k in range(5):
+        if k == 2:
+            p.run_part(0)
+            p.run_part(1)
+        else:
+            p.run()
+        q.run()
+        assert np.array_equal(p.fetch_triples(), want), k
+        assert np.array_equal(q.fetch_triples(), ref), k
+    for x in (p, q, r):
+        x.close()
+
+
 def test_run_part_order_enforced(human10):
     """Part 1's K3 resets the state the next part 0 starts from: a second
     part 0 before part 1, or a part 1 with no part 0 pending, is refused
