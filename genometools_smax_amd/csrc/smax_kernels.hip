@@ -2318,16 +2318,20 @@ struct SmaxNextRun {                  // K0's resets done by K3 (null: K0 runs)
 // scanned in LDS, then all 256 threads copy the slots' records to their final
 // positions (slot found by binary search in the LDS prefix), consecutive
 // threads on consecutive output records -> ascending lb overall, coalesced.
-// Also publishes the total.
+// Also publishes the total.  With split > 1, `split` workgroups share one
+// block: each scans the block's counts and copies its share of the records
+// (small shards: a few hundred blocks leave most SIMDs without a wave and
+// the copy latency-bound).
 __global__ void __launch_bounds__(256)
 smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
                     const uint32_t *block_sum, uint64_t nslots, const GtSmaxRecord *pool,
                     uint64_t pool_cap, const uint64_t *tile_off, GtSmaxRecord *out,
                     uint64_t capacity, uint64_t *count, uint64_t g00, SmaxNextRun nr,
-                    uint32_t *bs_clear) {
+                    uint32_t *bs_clear, uint32_t split) {
+  const uint32_t blk = blockIdx.x / split, part = blockIdx.x - blk * split;
   // block sums added up in K1b's launch: this block's entry of the next
   // run's buffer starts at zero
-  if (bs_clear != nullptr && threadIdx.x == 0) bs_clear[blockIdx.x] = 0;
+  if (bs_clear != nullptr && part == 0 && threadIdx.x == 0) bs_clear[blk] = 0;
   // the next run's resets (combined placement: no K0): K1b, the last reader
   // of the deferral count and pool cursor, has finished
   if (nr.defer_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2340,14 +2344,14 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   __shared__ uint8_t sWide[SMAX_CPB];
   __shared__ uint64_t sRed[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t s0 = blockIdx.x * (uint64_t) SMAX_CPB;
+  const uint64_t s0 = blk * (uint64_t) SMAX_CPB;
   // this workgroup's output offset: the record counts of all earlier
   // workgroups (summed per SMAX_CPB tiles by K1 / K1b)
   // (a separate one-workgroup prefix kernel over the block sums instead
   // measured 0.5 % longer at C3 and 2 % longer on an 8-way shard: the extra
   // launch costs more than these loads, profiles/r03j_k2b_ab.txt)
   uint64_t bs = 0;
-  for (uint32_t b = tid; b < blockIdx.x; b += 256) bs += block_sum[b];
+  for (uint32_t b = tid; b < blk; b += 256) bs += block_sum[b];
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
   if (lane == 0) sRed[wave] = bs;
@@ -2369,13 +2373,15 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   __syncthreads();
   const uint32_t total = sPre[SMAX_CPB];
   const uint64_t base = sRed[0] + sRed[1] + sRed[2] + sRed[3];
-  if (tid == 0 && s0 + SMAX_CPB >= nslots) *count = base + total;
+  if (tid == 0 && part == 0 && s0 + SMAX_CPB >= nslots) *count = base + total;
+  const uint32_t rlo = (uint32_t) ((uint64_t) total * part / split);
+  const uint32_t rhi = (uint32_t) ((uint64_t) total * (part + 1) / split);
   // four records per thread per round: their slot searches and loads are
   // independent, so their latencies overlap (one record at a time left the
   // kernel latency-bound: 28 us for the 2.5 M records of an 8-way C3 shard)
   constexpr int U = 4;
   static_assert(SMAX_CPB == 256, "8 halvings find a slot among SMAX_CPB");
-  for (uint32_t r0 = tid; r0 < total; r0 += 256 * U) {
+  for (uint32_t r0 = rlo + tid; r0 < rhi; r0 += 256 * U) {
     uint32_t los[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -2394,12 +2400,12 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
     for (int u = 0; u < U; u++) {
       const uint32_t r = r0 + 256u * u, lo = los[u];
       wide[u] = sWide[lo] != 0;
-      v[u] = (r < total && !wide[u]) ? slots[(s0 + lo) * (uint64_t) SMAX_SSLOT + (r - sPre[lo])] : 0;
+      v[u] = (r < rhi && !wide[u]) ? slots[(s0 + lo) * (uint64_t) SMAX_SSLOT + (r - sPre[lo])] : 0;
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t r = r0 + 256u * u, lo = los[u];
-      if (r >= total || base + r >= capacity) continue;
+      if (r >= rhi || base + r >= capacity) continue;
       const uint64_t tile = s0 + lo;
       if (wide[u]) {
         // K1b tile: its run in the pool (absent if the pool was full, which
@@ -2589,6 +2595,7 @@ struct GtSmaxPlan {
   bool k1b_wg;               // mode 4: one workgroup per K1b tile (GT_SMAX_K1B_WG=0: one wave)
   uint32_t comb_grid_wg;     // its grid (+1: head)
   uint32_t bs_wgs;           // block-sum workgroups appended to it (0: K2 runs; GT_SMAX_FUSE_BS=0)
+  uint32_t k3_split;         // K3 workgroups per block of 256 tiles (GT_SMAX_K3_SPLIT)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   hipEvent_t fork, join;
   uint32_t *err;
@@ -2751,6 +2758,24 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       fprintf(stderr, "gt_smax: K1 %s BWT, %d CUs x %d blocks/CU -> grid %u, %u tiles\n",
               p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
+    {
+      // K3: each block of 256 tiles split over two workgroups (each copies
+      // a share of its block's records), more until there are 8 workgroups
+      // per CU (at most 8 per block).  Measured (profiles/r03zc/):
+      // C3 (5,663 blocks) split 2 -0.8 % against 1 and -1 % against 4; a 3/8
+      // shard (708 blocks) split 4 -3.3 % against 1, -0.6 % against 8; C2
+      // (191 blocks, 3,365 records) +3 % with 8 -- tables of fewer than 256
+      // blocks keep one.  GT_SMAX_K3_SPLIT overrides.
+      const char *ks = getenv("GT_SMAX_K3_SPLIT");
+      uint32_t sp = 1;
+      if (ks) {
+        sp = (uint32_t) strtoul(ks, NULL, 0);
+      } else if (p->compact_grid >= 256) {
+        sp = 2;
+        while (sp < 8 && (uint64_t) p->compact_grid * sp < (uint64_t) dev_cus * 8u) sp *= 2;
+      }
+      p->k3_split = sp < 1 ? 1u : sp > 64 ? 64u : sp;
+    }
     // runtime K1b list (exact-queue overflow: ~1 tile in 10^4): grid-stride
     const uint64_t dg = ((uint64_t) p->num_tiles + 3) / 4;
     p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 2 ? dg : (uint64_t) dev_cus * 2);
@@ -3170,11 +3195,12 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
       nr.defer_base = p->n_static;
       nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
     }
-    hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid), dim3(256), 0, s,
+    hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid * p->k3_split), dim3(256), 0, s,
                        p->slots, p->tile_count, bs, (uint64_t) p->num_tiles,
                        p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
                        p->tile_off, p->out, p->capacity, p->count,
-                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE, nr, bs_clear);
+                       p->shard.base + p->tile_first * (uint64_t) SMAX_TILE, nr, bs_clear,
+                       p->k3_split);
     HIPCHK(hipGetLastError());
   }
   p->runs++;

@@ -212,6 +212,35 @@ def test_block_sums_in_k1b_launch(human10, fuse):
         x.close()
 
 
+@pytest.mark.parametrize("split", ["1", "3", "8"])
+def test_compact_split_blocks(human10, split):
+    """K3 with `split` workgroups per block of 256 tiles, each copying its
+    share of the block's records (GT_SMAX_K3_SPLIT): the oracle's records,
+    whole table and a middle shard, over repeated runs."""
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    old = os.environ.get("GT_SMAX_K3_SPLIT")
+    os.environ["GT_SMAX_K3_SPLIT"] = split
+    try:
+        p = esa.plan(20)
+        q = esa.plan(20, N // 3, 2 * N // 3)
+    finally:
+        if old is None:
+            os.environ.pop("GT_SMAX_K3_SPLIT", None)
+        else:
+            os.environ["GT_SMAX_K3_SPLIT"] = old
+    r = esa.plan(20, N // 3, 2 * N // 3)
+    r.run()
+    for _ in range(3):
+        p.run()
+        q.run()
+        assert np.array_equal(p.fetch_triples(), want)
+        assert np.array_equal(q.fetch_triples(), r.fetch_triples())
+    for x in (p, q, r):
+        x.close()
+
+
 def test_run_part_order_enforced(human10):
     """Part 1's K3 resets the state the next part 0 starts from: a second
     part 0 before part 1, or a part 1 with no part 0 pending, is refused
