@@ -1049,51 +1049,46 @@ __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t
   r.pb = pb;
 }
 
-// UP/EQ of the rows q in FFP (255 bytes after 255 bytes) from the staged u16
-// .llv values: the values of ranks crank-2 .. crank+19 come in with 11 LDS
-// dword reads (realigned to rank crank-2 with one funnel shift each), all 18
-// "value(k) vs value(k-1)" relations are decided with packed u16 max/xor,
+// Per tile, once a classification step meets a 255-after-255 row: the
+// relations of every staged .llv value to its predecessor in rank order, as
+// bit masks (bit r of GT: value(r) > value(r-1), of EQ: equal; r < 256) in
+// the wave's LDS scratch -- four 64-rank ballot rounds.  Each segment then
+// reads its 18 relations with two LDS dwords and a funnel shift per mask.
+__device__ __forceinline__ void ffp_masks(const Win &t, LDSP uint32_t *relm) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int r = 64 * j + lane;
+    bool gt = false, eq = false;
+    if (r >= 1 && r < t.nval) {
+      const uint32_t v = t.val16[r], vp = t.val16[r - 1];
+      gt = v > vp;
+      eq = v == vp;
+    }
+    const uint64_t g = __ballot(gt), e = __ballot(eq);
+    if (lane == 0) {
+      relm[2 * j] = (uint32_t) g;
+      relm[2 * j + 1] = (uint32_t) (g >> 32);
+      relm[8 + 2 * j] = (uint32_t) e;
+      relm[8 + 2 * j + 1] = (uint32_t) (e >> 32);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// UP/EQ of the rows q in FFP (255 bytes after 255 bytes) from the rank
+// relation masks (ffp_masks): bit k of gtm/eqm = rank crank+k vs crank+k-1,
 // and rank index k maps back to row q: k = 255 bytes of the segment before
 // q -- a plain shift when the segment's 255 bytes are one run (dense .llv
 // regions), otherwise one register-only step per row.  Replaces a loop of
 // two dependent LDS reads per row (a quarter of K1 on the 12 Gbp plant
 // genome, whose long repeat families are dense in .llv values).
-typedef unsigned short smax_u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t u16_nonzero(uint32_t x) {   // bit 15 / 31: lane != 0
-  return (((x & 0x7fff7fffu) + 0x7fff7fffu) | x) & 0x80008000u;
-}
-
-__device__ __forceinline__ void ffp_resolve(const Win &t, uint32_t F18, uint32_t FFP, uint32_t crank,
-                                            uint32_t *UP, uint32_t *EQ) {
-  // LDS byte address of rank crank - 2 (kept in the LDS address space: ds_read)
-  const uint32_t a0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) uint16_t *)
-                          t.val16 + 2u * crank - 4u;
-  typedef const __attribute__((address_space(3))) uint32_t lds_u32;
-  lds_u32 *wp = (lds_u32 *) (uintptr_t) (a0 & ~3u);
-  const uint32_t sh = (a0 & 2u) * 8u;
-  uint32_t w[11];
-#pragma unroll
-  for (int i = 0; i < 11; i++) w[i] = wp[i];
-  uint32_t R[10];                                               // R[i]: ranks crank-2+2i, +1
-#pragma unroll
-  for (int i = 0; i < 10; i++) R[i] = __builtin_amdgcn_alignbit(w[i + 1], w[i], sh);
-  uint32_t gtm = 0, eqm = 0;                                    // bit k: rank crank+k vs crank+k-1
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    const uint32_t C = R[i + 1];                                // ranks crank+2i, crank+2i+1
-    const uint32_t P = __builtin_amdgcn_alignbit(R[i + 1], R[i], 16);   // crank+2i-1, crank+2i
-    smax_u16x2 cv, pv;
-    __builtin_memcpy(&cv, &C, 4);
-    __builtin_memcpy(&pv, &P, 4);
-    const smax_u16x2 mv = __builtin_elementwise_max(cv, pv);
-    uint32_t M;
-    __builtin_memcpy(&M, &mv, 4);
-    const uint32_t nzx = u16_nonzero(C ^ P), nzy = u16_nonzero(M ^ C);
-    const uint32_t gt = nzx & ~nzy, eq = ~nzx & 0x80008000u;   // C > P: max is C, C != P
-    gtm |= ((gt >> 15) & 1u) << (2 * i) | (gt >> 31) << (2 * i + 1);
-    eqm |= ((eq >> 15) & 1u) << (2 * i) | (eq >> 31) << (2 * i + 1);
-  }
+__device__ __forceinline__ void ffp_resolve(const LDSP uint32_t *relm, uint32_t F18, uint32_t FFP,
+                                            uint32_t crank, uint32_t *UP, uint32_t *EQ) {
+  const uint32_t wi = crank >> 5, sh = crank & 31u;
+  const uint32_t gtm = __builtin_amdgcn_alignbit(relm[wi + 1], relm[wi], sh);
+  const uint32_t eqm = __builtin_amdgcn_alignbit(relm[8 + wi + 1], relm[8 + wi], sh);
   uint32_t up = 0, eqr = 0;
   const uint32_t low = F18 & (0u - F18);
   if ((F18 & (F18 + low)) == 0) {                               // one run from row q0
@@ -1129,14 +1124,14 @@ __device__ __forceinline__ void ffp_resolve(const Win &t, uint32_t F18, uint32_t
 template <bool FFPV>
 __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r, uint32_t crank,
                                              bool all_exact, uint32_t *Dm, uint32_t *D3m,
-                                             uint32_t *Lm) {
+                                             uint32_t *Lm, const LDSP uint32_t *relm = nullptr) {
   uint32_t UP = r.UP, EQ = r.EQ;
   uint32_t FFP = r.F18 & ((r.F18 << 1) | (r.pb == 255u ? 1u : 0u));    // 255 after 255
   bool unresolved = false;
   if (r.F18 != 0 && t.rank == nullptr) {
     unresolved = true;                      // no ranks (inconsistent index): exact queue
   } else if (FFPV && FFP != 0 && t.staged_all) {
-    ffp_resolve(t, r.F18, FFP, crank, &UP, &EQ);
+    ffp_resolve(relm, r.F18, FFP, crank, &UP, &EQ);
   } else {
     while (FFP) {
       const int q = __builtin_ctz(FFP);
@@ -1232,6 +1227,11 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   // segments in row order (an inactive segment holds no byte >= 128)
   uint32_t fbase = 0;
   LDSP uint16_t *rank = const_cast<LDSP uint16_t *>(t.rank);
+  // dense variant: the rank relation masks in the accepted-mask scratch
+  // (free until the exact evaluation), built at the first step that needs
+  // them (ffp_masks)
+  LDSP uint32_t *relm = (LDSP uint32_t *) accw;
+  bool relm_ready = false;
   if (rank != nullptr) fbase = t.halo_ff;   // plan time (llv_win): the halo's 255 bytes
 #pragma unroll
   for (int k = 0; k < 2; k++) {
@@ -1252,9 +1252,16 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       if (i < nseg) rank[(SMAX_LH + ro) >> 4] = (uint16_t) crank;
       fbase += ftot;
     }
+    if constexpr (FFPV) {
+      const uint32_t ffp = i < nseg ? rel.F18 & ((rel.F18 << 1) | (rel.pb == 255u ? 1u : 0u)) : 0u;
+      if (!relm_ready && rank != nullptr && __ballot(ffp != 0) != 0) {
+        ffp_masks(t, relm);
+        relm_ready = true;
+      }
+    }
     if (i < nseg) {
       // every row is owned: tiles holding rows before `begin` are static K1b
-      classify_fin<FFPV>(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq);
+      classify_fin<FFPV>(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq, relm);
     }
     const uint32_t F = rel.FF;
     uint32_t tot;

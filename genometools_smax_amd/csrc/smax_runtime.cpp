@@ -11,7 +11,7 @@
 //      are packed to their bit planes during the fill (0.5 B/row over PCIe
 //      and in HBM instead of 1 B/row), so no pass over byte BWT is left for
 //      the device;
-//   2. creates and runs each shard's plan (K1 -> K1b -> K2 -> K3, see
+//   2. creates and runs each shard's plan (K1 -> K1b + block sums -> K3, see
 //      smax_kernels.hip) on the device's stream;
 //   3. exchanges the 152-byte boundary records: an RCCL all-gather over the
 //      used devices (ncclAllGather on a communicator the library creates
