@@ -88,6 +88,12 @@
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
 #define SMAX_BSW 4                                    // block sums per K1b block-sum workgroup
+#define SMAX_SBB 64                                   // blocks per superblock sum (K3's two-level prefix)
+// one run's block-sum buffer (block sums added up in K1b's launch): the
+// blocks' sums, then the superblocks' sums
+__host__ __device__ __forceinline__ uint64_t smax_bs_stride(uint64_t nblocks) {
+  return nblocks + (nblocks + SMAX_SBB - 1) / SMAX_SBB;
+}
 #define SMAX_SLOT_WIDE 0x80000000u
 #define SMAX_LLV_CAP 240                              // .llv values staged in K1's LDS (u16):
                                                       // one 16-byte DMA per lane; windows
@@ -2073,20 +2079,32 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
   // Both add into the run's zeroed buffer (K3 clears the other one).
   const uint32_t tile_wgs = gridDim.x - a.bs_wgs;
   if (blockIdx.x >= tile_wgs) {
+    // wave w sums block b0 + w (4 counts per lane), one atomic per block;
+    // the workgroup's 4 blocks share a superblock: one atomic for it
+    // (atomics are issued at about one wave-instruction per 50 ns per CU:
+    // one per wave and block instead of per wave, block and level)
+    static_assert(SMAX_BSW == SMAX_THREADS / 64 && SMAX_SBB % SMAX_BSW == 0, "a block per wave");
     const uint32_t nb = (a.num_tiles + SMAX_CPB - 1) / SMAX_CPB;
-    const uint32_t b0 = (blockIdx.x - tile_wgs) * SMAX_BSW;
-    uint32_t v[SMAX_BSW];
+    const uint32_t b0 = (blockIdx.x - tile_wgs) * SMAX_BSW, b = b0 + (uint32_t) wave;
+    uint32_t v[SMAX_CPB / 64];
 #pragma unroll
-    for (int u = 0; u < SMAX_BSW; u++) {
-      const uint32_t tt = (b0 + u) * SMAX_CPB + threadIdx.x;
-      v[u] = b0 + u < nb && tt < a.num_tiles ? a.tile_count[tt] : 0u;
+    for (int u = 0; u < SMAX_CPB / 64; u++) {
+      const uint32_t tt = b * SMAX_CPB + 64u * u + lane;
+      v[u] = b < nb && tt < a.num_tiles ? a.tile_count[tt] : 0u;
     }
+    uint32_t c = 0;
 #pragma unroll
-    for (int u = 0; u < SMAX_BSW; u++) {
-      uint32_t c = (v[u] & SMAX_SLOT_WIDE) ? 0u : v[u];
+    for (int u = 0; u < SMAX_CPB / 64; u++) c += (v[u] & SMAX_SLOT_WIDE) ? 0u : v[u];
 #pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-      if (lane == 0 && c != 0 && b0 + u < nb) atomicAdd(&a.block_sum[b0 + u], c);
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (lane == 0) {
+      if (c != 0 && b < nb) atomicAdd(&a.block_sum[b], c);
+      sD.cnt[wave] = b < nb ? c : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t sc = sD.cnt[0] + sD.cnt[1] + sD.cnt[2] + sD.cnt[3];
+      if (sc != 0) atomicAdd(&a.block_sum[nb + b0 / SMAX_SBB], sc);   // their superblock
     }
     return;
   }
@@ -2204,7 +2222,11 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
         a.tile_count[tile] = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
       else if (!(a.dbg & 4096u))
         a.tile_count[tile] = total | SMAX_SLOT_WIDE;   // 16-byte records
-      if (a.bs_wgs && total != 0) atomicAdd(&a.block_sum[tile / SMAX_CPB], total);
+      if (a.bs_wgs && total != 0) {
+        const uint32_t nb = (a.num_tiles + SMAX_CPB - 1) / SMAX_CPB;
+        atomicAdd(&a.block_sum[tile / SMAX_CPB], total);
+        atomicAdd(&a.block_sum[nb + tile / SMAX_CPB / SMAX_SBB], total);
+      }
     }
     __syncthreads();
     const uint64_t off = sD.off;
@@ -2336,9 +2358,14 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
                     uint64_t capacity, uint64_t *count, uint64_t g00, SmaxNextRun nr,
                     uint32_t *bs_clear, uint32_t split) {
   const uint32_t blk = blockIdx.x / split, part = blockIdx.x - blk * split;
-  // block sums added up in K1b's launch: this block's entry of the next
-  // run's buffer starts at zero
-  if (bs_clear != nullptr && part == 0 && threadIdx.x == 0) bs_clear[blk] = 0;
+  const uint32_t nblocks = (uint32_t) ((nslots + SMAX_CPB - 1) / SMAX_CPB);
+  // block sums added up in K1b's launch: this block's entries (and its
+  // superblock's, by the superblock's first block) of the next run's buffer
+  // start at zero
+  if (bs_clear != nullptr && part == 0 && threadIdx.x == 0) {
+    bs_clear[blk] = 0;
+    if (blk % SMAX_SBB == 0) bs_clear[nblocks + blk / SMAX_SBB] = 0;
+  }
   // the next run's resets (combined placement: no K0): K1b, the last reader
   // of the deferral count and pool cursor, has finished
   if (nr.defer_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2358,7 +2385,18 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   // measured 0.5 % longer at C3 and 2 % longer on an 8-way shard: the extra
   // launch costs more than these loads, profiles/r03j_k2b_ab.txt)
   uint64_t bs = 0;
-  for (uint32_t b = tid; b < blk; b += 256) bs += block_sum[b];
+  if (bs_clear != nullptr) {
+    // two-level prefix (K1b's launch also sums superblocks of SMAX_SBB
+    // blocks): the earlier superblocks, then the earlier blocks of this
+    // one -- a flat loop over every earlier block costs O(blocks^2) loads
+    // over the launch (22.7 k blocks at C5: up to 89 per thread)
+    const uint32_t sb = blk / SMAX_SBB;
+    for (uint32_t k = tid; k < sb; k += 256) bs += block_sum[nblocks + k];
+    const uint32_t b = sb * SMAX_SBB + tid;
+    if (tid < SMAX_SBB && b < blk) bs += block_sum[b];
+  } else {
+    for (uint32_t b = tid; b < blk; b += 256) bs += block_sum[b];
+  }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
   if (lane == 0) sRed[wave] = bs;
@@ -2803,8 +2841,8 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
 
   // two buffers: with the block sums added up in K1b's launch, run r adds
   // into buffer r % 2 and its K3 clears the other
-  HIPCHK(dalloc(&p->block_sum, sizeof (uint32_t) * (2 * (uint64_t) p->compact_grid + 1)));
-  HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * (2 * (uint64_t) p->compact_grid + 1)));
+  HIPCHK(dalloc(&p->block_sum, sizeof (uint32_t) * (2 * smax_bs_stride(p->compact_grid) + 1)));
+  HIPCHK(hipMemset(p->block_sum, 0, sizeof (uint32_t) * (2 * smax_bs_stride(p->compact_grid) + 1)));
 
   HIPCHK(dalloc(&p->count, sizeof (uint64_t)));
   HIPCHK(hipMemset(p->count, 0, sizeof (uint64_t)));
@@ -3020,7 +3058,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.pool_cursor = p->pool_cursor;
   a.tile_off = p->tile_off;
   a.tile_count = p->tile_count;
-  a.block_sum = p->block_sum + (p->bs_wgs ? (p->runs & 1) * (uint64_t) p->compact_grid : 0);
+  a.block_sum = p->block_sum + (p->bs_wgs ? (p->runs & 1) * smax_bs_stride(p->compact_grid) : 0);
   a.bs_wgs = p->bs_wgs;
   a.bnd = p->bnd;
   a.defer_list = p->defer_list;
@@ -3187,8 +3225,8 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
     const bool nok0 = p->k1b_mode == 4 && !(p->dbg & 16384u);
     uint32_t *bs = p->block_sum, *bs_clear = nullptr;
     if (p->bs_wgs) {   // block sums added up in K1b's launch
-      bs = p->block_sum + (p->runs & 1) * (uint64_t) p->compact_grid;
-      bs_clear = p->block_sum + ((p->runs + 1) & 1) * (uint64_t) p->compact_grid;
+      bs = p->block_sum + (p->runs & 1) * smax_bs_stride(p->compact_grid);
+      bs_clear = p->block_sum + ((p->runs + 1) & 1) * smax_bs_stride(p->compact_grid);
     } else {
       hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
                          p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
