@@ -22,6 +22,12 @@ void smax_dev_free(void *ptr);                          // any device; NULL ok
 // device's pinned ring (the plan's work must be complete).
 hipError_t smax_d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, void *stream);
 
+// Packed BWT groups (GT_SMAX_PK_GROUPS layout) on the device from their code
+// planes (the low 32 bits of each group) and the groups holding a special
+// row, given as (group << 16 | special mask); enqueued on `stream`.
+hipError_t smax_groups_from_planes(uint64_t *groups, const uint32_t *planes, uint64_t ngroups,
+                                   const uint64_t *spec, uint64_t nspec, hipStream_t stream);
+
 // GT_SMAX_TIMING=1: phase times of the host-table entry points on stderr.
 double smax_phase_clock();
 void smax_phase_mark(const char *what, double *t);

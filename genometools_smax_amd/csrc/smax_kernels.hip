@@ -2468,6 +2468,41 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   }
 }
 
+// ------------------------------------------------------------ BWT groups
+
+// Packed BWT groups from their code planes and the special rows (the host
+// runtime stages 4 B per 16 rows over PCIe instead of 8 B):
+// groups[g] = planes[g], then each (group << 16 | mask) word of spec sets
+// its group's special plane (one word per group: no atomics)
+__global__ void __launch_bounds__(256)
+smax_groups_planes_kernel(uint64_t *groups, const uint32_t *planes, uint64_t ng) {
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t g = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; g < ng; g += stride)
+    groups[g] = planes[g];
+}
+__global__ void __launch_bounds__(256)
+smax_groups_spec_kernel(uint64_t *groups, uint64_t ng, const uint64_t *spec, uint64_t nspec) {
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < nspec; i += stride) {
+    const uint64_t w = spec[i], g = w >> 16;
+    if (g < ng) groups[g] |= (w & 0xffffull) << 32;
+  }
+}
+
+hipError_t smax_groups_from_planes(uint64_t *groups, const uint32_t *planes, uint64_t ngroups,
+                                   const uint64_t *spec, uint64_t nspec, hipStream_t stream) {
+  if (ngroups == 0) return hipSuccess;
+  const unsigned grid = (unsigned) std::min<uint64_t>((ngroups + 255) / 256, 65536);
+  hipLaunchKernelGGL(smax_groups_planes_kernel, dim3(grid), dim3(256), 0, stream, groups, planes,
+                     ngroups);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nspec == 0) return e;
+  const unsigned g2 = (unsigned) std::min<uint64_t>((nspec + 255) / 256, 65536);
+  hipLaunchKernelGGL(smax_groups_spec_kernel, dim3(g2), dim3(256), 0, stream, groups, ngroups,
+                     spec, nspec);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ llv index
 
 // K1's 2-plane window stream from the packed BWT: bwt2[g] = the code planes

@@ -38,6 +38,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -164,7 +165,7 @@ unsigned copy_threads(int ndev) {
   if (total == 0) total = 8u * (unsigned) std::max(1, std::min(ndev, 2));   // 16 measured no faster than 8 for one device
   unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   unsigned per = std::max(1u, std::min(total, hw) / (unsigned) std::max(1, ndev));
-  return std::min(per, 8u);
+  return std::min(per, 16u);
 }
 
 // Host -> device through the context's two pinned chunks: fill(off, n, buf)
@@ -199,11 +200,16 @@ hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
 }
 
 // packed groups [g0, g1) of bwt[0 .. len) (layout: GT_SMAX_PK_GROUPS in
-// include/gt_smax_hip.h); false when a symbol in [4, 254) is seen
-bool pack_groups(const uint8_t *bwt, uint64_t len, uint64_t g0, uint64_t g1, uint64_t *out) {
+// include/gt_smax_hip.h) as their code planes (low 32 bits of a group) in
+// out32, or whole groups in out64; the groups holding a special row are
+// appended to *spec as (group << 16 | special mask) when out32 is used.
+// False when a symbol in [4, 254) is seen.
+bool pack_bits(const uint8_t *bwt, uint64_t len, uint64_t g0, uint64_t g1, uint64_t *out64,
+               uint32_t *out32, std::vector<uint64_t> *spec, std::mutex *smu) {
   const __m128i k3 = _mm_set1_epi8(3), k254 = _mm_set1_epi8((char) 254), z = _mm_setzero_si128();
   __m128i bad = z;
   bool badscalar = false;
+  std::vector<uint64_t> mine;
   for (uint64_t gi = g0; gi < g1; gi++) {
     const int64_t r0 = ((int64_t) gi - 1) * 16;
     uint64_t w = 0;
@@ -229,9 +235,22 @@ bool pack_groups(const uint8_t *bwt, uint64_t len, uint64_t g0, uint64_t g1, uin
         }
       }
     }
-    out[gi - g0] = w;
+    if (out64 != nullptr) {
+      out64[gi - g0] = w;
+    } else {
+      out32[gi - g0] = (uint32_t) w;
+      if (w >> 32) mine.push_back(gi << 16 | (w >> 32));
+    }
+  }
+  if (!mine.empty()) {
+    std::lock_guard<std::mutex> g(*smu);
+    spec->insert(spec->end(), mine.begin(), mine.end());
   }
   return !badscalar && _mm_movemask_epi8(bad) == 0;
+}
+
+bool pack_groups(const uint8_t *bwt, uint64_t len, uint64_t g0, uint64_t g1, uint64_t *out) {
+  return pack_bits(bwt, len, g0, g1, out, nullptr, nullptr, nullptr);
 }
 
 // device records -> host (lcp, lb, rb) triples through the pinned ring: the
@@ -450,11 +469,33 @@ void device_phase1(Call *C, int d) {
       const uint64_t blen = S.len;
       bool nondna = env_on("GT_SMAX_BYTE_BWT");
       if (!nondna) {
+        // over PCIe only the two code planes (4 B per 16 rows) and the few
+        // groups holding a special row; the device rebuilds the u64 groups
+        // (half the BWT bytes of staging whole groups)
         DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
-        DCHK(stage_h2d(c, S.bwt, sizeof (uint64_t) * ng, C->nt,
-                       [bsrc, blen](uint64_t off, uint64_t n, char *buf) {
-                         return pack_groups(bsrc, blen, off / 8, (off + n) / 8, (uint64_t *) buf);
-                       }, &nondna));
+        void *planes = nullptr;
+        DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
+        std::vector<uint64_t> spec;
+        std::mutex smu;
+        hipError_t pe = stage_h2d(c, planes, sizeof (uint32_t) * ng, C->nt,
+                                  [bsrc, blen, &spec, &smu](uint64_t off, uint64_t n, char *buf) {
+                                    return pack_bits(bsrc, blen, off / 4, (off + n) / 4, nullptr,
+                                                     (uint32_t *) buf, &spec, &smu);
+                                  }, &nondna);
+        void *dspec = nullptr;
+        if (pe == hipSuccess && !nondna && !spec.empty()) {
+          pe = smax_dev_alloc(&dspec, sizeof (uint64_t) * spec.size());
+          if (pe == hipSuccess)
+            pe = hipMemcpyAsync(dspec, spec.data(), sizeof (uint64_t) * spec.size(),
+                                hipMemcpyHostToDevice, c->stream);
+        }
+        if (pe == hipSuccess && !nondna)
+          pe = smax_groups_from_planes((uint64_t *) S.bwt, (const uint32_t *) planes, ng,
+                                       (const uint64_t *) dspec, spec.size(), c->stream);
+        if (pe == hipSuccess) pe = hipStreamSynchronize(c->stream);
+        smax_dev_free(dspec);
+        smax_dev_free(planes);
+        DCHK(pe);
         S.sh.bwtpk_dev = nondna ? nullptr : (const uint64_t *) S.bwt;
       }
       if (nondna) {
@@ -649,6 +690,16 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
     uint64_t total = 0;
     for (auto &S : C.sh) { S.offset = total; total += S.count; }
     C.trip = (uint64_t *) malloc(sizeof (uint64_t) * 3 * (total + 1));
+    if (C.trip != NULL) {
+      // the converting threads first-touch every page of the fresh buffer:
+      // ask for transparent huge pages over its 2 MiB-aligned interior
+      // (one fault per 2 MiB instead of per 4 KiB; advice only, the buffer
+      // stays an ordinary malloc block for gt_smax_free)
+      const uintptr_t a0 = ((uintptr_t) C.trip + (2u << 20) - 1) & ~(uintptr_t) ((2u << 20) - 1);
+      const uintptr_t a1 = ((uintptr_t) C.trip + sizeof (uint64_t) * 3 * (total + 1)) &
+                           ~(uintptr_t) ((2u << 20) - 1);
+      if (a1 > a0) (void) madvise((void *) a0, a1 - a0, MADV_HUGEPAGE);
+    }
     if (C.trip == NULL) {
       seterr(errbuf, errlen, "out of memory for %lu intervals", (unsigned long) total);
     } else {

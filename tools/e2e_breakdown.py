@@ -18,7 +18,11 @@ esa = G.DeviceEsa(text, device=0, keep_suftab=False)
 host = esa.download()
 n, N = esa.totallength, esa.nonspecials
 esa.release()
+threads = [x for x in os.environ.get("THREADS_LIST", "").split(",") if x]
 for i in range(int(os.environ.get("CALLS", "6"))):
+    if threads:
+        os.environ["GT_SMAX_COPY_THREADS"] = threads[i % len(threads)]
+        print("GT_SMAX_COPY_THREADS=%s" % threads[i % len(threads)], file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     iv = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], n, N, 20, 1)
     print("call %d: %.1f ms, %d intervals" % (i, (time.perf_counter() - t0) * 1e3, len(iv)),
