@@ -162,7 +162,10 @@ void par_for(uint64_t n, unsigned nt, F f) {
 unsigned copy_threads(int ndev) {
   const char *v = getenv("GT_SMAX_COPY_THREADS");
   unsigned total = v ? (unsigned) strtoul(v, NULL, 0) : 0u;
-  if (total == 0) total = 8u * (unsigned) std::max(1, std::min(ndev, 2));   // 16 measured no faster than 8 for one device
+  // 12 per device: h2d of the C3 tables 92-95 ms with 8, 83-88 ms with 12
+  // or 16, 124 ms with 4 (profiles/r03zt/e2e_threads.txt; the box's cgroup
+  // allows 16 CPUs)
+  if (total == 0) total = 12u * (unsigned) std::max(1, std::min(ndev, 2));
   unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   unsigned per = std::max(1u, std::min(total, hw) / (unsigned) std::max(1, ndev));
   return std::min(per, 16u);
