@@ -485,7 +485,8 @@ def main():
             parity_ok = False
         e2e = {"value": N / t_e2e, "unit": "suffix-positions/s", "seconds": round(t_e2e, 4),
                "path": "gt_smax_hip_enumerate_to_buffer: pageable host .lcp/.bwt/.llv -> H2D "
-                       "(.bwt packed to bit planes during the staged fill) -> plan (llv index) -> "
+                       "(.bwt packed to its two code planes + the groups holding a special row during the "
+                       "staged fill, u64 groups rebuilt on the device) -> plan (llv index) -> "
                        "K1..K3 -> D2H of %d (lcp,lb,rb) triples" % len(iv),
                "vs_cpu_baseline": (N / t_e2e) / cpu["value"] if cpu else None}
         if cpu:
