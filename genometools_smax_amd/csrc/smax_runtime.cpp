@@ -44,6 +44,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <future>
 #include <map>
 #include <mutex>
 #include <string>
@@ -356,9 +357,16 @@ int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
            (unsigned long) in->nonspecials, (unsigned long) in->totallength);
     return -1;
   }
+  return 0;
+}
+
+// The .llv scan of the validation (positions ascending, inside the text, on
+// a 255 LCP byte): runs beside the staged upload (no device work starts
+// before it has passed, run_call's phase 1 waits for it before planning).
+int validate_llv(const GtSmaxInput *in, std::string *msg) {
   std::mutex mu;
   uint64_t first = UINT64_MAX;
-  par_for(in->numllv, 8, [&, in](uint64_t lo, uint64_t hi) {
+  par_for(in->numllv, std::max(1u, copy_threads(1) / 3), [&, in](uint64_t lo, uint64_t hi) {
     for (uint64_t i = lo; i < hi; i++) {
       if (in->llvtab[i].position > in->totallength ||
           (i > 0 && in->llvtab[i].position <= in->llvtab[i - 1].position) ||
@@ -370,7 +378,9 @@ int validate_input(const GtSmaxInput *in, char *errbuf, size_t errlen) {
     }
   });
   if (first != UINT64_MAX) {
-    seterr(errbuf, errlen, "inconsistent .llv entry %lu", (unsigned long) first);
+    char b[96];
+    snprintf(b, sizeof b, "inconsistent .llv entry %lu", (unsigned long) first);
+    *msg = b;
     return -1;
   }
   return 0;
@@ -412,6 +422,10 @@ struct Call {
   uint64_t *trip = nullptr;
   unsigned nt = 1;
   double t0 = 0;
+  // the .llv validation running beside the upload (validate_llv); every
+  // device thread waits for it before it creates a plan
+  std::shared_future<int> valid;
+  std::string valid_msg;
 };
 
 // all device threads meet here; returns false if any of them failed
@@ -531,6 +545,10 @@ void device_phase1(Call *C, int d) {
       S.sh.nonspecials = in->nonspecials;
       S.sh.device = dev;
       if (d == 0) smax_phase_mark(s == s0 ? "h2d" : "h2d(next)", &tp);
+      if (C->valid.valid() && C->valid.get() != 0) {   // no kernel over unvalidated tables
+        fail_dev(C, d, C->valid_msg);
+        goto out;
+      }
       if (gt_smax_plan_create(&S.plan, &S.sh, C->minlen, 0, eb, sizeof eb)) {
         fail_dev(C, d, eb);
         goto out;
@@ -640,6 +658,14 @@ void on_devices(Call *C, F f) {
 
 int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **trip_out,
              uint64_t *count_out, char *errbuf, size_t errlen) {
+  Call C;
+  // the .llv scan overlaps the staged upload; its future is waited for by
+  // every device thread before planning, and on every return path here
+  C.valid = std::async(std::launch::async, [in, &C] { return validate_llv(in, &C.valid_msg); }).share();
+  struct Join {
+    std::shared_future<int> &f;
+    ~Join() { if (f.valid()) f.wait(); }
+  } join{C.valid};
   const uint64_t N = in->nonspecials;
   const int avail = gt_smax_device_count();
   *trip_out = NULL;
@@ -649,10 +675,13 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
     return -1;
   }
   if (N < 2) {
+    if (C.valid.get() != 0) {
+      seterr(errbuf, errlen, "%s", C.valid_msg.c_str());
+      return -1;
+    }
     *trip_out = (uint64_t *) malloc(sizeof (uint64_t));
     return *trip_out ? 0 : -1;
   }
-  Call C;
   C.in = in;
   C.minlen = minlen;
   C.nshards = std::max(1, num_gpus);

@@ -126,6 +126,34 @@ def test_errors_are_reported():
         G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 0)
 
 
+@pytest.mark.parametrize("shards", [1, 3])
+def test_inconsistent_llv_is_refused(shards):
+    # the .llv scan runs beside the staged upload; no plan is created over
+    # tables it rejects, and the call reports the first bad entry (an entry
+    # whose position holds no 255 byte, then positions out of order)
+    e = oracle_esa("at1MB")
+    assert len(e.llv) > 2
+    good = e.llv.copy()
+    bad = good.copy()
+    k = len(bad) // 2
+    p = int(bad[k, 0])
+    assert e.lcpbytes[p] == 255
+    q = next(x for x in range(p + 1, int(bad[k + 1, 0])) if e.lcpbytes[x] != 255) \
+        if int(bad[k + 1, 0]) > p + 1 else None
+    if q is None:   # no gap to the next entry: move onto a non-255 byte before it
+        q = next(x for x in range(p - 1, int(bad[k - 1, 0]), -1) if e.lcpbytes[x] != 255)
+    bad[k, 0] = q
+    with pytest.raises(G.SmaxError, match="inconsistent .llv entry"):
+        G.enumerate_smax(e.lcpbytes, bad, e.bwt, e.n, e.nonspecials, 20, shards)
+    bad = good.copy()
+    bad[1, 0], bad[2, 0] = good[2, 0], good[1, 0]
+    with pytest.raises(G.SmaxError, match="inconsistent .llv entry"):
+        G.enumerate_smax(e.lcpbytes, bad, e.bwt, e.n, e.nonspecials, 20, shards)
+    # the same call on the good tables still works (state left clean)
+    assert np.array_equal(G.enumerate_smax(e.lcpbytes, good, e.bwt, e.n, e.nonspecials, 20, shards),
+                          O.linsmax(e.lcpbytes, good, e.bwt, e.nonspecials, 20))
+
+
 def _triplicated_text(rng, nwords):
     # words occurring three times, each copy closed by a separator: every
     # suffix inside a word shares exactly the rest of the word with its two
