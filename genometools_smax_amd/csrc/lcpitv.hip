@@ -38,6 +38,7 @@
 #include <string.h>
 
 #include "gt_lcpitv_hip.h"
+#include "smax_internal.h"
 
 static void li_seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
   if (errbuf == NULL || errlen == 0) return;
@@ -553,9 +554,9 @@ struct LiHostTables {
 };
 
 static void li_host_free(LiHostTables *h) {
-  if (h->lcp) (void) hipFree(h->lcp);
-  if (h->llv) (void) hipFree(h->llv);
-  if (h->suf) (void) hipFree(h->suf);
+  smax_dev_free(h->lcp);
+  smax_dev_free(h->llv);
+  smax_dev_free(h->suf);
   memset(h, 0, sizeof *h);
 }
 
@@ -579,16 +580,19 @@ static int li_host_plan(const GtSmaxInput *in, bool with_suf, LiHostTables *h, G
     return -1;
   }
   N = in->nonspecials;
-  LICHK(hipSetDevice(0));
-  LICHK(hipMalloc(&h->lcp, N + 1));
-  LICHK(hipMemcpy(h->lcp, in->lcptab, N + 1, hipMemcpyHostToDevice));
+  // the caller's current device (the entry points restore it); tables from
+  // the runtime's caching allocator, staged through its pinned ring
+  int dev = 0;
+  LICHK(hipGetDevice(&dev));
+  LICHK(smax_dev_alloc((void **) &h->lcp, N + 1));
+  LICHK(smax_stage_upload(h->lcp, in->lcptab, N + 1));
   if (in->numllv > 0) {
-    LICHK(hipMalloc(&h->llv, sizeof (GtSmaxLlv) * in->numllv));
-    LICHK(hipMemcpy(h->llv, in->llvtab, sizeof (GtSmaxLlv) * in->numllv, hipMemcpyHostToDevice));
+    LICHK(smax_dev_alloc((void **) &h->llv, sizeof (GtSmaxLlv) * in->numllv));
+    LICHK(smax_stage_upload(h->llv, in->llvtab, sizeof (GtSmaxLlv) * in->numllv));
   }
   if (with_suf && N > 0) {
-    LICHK(hipMalloc(&h->suf, (size_t) in->suftab_bytes * N));
-    LICHK(hipMemcpy(h->suf, in->suftab, (size_t) in->suftab_bytes * N, hipMemcpyHostToDevice));
+    LICHK(smax_dev_alloc(&h->suf, (size_t) in->suftab_bytes * N));
+    LICHK(smax_stage_upload(h->suf, in->suftab, (size_t) in->suftab_bytes * N));
   }
   din.lcp_dev = h->lcp;
   din.llv_dev = h->llv;
@@ -596,7 +600,7 @@ static int li_host_plan(const GtSmaxInput *in, bool with_suf, LiHostTables *h, G
   din.suf_dev = h->suf;
   din.suf_bytes = with_suf ? in->suftab_bytes : 8;
   din.nonspecials = N;
-  din.device = 0;
+  din.device = dev;
   if (gt_lcpitv_plan_create(plan, &din, errbuf, errlen) != 0) {
     li_host_free(h);
     return -1;
@@ -611,6 +615,7 @@ extern "C" int gt_lcpitv_hip_enumerate_to_buffer(const GtSmaxInput *in, uint64_t
                                                  uint64_t *count, char *errbuf, size_t errlen) {
   LiHostTables h;
   GtLcpitvPlan *plan = NULL;
+  SmaxDeviceGuard keep;
   *itv = NULL;
   *count = 0;
   if (li_host_plan(in, false, &h, &plan, errbuf, errlen) != 0) return -1;
@@ -619,8 +624,7 @@ extern "C" int gt_lcpitv_hip_enumerate_to_buffer(const GtSmaxInput *in, uint64_t
     *itv = (uint64_t *) malloc(sizeof (uint64_t) * 5 * n);
     if (*itv == NULL) {
       li_seterr(errbuf, errlen, "out of memory");
-    } else if (hipMemcpy(*itv, plan->itv, sizeof (uint64_t) * 5 * n, hipMemcpyDeviceToHost) !=
-               hipSuccess) {
+    } else if (smax_stage_download(*itv, plan->itv, sizeof (uint64_t) * 5 * n) != hipSuccess) {
       li_seterr(errbuf, errlen, "device to host copy failed");
       free(*itv);
       *itv = NULL;
@@ -650,6 +654,7 @@ static int li_replay(const GtSmaxInput *in, bool need_suf, Sink sink, char *errb
   GtLcpitvPlan *plan = NULL;
   uint64_t *ev = NULL, *host = NULL, E;
   int rc = 0;
+  SmaxDeviceGuard keep;
   if (need_suf && (in == NULL || in->suftab == NULL ||
                    (in->suftab_bytes != 4 && in->suftab_bytes != 8))) {
     li_seterr(errbuf, errlen, "leaf edges need suftab (4 or 8 bytes per entry)");

@@ -60,6 +60,7 @@
 #include <string.h>
 
 #include "gt_maxpairs_hip.h"
+#include "smax_internal.h"
 
 static void mp_seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
   if (errbuf == NULL || errlen == 0) return;
@@ -849,6 +850,8 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
   GtMaxpairsPlan *plan = NULL;
   GtMaxpairsDevInput din;
   uint64_t N;
+  int dev = 0;
+  SmaxDeviceGuard keep;
   *pairs = NULL;
   *count = 0;
   if (in == NULL || in->lcptab == NULL || in->bwttab == NULL || in->suftab == NULL) {
@@ -869,16 +872,18 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
     return -1;
   }
   N = in->nonspecials;
-  MPCHK(hipSetDevice(0));
-  MPCHK(hipMalloc(&lcp, N + 1));
-  MPCHK(hipMalloc(&bwt, N + 1));
-  MPCHK(hipMalloc(&suf, (size_t) in->suftab_bytes * (N + 1)));
-  MPCHK(hipMemcpy(lcp, in->lcptab, N + 1, hipMemcpyHostToDevice));
-  MPCHK(hipMemcpy(bwt, in->bwttab, N + 1, hipMemcpyHostToDevice));
-  MPCHK(hipMemcpy(suf, in->suftab, (size_t) in->suftab_bytes * (N + 1), hipMemcpyHostToDevice));
+  // the caller's current device (restored on return); tables from the
+  // runtime's caching allocator, staged through its pinned ring
+  MPCHK(hipGetDevice(&dev));
+  MPCHK(smax_dev_alloc((void **) &lcp, N + 1));
+  MPCHK(smax_dev_alloc((void **) &bwt, N + 1));
+  MPCHK(smax_dev_alloc(&suf, (size_t) in->suftab_bytes * (N + 1)));
+  MPCHK(smax_stage_upload(lcp, in->lcptab, N + 1));
+  MPCHK(smax_stage_upload(bwt, in->bwttab, N + 1));
+  MPCHK(smax_stage_upload(suf, in->suftab, (size_t) in->suftab_bytes * (N + 1)));
   if (in->numllv > 0) {
-    MPCHK(hipMalloc(&llv, sizeof (GtSmaxLlv) * in->numllv));
-    MPCHK(hipMemcpy(llv, in->llvtab, sizeof (GtSmaxLlv) * in->numllv, hipMemcpyHostToDevice));
+    MPCHK(smax_dev_alloc((void **) &llv, sizeof (GtSmaxLlv) * in->numllv));
+    MPCHK(smax_stage_upload(llv, in->llvtab, sizeof (GtSmaxLlv) * in->numllv));
   }
   din.lcp_dev = lcp;
   din.bwt_dev = bwt;
@@ -887,7 +892,7 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
   din.suf_dev = suf;
   din.suf_bytes = in->suftab_bytes;
   din.nonspecials = N;
-  din.device = 0;
+  din.device = dev;
   if (gt_maxpairs_plan_create(&plan, &din, minlen, errbuf, errlen) != 0) goto fail_quiet;
   if (gt_maxpairs_plan_count(plan, NULL) != 0 || gt_maxpairs_plan_total(plan, &total) != 0) {
     mp_seterr(errbuf, errlen, "maxpairs count pass failed");
@@ -899,26 +904,25 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
       mp_seterr(errbuf, errlen, "out of memory (%lu pairs)", (unsigned long) total);
       goto fail_quiet;
     }
-    MPCHK(hipMalloc(&out, sizeof (uint64_t) * 3 * total));
+    MPCHK(smax_dev_alloc((void **) &out, sizeof (uint64_t) * 3 * total));
     if (gt_maxpairs_plan_emit_ordered(plan, out, total, NULL) != 0) {
       mp_seterr(errbuf, errlen, "maxpairs emission pass failed");
       goto fail_quiet;
     }
     if (lines != nullptr) {
-      MPCHK(hipMalloc(&dsep, sizeof (uint64_t) * (nsep ? nsep : 1)));
-      if (nsep) MPCHK(hipMemcpy(dsep, sep, sizeof (uint64_t) * nsep, hipMemcpyHostToDevice));
-      if (gt_repfind_pairs_lines_dev(out, total, dsep, nsep, 0, lines, ldata, errbuf, errlen) != 0)
+      MPCHK(smax_dev_alloc((void **) &dsep, sizeof (uint64_t) * (nsep ? nsep : 1)));
+      if (nsep) MPCHK(smax_stage_upload(dsep, sep, sizeof (uint64_t) * nsep));
+      if (gt_repfind_pairs_lines_dev(out, total, dsep, nsep, dev, lines, ldata, errbuf, errlen) != 0)
         goto fail_quiet;
     } else {
-      MPCHK(hipMemcpy(*pairs, out, sizeof (uint64_t) * 3 * total, hipMemcpyDeviceToHost));
+      MPCHK(smax_stage_download(*pairs, out, sizeof (uint64_t) * 3 * total));
     }
   }
   *count = total;
   gt_maxpairs_plan_delete(plan);
   {
     void *bufs[] = {lcp, bwt, suf, llv, out, dsep};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   return 0;
 fail:
@@ -926,8 +930,7 @@ fail_quiet:
   gt_maxpairs_plan_delete(plan);
   {
     void *bufs[] = {lcp, bwt, suf, llv, out, dsep};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   free(*pairs);
   *pairs = NULL;

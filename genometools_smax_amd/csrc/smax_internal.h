@@ -22,6 +22,22 @@ void smax_dev_free(void *ptr);                          // any device; NULL ok
 // device's pinned ring (the plan's work must be complete).
 hipError_t smax_d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, void *stream);
 
+// Host <-> device copies through the current device's pinned staging ring
+// (threaded fill / copy-out overlapping the DMA; the host side stays
+// pageable), for the F2/F3 host-table entry points.  Synchronous.
+hipError_t smax_stage_upload(void *dst_dev, const void *src_host, uint64_t bytes);
+hipError_t smax_stage_download(void *dst_host, const void *src_dev, uint64_t bytes);
+
+// The calling thread's device on entry, restored when the guard goes out of
+// scope (the host-table entry points work on it and leave it as found).
+struct SmaxDeviceGuard {
+  int dev = -1;
+  SmaxDeviceGuard() { if (hipGetDevice(&dev) != hipSuccess) dev = -1; }
+  ~SmaxDeviceGuard() { if (dev >= 0) (void) hipSetDevice(dev); }
+  SmaxDeviceGuard(const SmaxDeviceGuard &) = delete;
+  SmaxDeviceGuard &operator=(const SmaxDeviceGuard &) = delete;
+};
+
 // Packed BWT groups (GT_SMAX_PK_GROUPS layout) on the device from their code
 // planes (the low 32 bits of each group) and the groups holding a special
 // row, given as (group << 16 | special mask); enqueued on `stream`.

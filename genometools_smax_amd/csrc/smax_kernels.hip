@@ -23,18 +23,14 @@
 //                            records than a slot holds); one extra workgroup
 //                            computes the boundary head, and its last
 //                            workgroups add up the records per 256 tiles
-//                            (K3's offsets; K2's work without its launch)
-//   K2  smax_block_sum_kernel  the same block sums as a launch of its own
-//                            (diagnostic builds and GT_SMAX_FUSE_BS=0; a
-//                            decoupled look-back inside K3 instead measured
-//                            1.3 -> 1.9 ms at C3: the prefix chain over 5663
-//                            workgroups serialises)
+//                            (K3's offsets; a separate block-sum launch was
+//                            measured and retired, and a decoupled look-back
+//                            inside K3 measured 1.3 -> 1.9 ms at C3: the
+//                            prefix chain over 5663 workgroups serialises)
 //   K3  smax_compact_kernel  ordered copy of the tiles' records -> ascending
 //                            lb; resets the deferral count and pool cursor
 //                            for the next run (their last reader, K1b, is done)
-// (smax_head_kernel -- "K0", the per-run resets -- and the older K1b
-// placements, GT_SMAX_K1B_MODE 0-3 with smax_defer_kernel, remain as
-// diagnostics.)
+// (smax_head_kernel -- "K0" -- runs only for an empty shard.)
 //
 // K1: every wave is an independent worker on 2048-row tiles (tile = wave id
 // + k * waves in grid; 8 generations of resident one-wave workgroups), no
@@ -120,7 +116,11 @@ struct SmaxScanArgs {
   const uint8_t *bwt;
   const uint64_t *bwtpk;     // packed BWT, 16 rows per u64 (index local_row/16 + 1), or null
   const uint32_t *bwt2;      // its two code planes alone, 16 rows per u32 (same index), or
-                             // null: K1's window stream when no window holds a special
+                             // null: K1's window stream when no window holds a special;
+                             // element local_row/16 + 1 of a tile start is 16-byte aligned
+  const uint4 *halo;         // 2-plane K1: per tile a 64-byte side record of its window's
+                             // halos (smax_halo_kernel), so the window stream reads no line
+                             // of a neighbouring tile
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
   const uint16_t *llv16;     // their values as u16 (plan time; windows with larger ones defer)
   uint64_t numllv;
@@ -281,8 +281,9 @@ struct Win {
   uint64_t N, end;            // global row bounds (plateau scans)
   const LDSP uint8_t *L;      // LDS window: index o = g - g0 + LH
   const LDSP uint8_t *B;      // BWT bytes of the window (byte kernel), or
-  const LDSP uint64_t *P;     // packed BWT of the window, 16 rows per word
-  bool p2;                    // P holds u32 words (code planes only, no specials)
+  const LDSP uint64_t *P;     // packed BWT of the window, 16 rows per word, or
+  const LDSP uint32_t *P2;    // its code planes alone (2-plane windows: p2)
+  bool p2;
   const LDSP uint16_t *rank;  // per 16-byte chunk: 255 bytes before it
   const LDSP uint32_t *val;   // LDS .llv values in rank order (nval of them), or
   const LDSP uint16_t *val16; // the same as u16 (K1 windows: values < 65536)
@@ -297,7 +298,8 @@ struct Win {
 
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.N = a.N; t.end = a.end;
-  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.p2 = false; t.rank = nullptr; t.val = nullptr;
+  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.P2 = nullptr; t.p2 = false; t.rank = nullptr;
+  t.val = nullptr;
   t.val16 = nullptr; t.nval = -1; t.halo_ff = 0; t.staged_all = false;
   t.g0 = 0; t.llv_base = 0;
 }
@@ -309,7 +311,7 @@ __device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
 // packed BWT group gi of the window as a u64 word (the 2-plane form reads
 // as the u64 form with no special bits)
 __device__ __forceinline__ uint64_t pk_word(const Win &t, uint32_t gi) {
-  return t.p2 ? (uint64_t) reinterpret_cast<const LDSP uint32_t *>(t.P)[gi] : t.P[gi];
+  return t.p2 ? (uint64_t) t.P2[gi] : t.P[gi];
 }
 
 // exact LCP of a row whose byte is 255
@@ -501,15 +503,16 @@ __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, 
   if (static_deferred(a, a.llv_win[t].y)) list[atomicAdd(count, 1u)] = (uint32_t) t;
 }
 
-// K0: per-run resets ahead of K1 (the pending-plateau slot, which any K1 or
-// K1b wave may fill, and K1's deferral count); for an empty shard (begin ==
-// end) also the boundary head, otherwise computed by K1b.
-__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a, int with_head) {
+// K0, an empty shard's whole pass (begin == end: no tile to scan): the
+// per-run resets (pending-plateau slot, pool cursor, deferral count) and the
+// boundary head.  Non-empty shards never launch it: K1 clears the pending
+// slot, the previous run's K3 resets the rest and K1b computes the head.
+__global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   a.bnd->pend_valid = 0;
   *a.pool_cursor = (unsigned long long) a.wide_cap * (SMAX_TILE / 2);   // past the wide slots
-  if (!(a.dbg & 16384u)) *a.defer_count = a.defer_base;   // diagnostic: K1b alone on K1's last list
-  if (with_head) compute_head(a);
+  *a.defer_count = a.defer_base;
+  compute_head(a);
 }
 
 // ------------------------------------------------------------ K1: scan
@@ -575,7 +578,6 @@ __device__ __forceinline__ void issue_lcp_llv(const SmaxScanArgs &a, uint64_t l0
   if (n != 0 && lane < SMAX_LLV_CAP / 8 && (uint32_t) (8 * lane) < n + (lo & 7u))
     glds16(a.llv16 + (lo & ~7u) + 8 * lane, wv);
 }
-template <bool BW2 = false>   // byte windows: no 2-plane form
 __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                              uint32_t lo, uint32_t n) {
   const int lane = threadIdx.x & 63;
@@ -605,28 +607,54 @@ __device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0,
 // small (the 4- and 8-way C3 splits) the step is 2-6 % shorter; on the whole
 // C3 table 6 % longer, on a table the MALL holds (C2) 4 % longer -- so the
 // plan picks it by shard size (GtSmaxPlan::nt).
+// a wave-uniform pointer as scalars (the asm's SGPR operands: uniform values
+// the compiler keeps in VGPRs -- the prologue's tile index -- would not fit
+// them; a no-op for values already in SGPRs)
+template <typename T>
+__device__ __forceinline__ const T *uni_ptr(const T *p) {
+  const uint64_t v = (uint64_t) p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t) v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32));
+  return reinterpret_cast<const T *>(((uint64_t) hi << 32) | lo);
+}
+
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
                                                 uint32_t lo, uint32_t n, const void *ibase,
-                                                uint32_t iaddr, uint32_t v16, uint32_t v4) {
+                                                uint32_t iaddr, uint32_t v16, uint32_t v4,
+                                                const void *hrec = nullptr) {
   const uint32_t wp = wl + (uint32_t) offsetof(SmaxWindowPk, P);
   const uint32_t wv = wl + (uint32_t) offsetof(SmaxWindowPk, val16);
-  const uint8_t *lb = a.lcp + l0 - SMAX_LH;
-  const uint8_t *pb = BW2 ? reinterpret_cast<const uint8_t *>(a.bwt2 + l0 / 16)
-                          : reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16);
-  const uint8_t *vb = reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u));
+  const uint8_t *vb = uni_ptr(reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u)));
   const uint32_t nl8 = n == 0 ? 0u : (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
   const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;   // < 64
   const uint64_t vmask = (1ull << nl) - 1;
   const uint64_t imask = 3ull;
-  const uint8_t *ib = reinterpret_cast<const uint8_t *>(ibase);
+  const uint8_t *ib = uni_ptr(reinterpret_cast<const uint8_t *>(ibase));
   uint32_t keep;
   uint64_t ex;
-  // 2-plane form: groups l0/16 .. l0/16+131 are 132 u32 = 33 lanes x 16 B
-  const uint64_t p2mask = (1ull << 33) - 1;
-  (void) p2mask;
-  if constexpr (BW2 && NT) {
-  asm volatile(
+  if constexpr (BW2) {
+    // 2-plane window from aligned pieces only (no line of a neighbouring
+    // tile): the tile's LCP rows [l0, l0+TILE) -> L[LH ..] (2 x 1 KiB), its
+    // 128 code-plane groups (bwt2 element l0/16 + 1 is 16-byte aligned: the
+    // plan offsets the array) -> P region byte 16 (32 lanes), and the 64-byte
+    // side record hrec (smax_halo_kernel): [0,16) left LCP halo -> L[0 ..];
+    // [16,32) right LCP halo -> L[LH+TILE ..] and [32,48) -> P region bytes
+    // [0,16), whose last word is the left halo group; [48,52) the right halo
+    // group -> P region byte 528.  The window's group gi is then at P region
+    // byte 12 + 4 gi (set_bwt_window).  Then the .llv values and the llv_win
+    // word of the tile after next, as in the u64 form.
+    static_assert(offsetof(SmaxWindowPk, P) == SMAX_LDSB, "P region right after the LCP window");
+    static_assert(SMAX_LDSB + 16 + 4 * 128 + 4 <= SMAX_LDSB + sizeof(((SmaxWindowPk *) 0)->P),
+                  "2-plane groups fit the P region");
+    const uint8_t *lb = uni_ptr(a.lcp + l0);
+    const uint8_t *pb = uni_ptr(reinterpret_cast<const uint8_t *>(a.bwt2 + l0 / 16 + 1));
+    const uint8_t *hb = uni_ptr(reinterpret_cast<const uint8_t *>(hrec));
+    const uint32_t m_l = wl + SMAX_LH, m_p = wp + 16, m_h1 = wl + SMAX_LH + SMAX_TILE - 16;
+    const uint32_t m_h2 = wp + 12 + 4 * 129 - 48;
+    const uint64_t m32 = 0xffffffffull;
+    if constexpr (NT) {
+    asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %4\n\t"
         "s_mov_b64 %1, exec\n\t"
@@ -635,10 +663,18 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %5\n\t"
         "s_mov_b64 exec, %14\n\t"
         "global_load_lds_dwordx4 %2, %9 offset:0 nt\n\t"
-        "s_mov_b64 exec, 3\n\t"
-        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_mov_b32 m0, %16\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %8 offset:2048 nt\n\t"
+        "global_load_lds_dwordx4 %2, %15 offset:0 nt\n\t"
+        "s_mov_b64 exec, 3\n\t"
+        "s_mov_b32 m0, %17\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %15 offset:16 nt\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_mov_b32 m0, %18\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, %15 offset:48 nt\n\t"
         "s_mov_b64 exec, %11\n\t"
         "s_mov_b32 m0, %6\n\t"
         "s_nop 0\n\t"
@@ -650,11 +686,11 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b64 exec, %1\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
-        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+        : "v"(v16), "v"(v4), "s"(m_l), "s"(m_p), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(m32), "s"(hb), "s"(wl), "s"(m_h1), "s"(m_h2)
         : "memory");
-  } else if constexpr (BW2) {
-  asm volatile(
+    } else {
+    asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %4\n\t"
         "s_mov_b64 %1, exec\n\t"
@@ -663,10 +699,18 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %5\n\t"
         "s_mov_b64 exec, %14\n\t"
         "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
-        "s_mov_b64 exec, 3\n\t"
-        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_mov_b32 m0, %16\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %8 offset:2048\n\t"
+        "global_load_lds_dwordx4 %2, %15 offset:0\n\t"
+        "s_mov_b64 exec, 3\n\t"
+        "s_mov_b32 m0, %17\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %15 offset:16\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_mov_b32 m0, %18\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %3, %15 offset:48\n\t"
         "s_mov_b64 exec, %11\n\t"
         "s_mov_b32 m0, %6\n\t"
         "s_nop 0\n\t"
@@ -678,10 +722,16 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b64 exec, %1\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
-        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+        : "v"(v16), "v"(v4), "s"(m_l), "s"(m_p), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(m32), "s"(hb), "s"(wl), "s"(m_h1), "s"(m_h2)
         : "memory");
-  } else if constexpr (NT) {
+    }
+    return;
+  }
+  const uint8_t *lb = uni_ptr(a.lcp + l0 - SMAX_LH);
+  const uint8_t *pb = uni_ptr(reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16));
+  (void) hrec;
+  if constexpr (NT) {
   asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %4\n\t"
@@ -740,22 +790,6 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
           "s"(vmask), "s"(ib), "s"(imask)
         : "memory");
   }
-}
-
-template <bool BW2 = false>
-__device__ __forceinline__ void issue_window(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
-                                             uint32_t lo, uint32_t n) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wp = __builtin_amdgcn_readfirstlane(lds_addr(w->P));
-  issue_lcp_llv(a, l0, w->L, w->val16, lo, n);
-  if (BW2) {   // 2-plane groups l0/16 .. l0/16 + 131 (u32 each): 33 lanes x 16 B
-    if (lane < 33) glds16(a.bwt2 + l0 / 16 + lane * 4, wp);
-    return;
-  }
-  // groups l0/16 .. l0/16 + 129 of the packed array (index = local_row/16 + 1)
-  const uint64_t *ps = a.bwtpk + l0 / 16;
-  glds16(ps + lane * 2, wp);                             // groups 0 .. 127
-  if (lane == 0) glds16(ps + 128, wp + 1024);            // groups 128, 129
 }
 
 __device__ __forceinline__ uint32_t seg_ge(const uint4 v, uint32_t mf) {
@@ -1060,6 +1094,12 @@ __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t
 // bit masks (bit r of GT: value(r) > value(r-1), of EQ: equal; r < 256) in
 // the wave's LDS scratch -- four 64-rank ballot rounds.  Each segment then
 // reads its 18 relations with two LDS dwords and a funnel shift per mask.
+// ffp_resolve funnels words crank >> 5 and the one after it of each set of 8
+// (for crank >= 224 the word after is the next set's first, or the word past
+// the masks); the bits it uses are those of ranks < nval <= SMAX_LLV_CAP, so
+// they all come from the set's own 8 words while SMAX_LLV_CAP <= 256 -- the
+// word after only supplies bits of ranks >= 256, which no row reads
+static_assert(SMAX_LLV_CAP <= 256, "rank relation masks: 8 words per set cover every rank");
 __device__ __forceinline__ void ffp_masks(const Win &t, LDSP uint32_t *relm) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -1369,19 +1409,29 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
-                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
-  issue_window_pk<NT, BW2>(a, l0, wl, lo, n, info, iaddr, v16, v4);
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4,
+                                           const uint4 *hrec) {
+  issue_window_pk<NT, BW2>(a, l0, wl, lo, n, info, iaddr, v16, v4, hrec);
 }
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
-                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4,
+                                           const uint4 *hrec) {
+  (void) hrec;
   issue_window(a, l0, w, lo, n);
   if ((threadIdx.x & 63) < 2) glds4(reinterpret_cast<const uint32_t *>(info) + (threadIdx.x & 63), iaddr);
 }
 
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = to_lds<uint8_t>(W->B); t.P = nullptr; }
-__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = to_lds<uint64_t>(W->P); t.B = nullptr; }
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) {
+  t.P = to_lds<uint64_t>(W->P);
+  // 2-plane windows: group gi of the window at byte 12 + 4 gi of the region
+  // (the tile's 128 groups 16-byte aligned for their LDS-DMA, the halo
+  // groups beside them from the side record: issue_window_pk)
+  t.P2 = reinterpret_cast<const LDSP uint32_t *>(reinterpret_cast<const LDSP uint8_t *>(t.P) + 12);
+  t.B = nullptr;
+}
 
 // A window's BWT region once the tile's exact starts are evaluated: the
 // staged records (SMAX_SSLOT u64) and the starts' results (2 x SMAX_DLIST
@@ -1508,11 +1558,14 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
           info1);
   }
   glds_wait();
-  issue_window<BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0],
-               __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
-               SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])));
-
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
+  // (the llv_win word of the tile after is loaded again into its slot:
+  // the same value)
+  issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase,
+                      __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
+                      SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])),
+                      a.llv_win + (tile + stride <= last ? tile + stride : last), info1, v16, v4,
+                      a.halo + 4 * (uint64_t) tile);
   // the previous tile's records (lane r holds record r) and count: stored
   // one iteration late, right after the window wait, so that those stores
   // (and the block-sum atomic) have a whole tile of work to complete before
@@ -1570,7 +1623,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       const uint32_t n2 = next + stride <= last ? next + stride : last;
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
-                 a.llv_win + n2, cur ? info1 : info0, v16, v4);
+                 a.llv_win + n2, cur ? info1 : info0, v16, v4, a.halo + 4 * (uint64_t) next);
     }
 
     if constexpr (DIAG) SMAX_STAMP(st, 1);
@@ -1843,130 +1896,6 @@ __device__ static bool eval_start_x(const SmaxScanArgs &a, const Win &t, const S
   return true;
 }
 
-__global__ void __launch_bounds__(SMAX_THREADS)
-smax_defer_kernel(SmaxScanArgs a) {
-  __shared__ __attribute__((aligned(16))) SmaxWindowX sWin[SMAX_THREADS / 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  SmaxWindowX *W = &sWin[wave];
-  Win t;
-  win_init(t, a);
-  if (a.k1b_head && blockIdx.x == gridDim.x - 1) {
-    // the last workgroup: the boundary head from the shard's first window
-    if (wave == 0) {
-      const uint64_t l0 = a.tile_first * (uint64_t) SMAX_TILE;
-      load_exact_window(a, l0, W);
-      head_from_window(a, W, a.base + l0);
-    }
-    return;
-  }
-  const uint32_t n = *a.defer_count;
-  const uint64_t ltm = lanemask_lt();
-  for (uint32_t i = blockIdx.x * (SMAX_THREADS / 64) + wave; i < n;
-       i += (gridDim.x - a.k1b_head) * (SMAX_THREADS / 64)) {
-    const uint64_t tile = a.defer_list[i];
-    const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;
-    const uint64_t g0 = a.base + l0;
-    const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
-    load_exact_window(a, l0, W);
-    uint64_t tmark = 0;   // diagnostic phase stamp (GT_SMAX_DEBUG 32768|65536 / |131072)
-    if ((a.dbg & 65536u)) tmark = __builtin_readcyclecounter();
-    t.g0 = g0;
-    t.L = to_lds<uint8_t>(W->L);
-    t.B = to_lds<uint8_t>(W->B);
-    t.P = nullptr;
-    t.rank = nullptr;     // 255 values beyond the window: global search
-    t.val = nullptr;
-    t.val16 = nullptr;
-    t.nval = -1;
-    // ballots: plateau ends (tile rows + right halo) and owned starts
-#pragma unroll 4
-    for (uint32_t s = 0; s < SMAX_XSTEPS; s++) {
-      const uint32_t b = s * 64 + lane, o = b + SMAX_LH;
-      bool ne = true, st = false;
-      if (o + 1 < SMAX_LDSB) {
-        const uint32_t c = W->X[o], nx = W->X[o + 1], pv = W->X[o - 1];
-        const uint64_t g = g0 + b;
-        ne = nx != c;
-        st = b < SMAX_TILE && c > pv && c >= a.minlen && g >= a.begin && g < a.end;
-      }
-      const uint64_t nem = __ballot(ne), stm = __ballot(st);
-      if (lane == 0) {
-        W->ne[s] = nem;
-        if (s < SMAX_TILE / 64) W->st[s] = stm;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if ((a.dbg & 131072u)) tmark = __builtin_readcyclecounter();
-    // the tile's records: list entry i owns wide slot wide_slot0 + i (a
-    // tile has at most SMAX_TILE / 2 records) -- one pass; beyond the wide
-    // slots, two passes over the starts (count, allocate a run from the
-    // pool's overflow part, write; eval_start_x is deterministic)
-    const uint32_t wslot = a.wide_slot0 + i;
-    const bool inwide = wslot < a.wide_cap;
-    GtSmaxRecord *wdst = nullptr;
-    uint32_t wcount = 0;
-    const bool nowrite = (a.dbg & (4096u | 32768u)) != 0;
-    if (inwide && !nowrite) {
-      wdst = a.pool + (uint64_t) wslot * (SMAX_TILE / 2);
-      if (lane == 0) a.tile_off[tile] = (uint64_t) wslot * (SMAX_TILE / 2);
-    }
-    for (int pass = 0; pass < 2; pass++) {
-      if (pass == 1) {
-        if (inwide || wcount == 0 || nowrite) break;
-        uint64_t off = 0;
-        if (lane == 0) {
-          off = atomicAdd(a.pool_cursor, (unsigned long long) wcount);
-          if (off + wcount > a.pool_cap) off = ~0ull;   // pool full: the host re-plans
-          a.tile_off[tile] = off;
-        }
-        off = __shfl(off, 0, 64);
-        if (off == ~0ull) break;
-        wdst = a.pool + off;
-        wcount = 0;
-      }
-      for (uint32_t q0 = 0; q0 < SMAX_TILE; q0 += SMAX_XQ) {
-        // compact this round's starts (row order)
-        uint32_t ns = 0;
-        for (uint32_t s = q0 / 64; s < (q0 + SMAX_XQ) / 64; s++) {
-          const uint64_t m = W->st[s];
-          if ((m >> lane) & 1u) W->list[ns + (uint32_t) __popcll(m & ltm)] = (uint16_t) (s * 64 + lane);
-          ns += (uint32_t) __popcll(m);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
-          bool acc = false;
-          uint32_t cur = 0, b = 0;
-          uint64_t j = 0;
-          if (i0 + lane < ns) {
-            b = W->list[i0 + lane];
-            acc = eval_start_x(a, t, W, g0, b, &cur, &j);
-          }
-          const uint64_t am = __ballot(acc);
-          if (acc && wdst != nullptr) {
-            GtSmaxRecord rec;
-            rec.lb = g0 + b - 1;
-            rec.lcp = cur;
-            rec.width = (uint32_t) (j - (g0 + b) + 2);
-            wdst[wcount + (uint32_t) __popcll(am & ltm)] = rec;
-          }
-          wcount += (uint32_t) __popcll(am);
-        }
-        __builtin_amdgcn_wave_barrier();   // list reused
-      }
-    }
-    if (a.dbg & 32768u)   // diagnostic: per-tile cycles (/16), no counts
-      wcount = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
-    if (lane == 0 && !(a.dbg & 4096u)) {
-      a.tile_count[tile] = wcount | ((a.dbg & 32768u) ? 0u : SMAX_SLOT_WIDE);   // 16-byte records
-    }
-    __builtin_amdgcn_wave_barrier();   // window reused by the next tile
-  }
-}
-
-
 // load_exact_window for a whole workgroup (256 threads): one 16-row chunk
 // per thread and every .llv entry of the window (<= SMAX_LDSB) fetched in
 // one round of at most 9 per thread, instead of one wave doing 3 chunks per
@@ -2049,7 +1978,7 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
 // waves share the ballot steps, and each takes one 512-row round of starts:
 // evaluated once into LDS (value, width,
 // accepted), the rounds' record counts are scanned across the waves and
-// the records written in row order.  Same results as smax_defer_kernel.
+// the records written in row order.
 struct SmaxDeferWG {
   SmaxWindowX win;
   uint16_t list[4][SMAX_XQ];        // per wave: its round's starts (row order)
@@ -2245,29 +2174,26 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
   }
 }
 
-// K1 instantiations.  Packed DNA BWT (0.5 B/row of BWT traffic) at 4
-// waves/SIMD is the production kernel; the _diag build keeps the
-// GT_SMAX_DEBUG ablation switches (used only when the variable is set).
-// Byte BWT (any alphabet): 3-4 waves/SIMD.
+// K1 instantiations, selected by the plan (plan_run_scan):
+//   smax_scan_kernel_b2[_dense][_nt]  2-plane BWT window stream (0.25 B/row of
+//       BWT; windows with a special BWT row go to the static K1b list), the
+//       production kernels; _dense: the 255-after-255 relations of a segment
+//       resolved vectorised (ffp_resolve), chosen above SMAX_FFPV_DENSITY .llv
+//       entries per row (C5, the 12 Gbp plant genome at 0.94 %: step 6.21 ->
+//       5.72 ms; C3 at 0.39 %: 1.7 % slower with it); _nt: non-temporal
+//       window loads (GtSmaxPlan::nt: 8- and 4-way shards of C3)
+//   smax_scan_kernel[_dense]  the u64 packed groups (0.5 B/row of BWT,
+//       specials included): shards where special BWT rows would send more
+//       than 1/256 of the windows to K1b (read sets)
+//   smax_scan_kernel_diag     the 2-plane kernel with the GT_SMAX_DEBUG
+//       ablation switches and GT_SMAX_STAMPS section stamps (diagnostics only)
+//   smax_scan_kernel_bytes    byte BWT windows (any alphabet), 4 waves/SIMD
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false>(a);
 }
-// dense .llv shards (plan picks it above SMAX_FFPV_DENSITY entries per row):
-// the 255-after-255 relations of a segment are resolved vectorised
-// (ffp_resolve); measured C5 (12 Gbp plant, 0.94 % of rows) step 6.21 ->
-// 5.72 ms, C3 (human, 0.39 %) 1.253 -> 1.272 ms, hence the switch
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true>(a);
 }
-// non-temporal window stream (GtSmaxPlan::nt)
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_nt(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, false, false, true>(a);
-}
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense_nt(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, false, true, true>(a);
-}
-// 2-plane BWT window stream (GtSmaxPlan::bw2: 0.25 B/row of BWT instead of
-// 0.5; windows holding a special BWT symbol go to the static K1b list)
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, false, false, true>(a);
 }
@@ -2281,7 +2207,7 @@ __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_dense_
   smax_scan_body<SmaxWindowPk, false, true, true, true>(a);
 }
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_diag(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, true>(a);
+  smax_scan_body<SmaxWindowPk, true, false, false, true>(a);
 }
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
   smax_scan_body<SmaxWindow, false>(a);
@@ -2315,28 +2241,9 @@ smax_pack_bwt_kernel(const uint8_t *bwt, uint64_t local_len, uint64_t ngroups, u
   if (other) atomicOr(flag, 1u);
 }
 
-// ------------------------------------------------------------ K2: block sums
-
-// The records of each SMAX_CPB consecutive tiles (one K3 workgroup's share),
-// from the per-tile counts K1 and K1b wrote.  A separate pass instead of
-// per-tile atomics in K1: the 256 tiles of one block are scanned at the same
-// time by 256 different waves, whose atomics to one address serialised and
-// held up each wave's next window wait.
-__global__ void __launch_bounds__(256)
-smax_block_sum_kernel(const uint32_t *tile_count, uint64_t ntiles, uint32_t *block_sum) {
-  __shared__ uint32_t sW[4];
-  const uint64_t t = blockIdx.x * (uint64_t) SMAX_CPB + threadIdx.x;
-  uint32_t c = t < ntiles ? (tile_count[t] & ~SMAX_SLOT_WIDE) : 0u;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-  if ((threadIdx.x & 63) == 0) sW[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) block_sum[blockIdx.x] = sW[0] + sW[1] + sW[2] + sW[3];
-}
-
 // ------------------------------------------------------------ K3: compact
 
-struct SmaxNextRun {                  // K0's resets done by K3 (null: K0 runs)
+struct SmaxNextRun {                  // the next run's resets, done by K3
   uint32_t *defer_count, *defer_last;
   unsigned long long *pool_cursor;
   uint32_t defer_base;
@@ -2362,13 +2269,13 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   // block sums added up in K1b's launch: this block's entries (and its
   // superblock's, by the superblock's first block) of the next run's buffer
   // start at zero
-  if (bs_clear != nullptr && part == 0 && threadIdx.x == 0) {
+  if (part == 0 && threadIdx.x == 0) {
     bs_clear[blk] = 0;
     if (blk % SMAX_SBB == 0) bs_clear[nblocks + blk / SMAX_SBB] = 0;
   }
-  // the next run's resets (combined placement: no K0): K1b, the last reader
-  // of the deferral count and pool cursor, has finished
-  if (nr.defer_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+  // the next run's resets: K1b, the last reader of the deferral count and
+  // pool cursor, has finished
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     *nr.defer_last = *nr.defer_count;
     *nr.defer_count = nr.defer_base;
     *nr.pool_cursor = nr.pool_start;
@@ -2385,7 +2292,7 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   // measured 0.5 % longer at C3 and 2 % longer on an 8-way shard: the extra
   // launch costs more than these loads, profiles/r03j_k2b_ab.txt)
   uint64_t bs = 0;
-  if (bs_clear != nullptr) {
+  {
     // two-level prefix (K1b's launch also sums superblocks of SMAX_SBB
     // blocks): the earlier superblocks, then the earlier blocks of this
     // one -- a flat loop over every earlier block costs O(blocks^2) loads
@@ -2394,8 +2301,6 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
     for (uint32_t k = tid; k < sb; k += 256) bs += block_sum[nblocks + k];
     const uint32_t b = sb * SMAX_SBB + tid;
     if (tid < SMAX_SBB && b < blk) bs += block_sum[b];
-  } else {
-    for (uint32_t b = tid; b < blk; b += 256) bs += block_sum[b];
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
@@ -2505,6 +2410,19 @@ hipError_t smax_groups_from_planes(uint64_t *groups, const uint32_t *planes, uin
 
 // ------------------------------------------------------------ llv index
 
+// Packed groups [g_lo, g_hi) holding a special BWT row (the plan's choice of
+// K1's window stream): one atomic per wave
+__global__ void __launch_bounds__(256)
+smax_special_groups_kernel(const uint64_t *pk, uint64_t g_lo, uint64_t g_hi, uint32_t *count) {
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  uint32_t c = 0;
+  for (uint64_t g = g_lo + blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; g < g_hi; g += stride)
+    c += ((pk[g] >> 32) & 0xffffull) != 0 ? 1u : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0 && c != 0) atomicAdd(count, c);
+}
+
 // K1's 2-plane window stream from the packed BWT: bwt2[g] = the code planes
 // of group g; a group with a special row flags every K1 window that reads it
 // (tile i's window: groups L/16 .. L/16 + 129, L = (tile_first + i) * TILE)
@@ -2525,6 +2443,23 @@ smax_bwt2_kernel(const uint64_t *pk, uint64_t ngroups, uint32_t *bwt2, uint2 *ll
           atomicOr(&llv_win[t - tile_first].y, SMAX_WIN_STATIC);
     }
   }
+}
+
+// Per tile of a 2-plane plan its window's halos as one 64-byte record (the
+// layout issue_window_pk's LDS-DMA expects): LCP rows [l0-16, l0) and
+// [l0+TILE, l0+TILE+16), the code-plane groups of those rows in bytes 44
+// and 48; the rest zero
+__global__ void __launch_bounds__(256)
+smax_halo_kernel(const uint8_t *lcp, const uint32_t *bwt2, uint64_t tile_first, uint32_t num_tiles,
+                 uint4 *halo) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= num_tiles) return;
+  const uint64_t l0 = (tile_first + t) * (uint64_t) SMAX_TILE;
+  uint4 *h = halo + 4 * (uint64_t) t;
+  h[0] = *reinterpret_cast<const uint4 *>(lcp + l0 - SMAX_LH);
+  h[1] = *reinterpret_cast<const uint4 *>(lcp + l0 + SMAX_TILE);
+  h[2] = make_uint4(0u, 0u, 0u, bwt2[l0 / 16]);                    // group of rows l0-16 ..
+  h[3] = make_uint4(bwt2[l0 / 16 + SMAX_TILE / 16 + 1], 0u, 0u, 0u);   // rows l0+TILE ..
 }
 
 // u16 copies of the .llv values (larger values are flagged per tile by the
@@ -2643,7 +2578,7 @@ struct GtSmaxPlan {
   uint64_t capacity;
   uint32_t num_tiles;
   uint64_t tile_first;
-  uint32_t grid, compact_grid, defer_grid;
+  uint32_t grid, compact_grid;
   GtSmaxRecord *out;         // capacity records, ascending lb
   uint64_t *slots;           // num_tiles * SMAX_SSLOT packed records (K1)
   GtSmaxRecord *pool;        // wide_cap wide slots + capacity records (K1b tiles' runs)
@@ -2651,33 +2586,31 @@ struct GtSmaxPlan {
   unsigned long long *pool_cursor;
   uint64_t *tile_off;        // num_tiles
   uint32_t *tile_count;      // num_tiles
-  uint32_t *block_sum;       // compact_grid record sums (K2, K3's output offsets)
+  uint32_t *block_sum;       // two buffers of block + superblock record sums (K3's offsets)
   uint64_t *count;
   GtSmaxBoundary *bnd;
   uint2 *llv_win;
   uint64_t *bwtpk;           // packed BWT (DNA shards), else null
   bool pk, pk_owned;          // packed windows; bwtpk allocated by the plan
-  uint32_t *bwt2;            // its code planes alone (K1's 2-plane window stream), or null
+  uint32_t *bwt2;            // its code planes alone (K1's 2-plane window stream), or null:
+                             // bwt2_alloc + 3, so element l0/16 + 1 of a tile is 16-byte aligned
+  uint32_t *bwt2_alloc;
+  uint4 *halo;               // 2-plane K1: 64-byte side record per tile (smax_halo_kernel)
   bool bw2;                  // K1 streams bwt2 (windows with a special BWT row: static K1b)
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
   uint2 *defer_info;         // beside each entry: the tile's llv_win words
   uint32_t *defer_count;
-  uint32_t *defer_last;      // combined placement: K1's last count (K3 resets the live one)
+  uint32_t *defer_last;      // K1's last count (K3 resets the live one for the next run)
   uint32_t *static_list;     // plan-time K1b list (edges, wide .llv windows) + count
   uint32_t *static_count;
-  uint32_t n_static, static_grid;
-  hipStream_t side;          // K1b over the static list runs here, concurrent with K1
-  int k1b_mode;              // placement of the static K1b (GT_SMAX_K1B_MODE)
-  uint32_t comb_grid;        // mode 4: grid of the combined K1b launch (+1: head)
-  bool dense;                // .llv entries per row above SMAX_FFPV_DENSITY: smax_scan_kernel_dense
-  bool nt;                   // window stream with the non-temporal policy (smax_scan_kernel*_nt)
-  bool k1b_wg;               // mode 4: one workgroup per K1b tile (GT_SMAX_K1B_WG=0: one wave)
-  uint32_t comb_grid_wg;     // its grid (+1: head)
-  uint32_t bs_wgs;           // block-sum workgroups appended to it (0: K2 runs; GT_SMAX_FUSE_BS=0)
+  uint32_t n_static;
+  bool dense;                // .llv entries per row above SMAX_FFPV_DENSITY: smax_scan_kernel*_dense
+  bool nt;                   // window stream with the non-temporal policy (smax_scan_kernel_b2*_nt)
+  uint32_t k1b_grid;         // K1b's tile workgroups (+1: the boundary head)
+  uint32_t bs_wgs;           // block-sum workgroups appended to K1b's grid
   uint32_t k3_split;         // K3 workgroups per block of 256 tiles (GT_SMAX_K3_SPLIT)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
-  hipEvent_t fork, join;
   uint32_t *err;
   uint32_t dbg;
   // optional K1 timing: event pairs recorded around the scan kernel
@@ -2685,7 +2618,10 @@ struct GtSmaxPlan {
   unsigned long long *stamps;    // GT_SMAX_STAMPS: K1 section cycles (diag build)
   int nslots;
   int tstride;               // K1 events on every tstride-th run (gt_smax_plan_timing_stride)
-  uint64_t runs;
+  uint64_t runs;             // runs since the timing was (re)configured (event slots)
+  uint32_t bs_buf;           // block-sum buffer (0/1) of the next run: flipped only by
+                             // plan_run_compact (its K3 clears the other buffer), never by
+                             // the timing calls, so a pass always adds into a cleared one
 };
 
 static SmaxScanArgs plan_args(GtSmaxPlan *p);
@@ -2816,7 +2752,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     }
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, !p->pk ? smax_scan_kernel_bytes : p->dbg ? smax_scan_kernel_diag
-                                                          : smax_scan_kernel,
+                                                          : smax_scan_kernel_b2,
         SMAX_K1_THREADS, 0));
     if (per_cu < 1) per_cu = 1;
     // 8 generations of resident workgroups: the dispatcher hands a finished
@@ -2856,10 +2792,6 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       }
       p->k3_split = sp < 1 ? 1u : sp > 64 ? 64u : sp;
     }
-    // runtime K1b list (exact-queue overflow: ~1 tile in 10^4): grid-stride
-    const uint64_t dg = ((uint64_t) p->num_tiles + 3) / 4;
-    p->defer_grid = (uint32_t) (dg < (uint64_t) dev_cus * 2 ? dg : (uint64_t) dev_cus * 2);
-    p->static_grid = (uint32_t) dev_cus * 8;   // capped below by the list length
   }
   smax_phase_mark(" occupancy", &tpc);
   HIPCHK(dalloc(&p->out, sizeof (GtSmaxRecord) * capacity));
@@ -2927,21 +2859,49 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   smax_phase_mark(" llv_index", &tpc);
   // K1's 2-plane window stream: the packed BWT without its special plane
   // (0.25 B per row instead of 0.5); a window that holds a special BWT row
-  // goes to the static K1b list, which reads the full packed form
-  // (GT_SMAX_BW2=0: K1 streams the u64 groups)
-  {
+  // goes to the static K1b list, which reads the full packed form.  The plan
+  // picks it unless that list would grow by more than 1/256 of the tiles
+  // (read sets: a separator every few hundred rows puts a special BWT row in
+  // most windows, and a K1b tile costs ~14 K1 tiles; K1 then streams the u64
+  // groups, specials and all).  GT_SMAX_BW2=0/1 overrides; the diagnostic
+  // kernel is a 2-plane one.
+  if (p->pk) {
     const char *b2 = getenv("GT_SMAX_BW2");
-    p->bw2 = p->pk && !(b2 && strtol(b2, NULL, 0) == 0) && p->num_tiles > 0;
+    const uint64_t g_lo = p->tile_first * (SMAX_TILE / 16);     // groups the windows read
+    const uint64_t g_hi = g_lo + (uint64_t) p->num_tiles * (SMAX_TILE / 16) + 2;
+    uint32_t *cnt = NULL, nsp = 0;
+    HIPCHK(dalloc(&cnt, sizeof (uint32_t)));
+    HIPCHK(hipMemset(cnt, 0, sizeof (uint32_t)));
+    hipLaunchKernelGGL(smax_special_groups_kernel,
+                       dim3((unsigned) std::min<uint64_t>((g_hi - g_lo + 255) / 256, 1u << 16)), dim3(256), 0, 0,
+                       p->bwtpk, g_lo, std::min<uint64_t>(g_hi, GT_SMAX_PK_GROUPS(shard->local_len)), cnt);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(&nsp, cnt, sizeof nsp, hipMemcpyDeviceToHost));
+    smax_dev_free(cnt);
+    // a special group flags at most two windows
+    p->bw2 = b2 ? strtol(b2, NULL, 0) != 0
+                 : p->dbg != 0 || 2ull * nsp <= std::max<uint32_t>(p->num_tiles / 256u, 64u);
     if (p->bw2) {
       const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
-      HIPCHK(dalloc(&p->bwt2, sizeof (uint32_t) * ngroups));
+      HIPCHK(dalloc(&p->bwt2_alloc, sizeof (uint32_t) * (ngroups + 4)));
+      p->bwt2 = p->bwt2_alloc + 3;
       hipLaunchKernelGGL(smax_bwt2_kernel, dim3((unsigned) std::min<uint64_t>((ngroups + 255) / 256, 1u << 20)),
                          dim3(256), 0, 0, p->bwtpk, ngroups, p->bwt2, p->llv_win, p->tile_first,
                          (uint64_t) p->num_tiles);
       HIPCHK(hipGetLastError());
+      // the windows' halos as side records: K1's window stream then reads
+      // only its own tile's lines (the halos had cost 384 B of neighbouring
+      // lines per 2048-row tile, 0.56 GB per C3 pass)
+      HIPCHK(dalloc(&p->halo, 64 * (uint64_t) p->num_tiles));
+      hipLaunchKernelGGL(smax_halo_kernel, dim3((p->num_tiles + 255) / 256), dim3(256), 0, 0,
+                         shard->lcp_dev, p->bwt2, p->tile_first, p->num_tiles, p->halo);
+      HIPCHK(hipGetLastError());
     }
   }
-  // static K1b list (needs llv_win)
+  // static K1b list (needs llv_win), copied to the front of K1b's list: one
+  // K1b launch after K1 runs the static tiles, then K1's deferrals (a second
+  // stream beside K1 cost a fork/join event pair per step, ~25 us,
+  // DESIGN.md §4)
   HIPCHK(dalloc(&p->static_list, sizeof (uint32_t) * ((uint64_t) p->num_tiles + 1)));
   HIPCHK(dalloc(&p->static_count, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->static_count, 0, sizeof (uint32_t)));
@@ -2955,85 +2915,59 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     p->wide_cap = p->n_static + std::max<uint32_t>(256u, p->num_tiles / 256u);
     HIPCHK(dalloc(&p->pool, sizeof (GtSmaxRecord) *
                                 ((uint64_t) p->wide_cap * (SMAX_TILE / 2) + capacity)));
-    const uint32_t need = (p->n_static + 3) / 4;
-    // + 1: the last workgroup computes the boundary head
-    p->static_grid = (need < p->static_grid ? need : p->static_grid) + 1;
+    if (p->n_static) {
+      HIPCHK(hipMemcpy(p->defer_list, p->static_list, sizeof (uint32_t) * p->n_static,
+                       hipMemcpyDeviceToDevice));
+      hipLaunchKernelGGL(smax_defer_info_kernel, dim3((p->n_static + 255) / 256), dim3(256), 0, 0,
+                         p->defer_list, p->n_static, p->llv_win, p->defer_info);
+      HIPCHK(hipGetLastError());
+    }
   }
   smax_phase_mark(" static_k1b", &tpc);
   {
-    // placement of the static K1b list (GT_SMAX_K1B_MODE, measured in
-    // DESIGN.md §5): 0 side stream beside K1, 1 before K1 on the caller's
-    // stream, 2 after K1, 3 side stream of the highest priority, launched
-    // ahead of K1
-    {
-      // density over the plan's own tiles (a shard plan over full tables
-      // sees every .llv entry): first entry of the first window to the end
-      // of the last one
-      const char *dv = getenv("GT_SMAX_DENSE");   // diagnostic override: 0 / 1
-      uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
-      if (p->num_tiles > 0) {
-        HIPCHK(hipMemcpy(&w0, p->llv_win, sizeof w0, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&w1, p->llv_win + (p->num_tiles - 1), sizeof w1, hipMemcpyDeviceToHost));
-      }
-      const uint64_t inrange = (uint64_t) w1.x + SMAX_WIN_N(w1.y) - w0.x;
-      const uint64_t rows = (uint64_t) p->num_tiles * SMAX_TILE;
-      p->dense = dv ? strtol(dv, NULL, 0) != 0
-                    : rows > 0 && (double) inrange > SMAX_FFPV_DENSITY * (double) rows;
+    // density over the plan's own tiles (a shard plan over full tables
+    // sees every .llv entry): first entry of the first window to the end
+    // of the last one
+    const char *dv = getenv("GT_SMAX_DENSE");   // diagnostic override: 0 / 1
+    uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
+    if (p->num_tiles > 0) {
+      HIPCHK(hipMemcpy(&w0, p->llv_win, sizeof w0, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(&w1, p->llv_win + (p->num_tiles - 1), sizeof w1, hipMemcpyDeviceToHost));
     }
-    {
-      // non-temporal window stream where it measured faster: the shard's
-      // stream (1.5 B per row) larger than the 256 MB MALL -- a smaller one
-      // is served from it on repeated passes, which nt gives up -- and at
-      // most 2^19 tiles (the 4- and 8-way C3 splits; the whole 3 Gbp table
-      // measured slower).  GT_SMAX_NT=0/1 overrides.
-      const char *ntv = getenv("GT_SMAX_NT");
-      const uint64_t stream_bytes = (uint64_t) p->num_tiles * SMAX_TILE * 3 / 2;
-      p->nt = ntv ? strtol(ntv, NULL, 0) != 0
-                  : stream_bytes > (256ull << 20) && p->num_tiles <= (1u << 19);
-    }
-    const char *m = getenv("GT_SMAX_K1B_MODE");
-    p->k1b_mode = m ? (int) strtol(m, NULL, 0) : 4;
-    if (p->k1b_mode == 4) {
-      // 4: one K1b launch after K1 over the static list followed by K1's
-      // deferrals (no second stream, no fork/join events: those cost
-      // ~25 us per step, measured on a 100 Mbp shard)
-      if (p->n_static) {
-        HIPCHK(hipMemcpy(p->defer_list, p->static_list, sizeof (uint32_t) * p->n_static,
-                         hipMemcpyDeviceToDevice));
-        hipLaunchKernelGGL(smax_defer_info_kernel, dim3((p->n_static + 255) / 256), dim3(256), 0, 0,
-                           p->defer_list, p->n_static, p->llv_win, p->defer_info);
-        HIPCHK(hipGetLastError());
-      }
-      p->comb_grid = std::max(p->defer_grid, p->static_grid - 1) + 1;   // static_grid has its +1
-      const char *wg = getenv("GT_SMAX_K1B_WG");
-      p->k1b_wg = wg ? strtol(wg, NULL, 0) != 0 : true;
-      // a workgroup per tile: the static list plus K1's deferrals (about one
-      // tile in 10^4) fit in one generation on all CUs
-      int ncu = 256;
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, shard->device) !=
-              hipSuccess || ncu < 1)
-        ncu = 256;
-      p->comb_grid_wg = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u,
-                                           (uint32_t) ncu * 8u) + 1;
-      // K3's block sums in the same launch (no K2): K1b's last workgroups
-      const char *fb = getenv("GT_SMAX_FUSE_BS");
-      // (measured against K2: C3 step -0.3 %, 3/8 shard -1.4 %, C2 -4.2 %,
-      // profiles/r03zb/fuse_bs_*.txt)
-      if ((fb ? strtol(fb, NULL, 0) != 0 : true) && p->k1b_wg && p->dbg == 0)
-        p->bs_wgs = (p->compact_grid + SMAX_BSW - 1) / SMAX_BSW;
-      // the first run's state (later runs: reset by the previous run's K3)
-      const unsigned long long pc = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
-      HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(p->pool_cursor, &pc, sizeof pc, hipMemcpyHostToDevice));
-    }
-    int lo = 0, hi = 0;
-    if (p->k1b_mode == 3 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
-      HIPCHK(hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, hi));
-    else
-      HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+    const uint64_t inrange = (uint64_t) w1.x + SMAX_WIN_N(w1.y) - w0.x;
+    const uint64_t rows = (uint64_t) p->num_tiles * SMAX_TILE;
+    p->dense = dv ? strtol(dv, NULL, 0) != 0
+                  : rows > 0 && (double) inrange > SMAX_FFPV_DENSITY * (double) rows;
   }
-  HIPCHK(hipEventCreateWithFlags(&p->fork, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&p->join, hipEventDisableTiming));
+  {
+    // non-temporal window stream where it measured faster: the shard's
+    // stream (1.5 B per row) larger than the 256 MB MALL -- a smaller one
+    // is served from it on repeated passes, which nt gives up -- and at
+    // most 2^19 tiles (the 4- and 8-way C3 splits; the whole 3 Gbp table
+    // measured slower).  2-plane windows only.  GT_SMAX_NT=0/1 overrides.
+    const char *ntv = getenv("GT_SMAX_NT");
+    const uint64_t stream_bytes = (uint64_t) p->num_tiles * SMAX_TILE * 3 / 2;
+    p->nt = p->bw2 && (ntv ? strtol(ntv, NULL, 0) != 0
+                           : stream_bytes > (256ull << 20) && p->num_tiles <= (1u << 19));
+  }
+  {
+    // K1b: a workgroup per tile -- the static list plus K1's deferrals
+    // (about one tile in 10^4) -- in one generation on all CUs where they fit;
+    // the first workgroup computes the boundary head
+    int ncu = 256;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, shard->device) !=
+            hipSuccess || ncu < 1)
+      ncu = 256;
+    p->k1b_grid = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u, (uint32_t) ncu * 8u) + 1;
+    // K3's block sums in the same launch (K2's work without its launch):
+    // K1b's last workgroups (measured against a separate block-sum kernel:
+    // C3 step -0.3 %, 3/8 shard -1.4 %, C2 -4.2 %, profiles/r03zb/fuse_bs_*.txt)
+    p->bs_wgs = (p->compact_grid + SMAX_BSW - 1) / SMAX_BSW;
+    // the first run's state (later runs: reset by the previous run's K3)
+    const unsigned long long pc = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
+    HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(p->pool_cursor, &pc, sizeof pc, hipMemcpyHostToDevice));
+  }
   *planp = p;
   return 0;
 fail:
@@ -3045,15 +2979,9 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2_alloc, p->halo,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
-  if (p->side) {
-    (void) hipStreamSynchronize(p->side);
-    (void) hipStreamDestroy(p->side);
-  }
-  if (p->fork) (void) hipEventDestroy(p->fork);
-  if (p->join) (void) hipEventDestroy(p->join);
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) smax_dev_free(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
@@ -3067,6 +2995,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.bwt = p->shard.bwt_dev;
   a.bwtpk = p->pk ? p->bwtpk : nullptr;
   a.bwt2 = p->bw2 ? p->bwt2 : nullptr;
+  a.halo = p->bw2 ? p->halo : nullptr;
   a.llv16 = p->llv16;
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;
@@ -3084,16 +3013,12 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.pool = p->pool;
   a.pool_cap = (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity;
   a.wide_cap = p->wide_cap;
-  a.wide_slot0 = p->n_static;   // the runtime list (the static list sets 0)
-  a.defer_base = 0;
-  if (p->k1b_mode == 4) {          // combined list: static entries at its front
-    a.wide_slot0 = 0;
-    a.defer_base = p->n_static;
-  }
+  a.wide_slot0 = 0;               // K1b's list: the static entries, then K1's
+  a.defer_base = p->n_static;
   a.pool_cursor = p->pool_cursor;
   a.tile_off = p->tile_off;
   a.tile_count = p->tile_count;
-  a.block_sum = p->block_sum + (p->bs_wgs ? (p->runs & 1) * smax_bs_stride(p->compact_grid) : 0);
+  a.block_sum = p->block_sum + p->bs_buf * smax_bs_stride(p->compact_grid);
   a.bs_wgs = p->bs_wgs;
   a.bnd = p->bnd;
   a.defer_list = p->defer_list;
@@ -3154,98 +3079,42 @@ extern "C" int gt_smax_plan_run_part(GtSmaxPlan *p, int part, void *stream) {
 static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
   char *errbuf = NULL;
   size_t errlen = 0;
+  SmaxScanArgs a = plan_args(p);
+  if (p->shard.begin >= p->shard.end) {
+    // empty shard: K0 alone (the boundary head, the per-run resets)
+    hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
+    return 0;
+  }
+  // no K0: K1 clears the pending-plateau slot, the previous run's K3 reset
+  // the deferral count and the pool cursor
+  a.k1_reset = 1u;
   {
-    SmaxScanArgs a = plan_args(p);
-    const int empty = p->shard.begin >= p->shard.end;
-    // combined placement: no K0 (its resets: K1 and the previous run's K3)
-    const bool nok0 = p->k1b_mode == 4 && !empty && !(p->dbg & 16384u);
-    if (!nok0) {
-      hipLaunchKernelGGL(smax_head_kernel, dim3(1), dim3(64), 0, s, a, empty);
-      HIPCHK(hipGetLastError());
-    }
-    a.k1_reset = nok0 ? 1u : 0u;
-    if (empty) {
-      HIPCHK(hipMemsetAsync(p->count, 0, sizeof (uint64_t), s));
-      return 0;
-    }
-    // fork point: after K0's resets (K1b over the static list then runs on
-    // the side stream, concurrent with K1; disjoint tiles)
-    SmaxScanArgs b = a;
-    b.defer_list = p->static_list;
-    b.defer_count = p->static_count;
-    b.k1b_head = 1;
-    b.wide_slot0 = 0;
-    const int mode = p->k1b_mode;
-    const bool side = mode == 0 || mode == 3;
-    if (mode == 4) b.defer_base = p->n_static;
-    if (mode == 1) {
-      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, s, b);
-      HIPCHK(hipGetLastError());
-    }
-    if (side) {
-      HIPCHK(hipEventRecord(p->fork, s));
-      HIPCHK(hipStreamWaitEvent(p->side, p->fork, 0));
-    }
-    if (mode == 3) {   // ahead of K1 on the high-priority stream
-      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, p->side, b);
-      HIPCHK(hipGetLastError());
-    }
     const uint64_t ts = p->tstride > 1 ? (uint64_t) p->tstride : 1u;
     const int slot = p->nslots && p->runs % ts == 0 ? (int) ((p->runs / ts) % (uint64_t) p->nslots)
                                                     : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
-    {
-      // diagnostic: extra dynamic LDS lowers residency (occupancy sensitivity)
-      const char *pad = getenv("GT_SMAX_LDS_PAD");
-      const unsigned lp = pad ? (unsigned) strtoul(pad, NULL, 0) : 0u;
-      if ((p->dbg & 16384u) && p->runs > 0)
-        ;   // diagnostic: re-run K1b on the first run's deferred tiles
-      else if (p->pk && p->dbg)
-        hipLaunchKernelGGL(smax_scan_kernel_diag, dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
-      else if (p->bw2 && p->dense)
-        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_dense_nt : smax_scan_kernel_b2_dense,
-                           dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
-      else if (p->bw2)
-        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_nt : smax_scan_kernel_b2, dim3(p->grid),
-                           dim3(SMAX_K1_THREADS), lp, s, a);
-      else if (p->pk && p->dense)
-        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_dense_nt : smax_scan_kernel_dense, dim3(p->grid),
-                           dim3(SMAX_K1_THREADS), lp, s, a);
-      else if (p->pk)
-        hipLaunchKernelGGL(p->nt ? smax_scan_kernel_nt : smax_scan_kernel, dim3(p->grid),
-                           dim3(SMAX_K1_THREADS), lp, s, a);
-      else
-        hipLaunchKernelGGL(smax_scan_kernel_bytes, dim3(p->grid), dim3(SMAX_K1_THREADS), lp, s, a);
-    }
+    const dim3 g(p->grid), b(SMAX_K1_THREADS);
+    if (!p->pk)
+      hipLaunchKernelGGL(smax_scan_kernel_bytes, g, b, 0, s, a);
+    else if (p->dbg)
+      hipLaunchKernelGGL(smax_scan_kernel_diag, g, b, 0, s, a);
+    else if (p->bw2 && p->dense)
+      hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_dense_nt : smax_scan_kernel_b2_dense, g, b, 0, s, a);
+    else if (p->bw2)
+      hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_nt : smax_scan_kernel_b2, g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL(p->dense ? smax_scan_kernel_dense : smax_scan_kernel, g, b, 0, s, a);
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
-    if (mode == 0) {
-      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, p->side, b);
-      HIPCHK(hipGetLastError());
-    }
-    if (mode == 2) {
-      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->static_grid), dim3(SMAX_THREADS), 0, s, b);
-      HIPCHK(hipGetLastError());
-    }
-    if (side) {
-      // join (the static K1b finishes inside K1), then K1b over K1's
-      // runtime list (exact-queue overflow)
-      HIPCHK(hipEventRecord(p->join, p->side));
-      HIPCHK(hipStreamWaitEvent(s, p->join, 0));
-    }
-    if (mode == 4) {
-      // static list + K1's deferrals in one launch; one workgroup
-      // computes the boundary head
-      SmaxScanArgs c = a;
-      c.k1b_head = 1;
-      if (p->k1b_wg)
-        hipLaunchKernelGGL(smax_defer_wg_kernel, dim3(p->comb_grid_wg + p->bs_wgs), dim3(SMAX_THREADS),
-                           0, s, c);
-      else
-        hipLaunchKernelGGL(smax_defer_kernel, dim3(p->comb_grid), dim3(SMAX_THREADS), 0, s, c);
-    } else {
-      hipLaunchKernelGGL(smax_defer_kernel, dim3(p->defer_grid), dim3(SMAX_THREADS), 0, s, a);
-    }
+  }
+  {
+    // K1b over the static list and K1's deferrals, one launch; its first
+    // workgroup computes the boundary head, its last ones the block sums
+    SmaxScanArgs c = a;
+    c.k1b_head = 1;
+    hipLaunchKernelGGL(smax_defer_wg_kernel, dim3(p->k1b_grid + p->bs_wgs), dim3(SMAX_THREADS), 0, s, c);
     HIPCHK(hipGetLastError());
   }
   return 0;
@@ -3257,24 +3126,17 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
   char *errbuf = NULL;
   size_t errlen = 0;
   {
-    const bool nok0 = p->k1b_mode == 4 && !(p->dbg & 16384u);
-    uint32_t *bs = p->block_sum, *bs_clear = nullptr;
-    if (p->bs_wgs) {   // block sums added up in K1b's launch
-      bs = p->block_sum + (p->runs & 1) * smax_bs_stride(p->compact_grid);
-      bs_clear = p->block_sum + ((p->runs + 1) & 1) * smax_bs_stride(p->compact_grid);
-    } else {
-      hipLaunchKernelGGL(smax_block_sum_kernel, dim3(p->compact_grid), dim3(256), 0, s,
-                         p->tile_count, (uint64_t) p->num_tiles, p->block_sum);
-      HIPCHK(hipGetLastError());
-    }
-    SmaxNextRun nr = {nullptr, nullptr, nullptr, 0u, 0ull};
-    if (nok0) {
-      nr.defer_count = p->defer_count;
-      nr.defer_last = p->defer_last;
-      nr.pool_cursor = p->pool_cursor;
-      nr.defer_base = p->n_static;
-      nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
-    }
+    // block sums added up in K1b's launch into this run's buffer; K3 clears
+    // the other one for the next run and resets the deferral state K1b was
+    // the last to read
+    uint32_t *bs = p->block_sum + p->bs_buf * smax_bs_stride(p->compact_grid);
+    uint32_t *bs_clear = p->block_sum + (p->bs_buf ^ 1u) * smax_bs_stride(p->compact_grid);
+    SmaxNextRun nr;
+    nr.defer_count = p->defer_count;
+    nr.defer_last = p->defer_last;
+    nr.pool_cursor = p->pool_cursor;
+    nr.defer_base = p->n_static;
+    nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid * p->k3_split), dim3(256), 0, s,
                        p->slots, p->tile_count, bs, (uint64_t) p->num_tiles,
                        p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
@@ -3283,6 +3145,7 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
                        p->k3_split);
     HIPCHK(hipGetLastError());
   }
+  p->bs_buf ^= 1u;
   p->runs++;
   return 0;
 fail:
@@ -3408,11 +3271,10 @@ fail:
 extern "C" uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *p) {
   uint32_t n = 0;
   if (hipSetDevice(p->shard.device) != hipSuccess) return 0xffffffffu;
-  // combined placement: K3 resets the live count; its last value is kept
-  if (hipMemcpy(&n, p->k1b_mode == 4 ? p->defer_last : p->defer_count, sizeof n,
-                hipMemcpyDeviceToHost) != hipSuccess)
+  // K3 resets the live count; its last value is kept
+  if (hipMemcpy(&n, p->defer_last, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
     return 0xffffffffu;
-  return p->k1b_mode == 4 ? n - p->n_static : n;   // K1's deferrals only
+  return n - p->n_static;   // K1's deferrals only
 }
 
 extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_t *deferred,
@@ -3424,10 +3286,9 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
   if (counts && !(p->dbg & 32768u))
     for (uint64_t i = 0; i < p->num_tiles; i++) counts[i] &= ~SMAX_SLOT_WIDE;   // slot-format flag
   uint32_t n = 0;
-  if (hipMemcpy(&n, p->k1b_mode == 4 ? p->defer_last : p->defer_count, sizeof n,
-                hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(&n, p->defer_last, sizeof n, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
-  const uint32_t base = p->k1b_mode == 4 ? p->n_static : 0;   // combined list: K1's part
+  const uint32_t base = p->n_static;   // K1b's list: K1's part follows the static entries
   n -= base;
   if (ndeferred) *ndeferred = n;
   if (deferred && n && hipMemcpy(deferred, p->defer_list + base, sizeof (uint32_t) * n,
@@ -3441,12 +3302,11 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
 // tiles); -1 if the plan has none
 extern "C" const char *gt_smax_plan_scan_kernel(const GtSmaxPlan *p) {
   // the selection of plan_run_scan
-  if (p->pk && p->dbg) return "smax_scan_kernel_diag";
+  if (!p->pk) return "smax_scan_kernel_bytes";
+  if (p->dbg) return "smax_scan_kernel_diag";
   if (p->bw2 && p->dense) return p->nt ? "smax_scan_kernel_b2_dense_nt" : "smax_scan_kernel_b2_dense";
   if (p->bw2) return p->nt ? "smax_scan_kernel_b2_nt" : "smax_scan_kernel_b2";
-  if (p->pk && p->dense) return p->nt ? "smax_scan_kernel_dense_nt" : "smax_scan_kernel_dense";
-  if (p->pk) return p->nt ? "smax_scan_kernel_nt" : "smax_scan_kernel";
-  return "smax_scan_kernel_bytes";
+  return p->dense ? "smax_scan_kernel_dense" : "smax_scan_kernel";
 }
 
 extern "C" int gt_smax_plan_stamps(GtSmaxPlan *p, unsigned long long *out8) {

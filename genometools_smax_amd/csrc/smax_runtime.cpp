@@ -289,6 +289,33 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
   return e == hipSuccess ? e2 : e;
 }
 
+// device bytes -> host through the pinned ring (chunk k+1's DMA overlaps the
+// threaded copy-out of chunk k)
+hipError_t d2h_bytes(DevCtx *c, void *dst, const void *dev, uint64_t bytes, unsigned nt) {
+  const uint64_t nch = (bytes + kStage - 1) / kStage;
+  hipError_t e = hipSuccess;
+  auto issue = [&](uint64_t j) {
+    const uint64_t n = std::min(kStage, bytes - j * kStage);
+    hipError_t r = hipMemcpyAsync(c->pin[j & 1], (const char *) dev + j * kStage, n,
+                                  hipMemcpyDeviceToHost, c->stream);
+    return r == hipSuccess ? hipEventRecord(c->ev[j & 1], c->stream) : r;
+  };
+  if (nch > 0) e = issue(0);
+  for (uint64_t k = 0; e == hipSuccess && k < nch; k++) {
+    if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
+    if ((e = hipEventSynchronize(c->ev[k & 1])) != hipSuccess) break;
+    const char *h = (const char *) c->pin[k & 1];
+    char *t0 = (char *) dst + k * kStage;
+    const uint64_t n = std::min(kStage, bytes - k * kStage);
+    par_for((n + 4095) / 4096, nt, [=](uint64_t lo, uint64_t hi) {
+      const uint64_t a = lo * 4096, b = std::min(n, hi * 4096);
+      if (a < b) memcpy(t0 + a, h + a, b - a);
+    });
+  }
+  hipError_t e2 = hipStreamSynchronize(c->stream);
+  return e == hipSuccess ? e2 : e;
+}
+
 // ------------------------------------------------------------ RCCL
 
 struct Rccl {
@@ -687,7 +714,12 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
   C.nshards = std::max(1, num_gpus);
   if ((uint64_t) C.nshards > N - 1) C.nshards = (int) (N - 1);
   C.ndev = std::min(C.nshards, avail);
-  for (int d = 0; d < C.ndev; d++) C.devs.push_back(d);
+  {
+    // the calling thread's device first, then the next ones (wrapping)
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || cur < 0 || cur >= avail) cur = 0;
+    for (int d = 0; d < C.ndev; d++) C.devs.push_back((cur + d) % avail);
+  }
   // contiguous shard blocks per device slot, the first slots one larger
   C.first.assign(C.ndev + 1, 0);
   for (int d = 0; d < C.ndev; d++)
@@ -704,6 +736,10 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
     S.len = S.end - S.base + 1;               // LCP[base .. end], BWT[base .. end]
     S.lo = llv_lower(in, S.base);
     S.hi = llv_lower(in, S.base + S.len);
+    // the searches run over a .llv that is validated beside the upload: with
+    // positions out of order hi can fall below lo (the call then fails with
+    // the validation's message, not with an underflowed allocation size)
+    if (S.hi < S.lo) S.hi = S.lo;
   }
   C.rccl = C.ndev > 1 || env_on("GT_SMAX_FORCE_RCCL");
   if (C.rccl) {
@@ -746,6 +782,8 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
       }
     }
   }
+  // a table the validation rejected explains any device-side failure too
+  if (rc != 0 && C.valid.valid() && C.valid.get() != 0) seterr(errbuf, errlen, "%s", C.valid_msg.c_str());
   if (rc != 0 && (errbuf == NULL || errlen == 0 || errbuf[0] == 0))
     for (auto &m : C.err)
       if (!m.empty()) { seterr(errbuf, errlen, "%s", m.c_str()); break; }
@@ -813,9 +851,15 @@ void smax_dev_free(void *ptr) {
     // right after run() must not hand its buffers to the next allocation
     // while K1..K3 still write them).  Outside the pool lock: other device
     // threads keep allocating meanwhile.
-    (void) hipDeviceSynchronize();
-    std::lock_guard<std::mutex> g(P.mu);
-    P.idle.insert({key, ptr});
+    // A device that reports an error (a faulted kernel) gets its block
+    // freed, not cached: nothing is known about what still touches it.
+    if (hipDeviceSynchronize() != hipSuccess) {
+      (void) hipGetLastError();
+      (void) hipFree(ptr);
+    } else {
+      std::lock_guard<std::mutex> g(P.mu);
+      P.idle.insert({key, ptr});
+    }
   }
   if (cur >= 0) (void) hipSetDevice(cur);
 }
@@ -842,6 +886,31 @@ hipError_t smax_d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt
   return d2h_triples(c, dst, dev, cnt, copy_threads(1));
 }
 
+hipError_t smax_stage_upload(void *dst, const void *src, uint64_t bytes) {
+  int d = 0;
+  DevCtx *c = nullptr;
+  hipError_t e = hipGetDevice(&d);
+  if (e == hipSuccess) e = ctx_get(d, &c);
+  if (e != hipSuccess || bytes == 0) return e;
+  std::lock_guard<std::mutex> g(c->mu);
+  const char *s = (const char *) src;
+  return stage_h2d(c, dst, bytes, copy_threads(1),
+                   [s](uint64_t off, uint64_t n, char *buf) {
+                     memcpy(buf, s + off, n);
+                     return true;
+                   }, nullptr);
+}
+
+hipError_t smax_stage_download(void *dst, const void *src, uint64_t bytes) {
+  int d = 0;
+  DevCtx *c = nullptr;
+  hipError_t e = hipGetDevice(&d);
+  if (e == hipSuccess) e = ctx_get(d, &c);
+  if (e != hipSuccess || bytes == 0) return e;
+  std::lock_guard<std::mutex> g(c->mu);
+  return d2h_bytes(c, dst, src, bytes, copy_threads(1));
+}
+
 // ============================================================ C-ABI
 
 extern "C" int gt_smax_pack_bwt(const uint8_t *bwt, uint64_t len, uint64_t *pk) {
@@ -864,6 +933,7 @@ extern "C" int gt_smax_hip_enumerate_to_buffer(const GtSmaxInput *in, unsigned i
                                                int num_gpus, uint64_t **lcp_lb_rb,
                                                uint64_t *count, char *errbuf, size_t errlen) {
   double tv = smax_phase_clock();
+  SmaxDeviceGuard keep;   // the device threads set their own; the caller's is restored
   if (errbuf && errlen) errbuf[0] = 0;
   if (validate_input(in, errbuf, errlen)) return -1;
   smax_phase_mark("validate", &tv);

@@ -72,7 +72,17 @@ typedef struct {
 typedef int (*GtSmaxIntervalFunc)(void *data, uint64_t lcp, uint64_t lb,
                                   uint64_t rb);
 
-/* Device output record: interval [lb .. lb+width-1] with lcp-value lcp. */
+/* Device output record: interval [lb .. lb+width-1] with lcp-value lcp.
+ *
+ * Width limits (the reference carries GtUword lcp values,
+ * src/match/lcpoverflow.h:26-30, src/match/esa_visitor_rep.h:46-51): an
+ * lcp-value must be below 2^32 and one shard may hold at most 2^32 - 1 .llv
+ * entries.  Tables beyond either are REFUSED, never truncated: the plan and
+ * the host-table entry points return -1 with "lcp value >= 2^32 in .llv" or
+ * "more than 2^32 .llv entries in one shard" (tests/test_smax_gpu.py::
+ * test_width_limits_are_refused).  A longest repeat of 4 Gbp would need a
+ * multi-Gbp duplication inside one genome; more .llv entries per shard than
+ * 2^32 are split by a larger num_gpus (shards) first. */
 typedef struct {
   uint64_t lb;
   uint32_t lcp;

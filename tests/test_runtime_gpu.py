@@ -111,10 +111,32 @@ def test_host_entry_variants(shards, env):
     assert np.array_equal(got, want), (shards, env, len(got), len(want))
 
 
-def test_more_shards_than_devices_through_rccl():
+@pytest.mark.parametrize("shards", [7, 8])
+def test_more_shards_than_devices_through_rccl(shards):
+    """num_gpus = 7 / 8 on one device through the in-library RCCL path (a
+    one-rank communicator: GT_SMAX_FORCE_RCCL), C4's shard count included."""
     e = oracle_esa("at1MB")
     want = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 8)
-    got = _host_call(e, 8, 7, GT_SMAX_FORCE_RCCL=1)
+    got = _host_call(e, 8, shards, GT_SMAX_FORCE_RCCL=1)
+    assert np.array_equal(got, want)
+
+
+def test_eight_shards_rccl_human(human10):
+    """The C-ABI with num_gpus = 8 over a 10 Mbp human-like index on one
+    device through the RCCL all-gather path: eight shards' boundary records
+    exchanged, stitched, bit-exact with the oracle."""
+    esa, host = human10
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    old = os.environ.get("GT_SMAX_FORCE_RCCL")
+    os.environ["GT_SMAX_FORCE_RCCL"] = "1"
+    try:
+        got = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], esa.totallength,
+                               esa.nonspecials, 20, 8)
+    finally:
+        if old is None:
+            os.environ.pop("GT_SMAX_FORCE_RCCL", None)
+        else:
+            os.environ["GT_SMAX_FORCE_RCCL"] = old
     assert np.array_equal(got, want)
 
 
@@ -144,15 +166,51 @@ def test_timing_stride(human10):
     p.close()
 
 
+@pytest.mark.parametrize("odd", [1, 3])
+def test_timing_reset_keeps_block_sums(human10, odd):
+    """The timing calls reset the run counter; the block-sum buffer a pass
+    adds into must not follow it (after an odd number of runs the
+    next pass added into the buffer the last pass filled).  Odd runs, then
+    enable_timing, then more runs -- whole and split -- each checked against
+    the oracle, whole table and a middle shard."""
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    p = esa.plan(20)
+    q = esa.plan(20, N // 3, 2 * N // 3)
+    r = esa.plan(20, N // 3, 2 * N // 3)
+    r.run()
+    ref = r.fetch_triples()
+    for _ in range(odd):
+        p.run()
+        q.run()
+    for stride in (1, 4):
+        p.enable_timing(8, stride)
+        q.enable_timing(8, stride)
+        for k in range(3):
+            if k == 1:
+                p.run_part(0)
+                p.enable_timing(8, stride)    # a reset between the two parts
+                p.run_part(1)
+            else:
+                p.run()
+            q.run()
+            assert np.array_equal(p.fetch_triples(), want), (odd, stride, k)
+            assert np.array_equal(q.fetch_triples(), ref), (odd, stride, k)
+    for x in (p, q, r):
+        x.close()
+
+
 @pytest.mark.parametrize("bw2", ["0", "1"])
 @pytest.mark.parametrize("nt", ["0", "1"])
 @pytest.mark.parametrize("dense", ["0", "1"])
 def test_window_stream_policy(human10, nt, dense, bw2):
     """Both window-stream policies of K1 (GT_SMAX_NT; the plan picks nt by
-    shard size), both K1 variants and both BWT window forms (GT_SMAX_BW2: the
-    2-plane stream, windows with a special BWT row left to K1b; or the u64
-    groups) give the oracle's records, whole table and a middle shard's plan
-    run (against the plain-policy plan)."""
+    shard size, 2-plane windows only), both K1 variants and both BWT window
+    forms (GT_SMAX_BW2: the 2-plane stream, windows with a special BWT row
+    left to K1b; or the u64 groups) give the oracle's records, whole table
+    and a middle shard's plan run (against the plain-policy plan); the plan
+    launches the variant the switches name."""
     esa, host = human10
     N = esa.nonspecials
     want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
@@ -167,6 +225,9 @@ def test_window_stream_policy(human10, nt, dense, bw2):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+    name = ("smax_scan_kernel" + ("_b2" if bw2 == "1" else "") + ("_dense" if dense == "1" else "")
+            + ("_nt" if nt == "1" and bw2 == "1" else ""))
+    assert p.scan_kernel() == name and q.scan_kernel() == name, (p.scan_kernel(), name)
     p.run()
     assert np.array_equal(p.fetch_triples(), want)
     r = esa.plan(20, N // 3, 2 * N // 3)
@@ -177,25 +238,16 @@ def test_window_stream_policy(human10, nt, dense, bw2):
         x.close()
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_block_sums_in_k1b_launch(human10, fuse):
-    """K3's block sums added up by K1b's last workgroups (GT_SMAX_FUSE_BS=1,
-    no K2; two buffers alternate by run) or by K2: the oracle's records over
+def test_block_sums_in_k1b_launch(human10):
+    """K3's block sums added up by K1b's last workgroups (two buffers: each
+    run adds into one, its K3 clears the other): the oracle's records over
     five consecutive runs (both buffers twice), split runs included, whole
     table and a middle shard."""
     esa, host = human10
     N = esa.nonspecials
     want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
-    old = os.environ.get("GT_SMAX_FUSE_BS")
-    os.environ["GT_SMAX_FUSE_BS"] = fuse
-    try:
-        p = esa.plan(20)
-        q = esa.plan(20, N // 3, 2 * N // 3)
-    finally:
-        if old is None:
-            os.environ.pop("GT_SMAX_FUSE_BS", None)
-        else:
-            os.environ["GT_SMAX_FUSE_BS"] = old
+    p = esa.plan(20)
+    q = esa.plan(20, N // 3, 2 * N // 3)
     r = esa.plan(20, N // 3, 2 * N // 3)
     r.run()
     ref = r.fetch_triples()

@@ -266,3 +266,91 @@ def test_dense_llv_kernel_variant(monkeypatch, dense):
     e = oracle_esa("at1MB")
     for minlen in (20, 255, 300):
         assert np.array_equal(_gpu(e, minlen), _cpu(e, minlen)), minlen
+
+
+def test_width_limits_are_refused():
+    """The device record carries a 32-bit lcp (GtSmaxRecord.lcp) and K1 indexes
+    a shard's .llv with 32 bits; the reference carries GtUword lcp values
+    (src/match/lcpoverflow.h:26-30).  Tables past those widths are refused
+    with a message, never truncated: an .llv value >= 2^32 through the plan
+    and through the host-table entry point, and more than 2^32 .llv entries
+    in one shard through the plan (refused before any kernel reads them)."""
+    import torch
+    e = oracle_esa("at1MB")
+    assert len(e.llv) > 2
+    big = e.llv.copy()
+    big[len(big) // 2, 1] = (1 << 32) + 7
+    with pytest.raises(G.SmaxError, match=r"lcp value >= 2\^32 in \.llv"):
+        G.enumerate_smax(e.lcpbytes, big, e.bwt, e.n, e.nonspecials, 20)
+    with pytest.raises(G.SmaxError, match=r"lcp value >= 2\^32 in \.llv"):
+        G.enumerate_smax(e.lcpbytes, big, e.bwt, e.n, e.nonspecials, 20, 3)
+
+    def padded(a, n):
+        t = torch.zeros(G.PAD_FRONT + n + G.PAD_BACK, dtype=torch.uint8, device="cuda")
+        t[G.PAD_FRONT:G.PAD_FRONT + len(a)] = torch.from_numpy(np.ascontiguousarray(a))
+        return t, t.data_ptr() + G.PAD_FRONT
+
+    N = e.nonspecials
+    length = N + 1
+    lcp_t, lcp_p = padded(e.lcpbytes[:length], length)
+    bwt_t, bwt_p = padded(e.bwt[:length], length)
+    llv_t = torch.from_numpy(np.ascontiguousarray(
+        np.vstack([big, np.zeros((1, 2), np.uint64)]).view(np.int64))).cuda()
+    with pytest.raises(G.SmaxError, match=r"lcp value >= 2\^32 in \.llv"):
+        G.SmaxPlan(lcp_p, bwt_p, llv_t.data_ptr(), len(big), 0, length, 1, N, N, 20)
+    with pytest.raises(G.SmaxError, match=r"more than 2\^32 \.llv entries"):
+        G.SmaxPlan(lcp_p, bwt_p, llv_t.data_ptr(), (1 << 32) + 1, 0, length, 1, N, N, 20)
+    # the good tables still plan and run after the refusals
+    good_t = torch.from_numpy(np.ascontiguousarray(
+        np.vstack([e.llv, np.zeros((1, 2), np.uint64)]).view(np.int64))).cuda()
+    p = G.SmaxPlan(lcp_p, bwt_p, good_t.data_ptr(), len(e.llv), 0, length, 1, N, N, 20)
+    p.run()
+    assert np.array_equal(p.fetch_triples(), _cpu(e, 20))
+    p.close()
+
+
+def test_read_set_keeps_packed_groups_in_k1():
+    """Read sets put a separator every few hundred rows, so most K1 windows
+    hold a special BWT row; the plan then keeps K1 on the u64 packed groups
+    (smax_scan_kernel) instead of sending those windows to K1b with the
+    2-plane stream.  Records equal the oracle's either way (GT_SMAX_BW2=1
+    forces the 2-plane stream: nearly every tile in K1b)."""
+    import os
+    rng = np.random.default_rng(31)
+    fams = [rng.integers(0, 4, 150, dtype=np.uint8) for _ in range(40)]
+    parts = []
+    for _ in range(20000):
+        r = rng.integers(0, 4, 100, dtype=np.uint8)
+        if rng.random() < 0.5:   # reads from shared families: long lcps, smax intervals
+            f = fams[int(rng.integers(0, len(fams)))]
+            at = int(rng.integers(0, 50))
+            r = f[at:at + 100].copy()
+            r[rng.random(100) < 0.02] = rng.integers(0, 4, dtype=np.uint8)
+        parts += [r, np.array([255], dtype=np.uint8)]
+    t = np.concatenate(parts[:-1])
+    esa = G.DeviceEsa(t, device=0)
+    host = esa.download()
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    assert len(want) > 1000
+    p = esa.plan(20)
+    assert p.scan_kernel() == "smax_scan_kernel", p.scan_kernel()
+    p.run()
+    assert np.array_equal(p.fetch_triples(), want)
+    p.close()
+    old = os.environ.get("GT_SMAX_BW2")
+    os.environ["GT_SMAX_BW2"] = "1"
+    try:
+        q = esa.plan(20)
+    finally:
+        if old is None:
+            os.environ.pop("GT_SMAX_BW2", None)
+        else:
+            os.environ["GT_SMAX_BW2"] = old
+    assert q.scan_kernel() == "smax_scan_kernel_b2"
+    q.run()
+    assert np.array_equal(q.fetch_triples(), want)
+    q.close()
+    # the host-table entry point chooses the same way (its own staged tables)
+    assert np.array_equal(G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"],
+                                           esa.totallength, esa.nonspecials, 20, 2), want)
+    esa.release()

@@ -15,6 +15,7 @@
 #   prof:CONFIG      rocprofv3 --kernel-trace --stats of a bench run
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
+#   e2ecold:CONFIG   tools/e2e_cold.py: first drop-in call of a fresh process (+ phases)
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
 #   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
@@ -125,6 +126,10 @@ for S in "$@"; do
         python3 "$R/tools/shard_step.py" human 3e9 20 "$W" > "$O/profshards_$W.txt" 2>&1)
       python3 tools/rocpd_summary.py stats "$O/profshards_$W/p_results.db" "$O/kernel_stats_shards_$W.csv"
       rm -rf "$O/profshards_$W" ;;
+    e2ecold:*)
+      # cold end-to-end: first call of the drop-in entry point in a fresh process
+      timeout -k 10 900 python -u tools/e2e_cold.py "${S#e2ecold:}" 3 > "$O/e2e_cold_${S#e2ecold:}.json" \
+        2> "$O/e2e_cold_${S#e2ecold:}.err" ;;
     shards:*)
       W=${S#shards:}
       timeout -k 10 600 python -u tools/shard_step.py human 3e9 20 "$W" > "$O/shards_$W.txt" 2>&1 ;;
