@@ -233,7 +233,11 @@ def main():
         # one GPU: all n+1 rows (the host-table leg hands the whole tables
         # to the drop-in entry point); ranks: LCP[begin-1 .. end] only
         lo, hi = (0, n + 1) if world == 1 else (begin - 1, end + 1)
-        esa = G.DeviceEsa64(text, device=local, row_lo=lo, row_hi=hi)
+        # ranks sharing one GPU (rehearsal) size their sort batches down: each
+        # builder would otherwise take what the free HBM allows (~96 B per
+        # suffix of a batch) and eight of them at once overcommit the device
+        esa = G.DeviceEsa64(text, device=local, row_lo=lo, row_hi=hi,
+                            batch_max=(1 << 27) if args.one_gpu and world > 1 else 0)
         builder = "64-bit range builder, rows [%d, %d)" % (lo, hi)
     else:
         esa = G.DeviceEsa(text, device=local, keep_suftab=False)

@@ -17,6 +17,8 @@
 // off, GT_SMAX_NO_CACHE=1); gt_smax_release_cache() frees everything cached.
 hipError_t smax_dev_alloc(void **ptr, size_t bytes);   // on the current device
 void smax_dev_free(void *ptr);                          // any device; NULL ok
+// in_use = false: the block never had work enqueued on it (no device wait)
+void smax_dev_free_ex(void *ptr, bool in_use);
 
 // Device records of a plan -> host (lcp, lb, rb) triples through the
 // device's pinned ring (the plan's work must be complete).
@@ -43,6 +45,12 @@ struct SmaxDeviceGuard {
 // row, given as (group << 16 | special mask); enqueued on `stream`.
 hipError_t smax_groups_from_planes(uint64_t *groups, const uint32_t *planes, uint64_t ngroups,
                                    const uint64_t *spec, uint64_t nspec, hipStream_t stream);
+
+// Allocates and frees (into the cache) every buffer a plan over `shard`
+// will take and loads the scan kernels' code object: run ahead of
+// gt_smax_plan_create (e.g. beside the tables' upload) it takes the cold
+// allocations off the plan's path.  Current device.
+hipError_t smax_plan_reserve(const GtSmaxDevShard *shard, uint64_t capacity);
 
 // GT_SMAX_TIMING=1: phase times of the host-table entry points on stderr.
 double smax_phase_clock();

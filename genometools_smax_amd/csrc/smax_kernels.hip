@@ -1002,10 +1002,12 @@ __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0
 // Left diversity of the 16 rows c of segment `so` for the two interval
 // shapes decided here: *div2 = {BWT[c-1], BWT[c]} pairwise distinct (specials
 // unique), *div3 = {BWT[c-1], BWT[c], BWT[c+1]} pairwise distinct.
+// (packed windows: w, pw, nw = the segment's group and its neighbours,
+// read by classify_rel together with the LCP bytes)
 __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t *div2,
-                                            uint32_t *div3) {
+                                            uint32_t *div3, uint64_t w = 0, uint64_t pw = 0,
+                                            uint64_t nw = 0) {
   if (t.B == nullptr) {   // packed window
-    const uint64_t w = pk_word(t, so >> 4), pw = pk_word(t, (so >> 4) - 1), nw = pk_word(t, (so >> 4) + 1);
     // both code planes at once (low plane bits 0..15, high plane 16..31)
     const uint32_t c = (uint32_t) w, pc = (uint32_t) pw, nc = (uint32_t) nw;
     const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
@@ -1057,6 +1059,9 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
 // from the exact .llv values by rank (crank = 255 bytes before the segment).
 struct SegRel {
   uint32_t UP, EQ, GE, FF, F18, pb;
+  uint4 v;                  // the segment's 16 LCP bytes (the record output reads them)
+  uint64_t pw, w, nw;       // packed windows: BWT groups of the segment and its neighbours
+                            // (segment_div), read with the bytes: one LDS round trip
 };
 
 // Part 1: the relations of rows 0..17 of segment `so` to their predecessors
@@ -1065,7 +1070,13 @@ __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t
   const LDSP uint8_t *L = t.L;
   const uint4 v = lds_ld16(&L[so]);
   const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
+  if (t.B == nullptr) {
+    r.w = pk_word(t, so >> 4);
+    r.pw = pk_word(t, (so >> 4) - 1);
+    r.nw = pk_word(t, (so >> 4) + 1);
+  }
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+  r.v = v;
   uint32_t up[4], eq[4], ge[4], ff[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1205,7 +1216,7 @@ __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r
   // the exact queue only receives starts that can still be accepted (on
   // repeat-rich DNA most plateau starts share their left symbols)
   uint32_t div2, div3;
-  segment_div(t, so, &div2, &div3);
+  segment_div(t, so, &div2, &div3, r.w, r.pw, r.nw);
   if (all_exact || unresolved) {
     *Lm = A & div2;
     *Dm = 0;
@@ -1254,19 +1265,30 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   uint8_t *segl = reinterpret_cast<uint8_t *>(ent + DL);
   // accepted exact starts, one 16-bit row mask per compacted segment
   uint32_t *accw = ent + DL + 2 * 64 / 4;
-  // compact the active segments (id = round * 64 + lane, row order)
+  // compact the active segments (id = round * 64 + lane, row order): the
+  // k-th active segment goes to step k / 64, lane k % 64.  Two forward
+  // permutes (ds_permute_b32: no LDS memory, one round trip) instead of an
+  // LDS list written and read back: lane d0 receives the d0-th active
+  // first-half segment; the second-half ones go to lanes (n0 + j) mod 64
+  // (step 0 for n0 + j < 64, step 1 otherwise -- one lane never holds both,
+  // n1 <= 64).  Inactive segments fill the other lanes, so each permute is a
+  // bijection.
   const uint64_t ltm = lanemask_lt();
   const uint64_t m0 = __ballot(segpre & 1u), m1 = __ballot((segpre >> 1) & 1u);
-  const uint32_t n0 = (uint32_t) __popcll(m0), nseg = n0 + (uint32_t) __popcll(m1);
-  if (segpre & 1u) segl[__popcll(m0 & ltm)] = (uint8_t) lane;
-  if (segpre & 2u) segl[n0 + __popcll(m1 & ltm)] = (uint8_t) (64 + lane);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  const uint32_t n0 = (uint32_t) __popcll(m0), n1 = (uint32_t) __popcll(m1), nseg = n0 + n1;
+  const bool a0 = (segpre & 1u) != 0, a1 = (segpre & 2u) != 0;
+  const uint32_t d0 = a0 ? (uint32_t) __popcll(m0 & ltm) : n0 + (uint32_t) __popcll(~m0 & ltm);
+  const uint32_t d1 = (a1 ? n0 + (uint32_t) __popcll(m1 & ltm)
+                          : n0 + n1 + (uint32_t) __popcll(~m1 & ltm)) & 63u;
+  const uint32_t segA = (uint32_t) __builtin_amdgcn_ds_permute((int) (d0 * 4u), lane);
+  const uint32_t segB = (uint32_t) __builtin_amdgcn_ds_permute((int) (d1 * 4u), 64 + lane);
+  (void) segl;
   // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones; set
   // for every step k < nsteps and read only there (no zero-fill: each
   // initialiser was a per-tile VALU move, and VALU issue bounds K1)
   uint32_t Dm0, Lm0, Dm1, Lm1, Lpre0, Lpre1, ro0, ro1;
   uint32_t W30, W31, F0, F1, R0, R1;
+  uint4 V0, V1;                      // the steps' segment bytes (record output)
   uint32_t nL = 0;
   const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
   // 255-byte ranks: the left halo's count, then a prefix over the compacted
@@ -1287,7 +1309,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     SegRel rel;                     // fields other than FF read only for i < nseg
     rel.FF = 0;
     if (i < nseg) {
-      const uint32_t sid = segl[i];
+      const uint32_t sid = (k == 0 && (uint32_t) lane < n0) ? segA : segB;
       ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
       classify_rel(t, SMAX_LH + ro, mf, rel);
     }
@@ -1321,8 +1343,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
       }
     }
-    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; R0 = crank; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
-    else { Dm1 = D; W31 = D3; F1 = F; R1 = crank; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
+    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; R0 = crank; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; V0 = rel.v; }
+    else { Dm1 = D; W31 = D3; F1 = F; R1 = crank; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; V1 = rel.v; }
     nL += tot;
   }
   if (rank != nullptr && lane == 0) {   // halo chunks (ranks of rows the slow paths may read)
@@ -1375,6 +1397,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1, W3 = k == 0 ? W30 : W31;
     const uint32_t Fk = k == 0 ? F0 : F1, Rk = k == 0 ? R0 : R1;
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
+    const uint4 Vk = k == 0 ? V0 : V1;
     const uint32_t si = k * 64 + lane;
     uint32_t acc = D;
     if (Lq != 0 && !(a.dbg & 4u)) acc |= (accw[si >> 1] >> (16u * (si & 1u))) & 0xffffu;
@@ -1387,7 +1410,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       // packed slot record: row in the tile + 1 (11 bits) | width (21) | lcp (32)
       uint32_t lcp, width;
       if ((D >> q) & 1u) {
-        const uint32_t b = sL[SMAX_LH + ro + q];
+        const uint32_t wq = q < 4 ? Vk.x : q < 8 ? Vk.y : q < 12 ? Vk.z : Vk.w;
+        const uint32_t b = (wq >> (8 * (q & 3))) & 0xffu;   // LCP[ro + q], from registers
         lcp = b < 255 ? b : llv_by_rank(t, Rk + (uint32_t) __popc(Fk & ((1u << q) - 1)));
         width = 2 + ((W3 >> q) & 1u);
       } else {
@@ -1465,13 +1489,15 @@ __device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint3
   return (ff & 0x80808080u) != 0 || (pack16(g) & d2) != 0;
 }
 
+// v0, v1: the lane's two segments (window offsets so, so + 1024), read by
+// the caller ahead of the next window's DMA issue so that their LDS latency
+// overlaps it
 __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
-                                                   uint32_t wlo, uint32_t wn) {
+                                                   uint32_t wlo, uint32_t wn, const uint4 v0,
+                                                   const uint4 v1) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint32_t so = SMAX_LH + lane * 16;
-  const uint4 v0 = lds_ld16(&t.L[so]);
-  const uint4 v1 = lds_ld16(&t.L[so + 1024]);
   uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
   if (t.B == nullptr && !(a.dbg & 1u) &&
       __popcll(__ballot(segpre_bits & 1u)) + __popcll(__ballot(segpre_bits & 2u)) > 64) {
@@ -1606,6 +1632,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // 16-byte LDS read
     // (wave-uniform: to scalars first, then scalar selects)
     const uint4 info = *reinterpret_cast<const uint4 *>(&sInfo[wave][0][0]);
+    // the lane's two segments of this (landed) window, read before the next
+    // window's DMA issue below (independent: the DMA fills the other window)
+    const uint4 sv0 = lds_ld16(&t.L[SMAX_LH + lane * 16]);
+    const uint4 sv1 = lds_ld16(&t.L[SMAX_LH + lane * 16 + 1024]);
     const uint32_t ix = __builtin_amdgcn_readfirstlane(info.x);
     const uint32_t iy = __builtin_amdgcn_readfirstlane(info.y);
     const uint32_t iz = __builtin_amdgcn_readfirstlane(info.z);
@@ -1628,7 +1658,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 
     if constexpr (DIAG) SMAX_STAMP(st, 1);
     t.halo_ff = SMAX_WIN_HALO(wnf);
-    uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
+    uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn, sv0, sv1);
     if constexpr (DIAG) SMAX_STAMP(st, 2);
     if (a.dbg & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
       if (a.dbg & (1u << 17)) {
@@ -2674,6 +2704,40 @@ static uint32_t plan_tiles(const GtSmaxDevShard *s, uint64_t *first) {
   return (uint32_t) (hi - lo + 1);
 }
 
+
+// Warms the runtime's caching allocator for a plan over `shard` (every
+// buffer gt_smax_plan_create will take, at its size -- K1b's record pool at
+// an upper estimate, the cache serves a block of up to twice the request)
+// and loads the scan kernels' code object, so that a plan created right
+// after costs no cold hipMalloc: the host-table entry point runs this on a
+// helper thread beside the staged upload of the shard's tables.
+hipError_t smax_plan_reserve(const GtSmaxDevShard *shard, uint64_t capacity) {
+  if (shard->begin < 1 || shard->begin > shard->end) return hipSuccess;
+  uint64_t first = 0;
+  const uint64_t nt = plan_tiles(shard, &first);
+  if (capacity == 0) capacity = (shard->end - shard->begin) / 64 + 4096;
+  const uint64_t cg = (nt + SMAX_CPB - 1) / SMAX_CPB;
+  const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
+  const uint64_t wide_est = nt / 256 + std::max<uint64_t>(256u, nt / 256u);
+  const size_t sizes[] = {
+      sizeof (GtSmaxRecord) * capacity, sizeof (uint64_t) * SMAX_SSLOT * nt,
+      sizeof (unsigned long long), sizeof (uint64_t) * nt, sizeof (uint32_t) * nt,
+      sizeof (uint32_t) * (2 * smax_bs_stride(cg) + 1), sizeof (uint64_t), sizeof (GtSmaxBoundary),
+      sizeof (uint2) * (nt + 2), sizeof (uint32_t), sizeof (uint32_t) * (2 * nt + 1),
+      sizeof (uint2) * (2 * nt + 1), sizeof (uint32_t), sizeof (uint32_t), sizeof (uint32_t),
+      sizeof (uint16_t) * (shard->numllv + 16), sizeof (uint32_t), sizeof (uint32_t) * (ngroups + 4),
+      64 * nt, sizeof (uint32_t) * (nt + 1), sizeof (uint32_t),
+      sizeof (GtSmaxRecord) * (wide_est * (SMAX_TILE / 2) + capacity)};
+  constexpr size_t K = sizeof sizes / sizeof sizes[0];
+  void *blk[K] = {};
+  hipError_t e = hipSuccess;
+  for (size_t i = 0; i < K && e == hipSuccess; i++) e = smax_dev_alloc(&blk[i], sizes[i]);
+  for (size_t i = 0; i < K; i++) smax_dev_free_ex(blk[i], false);
+  int per_cu = 0;   // loads the code object (the first query or launch of a kernel does)
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smax_scan_kernel_b2, SMAX_K1_THREADS, 0);
+  return e;
+}
 
 extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                                    const GtSmaxDevShard *shard,

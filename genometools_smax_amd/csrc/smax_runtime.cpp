@@ -499,6 +499,28 @@ void device_phase1(Call *C, int d) {
     double tp = smax_phase_clock();
     for (int s = s0; s < s1; s++) {
       Shard &S = C->sh[s];
+      // the plan's buffers into the device cache (and the code object
+      // loaded) on a helper thread while this thread stages the tables: a
+      // first call otherwise pays ~30 ms of cold allocations in plan creation
+      std::thread reserve;
+      {
+        GtSmaxDevShard g;
+        memset(&g, 0, sizeof g);
+        g.numllv = S.hi - S.lo;
+        g.base = S.base;
+        g.local_len = S.len;
+        g.begin = S.begin;
+        g.end = S.end;
+        g.nonspecials = in->nonspecials;
+        g.device = dev;
+        reserve = std::thread([g, dev] {
+          if (hipSetDevice(dev) == hipSuccess) (void) smax_plan_reserve(&g, 0);
+        });
+      }
+      struct JoinT {
+        std::thread &t;
+        ~JoinT() { if (t.joinable()) t.join(); }
+      } join_reserve{reserve};
       DCHK(alloc_table(&S.lcp, S.len));
       const char *lsrc = (const char *) in->lcptab + S.base;
       DCHK(stage_h2d(c, (char *) S.lcp + GT_SMAX_PAD_FRONT, S.len, C->nt,
@@ -576,6 +598,7 @@ void device_phase1(Call *C, int d) {
         fail_dev(C, d, C->valid_msg);
         goto out;
       }
+      reserve.join();
       if (gt_smax_plan_create(&S.plan, &S.sh, C->minlen, 0, eb, sizeof eb)) {
         fail_dev(C, d, eb);
         goto out;
@@ -828,7 +851,9 @@ hipError_t smax_dev_alloc(void **ptr, size_t bytes) {
   return hipSuccess;
 }
 
-void smax_dev_free(void *ptr) {
+void smax_dev_free(void *ptr) { smax_dev_free_ex(ptr, true); }
+
+void smax_dev_free_ex(void *ptr, bool in_use) {
   if (ptr == nullptr) return;
   Pool &P = pool();
   std::pair<int, size_t> key;
@@ -853,7 +878,8 @@ void smax_dev_free(void *ptr) {
     // threads keep allocating meanwhile.
     // A device that reports an error (a faulted kernel) gets its block
     // freed, not cached: nothing is known about what still touches it.
-    if (hipDeviceSynchronize() != hipSuccess) {
+    // (in_use false: a block no work was ever enqueued on -- no wait.)
+    if (in_use && hipDeviceSynchronize() != hipSuccess) {
       (void) hipGetLastError();
       (void) hipFree(ptr);
     } else {

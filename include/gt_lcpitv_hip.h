@@ -55,7 +55,10 @@ typedef struct {
   int (*lcp_interval)(void *data, uint64_t lcp, uint64_t lb, uint64_t rb);
 } GtLcpitvVisitor;
 
-/* in->suftab is required when v->leaf_edge is set (leaf numbers). */
+/* in->suftab is required when v->leaf_edge is set (leaf numbers).  Like
+ * every host-table entry point here: runs on the calling thread's current
+ * HIP device and leaves it current; tables staged through the library's
+ * pinned ring into its caching allocator. */
 int gt_esa_bottomup_hip(const GtSmaxInput *in, const GtLcpitvVisitor *v, void *data,
                         char *errbuf, size_t errlen);
 

@@ -51,7 +51,10 @@ extern "C" {
 /* GtProcessmaxpairs analogue (without the encseq / GtError arguments). */
 typedef int (*GtMaxpairsFunc)(void *data, uint64_t len, uint64_t pos1, uint64_t pos2);
 
-/* in->suftab is required (4 or 8 bytes per entry). */
+/* in->suftab is required (4 or 8 bytes per entry).  The host-table entry
+ * points run on the calling thread's current HIP device and leave it
+ * current; the tables are staged through the library's pinned ring into its
+ * caching allocator (released by gt_smax_release_cache). */
 int gt_maxpairs_hip_enumerate(const GtSmaxInput *in, unsigned int minlen,
                               GtMaxpairsFunc cb, void *data,
                               char *errbuf, size_t errlen);

@@ -107,7 +107,9 @@ void gt_smax_free(void *ptr);
  * second call does not pay multi-GB allocations again; this returns all of
  * it (GT_SMAX_NO_CACHE=1 in the environment frees before every return).
  * num_gpus > 1 splits the suffix rows into num_gpus shards over the visible
- * devices (contiguous blocks of shards per device, one host thread each);
+ * devices, the calling thread's current device first and then the next ones
+ * (contiguous blocks of shards per device, one host thread each; the
+ * caller's current device is current again on return);
  * the shards' boundary records are exchanged with one RCCL all-gather over
  * those devices (communicators created by the library and cached), or by
  * device-to-device copies when one device holds all shards. */

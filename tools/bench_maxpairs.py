@@ -96,6 +96,29 @@ def main():
                "sample": "oracle orc_maxpairs (restated gt_esa_bottomup_maxpairs, 1 core) over all "
                          "%d rows: %.2fs; pair set identical to the GPU's: %s; reference emission order "
                          "identical to the GPU's ordered pass: %s" % (N, tc, same, same_order)}
+    # the host-table entry points (the `gt repfind -l` runner's drop-in,
+    # src/match/esa-maxpairs.c:476-520, and the F3 tree): pageable host
+    # tables -> staged H2D -> count/emit (reference order) -> D2H, in this
+    # process after the device steps; and the F3 lcp-interval tree likewise
+    h = esa.download(suftab=True)
+    n = esa.totallength
+    plan.close()
+    host = {}
+    for name, fn in (("maxpairs_enumerate_to_buffer",
+                      lambda: G.enumerate_maxpairs(h["lcptab"], h["llvtab"], h["bwttab"], h["suftab"],
+                                                   n, N, args.minlen)),
+                     ("lcpitv_enumerate_to_buffer",
+                      lambda: G.enumerate_lcp_intervals(h["lcptab"], h["llvtab"], n, N))):
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = fn()
+            ts.append(time.perf_counter() - t0)
+        host[name] = {"seconds_first": round(ts[0], 4), "seconds_best": round(min(ts), 4),
+                      "value_best": N / min(ts), "records": len(r)}
+        if name.startswith("maxpairs") and cpu is not None:
+            host[name]["identical_to_oracle"] = bool(np.array_equal(r, ref))
+        del r
     print(json.dumps({
         "metric": "suffix-positions/s (maximal pairs, gt repfind -l %d)" % args.minlen,
         "value": N / el, "unit": "suffix-positions/s", "n_gpus": 1, "steps": args.steps,
@@ -105,8 +128,8 @@ def main():
                    "nonspecials": N},
         "maximal_pairs": total, "maximal_pairs_per_s": total / el,
         "ms_per_step_reference_order": elo * 1e3,
+        "host_entry_points": host,
         "cpu_baseline": cpu}), flush=True)
-    plan.close()
     esa.release()
 
 

@@ -16,6 +16,7 @@
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
 #   e2ecold:CONFIG   tools/e2e_cold.py: first drop-in call of a fresh process (+ phases)
+#   mp:KIND          tools/bench_maxpairs.py (F2/F3, 100 Mbp of KIND, minlen 20)
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
 #   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
@@ -84,7 +85,7 @@ for S in "$@"; do
       # library (A) against LIBB (B) in one process, interleaved rounds
       IFS=: read -r _ LIBB KIND BASES MINLEN SHARD <<< "$S"
       timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" "$LIBB" 8 "$SHARD" \
-        > "$O/ab_${KIND}_${SHARD//\//of}.txt" 2>&1 ;;
+        > "$O/ab_${KIND}_${SHARD//\//of}_vs_$(basename "$(dirname "$LIBB")").txt" 2>&1 ;;
     ablate:*)
       # ablate:V1,V2,...  K1 time under GT_SMAX_DEBUG ablation bits at C3 (diag build)
       timeout -k 10 600 python -u tools/k1_ablate.py human 3e9 "${S#ablate:}" > "$O/ablate.txt" 2>&1 ;;
@@ -126,6 +127,10 @@ for S in "$@"; do
         python3 "$R/tools/shard_step.py" human 3e9 20 "$W" > "$O/profshards_$W.txt" 2>&1)
       python3 tools/rocpd_summary.py stats "$O/profshards_$W/p_results.db" "$O/kernel_stats_shards_$W.csv"
       rm -rf "$O/profshards_$W" ;;
+    mp:*)
+      # F2/F3 secondary bench line (tools/bench_maxpairs.py): device steps + host entry points
+      timeout -k 10 600 python -u tools/bench_maxpairs.py --kind "${S#mp:}" > "$O/bench_maxpairs_${S#mp:}.json" \
+        2> "$O/bench_maxpairs_${S#mp:}.err" ;;
     e2ecold:*)
       # cold end-to-end: first call of the drop-in entry point in a fresh process
       timeout -k 10 900 python -u tools/e2e_cold.py "${S#e2ecold:}" 3 > "$O/e2e_cold_${S#e2ecold:}.json" \
