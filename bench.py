@@ -639,7 +639,10 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": cfg["workload"], "minlen": minlen, "totallength": n,
-                       "nonspecials": N, "llv_entries": numllv, "global_batch": N,
+                       "nonspecials": N,
+                       # N > 1: the range build holds rank 0's rows only
+                       ("llv_entries" if world == 1 else "llv_entries_rank0_rows"): numllv,
+                       "global_batch": N,
                        "parallelism": "sa-range-shard x%d + %s all-gather stitch"
                        % (world, "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)")
                        if world > 1 else "single GPU"},

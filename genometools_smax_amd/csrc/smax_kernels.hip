@@ -65,6 +65,25 @@
 #include "gt_smax_hip.h"
 #include "smax_internal.h"
 
+// K1 build switch (A/B): SMAX_SINFO -- the tiles' llv_win words by scalar
+// loads a tile ahead (instead of LDS-DMA into a ring slot + LDS read)
+#ifndef SMAX_SINFO
+#define SMAX_SINFO 0
+#endif
+// SMAX_PRIO (A/B): wave priority raised while a wave works on a landed window
+// (s_setprio), lowered before it waits for the next
+#ifndef SMAX_PRIO
+#define SMAX_PRIO 0
+#endif
+#if SMAX_SINFO
+#define SMAX_ASM_INFO ""
+#else
+#define SMAX_ASM_INFO                        \
+  "s_mov_b64 exec, %13\n\t"                 \
+  "s_mov_b32 m0, %7\n\t"                    \
+  "s_nop 0\n\t"                             \
+  "global_load_lds_dword %3, %12 offset:0\n\t"
+#endif
 #define SMAX_THREADS 256                              // 4 waves per K1b / K2 / K3 workgroup
 // K1 workgroup: ONE wave.  K1's waves share nothing (no barrier, each its own
 // LDS windows), so a one-wave workgroup frees its LDS and wave slot as soon
@@ -116,11 +135,7 @@ struct SmaxScanArgs {
   const uint8_t *bwt;
   const uint64_t *bwtpk;     // packed BWT, 16 rows per u64 (index local_row/16 + 1), or null
   const uint32_t *bwt2;      // its two code planes alone, 16 rows per u32 (same index), or
-                             // null: K1's window stream when no window holds a special;
-                             // element local_row/16 + 1 of a tile start is 16-byte aligned
-  const uint4 *halo;         // 2-plane K1: per tile a 64-byte side record of its window's
-                             // halos (smax_halo_kernel), so the window stream reads no line
-                             // of a neighbouring tile
+                             // null: K1's window stream when no window holds a special
   const GtSmaxLlv *llv;      // shard's llv entries (global positions)
   const uint16_t *llv16;     // their values as u16 (plan time; windows with larger ones defer)
   uint64_t numllv;
@@ -281,9 +296,8 @@ struct Win {
   uint64_t N, end;            // global row bounds (plateau scans)
   const LDSP uint8_t *L;      // LDS window: index o = g - g0 + LH
   const LDSP uint8_t *B;      // BWT bytes of the window (byte kernel), or
-  const LDSP uint64_t *P;     // packed BWT of the window, 16 rows per word, or
-  const LDSP uint32_t *P2;    // its code planes alone (2-plane windows: p2)
-  bool p2;
+  const LDSP uint64_t *P;     // packed BWT of the window, 16 rows per word
+  bool p2;                    // P holds u32 words (code planes only, no specials)
   const LDSP uint16_t *rank;  // per 16-byte chunk: 255 bytes before it
   const LDSP uint32_t *val;   // LDS .llv values in rank order (nval of them), or
   const LDSP uint16_t *val16; // the same as u16 (K1 windows: values < 65536)
@@ -298,8 +312,7 @@ struct Win {
 
 __device__ __forceinline__ void win_init(Win &t, const SmaxScanArgs &a) {
   t.N = a.N; t.end = a.end;
-  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.P2 = nullptr; t.p2 = false; t.rank = nullptr;
-  t.val = nullptr;
+  t.L = nullptr; t.B = nullptr; t.P = nullptr; t.p2 = false; t.rank = nullptr; t.val = nullptr;
   t.val16 = nullptr; t.nval = -1; t.halo_ff = 0; t.staged_all = false;
   t.g0 = 0; t.llv_base = 0;
 }
@@ -311,7 +324,7 @@ __device__ __forceinline__ int64_t win_off(const Win &t, uint64_t g) {
 // packed BWT group gi of the window as a u64 word (the 2-plane form reads
 // as the u64 form with no special bits)
 __device__ __forceinline__ uint64_t pk_word(const Win &t, uint32_t gi) {
-  return t.p2 ? (uint64_t) t.P2[gi] : t.P[gi];
+  return t.p2 ? (uint64_t) reinterpret_cast<const LDSP uint32_t *>(t.P)[gi] : t.P[gi];
 }
 
 // exact LCP of a row whose byte is 255
@@ -621,8 +634,7 @@ __device__ __forceinline__ const T *uni_ptr(const T *p) {
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
                                                 uint32_t lo, uint32_t n, const void *ibase,
-                                                uint32_t iaddr, uint32_t v16, uint32_t v4,
-                                                const void *hrec = nullptr) {
+                                                uint32_t iaddr, uint32_t v16, uint32_t v4) {
   const uint32_t wp = wl + (uint32_t) offsetof(SmaxWindowPk, P);
   const uint32_t wv = wl + (uint32_t) offsetof(SmaxWindowPk, val16);
   const uint8_t *vb = uni_ptr(reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u)));
@@ -634,25 +646,12 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   uint32_t keep;
   uint64_t ex;
   if constexpr (BW2) {
-    // 2-plane window from aligned pieces only (no line of a neighbouring
-    // tile): the tile's LCP rows [l0, l0+TILE) -> L[LH ..] (2 x 1 KiB), its
-    // 128 code-plane groups (bwt2 element l0/16 + 1 is 16-byte aligned: the
-    // plan offsets the array) -> P region byte 16 (32 lanes), and the 64-byte
-    // side record hrec (smax_halo_kernel): [0,16) left LCP halo -> L[0 ..];
-    // [16,32) right LCP halo -> L[LH+TILE ..] and [32,48) -> P region bytes
-    // [0,16), whose last word is the left halo group; [48,52) the right halo
-    // group -> P region byte 528.  The window's group gi is then at P region
-    // byte 12 + 4 gi (set_bwt_window).  Then the .llv values and the llv_win
-    // word of the tile after next, as in the u64 form.
-    static_assert(offsetof(SmaxWindowPk, P) == SMAX_LDSB, "P region right after the LCP window");
-    static_assert(SMAX_LDSB + 16 + 4 * 128 + 4 <= SMAX_LDSB + sizeof(((SmaxWindowPk *) 0)->P),
-                  "2-plane groups fit the P region");
-    const uint8_t *lb = uni_ptr(a.lcp + l0);
-    const uint8_t *pb = uni_ptr(reinterpret_cast<const uint8_t *>(a.bwt2 + l0 / 16 + 1));
-    const uint8_t *hb = uni_ptr(reinterpret_cast<const uint8_t *>(hrec));
-    const uint32_t m_l = wl + SMAX_LH, m_p = wp + 16, m_h1 = wl + SMAX_LH + SMAX_TILE - 16;
-    const uint32_t m_h2 = wp + 12 + 4 * 129 - 48;
-    const uint64_t m32 = 0xffffffffull;
+    // 2-plane window: LCP rows [l0-LH, l0+TILE+RH) (2 x 1 KiB + 2 lanes),
+    // code-plane groups l0/16 .. l0/16+131 (33 lanes x 16 B), the .llv
+    // values, the llv_win word of the tile after next
+    const uint8_t *lb = uni_ptr(a.lcp + l0 - SMAX_LH);
+    const uint8_t *pb = uni_ptr(reinterpret_cast<const uint8_t *>(a.bwt2 + l0 / 16));
+    const uint64_t p2mask = (1ull << 33) - 1;
     if constexpr (NT) {
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -663,31 +662,20 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %5\n\t"
         "s_mov_b64 exec, %14\n\t"
         "global_load_lds_dwordx4 %2, %9 offset:0 nt\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "s_mov_b32 m0, %16\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %15 offset:0 nt\n\t"
         "s_mov_b64 exec, 3\n\t"
-        "s_mov_b32 m0, %17\n\t"
+        "s_mov_b32 m0, %4\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %15 offset:16 nt\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "s_mov_b32 m0, %18\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %3, %15 offset:48 nt\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:2048 nt\n\t"
         "s_mov_b64 exec, %11\n\t"
         "s_mov_b32 m0, %6\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
-        "s_mov_b64 exec, %13\n\t"
-        "s_mov_b32 m0, %7\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %3, %12 offset:0\n\t"
+        SMAX_ASM_INFO
         "s_mov_b64 exec, %1\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
-        : "v"(v16), "v"(v4), "s"(m_l), "s"(m_p), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(m32), "s"(hb), "s"(wl), "s"(m_h1), "s"(m_h2)
+        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
         : "memory");
     } else {
     asm volatile(
@@ -699,38 +687,26 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %5\n\t"
         "s_mov_b64 exec, %14\n\t"
         "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "s_mov_b32 m0, %16\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %15 offset:0\n\t"
         "s_mov_b64 exec, 3\n\t"
-        "s_mov_b32 m0, %17\n\t"
+        "s_mov_b32 m0, %4\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %15 offset:16\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "s_mov_b32 m0, %18\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %3, %15 offset:48\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:2048\n\t"
         "s_mov_b64 exec, %11\n\t"
         "s_mov_b32 m0, %6\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
-        "s_mov_b64 exec, %13\n\t"
-        "s_mov_b32 m0, %7\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %3, %12 offset:0\n\t"
+        SMAX_ASM_INFO
         "s_mov_b64 exec, %1\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
-        : "v"(v16), "v"(v4), "s"(m_l), "s"(m_p), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(m32), "s"(hb), "s"(wl), "s"(m_h1), "s"(m_h2)
+        : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
         : "memory");
     }
     return;
   }
   const uint8_t *lb = uni_ptr(a.lcp + l0 - SMAX_LH);
   const uint8_t *pb = uni_ptr(reinterpret_cast<const uint8_t *>(a.bwtpk + l0 / 16));
-  (void) hrec;
   if constexpr (NT) {
   asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -750,10 +726,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %6\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
-        "s_mov_b64 exec, %13\n\t"
-        "s_mov_b32 m0, %7\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %3, %12 offset:0\n\t"
+        SMAX_ASM_INFO
         "s_mov_b64 exec, %1\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
@@ -779,10 +752,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %6\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
-        "s_mov_b64 exec, %13\n\t"
-        "s_mov_b32 m0, %7\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %3, %12 offset:0\n\t"
+        SMAX_ASM_INFO
         "s_mov_b64 exec, %1\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
@@ -1002,12 +972,10 @@ __device__ __forceinline__ uint32_t bytes_sp(uint32_t w) { return bytes_ff(w | 0
 // Left diversity of the 16 rows c of segment `so` for the two interval
 // shapes decided here: *div2 = {BWT[c-1], BWT[c]} pairwise distinct (specials
 // unique), *div3 = {BWT[c-1], BWT[c], BWT[c+1]} pairwise distinct.
-// (packed windows: w, pw, nw = the segment's group and its neighbours,
-// read by classify_rel together with the LCP bytes)
 __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t *div2,
-                                            uint32_t *div3, uint64_t w = 0, uint64_t pw = 0,
-                                            uint64_t nw = 0) {
+                                            uint32_t *div3) {
   if (t.B == nullptr) {   // packed window
+    const uint64_t w = pk_word(t, so >> 4), pw = pk_word(t, (so >> 4) - 1), nw = pk_word(t, (so >> 4) + 1);
     // both code planes at once (low plane bits 0..15, high plane 16..31)
     const uint32_t c = (uint32_t) w, pc = (uint32_t) pw, nc = (uint32_t) nw;
     const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
@@ -1059,9 +1027,6 @@ __device__ __forceinline__ void segment_div(const Win &t, uint32_t so, uint32_t 
 // from the exact .llv values by rank (crank = 255 bytes before the segment).
 struct SegRel {
   uint32_t UP, EQ, GE, FF, F18, pb;
-  uint4 v;                  // the segment's 16 LCP bytes (the record output reads them)
-  uint64_t pw, w, nw;       // packed windows: BWT groups of the segment and its neighbours
-                            // (segment_div), read with the bytes: one LDS round trip
 };
 
 // Part 1: the relations of rows 0..17 of segment `so` to their predecessors
@@ -1070,13 +1035,7 @@ __device__ __forceinline__ void classify_rel(const Win &t, uint32_t so, uint32_t
   const LDSP uint8_t *L = t.L;
   const uint4 v = lds_ld16(&L[so]);
   const uint32_t pb = L[so - 1], nb = L[so + 16], nb2 = L[so + 17];
-  if (t.B == nullptr) {
-    r.w = pk_word(t, so >> 4);
-    r.pw = pk_word(t, (so >> 4) - 1);
-    r.nw = pk_word(t, (so >> 4) + 1);
-  }
   const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  r.v = v;
   uint32_t up[4], eq[4], ge[4], ff[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -1216,7 +1175,7 @@ __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r
   // the exact queue only receives starts that can still be accepted (on
   // repeat-rich DNA most plateau starts share their left symbols)
   uint32_t div2, div3;
-  segment_div(t, so, &div2, &div3, r.w, r.pw, r.nw);
+  segment_div(t, so, &div2, &div3);
   if (all_exact || unresolved) {
     *Lm = A & div2;
     *Dm = 0;
@@ -1262,7 +1221,6 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   // BWT symbols); the next DMA into this window is issued after the records
   // have moved to registers (smax_scan_body)
   uint32_t *res_lcp = reinterpret_cast<uint32_t *>(stg + SMAX_SSLOT), *res_w = res_lcp + DL;
-  uint8_t *segl = reinterpret_cast<uint8_t *>(ent + DL);
   // accepted exact starts, one 16-bit row mask per compacted segment
   uint32_t *accw = ent + DL + 2 * 64 / 4;
   // compact the active segments (id = round * 64 + lane, row order): the
@@ -1282,13 +1240,11 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
                           : n0 + n1 + (uint32_t) __popcll(~m1 & ltm)) & 63u;
   const uint32_t segA = (uint32_t) __builtin_amdgcn_ds_permute((int) (d0 * 4u), lane);
   const uint32_t segB = (uint32_t) __builtin_amdgcn_ds_permute((int) (d1 * 4u), 64 + lane);
-  (void) segl;
   // per step: D = decided records (2 or 3 rows), W3 = the 3-row ones; set
   // for every step k < nsteps and read only there (no zero-fill: each
   // initialiser was a per-tile VALU move, and VALU issue bounds K1)
   uint32_t Dm0, Lm0, Dm1, Lm1, Lpre0, Lpre1, ro0, ro1;
   uint32_t W30, W31, F0, F1, R0, R1;
-  uint4 V0, V1;                      // the steps' segment bytes (record output)
   uint32_t nL = 0;
   const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
   // 255-byte ranks: the left halo's count, then a prefix over the compacted
@@ -1343,8 +1299,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
       }
     }
-    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; R0 = crank; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; V0 = rel.v; }
-    else { Dm1 = D; W31 = D3; F1 = F; R1 = crank; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; V1 = rel.v; }
+    if (k == 0) { Dm0 = D; W30 = D3; F0 = F; R0 = crank; Lm0 = Lq; Lpre0 = nL + excl; ro0 = ro; }
+    else { Dm1 = D; W31 = D3; F1 = F; R1 = crank; Lm1 = Lq; Lpre1 = nL + excl; ro1 = ro; }
     nL += tot;
   }
   if (rank != nullptr && lane == 0) {   // halo chunks (ranks of rows the slow paths may read)
@@ -1397,7 +1353,6 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     const uint32_t D = k == 0 ? Dm0 : Dm1, Lq = k == 0 ? Lm0 : Lm1, W3 = k == 0 ? W30 : W31;
     const uint32_t Fk = k == 0 ? F0 : F1, Rk = k == 0 ? R0 : R1;
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
-    const uint4 Vk = k == 0 ? V0 : V1;
     const uint32_t si = k * 64 + lane;
     uint32_t acc = D;
     if (Lq != 0 && !(a.dbg & 4u)) acc |= (accw[si >> 1] >> (16u * (si & 1u))) & 0xffffu;
@@ -1410,8 +1365,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
       // packed slot record: row in the tile + 1 (11 bits) | width (21) | lcp (32)
       uint32_t lcp, width;
       if ((D >> q) & 1u) {
-        const uint32_t wq = q < 4 ? Vk.x : q < 8 ? Vk.y : q < 12 ? Vk.z : Vk.w;
-        const uint32_t b = (wq >> (8 * (q & 3))) & 0xffu;   // LCP[ro + q], from registers
+        const uint32_t b = sL[SMAX_LH + ro + q];
         lcp = b < 255 ? b : llv_by_rank(t, Rk + (uint32_t) __popc(Fk & ((1u << q) - 1)));
         width = 2 + ((W3 >> q) & 1u);
       } else {
@@ -1433,29 +1387,19 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
-                                           uint32_t iaddr, uint32_t v16, uint32_t v4,
-                                           const uint4 *hrec) {
-  issue_window_pk<NT, BW2>(a, l0, wl, lo, n, info, iaddr, v16, v4, hrec);
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
+  issue_window_pk<NT, BW2>(a, l0, wl, lo, n, info, iaddr, v16, v4);
 }
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
-                                           uint32_t iaddr, uint32_t v16, uint32_t v4,
-                                           const uint4 *hrec) {
-  (void) hrec;
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
   issue_window(a, l0, w, lo, n);
   if ((threadIdx.x & 63) < 2) glds4(reinterpret_cast<const uint32_t *>(info) + (threadIdx.x & 63), iaddr);
 }
 
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = to_lds<uint8_t>(W->B); t.P = nullptr; }
-__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) {
-  t.P = to_lds<uint64_t>(W->P);
-  // 2-plane windows: group gi of the window at byte 12 + 4 gi of the region
-  // (the tile's 128 groups 16-byte aligned for their LDS-DMA, the halo
-  // groups beside them from the side record: issue_window_pk)
-  t.P2 = reinterpret_cast<const LDSP uint32_t *>(reinterpret_cast<const LDSP uint8_t *>(t.P) + 12);
-  t.B = nullptr;
-}
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = to_lds<uint64_t>(W->P); t.B = nullptr; }
 
 // A window's BWT region once the tile's exact starts are evaluated: the
 // staged records (SMAX_SSLOT u64) and the starts' results (2 x SMAX_DLIST
@@ -1489,15 +1433,13 @@ __device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint3
   return (ff & 0x80808080u) != 0 || (pack16(g) & d2) != 0;
 }
 
-// v0, v1: the lane's two segments (window offsets so, so + 1024), read by
-// the caller ahead of the next window's DMA issue so that their LDS latency
-// overlaps it
 __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
-                                                   uint32_t wlo, uint32_t wn, const uint4 v0,
-                                                   const uint4 v1) {
+                                                   uint32_t wlo, uint32_t wn) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const uint32_t so = SMAX_LH + lane * 16;
+  const uint4 v0 = lds_ld16(&t.L[so]);
+  const uint4 v1 = lds_ld16(&t.L[so + 1024]);
   uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
   if (t.B == nullptr && !(a.dbg & 1u) &&
       __popcll(__ballot(segpre_bits & 1u)) + __popcll(__ballot(segpre_bits & 2u)) > 64) {
@@ -1577,6 +1519,19 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   const uint32_t wbase = __builtin_amdgcn_readfirstlane(lds_addr(&sWin[wave][0]));
   const uint32_t info0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
   const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
+  const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
+#if SMAX_SINFO
+  // llv_win words by scalar loads (K1 never writes them: constant address
+  // space), the next tile's a whole tile ahead of its use
+  typedef const __attribute__((address_space(4))) uint64_t *CInfo;   // {lo, count word}
+  const CInfo cwin = (CInfo) a.llv_win;
+  uint64_t inf_cur = cwin[tile];
+  uint64_t inf_nxt = cwin[tile + stride <= last ? tile + stride : last];
+  issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase,
+                      (uint32_t) inf_cur, SMAX_WIN_N((uint32_t) (inf_cur >> 32)), a.llv_win, info1,
+                      v16, v4);
+  (void) info0;
+#else
   if (lane < 2) {
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + (tile + stride <= last ? tile + stride
@@ -1584,14 +1539,13 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
           info1);
   }
   glds_wait();
-  const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
   // (the llv_win word of the tile after is loaded again into its slot:
   // the same value)
   issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase,
                       __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
                       SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])),
-                      a.llv_win + (tile + stride <= last ? tile + stride : last), info1, v16, v4,
-                      a.halo + 4 * (uint64_t) tile);
+                      a.llv_win + (tile + stride <= last ? tile + stride : last), info1, v16, v4);
+#endif
   // the previous tile's records (lane r holds record r) and count: stored
   // one iteration late, right after the window wait, so that those stores
   // (and the block-sum atomic) have a whole tile of work to complete before
@@ -1623,19 +1577,22 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
+    if (SMAX_PRIO) __builtin_amdgcn_s_setprio(SMAX_PRIO);
     if constexpr (DIAG) SMAX_STAMP(st, 0);
     if (ptile != ~0u) {
       smax_flush_tile(a, ptile, prec, pcnt);
       ptile = ~0u;
     }
+#if SMAX_SINFO
+    const uint32_t wlo = (uint32_t) inf_cur, wnf = (uint32_t) (inf_cur >> 32), wn = SMAX_WIN_N(wnf);
+    const uint32_t nlo = (uint32_t) inf_nxt, nn = SMAX_WIN_N((uint32_t) (inf_nxt >> 32));
+#else
     // .llv windows of this tile and the next {lo, packed count word}: one
     // 16-byte LDS read
     // (wave-uniform: to scalars first, then scalar selects)
     const uint4 info = *reinterpret_cast<const uint4 *>(&sInfo[wave][0][0]);
-    // the lane's two segments of this (landed) window, read before the next
-    // window's DMA issue below (independent: the DMA fills the other window)
-    const uint4 sv0 = lds_ld16(&t.L[SMAX_LH + lane * 16]);
-    const uint4 sv1 = lds_ld16(&t.L[SMAX_LH + lane * 16 + 1024]);
+#endif
+#if !SMAX_SINFO
     const uint32_t ix = __builtin_amdgcn_readfirstlane(info.x);
     const uint32_t iy = __builtin_amdgcn_readfirstlane(info.y);
     const uint32_t iz = __builtin_amdgcn_readfirstlane(info.z);
@@ -1645,6 +1602,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const uint32_t wn = SMAX_WIN_N(wnf);
     const uint32_t nlo = cur ? ix : iz;
     const uint32_t nn = SMAX_WIN_N(cur ? iy : iw);
+#endif
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
@@ -1653,12 +1611,16 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       const uint32_t n2 = next + stride <= last ? next + stride : last;
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
-                 a.llv_win + n2, cur ? info1 : info0, v16, v4, a.halo + 4 * (uint64_t) next);
+                 a.llv_win + n2, cur ? info1 : info0, v16, v4);
+#if SMAX_SINFO
+      inf_cur = inf_nxt;
+      inf_nxt = cwin[n2];      // used one tile later
+#endif
     }
 
     if constexpr (DIAG) SMAX_STAMP(st, 1);
     t.halo_ff = SMAX_WIN_HALO(wnf);
-    uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn, sv0, sv1);
+    uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
     if constexpr (DIAG) SMAX_STAMP(st, 2);
     if (a.dbg & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
       if (a.dbg & (1u << 17)) {
@@ -1714,6 +1676,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       if (st != nullptr) st->acc[7]++;
     }
 
+    if (SMAX_PRIO) __builtin_amdgcn_s_setprio(0);
     tile = next;
     if (tile >= a.num_tiles) break;
   }
@@ -2475,23 +2438,6 @@ smax_bwt2_kernel(const uint64_t *pk, uint64_t ngroups, uint32_t *bwt2, uint2 *ll
   }
 }
 
-// Per tile of a 2-plane plan its window's halos as one 64-byte record (the
-// layout issue_window_pk's LDS-DMA expects): LCP rows [l0-16, l0) and
-// [l0+TILE, l0+TILE+16), the code-plane groups of those rows in bytes 44
-// and 48; the rest zero
-__global__ void __launch_bounds__(256)
-smax_halo_kernel(const uint8_t *lcp, const uint32_t *bwt2, uint64_t tile_first, uint32_t num_tiles,
-                 uint4 *halo) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= num_tiles) return;
-  const uint64_t l0 = (tile_first + t) * (uint64_t) SMAX_TILE;
-  uint4 *h = halo + 4 * (uint64_t) t;
-  h[0] = *reinterpret_cast<const uint4 *>(lcp + l0 - SMAX_LH);
-  h[1] = *reinterpret_cast<const uint4 *>(lcp + l0 + SMAX_TILE);
-  h[2] = make_uint4(0u, 0u, 0u, bwt2[l0 / 16]);                    // group of rows l0-16 ..
-  h[3] = make_uint4(bwt2[l0 / 16 + SMAX_TILE / 16 + 1], 0u, 0u, 0u);   // rows l0+TILE ..
-}
-
 // u16 copies of the .llv values (larger values are flagged per tile by the
 // index kernel; those windows never read this array)
 __global__ void __launch_bounds__(256)
@@ -2622,10 +2568,7 @@ struct GtSmaxPlan {
   uint2 *llv_win;
   uint64_t *bwtpk;           // packed BWT (DNA shards), else null
   bool pk, pk_owned;          // packed windows; bwtpk allocated by the plan
-  uint32_t *bwt2;            // its code planes alone (K1's 2-plane window stream), or null:
-                             // bwt2_alloc + 3, so element l0/16 + 1 of a tile is 16-byte aligned
-  uint32_t *bwt2_alloc;
-  uint4 *halo;               // 2-plane K1: 64-byte side record per tile (smax_halo_kernel)
+  uint32_t *bwt2;            // its code planes alone (K1's 2-plane window stream), or null
   bool bw2;                  // K1 streams bwt2 (windows with a special BWT row: static K1b)
   uint16_t *llv16;           // .llv values as u16 (numllv + 2)
   uint32_t *defer_list;      // K1 -> K1b tile list (num_tiles) + count
@@ -2947,18 +2890,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                  : p->dbg != 0 || 2ull * nsp <= std::max<uint32_t>(p->num_tiles / 256u, 64u);
     if (p->bw2) {
       const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
-      HIPCHK(dalloc(&p->bwt2_alloc, sizeof (uint32_t) * (ngroups + 4)));
-      p->bwt2 = p->bwt2_alloc + 3;
+      HIPCHK(dalloc(&p->bwt2, sizeof (uint32_t) * ngroups));
       hipLaunchKernelGGL(smax_bwt2_kernel, dim3((unsigned) std::min<uint64_t>((ngroups + 255) / 256, 1u << 20)),
                          dim3(256), 0, 0, p->bwtpk, ngroups, p->bwt2, p->llv_win, p->tile_first,
                          (uint64_t) p->num_tiles);
-      HIPCHK(hipGetLastError());
-      // the windows' halos as side records: K1's window stream then reads
-      // only its own tile's lines (the halos had cost 384 B of neighbouring
-      // lines per 2048-row tile, 0.56 GB per C3 pass)
-      HIPCHK(dalloc(&p->halo, 64 * (uint64_t) p->num_tiles));
-      hipLaunchKernelGGL(smax_halo_kernel, dim3((p->num_tiles + 255) / 256), dim3(256), 0, 0,
-                         shard->lcp_dev, p->bwt2, p->tile_first, p->num_tiles, p->halo);
       HIPCHK(hipGetLastError());
     }
   }
@@ -3043,7 +2978,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2_alloc, p->halo,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
@@ -3059,7 +2994,6 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.bwt = p->shard.bwt_dev;
   a.bwtpk = p->pk ? p->bwtpk : nullptr;
   a.bwt2 = p->bw2 ? p->bwt2 : nullptr;
-  a.halo = p->bw2 ? p->halo : nullptr;
   a.llv16 = p->llv16;
   a.llv = p->shard.llv_dev;
   a.numllv = p->shard.numllv;

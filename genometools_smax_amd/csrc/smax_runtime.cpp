@@ -44,6 +44,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
+#include <functional>
 #include <future>
 #include <map>
 #include <mutex>
@@ -111,7 +113,16 @@ void release_idle(int device) {   // pool.mu held
 
 // ------------------------------------------------------------ per device
 
-constexpr uint64_t kStage = 64ull << 20;   // pinned staging chunk (bytes)
+// pinned staging chunk (bytes): 64 MiB, GT_SMAX_STAGE_MB overrides
+uint64_t stage_bytes() {
+  static const uint64_t b = [] {
+    const char *v = getenv("GT_SMAX_STAGE_MB");
+    const uint64_t mb = v ? strtoull(v, NULL, 0) : 64;
+    return (mb < 1 ? 1 : mb > 1024 ? 1024 : mb) << 20;
+  }();
+  return b;
+}
+#define kStage stage_bytes()
 
 struct DevCtx {
   int device = -1;
@@ -119,7 +130,15 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   void *pin[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
+  // the ring's second chunk is pinned on a helper thread while the first
+  // chunk's fill and DMA run (a first call pays the page pinning of one
+  // chunk before its first DMA, not two); ring_ready waits for it
+  std::shared_future<hipError_t> pin1;
 };
+
+hipError_t ring_ready(DevCtx *c) {
+  return c->pin1.valid() ? c->pin1.get() : hipSuccess;
+}
 
 std::mutex g_ctx_mu;
 std::map<int, DevCtx *> g_ctx;
@@ -132,10 +151,13 @@ hipError_t ctx_get(int device, DevCtx **out) {
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  for (int i = 0; i < 2 && e == hipSuccess; i++) {
-    e = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
-  }
+  for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
+  if (e == hipSuccess)
+    c->pin1 = std::async(std::launch::async, [c, device] {
+                hipError_t r = hipSetDevice(device);
+                return r == hipSuccess ? hipHostMalloc(&c->pin[1], kStage, hipHostMallocDefault) : r;
+              }).share();
   if (e != hipSuccess) {
     for (int i = 0; i < 2; i++) {
       if (c->pin[i]) (void) hipHostFree(c->pin[i]);
@@ -150,14 +172,75 @@ hipError_t ctx_get(int device, DevCtx **out) {
   return hipSuccess;
 }
 
-// f(lo, hi) over [0, n) on nt threads (the calling thread takes the first part)
+// Persistent worker threads for the staging fills and copy-outs: a call
+// runs one fill per 64 MiB chunk, and spawning its helpers each time cost
+// ~11 thread creations per chunk (hundreds per call).  Workers are created on
+// first use and live for the process; several device threads may submit at
+// once (each par_for waits for its own tasks only).
+class WorkPool {
+ public:
+  static WorkPool &get() {
+    static WorkPool *p = new WorkPool;   // never destroyed: no join at exit
+    return *p;
+  }
+  void ensure(unsigned n) {
+    std::lock_guard<std::mutex> g(mu_);
+    while (workers_ < n) {
+      std::thread([this] { loop(); }).detach();
+      workers_++;
+    }
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  unsigned workers_ = 0;
+};
+
+// f(lo, hi) over [0, n) on nt threads (the calling thread takes the first
+// part, pool workers the others)
 template <typename F>
 void par_for(uint64_t n, unsigned nt, F f) {
   if (nt <= 1 || n < (1u << 10)) { f(0, n); return; }
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < nt; t++) th.emplace_back([=] { f(n * t / nt, n * (t + 1) / nt); });
+  static std::atomic<unsigned> active{0};
+  struct Active {
+    Active() { active++; }
+    ~Active() { active--; }
+  } in_flight;
+  WorkPool &P = WorkPool::get();
+  P.ensure(std::min((nt - 1) * active.load(), 64u));   // enough for every concurrent caller
+  std::mutex mu;
+  std::condition_variable cv;
+  unsigned left = nt - 1;
+  for (unsigned t = 1; t < nt; t++)
+    P.submit([&, t] {
+      f(n * t / nt, n * (t + 1) / nt);
+      std::lock_guard<std::mutex> g(mu);
+      if (--left == 0) cv.notify_one();
+    });
   f(0, n / nt);
-  for (auto &x : th) x.join();
+  std::unique_lock<std::mutex> g(mu);
+  cv.wait(g, [&] { return left == 0; });
 }
 
 unsigned copy_threads(int ndev) {
@@ -183,6 +266,7 @@ hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
   for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += kStage, k++) {
     const int b = (int) (k & 1);
     const uint64_t n = std::min(kStage, len - off);
+    if (k == 1 && (e = ring_ready(c)) != hipSuccess) break;
     if (k >= 2 && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
     char *buf = (char *) c->pin[b];
     std::atomic<bool> ok{true};
@@ -263,7 +347,8 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
                        unsigned nt) {
   const uint64_t CH = kStage / sizeof (GtSmaxRecord);
   const uint64_t nch = (cnt + CH - 1) / CH;
-  hipError_t e = hipSuccess;
+  hipError_t e = nch > 1 ? ring_ready(c) : hipSuccess;
+  if (e != hipSuccess) return e;
   auto issue = [&](uint64_t j) {
     const uint64_t n = std::min(CH, cnt - j * CH);
     hipError_t r = hipMemcpyAsync(c->pin[j & 1], dev + j * CH, sizeof (GtSmaxRecord) * n,
@@ -293,7 +378,8 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
 // threaded copy-out of chunk k)
 hipError_t d2h_bytes(DevCtx *c, void *dst, const void *dev, uint64_t bytes, unsigned nt) {
   const uint64_t nch = (bytes + kStage - 1) / kStage;
-  hipError_t e = hipSuccess;
+  hipError_t e = nch > 1 ? ring_ready(c) : hipSuccess;
+  if (e != hipSuccess) return e;
   auto issue = [&](uint64_t j) {
     const uint64_t n = std::min(kStage, bytes - j * kStage);
     hipError_t r = hipMemcpyAsync(c->pin[j & 1], (const char *) dev + j * kStage, n,
@@ -492,8 +578,10 @@ void device_phase1(Call *C, int d) {
   const int dev = C->devs[d];
   const int s0 = C->first[d], s1 = C->first[d + 1], kmax = C->first[1] - C->first[0];
   void *send = nullptr, *recv = nullptr, *all = nullptr;
+  double tc = smax_phase_clock();
   DCHK(hipSetDevice(dev));
   DCHK(ctx_get(dev, &c));
+  if (d == 0) smax_phase_mark("ctx", &tc);   // stream + pinned ring (first call per device)
   {
     std::lock_guard<std::mutex> g(c->mu);
     double tp = smax_phase_clock();
@@ -503,7 +591,15 @@ void device_phase1(Call *C, int d) {
       // loaded) on a helper thread while this thread stages the tables: a
       // first call otherwise pays ~30 ms of cold allocations in plan creation
       std::thread reserve;
+      struct JoinT {
+        std::thread &t;
+        ~JoinT() { if (t.joinable()) t.join(); }
+      } join_reserve{reserve};
+      DCHK(alloc_table(&S.lcp, S.len));
       {
+        // started after the LCP table's allocation, so that its own cold
+        // allocations (the BWT buffers, the .llv copy, the plan's) queue
+        // behind the upload's first DMA rather than ahead of it
         GtSmaxDevShard g;
         memset(&g, 0, sizeof g);
         g.numllv = S.hi - S.lo;
@@ -514,14 +610,16 @@ void device_phase1(Call *C, int d) {
         g.nonspecials = in->nonspecials;
         g.device = dev;
         reserve = std::thread([g, dev] {
-          if (hipSetDevice(dev) == hipSuccess) (void) smax_plan_reserve(&g, 0);
+          if (hipSetDevice(dev) != hipSuccess) return;
+          const uint64_t ng = GT_SMAX_PK_GROUPS(g.local_len);
+          const size_t sz[3] = {sizeof (uint64_t) * ng, sizeof (uint32_t) * ng,
+                                sizeof (GtSmaxLlv) * (g.numllv + 1)};
+          void *b[3] = {nullptr, nullptr, nullptr};
+          for (int i = 0; i < 3; i++) (void) smax_dev_alloc(&b[i], sz[i]);
+          for (int i = 0; i < 3; i++) smax_dev_free_ex(b[i], false);
+          (void) smax_plan_reserve(&g, 0);
         });
       }
-      struct JoinT {
-        std::thread &t;
-        ~JoinT() { if (t.joinable()) t.join(); }
-      } join_reserve{reserve};
-      DCHK(alloc_table(&S.lcp, S.len));
       const char *lsrc = (const char *) in->lcptab + S.base;
       DCHK(stage_h2d(c, (char *) S.lcp + GT_SMAX_PAD_FRONT, S.len, C->nt,
                      [lsrc](uint64_t off, uint64_t n, char *buf) {
@@ -779,6 +877,7 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
   on_devices(&C, device_phase1);
   if (!C.failed) {
     uint64_t total = 0;
+    double tt = smax_phase_clock();
     for (auto &S : C.sh) { S.offset = total; total += S.count; }
     C.trip = (uint64_t *) malloc(sizeof (uint64_t) * 3 * (total + 1));
     if (C.trip != NULL) {
@@ -791,6 +890,7 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
                            ~(uintptr_t) ((2u << 20) - 1);
       if (a1 > a0) (void) madvise((void *) a0, a1 - a0, MADV_HUGEPAGE);
     }
+    smax_phase_mark("triples_alloc", &tt);
     if (C.trip == NULL) {
       seterr(errbuf, errlen, "out of memory for %lu intervals", (unsigned long) total);
     } else {
@@ -811,6 +911,7 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
     for (auto &m : C.err)
       if (!m.empty()) { seterr(errbuf, errlen, "%s", m.c_str()); break; }
   free(C.trip);
+  double tr = smax_phase_clock();
   for (auto &S : C.sh) {
     if (S.plan) gt_smax_plan_delete(S.plan);
     smax_dev_free(S.lcp);
@@ -818,6 +919,7 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
     smax_dev_free(S.llv);
   }
   if (env_on("GT_SMAX_NO_CACHE")) gt_smax_release_cache();
+  smax_phase_mark("release", &tr);
   return rc;
 }
 

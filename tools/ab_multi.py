@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Diagnostic A/B/C/...: several builds of the library in ONE process on the
+same device tables (the in-tree build first, then each LIB given), plans
+created by each, runs rotated in rounds so that clock and thermal drift hit
+all alike.  Prints per-build median step and K1 time (HIP events) and
+whether each build's records equal the first's.
+
+  ab_multi.py KIND BASES MINLEN SHARD ROUNDS LIB [LIB ...]
+  (SHARD = i/w: plans over one shard's rows of the w-way split; a LIB path's
+  parent directory names the build in the output)"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import genometools_smax_amd as G  # noqa: E402
+
+kind, bases, minlen = sys.argv[1], int(float(sys.argv[2])), int(sys.argv[3])
+si, sw = (int(x) for x in sys.argv[4].split("/"))
+rounds = int(sys.argv[5])
+paths = [G.LIB_PATH] + sys.argv[6:]
+names = ["in-tree"] + [os.path.basename(os.path.dirname(p)) for p in sys.argv[6:]]
+libs = []
+for p in paths:
+    G._lib, G.LIB_PATH = None, p
+    libs.append(G.lib())
+G._lib, G.LIB_PATH = libs[0], paths[0]
+
+text = G.synth_genome(kind, bases, {"uniform": 42, "human": 1, "plant": 2}[kind])
+esa = G.DeviceEsa(text) if len(text) + 1 < 2 ** 32 else G.DeviceEsa64(text)
+del text
+N = esa.nonspecials
+begin, end = 1 + (N - 1) * si // sw, 1 + (N - 1) * (si + 1) // sw
+print("rows [%d, %d) (shard %d/%d), builds: %s" % (begin, end, si, sw, ", ".join(names)), flush=True)
+plans = []
+for L in libs:
+    G._lib = L
+    plans.append(esa.plan(minlen, begin, end))
+G._lib = libs[0]
+s = torch.cuda.current_stream()
+sp = s.cuda_stream
+step = {n: [] for n in names}
+k1 = {n: [] for n in names}
+
+
+def timed(L, p, n=30):
+    for _ in range(3):
+        L.gt_smax_plan_run(p.plan, sp)
+    L.gt_smax_plan_timing(p.plan, n)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(n):
+        L.gt_smax_plan_run(p.plan, sp)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms, k = ctypes.c_double(), ctypes.c_int()
+    L.gt_smax_plan_timing_read(p.plan, ctypes.byref(ms), ctypes.byref(k))
+    return e0.elapsed_time(e1) / n, ms.value / max(k.value, 1)
+
+
+m = len(libs)
+for r in range(rounds):
+    order = [(r + j) % m for j in range(m)]          # rotate who goes first
+    line = []
+    for j in order:
+        a, b = timed(libs[j], plans[j])
+        step[names[j]].append(a)
+        k1[names[j]].append(b)
+        line.append("%s %.4f" % (names[j], a))
+    print("round %d: %s" % (r, "  ".join(line)), flush=True)
+
+
+def med(x):
+    x = sorted(x)
+    return x[len(x) // 2]
+
+
+base = med(step[names[0]])
+for j, n in enumerate(names):
+    print("median %-12s step %.4f ms (x%.4f of %s)  K1 %.4f ms  rest %.4f ms"
+          % (n, med(step[n]), med(step[n]) / base, names[0], med(k1[n]), med(step[n]) - med(k1[n])),
+          flush=True)
+G._lib = libs[0]
+want = plans[0].fetch_triples()
+for j in range(1, m):
+    G._lib = libs[j]
+    got = plans[j].fetch_triples()
+    print("records %s == %s: %s (%d / %d)" % (names[j], names[0], bool((got == want).all())
+                                              if got.shape == want.shape else False, len(got), len(want)),
+          flush=True)
+for j, p in enumerate(plans):
+    G._lib = libs[j]
+    p.close()
+G._lib = libs[0]
+esa.release()

@@ -21,6 +21,7 @@
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
 #   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
 #   tilestats:CONFIG tools/tile_stats.py (active segments and records per K1 tile)
+#   abm:KIND:BASES:MINLEN:SHARD:LIB,... the in-tree library and several others, one process
 #   ab:LIB:KIND:BASES:MINLEN:SHARD   A/B of the in-tree library against LIB
 #                    (tools/ab_interleave.py, 8 interleaved rounds)
 #
@@ -86,6 +87,12 @@ for S in "$@"; do
       IFS=: read -r _ LIBB KIND BASES MINLEN SHARD <<< "$S"
       timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" "$LIBB" 8 "$SHARD" \
         > "$O/ab_${KIND}_${SHARD//\//of}_vs_$(basename "$(dirname "$LIBB")").txt" 2>&1 ;;
+    abm:*)
+      # abm:KIND:BASES:MINLEN:SHARD:LIB[,LIB...] -- tools/ab_multi.py, the in-tree
+      # library and each LIB in one process, rotated rounds
+      IFS=: read -r _ KIND BASES MINLEN SHARD LIBS <<< "$S"
+      timeout -k 10 600 python -u tools/ab_multi.py "$KIND" "$BASES" "$MINLEN" "$SHARD" 8 ${LIBS//,/ } \
+        > "$O/abm_${KIND}_${SHARD//\//of}.txt" 2>&1 ;;
     ablate:*)
       # ablate:V1,V2,...  K1 time under GT_SMAX_DEBUG ablation bits at C3 (diag build)
       timeout -k 10 600 python -u tools/k1_ablate.py human 3e9 "${S#ablate:}" > "$O/ablate.txt" 2>&1 ;;
