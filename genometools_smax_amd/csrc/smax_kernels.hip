@@ -65,25 +65,16 @@
 #include "gt_smax_hip.h"
 #include "smax_internal.h"
 
-// K1 build switch (A/B): SMAX_SINFO -- the tiles' llv_win words by scalar
-// loads a tile ahead (instead of LDS-DMA into a ring slot + LDS read)
-#ifndef SMAX_SINFO
-#define SMAX_SINFO 0
-#endif
-// SMAX_PRIO (A/B): wave priority raised while a wave works on a landed window
-// (s_setprio), lowered before it waits for the next
-#ifndef SMAX_PRIO
-#define SMAX_PRIO 0
-#endif
-#if SMAX_SINFO
-#define SMAX_ASM_INFO ""
-#else
+// per-chunk 255-byte ranks: K1 windows stage at most SMAX_LLV_CAP (< 256)
+// .llv entries (more: the tile is static, K1b), so a byte holds every rank
+typedef uint8_t SmaxRank;
+// the next-but-one tile's llv_win words into their LDS ring slot (lanes 0-1),
+// part of every window DMA
 #define SMAX_ASM_INFO                        \
   "s_mov_b64 exec, %13\n\t"                 \
   "s_mov_b32 m0, %7\n\t"                    \
   "s_nop 0\n\t"                             \
   "global_load_lds_dword %3, %12 offset:0\n\t"
-#endif
 #define SMAX_THREADS 256                              // 4 waves per K1b / K2 / K3 workgroup
 // K1 workgroup: ONE wave.  K1's waves share nothing (no barrier, each its own
 // LDS windows), so a one-wave workgroup frees its LDS and wave slot as soon
@@ -298,7 +289,7 @@ struct Win {
   const LDSP uint8_t *B;      // BWT bytes of the window (byte kernel), or
   const LDSP uint64_t *P;     // packed BWT of the window, 16 rows per word
   bool p2;                    // P holds u32 words (code planes only, no specials)
-  const LDSP uint16_t *rank;  // per 16-byte chunk: 255 bytes before it
+  const LDSP SmaxRank *rank;  // per 16-byte chunk: 255 bytes before it
   const LDSP uint32_t *val;   // LDS .llv values in rank order (nval of them), or
   const LDSP uint16_t *val16; // the same as u16 (K1 windows: values < 65536)
   int nval;                   // -1: values not staged (read global by rank)
@@ -564,8 +555,18 @@ struct SmaxWindowPk {          // packed BWT (DNA): 0.5 B per row
   uint64_t P[SMAX_LDSB / 16 + 2];   // + 2: the tail DMA moves 2 lanes x 16 B
   uint16_t val16[SMAX_LLV_CAP];
 };
-// window_scratch: 64 staged records + 2 x 64 results in the BWT region
-static_assert(sizeof(((SmaxWindowPk *) 0)->P) >= 64 * 8 + 2 * 64 * 4, "packed window scratch");
+// window_scratch: the 64 staged records in the BWT region
+static_assert(sizeof(((SmaxWindowPk *) 0)->P) >= 64 * 8, "packed window scratch");
+// 2-plane window (the 6-wave K1: 6,816 B of LDS per one-wave workgroup, 24
+// per CU, at most 80 VGPRs): groups l0/16 .. l0/16+131 as u32 (the 33-lane
+// DMA); once the BWT is dead, the tile's 64 staged records
+struct SmaxWindowB2 {
+  uint8_t L[SMAX_LDSB];
+  uint64_t P[(SMAX_LDSB / 16 + 2) / 2];   // 132 u32 = 528 B
+  uint16_t val16[SMAX_LLV_CAP];
+};
+static_assert(sizeof(((SmaxWindowB2 *) 0)->P) >= 64 * 8, "2-plane window scratch");
+static_assert(sizeof(SmaxWindowB2) == 3088, "6-wave LDS budget");
 static_assert(SMAX_LDSB >= 64 * 8 + 2 * 64 * 4, "byte window scratch");
 
 // Issue the DMA of tile `l0` (local index) into the calling wave's window
@@ -631,12 +632,12 @@ __device__ __forceinline__ const T *uni_ptr(const T *p) {
   return reinterpret_cast<const T *>(((uint64_t) hi << 32) | lo);
 }
 
-template <bool NT, bool BW2 = false>
+template <bool NT, bool BW2 = false, typename WinT = SmaxWindowPk>
 __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
                                                 uint32_t lo, uint32_t n, const void *ibase,
                                                 uint32_t iaddr, uint32_t v16, uint32_t v4) {
-  const uint32_t wp = wl + (uint32_t) offsetof(SmaxWindowPk, P);
-  const uint32_t wv = wl + (uint32_t) offsetof(SmaxWindowPk, val16);
+  const uint32_t wp = wl + (uint32_t) offsetof(WinT, P);
+  const uint32_t wv = wl + (uint32_t) offsetof(WinT, val16);
   const uint8_t *vb = uni_ptr(reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u)));
   const uint32_t nl8 = n == 0 ? 0u : (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
   const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;   // < 64
@@ -962,7 +963,7 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
 // of >= 2 rows (LCP[c+1] == LCP[c]) -- are queued ("L" rows) and evaluated
 // exactly, 64 at a time (eval_start).  Records are then written in row
 // order by their owning lanes.
-#define SMAX_DLIST 64                                 // queued exact starts per tile
+#define SMAX_DLIST 56                                 // queued exact starts per tile
 
 
 // high bit of each byte >= 254 (WILDCARD / SEPARATOR / UNDEFBWTCHAR)
@@ -1216,13 +1217,16 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
   const bool all_exact = a.minlen > 128;
-  // the exact starts' results and the staged records live in the window's
-  // BWT region, dead once the starts are evaluated (nothing after reads
-  // BWT symbols); the next DMA into this window is issued after the records
-  // have moved to registers (smax_scan_body)
-  uint32_t *res_lcp = reinterpret_cast<uint32_t *>(stg + SMAX_SSLOT), *res_w = res_lcp + DL;
+  // the staged records live in the window's BWT region, dead once the
+  // starts are evaluated (nothing after reads BWT symbols); the next DMA
+  // into this window is issued after the records have moved to registers
+  // (smax_scan_body)
+  // results packed into the queue entries (every lane has read its own
+  // entry before any result is written): LCP value (16 bits) | width << 16;
+  // a larger value or width sends the tile to K1b
+  uint32_t *res = ent;
   // accepted exact starts, one 16-bit row mask per compacted segment
-  uint32_t *accw = ent + DL + 2 * 64 / 4;
+  uint32_t *accw = ent + DL;
   // compact the active segments (id = round * 64 + lane, row order): the
   // k-th active segment goes to step k / 64, lane k % 64.  Two forward
   // permutes (ds_permute_b32: no LDS memory, one round trip) instead of an
@@ -1250,7 +1254,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   // 255-byte ranks: the left halo's count, then a prefix over the compacted
   // segments in row order (an inactive segment holds no byte >= 128)
   uint32_t fbase = 0;
-  LDSP uint16_t *rank = const_cast<LDSP uint16_t *>(t.rank);
+  LDSP SmaxRank *rank = const_cast<LDSP SmaxRank *>(t.rank);
   // dense variant: the rank relation masks in the accepted-mask scratch
   // (free until the exact evaluation), built at the first step that needs
   // them (ffp_masks)
@@ -1273,7 +1277,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     if (rank != nullptr) {
       uint32_t ftot;
       crank = fbase + wave_excl((uint32_t) __popc(rel.FF), &ftot);
-      if (i < nseg) rank[(SMAX_LH + ro) >> 4] = (uint16_t) crank;
+      if (i < nseg) rank[(SMAX_LH + ro) >> 4] = (SmaxRank) crank;
       fbase += ftot;
     }
     if constexpr (FFPV) {
@@ -1305,7 +1309,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   }
   if (rank != nullptr && lane == 0) {   // halo chunks (ranks of rows the slow paths may read)
     rank[0] = 0;
-    rank[1 + SMAX_TILE / 16] = (uint16_t) fbase;
+    rank[1 + SMAX_TILE / 16] = (SmaxRank) fbase;
   }
   SMAX_STAMP(st, 3);
   if (nL > DL) return UINT32_MAX;
@@ -1333,8 +1337,8 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (i < nL) {
-      res_lcp[i] = cur;
-      res_w[i] = width;
+      res[i] = cur | (width << 16);
+      wide = wide || (cur | width) >= 65536u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1370,8 +1374,9 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         width = 2 + ((W3 >> q) & 1u);
       } else {
         const uint32_t i = Lpre + (uint32_t) __popc(Lq & ((1u << q) - 1));
-        lcp = res_lcp[i];
-        width = res_w[i];
+        const uint32_t rw = res[i];
+        lcp = rw & 0xffffu;
+        width = rw >> 16;
       }
       if (!(a.dbg & (4096u | (1u << 21))))
         stg[min(pos, (uint32_t) SMAX_SSLOT - 1u)] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
@@ -1391,6 +1396,13 @@ __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, S
   issue_window_pk<NT, BW2>(a, l0, wl, lo, n, info, iaddr, v16, v4);
 }
 template <bool NT, bool BW2 = false>
+__device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowB2 *w,
+                                           uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
+                                           uint32_t iaddr, uint32_t v16, uint32_t v4) {
+  static_assert(BW2, "SmaxWindowB2 holds the 2-plane form only");
+  issue_window_pk<NT, BW2, SmaxWindowB2>(a, l0, wl, lo, n, info, iaddr, v16, v4);
+}
+template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
                                            uint32_t iaddr, uint32_t v16, uint32_t v4) {
@@ -1400,16 +1412,17 @@ __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, S
 
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindow *W) { t.B = to_lds<uint8_t>(W->B); t.P = nullptr; }
 __device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowPk *W) { t.P = to_lds<uint64_t>(W->P); t.B = nullptr; }
+__device__ __forceinline__ void set_bwt_window(Win &t, SmaxWindowB2 *W) { t.P = to_lds<uint64_t>(W->P); t.B = nullptr; }
 
 // A window's BWT region once the tile's exact starts are evaluated: the
-// staged records (SMAX_SSLOT u64) and the starts' results (2 x SMAX_DLIST
-// u32); nothing of the tile reads BWT symbols after that point, and the
-// wave's next DMA into this window follows the move of the records to
-// registers.  Keeps K1 inside 32 KiB of LDS per workgroup (5 per CU).
+// staged records (SMAX_SSLOT u64); nothing of the tile reads BWT symbols
+// after that point, and the wave's next DMA into this window follows the
+// move of the records to registers.
 __device__ __forceinline__ uint64_t *window_scratch(SmaxWindow *W) {
   return reinterpret_cast<uint64_t *>(W->B);
 }
 __device__ __forceinline__ uint64_t *window_scratch(SmaxWindowPk *W) { return W->P; }
+__device__ __forceinline__ uint64_t *window_scratch(SmaxWindowB2 *W) { return W->P; }
 
 // Filter of a landed window (one wave): per-lane segment "any byte >=
 // min(minlen,128)" bits; the .llv values are staged with the window, their
@@ -1433,7 +1446,7 @@ __device__ __forceinline__ bool seg_can_start(const Win &t, const uint4 v, uint3
   return (ff & 0x80808080u) != 0 || (pack16(g) & d2) != 0;
 }
 
-__device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, uint16_t *rank,
+__device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a, SmaxRank *rank,
                                                    uint32_t wlo, uint32_t wn) {
   const int lane = threadIdx.x & 63;
   const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
@@ -1454,7 +1467,7 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   t.llv_base = wlo;
   // no .llv entry in the window: no 255 byte (in a consistent index; a
   // stray 255 still resolves exactly through the global .llv search)
-  t.rank = wn == 0 ? nullptr : to_lds<uint16_t>(rank);
+  t.rank = wn == 0 ? nullptr : to_lds<SmaxRank>(rank);
   t.nval = -1;
   if (wn != 0) {
     const uint32_t cap = SMAX_LLV_CAP - (wlo & 7u);   // staged from the 8-aligned index below wlo
@@ -1490,12 +1503,11 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // no workgroup barrier anywhere in K1
   __shared__ __attribute__((aligned(16))) WinT sWin[SMAX_K1_THREADS / 64][2];
   __shared__ __attribute__((aligned(16))) uint32_t sInfo[SMAX_K1_THREADS / 64][2][2];
-  __shared__ uint16_t sRank[SMAX_K1_THREADS / 64][SMAX_NCHUNK];
-  // per wave: wave_detect_direct's queue of exact starts, compacted segment
-  // ids and accepted masks (the starts' results and the tile's staged
-  // records go to the current window's BWT region once it is dead:
-  // window_scratch)
-  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_DLIST + 2 * 64 / 4 + 64];
+  __shared__ SmaxRank sRank[SMAX_K1_THREADS / 64][SMAX_NCHUNK];
+  // per wave: wave_detect_direct's queue of exact starts (then their
+  // packed results) and accepted masks (the tile's staged records go to
+  // the current window's BWT region once it is dead: window_scratch)
+  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_DLIST + 64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1513,25 +1525,13 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   Win t;
   win_init(t, a);
   t.staged_all = true;   // non-static tiles: all window values staged
-  uint16_t *rank = sRank[wave];
+  SmaxRank *rank = sRank[wave];
 
   // prologue: .llv windows of the first two tiles, then the first window
   const uint32_t wbase = __builtin_amdgcn_readfirstlane(lds_addr(&sWin[wave][0]));
   const uint32_t info0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
   const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
-#if SMAX_SINFO
-  // llv_win words by scalar loads (K1 never writes them: constant address
-  // space), the next tile's a whole tile ahead of its use
-  typedef const __attribute__((address_space(4))) uint64_t *CInfo;   // {lo, count word}
-  const CInfo cwin = (CInfo) a.llv_win;
-  uint64_t inf_cur = cwin[tile];
-  uint64_t inf_nxt = cwin[tile + stride <= last ? tile + stride : last];
-  issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase,
-                      (uint32_t) inf_cur, SMAX_WIN_N((uint32_t) (inf_cur >> 32)), a.llv_win, info1,
-                      v16, v4);
-  (void) info0;
-#else
   if (lane < 2) {
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + (tile + stride <= last ? tile + stride
@@ -1545,7 +1545,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
                       __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
                       SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])),
                       a.llv_win + (tile + stride <= last ? tile + stride : last), info1, v16, v4);
-#endif
   // the previous tile's records (lane r holds record r) and count: stored
   // one iteration late, right after the window wait, so that those stores
   // (and the block-sum atomic) have a whole tile of work to complete before
@@ -1577,22 +1576,15 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
-    if (SMAX_PRIO) __builtin_amdgcn_s_setprio(SMAX_PRIO);
     if constexpr (DIAG) SMAX_STAMP(st, 0);
     if (ptile != ~0u) {
       smax_flush_tile(a, ptile, prec, pcnt);
       ptile = ~0u;
     }
-#if SMAX_SINFO
-    const uint32_t wlo = (uint32_t) inf_cur, wnf = (uint32_t) (inf_cur >> 32), wn = SMAX_WIN_N(wnf);
-    const uint32_t nlo = (uint32_t) inf_nxt, nn = SMAX_WIN_N((uint32_t) (inf_nxt >> 32));
-#else
     // .llv windows of this tile and the next {lo, packed count word}: one
     // 16-byte LDS read
     // (wave-uniform: to scalars first, then scalar selects)
     const uint4 info = *reinterpret_cast<const uint4 *>(&sInfo[wave][0][0]);
-#endif
-#if !SMAX_SINFO
     const uint32_t ix = __builtin_amdgcn_readfirstlane(info.x);
     const uint32_t iy = __builtin_amdgcn_readfirstlane(info.y);
     const uint32_t iz = __builtin_amdgcn_readfirstlane(info.z);
@@ -1602,7 +1594,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const uint32_t wn = SMAX_WIN_N(wnf);
     const uint32_t nlo = cur ? ix : iz;
     const uint32_t nn = SMAX_WIN_N(cur ? iy : iw);
-#endif
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
@@ -1612,10 +1603,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
-#if SMAX_SINFO
-      inf_cur = inf_nxt;
-      inf_nxt = cwin[n2];      // used one tile later
-#endif
     }
 
     if constexpr (DIAG) SMAX_STAMP(st, 1);
@@ -1676,7 +1663,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       if (st != nullptr) st->acc[7]++;
     }
 
-    if (SMAX_PRIO) __builtin_amdgcn_s_setprio(0);
     tile = next;
     if (tile >= a.num_tiles) break;
   }
@@ -2170,13 +2156,14 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
 // K1 instantiations, selected by the plan (plan_run_scan):
 //   smax_scan_kernel_b2[_dense][_nt]  2-plane BWT window stream (0.25 B/row of
 //       BWT; windows with a special BWT row go to the static K1b list), the
-//       production kernels; _dense: the 255-after-255 relations of a segment
+//       production kernels, 6 waves/SIMD (SmaxWindowB2; against 5 with the
+//       packed window: C3 step -2.6 %, 3/8 shard -2.1 %, profiles/r04g/); _dense: the 255-after-255 relations of a segment
 //       resolved vectorised (ffp_resolve), chosen above SMAX_FFPV_DENSITY .llv
 //       entries per row (C5, the 12 Gbp plant genome at 0.94 %: step 6.21 ->
 //       5.72 ms; C3 at 0.39 %: 1.7 % slower with it); _nt: non-temporal
 //       window loads (GtSmaxPlan::nt: 8- and 4-way shards of C3)
 //   smax_scan_kernel[_dense]  the u64 packed groups (0.5 B/row of BWT,
-//       specials included): shards where special BWT rows would send more
+//       specials included; 5 waves/SIMD): shards where special BWT rows would send more
 //       than 1/256 of the windows to K1b (read sets)
 //   smax_scan_kernel_diag     the 2-plane kernel with the GT_SMAX_DEBUG
 //       ablation switches and GT_SMAX_STAMPS section stamps (diagnostics only)
@@ -2187,20 +2174,20 @@ __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel(SmaxScanA
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_dense(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowPk, false, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, false, false, false, true>(a);
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_b2(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowB2, false, false, false, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_dense(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, false, true, false, true>(a);
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_b2_dense(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowB2, false, true, false, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_nt(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, false, false, true, true>(a);
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_b2_nt(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowB2, false, false, true, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_b2_dense_nt(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, false, true, true, true>(a);
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_b2_dense_nt(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowB2, false, true, true, true>(a);
 }
-__global__ void __launch_bounds__(SMAX_K1_THREADS, 5) smax_scan_kernel_diag(SmaxScanArgs a) {
-  smax_scan_body<SmaxWindowPk, true, false, false, true>(a);
+__global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_diag(SmaxScanArgs a) {
+  smax_scan_body<SmaxWindowB2, true, false, false, true>(a);
 }
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
   smax_scan_body<SmaxWindow, false>(a);
