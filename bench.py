@@ -131,12 +131,12 @@ def cold_e2e(G, host, n, N, minlen, want, log, calls=2):
         if not ok:
             log("FAIL: cold end-to-end result (%d intervals) differs from the CPU oracle (%d)"
                 % (len(got), len(want)))
-        phases, call = [], -1
+        phases, phases2, call = [], [], -1
         for ln in r.stderr.splitlines():
             if ln.startswith("[gt_smax call]"):
                 call = int(ln.split("]", 1)[1])
-            elif ln.startswith("[gt_smax timing]") and call == 0:
-                phases.append(" ".join(ln.split("]", 1)[1].split()))
+            elif ln.startswith("[gt_smax timing]") and call in (0, 1):
+                (phases if call == 0 else phases2).append(" ".join(ln.split("]", 1)[1].split()))
         t = res["calls_s"]
         log("cold end-to-end: HIP init %.3fs, calls %s s" % (res["hip_init_s"], t))
         return {"parity_ok": ok, "value": N / t[0], "unit": "suffix-positions/s",
@@ -145,7 +145,8 @@ def cold_e2e(G, host, n, N, minlen, want, log, calls=2):
                 "process": "fresh process (bin/gt-smax-e2e, C, links libgtsmax_hip.so only): "
                            "first gt_smax_hip_enumerate_to_buffer call; the HIP runtime's "
                            "initialisation (gt_smax_device_count before it) is hip_init_s",
-                "phases_first_call": phases or None}
+                "phases_first_call": phases or None,
+                "phases_second_call": phases2 or None}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

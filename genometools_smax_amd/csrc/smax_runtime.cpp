@@ -124,20 +124,38 @@ uint64_t stage_bytes() {
 }
 #define kStage stage_bytes()
 
+// pinned chunks in the H2D ring: 2, GT_SMAX_RING (2..4) overrides
+constexpr int kRingMax = 4;
+int ring_depth() {
+  static const int r = [] {
+    const char *v = getenv("GT_SMAX_RING");
+    const long d = v ? strtol(v, NULL, 0) : 2;
+    return (int) (d < 2 ? 2 : d > kRingMax ? kRingMax : d);
+  }();
+  return r;
+}
+
 struct DevCtx {
   int device = -1;
   std::mutex mu;                 // one call at a time uses the ring
   hipStream_t stream = nullptr;
-  void *pin[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  // the ring's second chunk is pinned on a helper thread while the first
-  // chunk's fill and DMA run (a first call pays the page pinning of one
-  // chunk before its first DMA, not two); ring_ready waits for it
-  std::shared_future<hipError_t> pin1;
+  void *pin[kRingMax] = {};
+  hipEvent_t ev[kRingMax] = {};
+  // the ring's other chunks are pinned one after another on a helper thread
+  // while the first chunk's fill and DMA run (a first call pays the page
+  // pinning of one chunk before its first DMA, not all); chunk_ready(c, i)
+  // waits for chunk i, ring_ready for all of them
+  std::promise<hipError_t> pinned[kRingMax];
+  std::shared_future<hipError_t> pin_done[kRingMax];
 };
 
+hipError_t chunk_ready(DevCtx *c, int i) {
+  return c->pin_done[i].valid() ? c->pin_done[i].get() : hipSuccess;
+}
 hipError_t ring_ready(DevCtx *c) {
-  return c->pin1.valid() ? c->pin1.get() : hipSuccess;
+  hipError_t e = hipSuccess;
+  for (int i = 1; i < ring_depth() && e == hipSuccess; i++) e = chunk_ready(c, i);
+  return e;
 }
 
 std::mutex g_ctx_mu;
@@ -151,15 +169,21 @@ hipError_t ctx_get(int device, DevCtx **out) {
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
+    e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
-  if (e == hipSuccess)
-    c->pin1 = std::async(std::launch::async, [c, device] {
-                hipError_t r = hipSetDevice(device);
-                return r == hipSuccess ? hipHostMalloc(&c->pin[1], kStage, hipHostMallocDefault) : r;
-              }).share();
+  if (e == hipSuccess) {
+    for (int i = 1; i < ring_depth(); i++) c->pin_done[i] = c->pinned[i].get_future().share();
+    std::thread([c, device] {
+      hipError_t r = hipSetDevice(device);
+      for (int i = 1; i < ring_depth(); i++) {
+        if (r == hipSuccess) r = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
+        c->pinned[i].set_value(r);
+      }
+    }).detach();
+  }
   if (e != hipSuccess) {
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < kRingMax; i++) {
       if (c->pin[i]) (void) hipHostFree(c->pin[i]);
       if (c->ev[i]) (void) hipEventDestroy(c->ev[i]);
     }
@@ -255,19 +279,20 @@ unsigned copy_threads(int ndev) {
   return std::min(per, 16u);
 }
 
-// Host -> device through the context's two pinned chunks: fill(off, n, buf)
-// writes destination bytes [off, off+n) into buf (on nt threads) while the
-// DMA engine drains the other chunk.  fill returns false to abort (*aborted).
+// Host -> device through the context's ring of pinned chunks: fill(off, n,
+// buf) writes destination bytes [off, off+n) into buf (on nt threads) while
+// the DMA engine drains the others.  fill returns false to abort (*aborted).
 template <typename Fill>
 hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
                      bool *aborted) {
   hipError_t e = hipSuccess;
   if (aborted) *aborted = false;
+  const uint64_t R = (uint64_t) ring_depth();
   for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += kStage, k++) {
-    const int b = (int) (k & 1);
+    const int b = (int) (k % R);
     const uint64_t n = std::min(kStage, len - off);
-    if (k == 1 && (e = ring_ready(c)) != hipSuccess) break;
-    if (k >= 2 && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
+    if (k >= 1 && k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
+    if (k >= R && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
     char *buf = (char *) c->pin[b];
     std::atomic<bool> ok{true};
     // split at 64-byte units (whole packed groups for the BWT fill)
@@ -584,7 +609,7 @@ void device_phase1(Call *C, int d) {
   if (d == 0) smax_phase_mark("ctx", &tc);   // stream + pinned ring (first call per device)
   {
     std::lock_guard<std::mutex> g(c->mu);
-    double tp = smax_phase_clock();
+    double tp = smax_phase_clock(), th = tp;   // th: the upload's parts
     for (int s = s0; s < s1; s++) {
       Shard &S = C->sh[s];
       // the plan's buffers into the device cache (and the code object
@@ -626,6 +651,7 @@ void device_phase1(Call *C, int d) {
                        memcpy(buf, lsrc + off, n);
                        return true;
                      }, nullptr));
+      if (d == 0) smax_phase_mark(" h2d.lcp", &th);
       // BWT: bit planes packed during the fill; a non-DNA alphabet aborts
       // the packed upload and stages the bytes instead
       const uint64_t ng = GT_SMAX_PK_GROUPS(S.len);
@@ -673,6 +699,7 @@ void device_phase1(Call *C, int d) {
                        }, nullptr));
         S.sh.bwt_dev = (const uint8_t *) S.bwt + GT_SMAX_PAD_FRONT;
       }
+      if (d == 0) smax_phase_mark(" h2d.bwt", &th);
       DCHK(smax_dev_alloc(&S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo + 1)));
       if (S.hi > S.lo) {
         const char *vsrc = (const char *) (in->llvtab + S.lo);

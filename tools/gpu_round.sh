@@ -14,8 +14,10 @@
 #   sq2:CONFIG       K1 SQ active-per-pipe / waitcnt counters -> sq2_CONFIG.json
 #   prof:CONFIG      rocprofv3 --kernel-trace --stats of a bench run
 #                    -> kernel_stats_CONFIG.csv + the bench line under it
+#   timeline:SHARD   kernel trace of repeated C3 shard steps -> per-kernel durations and gaps
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
 #   e2ecold:CONFIG   tools/e2e_cold.py: first drop-in call of a fresh process (+ phases)
+#   e2esweep:CONFIG:K=V,..;..  e2ecold per runtime setting (fresh process each)
 #   mp:KIND          tools/bench_maxpairs.py (F2/F3, 100 Mbp of KIND, minlen 20)
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
@@ -142,6 +144,21 @@ for S in "$@"; do
       # cold end-to-end: first call of the drop-in entry point in a fresh process
       timeout -k 10 900 python -u tools/e2e_cold.py "${S#e2ecold:}" 3 > "$O/e2e_cold_${S#e2ecold:}.json" \
         2> "$O/e2e_cold_${S#e2ecold:}.err" ;;
+    timeline:*)
+      # timeline:SHARD -- kernel trace (CSV) of repeated plan steps of one C3
+      # shard: per-kernel durations and the gaps between them
+      SH=${S#timeline:}
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv \
+        -d "$O/tl_${SH//\//of}" -o p -- python3 "$R/tools/ab_multi.py" human 3e9 20 "$SH" 2 \
+        > "$O/tl_${SH//\//of}.log" 2>&1)
+      python3 tools/step_timeline.py "$O/tl_${SH//\//of}" > "$O/timeline_${SH//\//of}.txt"
+      rm -rf "$O/tl_${SH//\//of}" ;;
+    e2esweep:*)
+      # e2esweep:CONFIG:K=V,..;K=V,.. -- first/second call per runtime setting
+      IFS=: read -r _ C SETS <<< "$S"
+      IFS=';' read -r -a SA <<< "$SETS"
+      timeout -k 10 1000 python -u tools/e2e_cold.py "$C" 2 "${SA[@]}" > "$O/e2e_sweep_$C.json" \
+        2> "$O/e2e_sweep_$C.err" ;;
     shards:*)
       W=${S#shards:}
       timeout -k 10 600 python -u tools/shard_step.py human 3e9 20 "$W" > "$O/shards_$W.txt" 2>&1 ;;
