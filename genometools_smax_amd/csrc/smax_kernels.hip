@@ -2271,21 +2271,26 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
   // (a separate one-workgroup prefix kernel over the block sums instead
   // measured 0.5 % longer at C3 and 2 % longer on an 8-way shard: the extra
   // launch costs more than these loads, profiles/r03j_k2b_ab.txt)
+  // this block's counts: loaded first, in flight beside the block-sum loads
+  // (independent of them)
+  const uint32_t cw = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
   uint64_t bs = 0;
   {
     // two-level prefix (K1b's launch also sums superblocks of SMAX_SBB
     // blocks): the earlier superblocks, then the earlier blocks of this
     // one -- a flat loop over every earlier block costs O(blocks^2) loads
     // over the launch (22.7 k blocks at C5: up to 89 per thread)
+    // (both levels' loads issued before either is summed: one round trip)
     const uint32_t sb = blk / SMAX_SBB;
-    for (uint32_t k = tid; k < sb; k += 256) bs += block_sum[nblocks + k];
     const uint32_t b = sb * SMAX_SBB + tid;
-    if (tid < SMAX_SBB && b < blk) bs += block_sum[b];
+    const uint32_t x0 = (uint32_t) tid < sb ? block_sum[nblocks + tid] : 0u;
+    const uint32_t x1 = tid < SMAX_SBB && b < blk ? block_sum[b] : 0u;
+    for (uint32_t k = tid + 256; k < sb; k += 256) bs += block_sum[nblocks + k];   // > 256 superblocks
+    bs += (uint64_t) x0 + x1;
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) bs += __shfl_xor(bs, d, 64);
   if (lane == 0) sRed[wave] = bs;
-  const uint32_t cw = s0 + tid < nslots ? slot_count[s0 + tid] : 0u;
   const uint32_t c = cw & ~SMAX_SLOT_WIDE;
   sWide[tid] = (cw & SMAX_SLOT_WIDE) ? 1 : 0;
   uint32_t incl = c;

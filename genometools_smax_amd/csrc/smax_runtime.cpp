@@ -77,6 +77,10 @@ bool env_on(const char *name) {
   const char *v = getenv(name);
   return v != NULL && *v && strcmp(v, "0") != 0;
 }
+bool env_off(const char *name) {
+  const char *v = getenv(name);
+  return v != NULL && strcmp(v, "0") == 0;
+}
 
 // ------------------------------------------------------------ device cache
 
@@ -168,11 +172,10 @@ hipError_t ctx_get(int device, DevCtx **out) {
   DevCtx *c = new DevCtx;
   c->device = device;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-  for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
-    e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
-  if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
   if (e == hipSuccess) {
+    // the ring's other chunks are pinned on a helper thread from the start,
+    // beside this thread's stream creation and first chunk (a first call
+    // otherwise waits ~14 ms for the second chunk after its first DMA)
     for (int i = 1; i < ring_depth(); i++) c->pin_done[i] = c->pinned[i].get_future().share();
     std::thread([c, device] {
       hipError_t r = hipSetDevice(device);
@@ -182,7 +185,12 @@ hipError_t ctx_get(int device, DevCtx **out) {
       }
     }).detach();
   }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
+    e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
   if (e != hipSuccess) {
+    (void) ring_ready(c);   // the helper may still write pin[1..]
     for (int i = 0; i < kRingMax; i++) {
       if (c->pin[i]) (void) hipHostFree(c->pin[i]);
       if (c->ev[i]) (void) hipEventDestroy(c->ev[i]);
@@ -634,6 +642,7 @@ void device_phase1(Call *C, int d) {
         g.end = S.end;
         g.nonspecials = in->nonspecials;
         g.device = dev;
+        if (!env_off("GT_SMAX_RESERVE"))   // diagnostic: GT_SMAX_RESERVE=0 skips it
         reserve = std::thread([g, dev] {
           if (hipSetDevice(dev) != hipSuccess) return;
           const uint64_t ng = GT_SMAX_PK_GROUPS(g.local_len);
@@ -723,7 +732,7 @@ void device_phase1(Call *C, int d) {
         fail_dev(C, d, C->valid_msg);
         goto out;
       }
-      reserve.join();
+      if (reserve.joinable()) reserve.join();
       if (gt_smax_plan_create(&S.plan, &S.sh, C->minlen, 0, eb, sizeof eb)) {
         fail_dev(C, d, eb);
         goto out;

@@ -49,6 +49,9 @@ if len(settings) == 1:
 else:
     print(json.dumps(out, indent=1))
     for k, r in out.items():
+        if not r or "seconds" not in r:
+            print("%-34s failed" % k, file=sys.stderr)
+            continue
         h2d = lambda ph: " ".join(x for x in (ph or []) if x.split()[0].startswith("h2d")) or "-"
         print("%-34s first %.4f s  second %s s  h2d %s / %s" %
               (k, r["seconds"], r["second_call_s"], h2d(r["phases_first_call"]),
