@@ -77,10 +77,6 @@ bool env_on(const char *name) {
   const char *v = getenv(name);
   return v != NULL && *v && strcmp(v, "0") != 0;
 }
-bool env_off(const char *name) {
-  const char *v = getenv(name);
-  return v != NULL && strcmp(v, "0") == 0;
-}
 
 // ------------------------------------------------------------ device cache
 
@@ -145,10 +141,10 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   void *pin[kRingMax] = {};
   hipEvent_t ev[kRingMax] = {};
-  // the ring's other chunks are pinned one after another on a helper thread
-  // while the first chunk's fill and DMA run (a first call pays the page
-  // pinning of one chunk before its first DMA, not all); chunk_ready(c, i)
-  // waits for chunk i, ring_ready for all of them
+  // the ring's chunks are pinned on helper threads, one per chunk, beside
+  // the stream creation (a first call pays about one chunk's pinning, not
+  // one per chunk in turn); chunk_ready(c, i) waits for chunk i, ring_ready
+  // for all of them
   std::promise<hipError_t> pinned[kRingMax];
   std::shared_future<hipError_t> pin_done[kRingMax];
 };
@@ -158,7 +154,10 @@ hipError_t chunk_ready(DevCtx *c, int i) {
 }
 hipError_t ring_ready(DevCtx *c) {
   hipError_t e = hipSuccess;
-  for (int i = 1; i < ring_depth() && e == hipSuccess; i++) e = chunk_ready(c, i);
+  for (int i = 0; i < ring_depth(); i++) {
+    const hipError_t r = chunk_ready(c, i);
+    if (e == hipSuccess) e = r;
+  }
   return e;
 }
 
@@ -173,24 +172,23 @@ hipError_t ctx_get(int device, DevCtx **out) {
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) {
-    // the ring's other chunks are pinned on a helper thread from the start,
-    // beside this thread's stream creation and first chunk (a first call
-    // otherwise waits ~14 ms for the second chunk after its first DMA)
-    for (int i = 1; i < ring_depth(); i++) c->pin_done[i] = c->pinned[i].get_future().share();
-    std::thread([c, device] {
-      hipError_t r = hipSetDevice(device);
-      for (int i = 1; i < ring_depth(); i++) {
+    // every ring chunk pinned on its own helper thread from the start, beside
+    // this thread's stream creation (pinned one after another, a first call
+    // waited ~14 ms per chunk)
+    for (int i = 0; i < ring_depth(); i++) {
+      c->pin_done[i] = c->pinned[i].get_future().share();
+      std::thread([c, device, i] {
+        hipError_t r = hipSetDevice(device);
         if (r == hipSuccess) r = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
         c->pinned[i].set_value(r);
-      }
-    }).detach();
+      }).detach();
+    }
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
     e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
-  if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
   if (e != hipSuccess) {
-    (void) ring_ready(c);   // the helper may still write pin[1..]
+    (void) ring_ready(c);   // the helpers may still write pin[]
     for (int i = 0; i < kRingMax; i++) {
       if (c->pin[i]) (void) hipHostFree(c->pin[i]);
       if (c->ev[i]) (void) hipEventDestroy(c->ev[i]);
@@ -299,7 +297,7 @@ hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
   for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += kStage, k++) {
     const int b = (int) (k % R);
     const uint64_t n = std::min(kStage, len - off);
-    if (k >= 1 && k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
+    if (k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
     if (k >= R && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
     char *buf = (char *) c->pin[b];
     std::atomic<bool> ok{true};
@@ -317,6 +315,73 @@ hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
     if (e == hipSuccess) e = hipEventRecord(c->ev[b], c->stream);
   }
   hipError_t e2 = hipStreamSynchronize(c->stream);   // the ring is free again on return
+  return e == hipSuccess ? e2 : e;
+}
+
+// Several uploads through one pass of the ring, their chunks interleaved in
+// proportion to their sizes (each next chunk from the least advanced
+// segment): a segment whose fill is CPU-bound (the BWT plane packing reads
+// 16 source bytes per 4 staged) then fills while the DMA engine drains the
+// chunks of a copy-bound one (the LCP bytes) queued before it, instead of
+// the two running one after the other.  A segment whose fill returns false
+// stops (*aborted set; the others go on); without `aborted` that fails the
+// upload.
+struct StageSeg {
+  void *dst;
+  uint64_t len;
+  std::function<bool(uint64_t, uint64_t, char *)> fill;
+  bool *aborted;
+  uint64_t done;
+  bool stop;
+};
+
+hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) {
+  hipError_t e = hipSuccess;
+  const uint64_t R = (uint64_t) ring_depth();
+  for (auto &sg : segs) {
+    sg.done = 0;
+    sg.stop = false;
+    if (sg.aborted) *sg.aborted = false;
+  }
+  for (uint64_t k = 0; e == hipSuccess; k++) {
+    int pick = -1;
+    double best = 2.0;
+    for (size_t i = 0; i < segs.size(); i++) {
+      const StageSeg &sg = segs[i];
+      if (sg.stop || sg.done >= sg.len) continue;
+      const double f = (double) sg.done / (double) sg.len;
+      if (f < best) {
+        best = f;
+        pick = (int) i;
+      }
+    }
+    if (pick < 0) break;
+    StageSeg &sg = segs[(size_t) pick];
+    const int b = (int) (k % R);
+    const uint64_t off = sg.done, n = std::min(kStage, sg.len - off);
+    if (k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
+    if (k >= R && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
+    char *buf = (char *) c->pin[b];
+    std::atomic<bool> ok{true};
+    const uint64_t units = (n + 63) / 64;   // 64-byte units (whole packed groups)
+    par_for(units, nt, [&, buf, off](uint64_t ulo, uint64_t uhi) {
+      const uint64_t lo = ulo * 64, hi = std::min(n, uhi * 64);
+      if (lo < hi && !sg.fill(off + lo, hi - lo, buf + lo)) ok = false;
+    });
+    if (!ok) {
+      sg.stop = true;
+      if (sg.aborted) {
+        *sg.aborted = true;
+        continue;   // slot b stays free; its last DMA was waited for above
+      }
+      e = hipErrorInvalidValue;
+      break;
+    }
+    e = hipMemcpyAsync((char *) sg.dst + off, buf, n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(c->ev[b], c->stream);
+    sg.done += n;
+  }
+  hipError_t e2 = hipStreamSynchronize(c->stream);
   return e == hipSuccess ? e2 : e;
 }
 
@@ -380,7 +445,7 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
                        unsigned nt) {
   const uint64_t CH = kStage / sizeof (GtSmaxRecord);
   const uint64_t nch = (cnt + CH - 1) / CH;
-  hipError_t e = nch > 1 ? ring_ready(c) : hipSuccess;
+  hipError_t e = nch > 1 ? ring_ready(c) : chunk_ready(c, 0);
   if (e != hipSuccess) return e;
   auto issue = [&](uint64_t j) {
     const uint64_t n = std::min(CH, cnt - j * CH);
@@ -411,7 +476,7 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
 // threaded copy-out of chunk k)
 hipError_t d2h_bytes(DevCtx *c, void *dst, const void *dev, uint64_t bytes, unsigned nt) {
   const uint64_t nch = (bytes + kStage - 1) / kStage;
-  hipError_t e = nch > 1 ? ring_ready(c) : hipSuccess;
+  hipError_t e = nch > 1 ? ring_ready(c) : chunk_ready(c, 0);
   if (e != hipSuccess) return e;
   auto issue = [&](uint64_t j) {
     const uint64_t n = std::min(kStage, bytes - j * kStage);
@@ -628,11 +693,21 @@ void device_phase1(Call *C, int d) {
         std::thread &t;
         ~JoinT() { if (t.joinable()) t.join(); }
       } join_reserve{reserve};
+      // the tables' device buffers first (the BWT as its code planes, 4 B per
+      // 16 rows, plus the u64 groups the device rebuilds from them)
+      const uint64_t ng = GT_SMAX_PK_GROUPS(S.len);
+      const uint8_t *bsrc = in->bwttab + S.base;
+      const uint64_t blen = S.len;
+      bool nondna = env_on("GT_SMAX_BYTE_BWT");
+      void *planes = nullptr;
       DCHK(alloc_table(&S.lcp, S.len));
+      if (!nondna) {
+        DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
+        DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
+      }
+      DCHK(smax_dev_alloc(&S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo + 1)));
       {
-        // started after the LCP table's allocation, so that its own cold
-        // allocations (the BWT buffers, the .llv copy, the plan's) queue
-        // behind the upload's first DMA rather than ahead of it
+        // the plan's own buffers into the cache beside the upload
         GtSmaxDevShard g;
         memset(&g, 0, sizeof g);
         g.numllv = S.hi - S.lo;
@@ -642,45 +717,39 @@ void device_phase1(Call *C, int d) {
         g.end = S.end;
         g.nonspecials = in->nonspecials;
         g.device = dev;
-        if (!env_off("GT_SMAX_RESERVE"))   // diagnostic: GT_SMAX_RESERVE=0 skips it
         reserve = std::thread([g, dev] {
-          if (hipSetDevice(dev) != hipSuccess) return;
-          const uint64_t ng = GT_SMAX_PK_GROUPS(g.local_len);
-          const size_t sz[3] = {sizeof (uint64_t) * ng, sizeof (uint32_t) * ng,
-                                sizeof (GtSmaxLlv) * (g.numllv + 1)};
-          void *b[3] = {nullptr, nullptr, nullptr};
-          for (int i = 0; i < 3; i++) (void) smax_dev_alloc(&b[i], sz[i]);
-          for (int i = 0; i < 3; i++) smax_dev_free_ex(b[i], false);
-          (void) smax_plan_reserve(&g, 0);
+          if (hipSetDevice(dev) == hipSuccess) (void) smax_plan_reserve(&g, 0);
         });
       }
-      const char *lsrc = (const char *) in->lcptab + S.base;
-      DCHK(stage_h2d(c, (char *) S.lcp + GT_SMAX_PAD_FRONT, S.len, C->nt,
-                     [lsrc](uint64_t off, uint64_t n, char *buf) {
-                       memcpy(buf, lsrc + off, n);
-                       return true;
-                     }, nullptr));
-      if (d == 0) smax_phase_mark(" h2d.lcp", &th);
-      // BWT: bit planes packed during the fill; a non-DNA alphabet aborts
-      // the packed upload and stages the bytes instead
-      const uint64_t ng = GT_SMAX_PK_GROUPS(S.len);
-      const uint8_t *bsrc = in->bwttab + S.base;
-      const uint64_t blen = S.len;
-      bool nondna = env_on("GT_SMAX_BYTE_BWT");
-      if (!nondna) {
-        // over PCIe only the two code planes (4 B per 16 rows) and the few
-        // groups holding a special row; the device rebuilds the u64 groups
-        // (half the BWT bytes of staging whole groups)
-        DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
-        void *planes = nullptr;
-        DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
+      {
+        // one pass of the ring over the LCP bytes, the BWT planes (packed
+        // during the fill; a non-DNA alphabet stops that segment and the
+        // bytes are staged after) and the .llv entries
         std::vector<uint64_t> spec;
         std::mutex smu;
-        hipError_t pe = stage_h2d(c, planes, sizeof (uint32_t) * ng, C->nt,
-                                  [bsrc, blen, &spec, &smu](uint64_t off, uint64_t n, char *buf) {
-                                    return pack_bits(bsrc, blen, off / 4, (off + n) / 4, nullptr,
-                                                     (uint32_t *) buf, &spec, &smu);
-                                  }, &nondna);
+        const char *lsrc = (const char *) in->lcptab + S.base;
+        std::vector<StageSeg> segs;
+        segs.push_back({(char *) S.lcp + GT_SMAX_PAD_FRONT, S.len,
+                        [lsrc](uint64_t off, uint64_t n, char *buf) {
+                          memcpy(buf, lsrc + off, n);
+                          return true;
+                        }, nullptr, 0, false});
+        if (!nondna)
+          segs.push_back({planes, sizeof (uint32_t) * ng,
+                          [bsrc, blen, &spec, &smu](uint64_t off, uint64_t n, char *buf) {
+                            return pack_bits(bsrc, blen, off / 4, (off + n) / 4, nullptr,
+                                             (uint32_t *) buf, &spec, &smu);
+                          }, &nondna, 0, false});
+        if (S.hi > S.lo) {
+          const char *vsrc = (const char *) (in->llvtab + S.lo);
+          segs.push_back({S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo),
+                          [vsrc](uint64_t off, uint64_t n, char *buf) {
+                            memcpy(buf, vsrc + off, n);
+                            return true;
+                          }, nullptr, 0, false});
+        }
+        hipError_t pe = stage_h2d_multi(c, segs, C->nt);
+        if (d == 0) smax_phase_mark(" h2d.ring", &th);
         void *dspec = nullptr;
         if (pe == hipSuccess && !nondna && !spec.empty()) {
           pe = smax_dev_alloc(&dspec, sizeof (uint64_t) * spec.size());
@@ -707,16 +776,6 @@ void device_phase1(Call *C, int d) {
                          return true;
                        }, nullptr));
         S.sh.bwt_dev = (const uint8_t *) S.bwt + GT_SMAX_PAD_FRONT;
-      }
-      if (d == 0) smax_phase_mark(" h2d.bwt", &th);
-      DCHK(smax_dev_alloc(&S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo + 1)));
-      if (S.hi > S.lo) {
-        const char *vsrc = (const char *) (in->llvtab + S.lo);
-        DCHK(stage_h2d(c, S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo), C->nt,
-                       [vsrc](uint64_t off, uint64_t n, char *buf) {
-                         memcpy(buf, vsrc + off, n);
-                         return true;
-                       }, nullptr));
       }
       S.sh.lcp_dev = (const uint8_t *) S.lcp + GT_SMAX_PAD_FRONT;
       S.sh.llv_dev = (const GtSmaxLlv *) S.llv;
