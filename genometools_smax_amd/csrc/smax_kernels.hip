@@ -65,24 +65,6 @@
 #include "gt_smax_hip.h"
 #include "smax_internal.h"
 
-// SMAX_WT (A/B): write-through (sc1) stores for K1's slot records and counts
-// (bit 0) and K3's output records (bit 1): no dirty L2 lines left for the
-// kernel-end write-back (5.8 us from K1's end to K1b's start, none from
-// K1b's to K3's: profiles/r04j/timeline_*.txt)
-#ifndef SMAX_WT
-#define SMAX_WT 0
-#endif
-__device__ __forceinline__ void st_wt_u64(uint64_t *p, uint64_t v) {
-  asm volatile("global_store_dwordx2 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_wt_u32(uint32_t *p, uint32_t v) {
-  asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_wt_u128(void *p, uint4 v) {
-  typedef uint32_t U4 __attribute__((ext_vector_type(4)));
-  const U4 w = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(w) : "memory");
-}
 // per-chunk 255-byte ranks: K1 windows stage at most SMAX_LLV_CAP (< 256)
 // .llv entries (more: the tile is static, K1b), so a byte holds every rank
 typedef uint8_t SmaxRank;
@@ -1501,15 +1483,9 @@ __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t 
                                                 uint32_t cnt) {
   const int lane = threadIdx.x & 63;
   if (a.dbg & 4096u) return;
-  if ((uint32_t) lane < cnt && !(a.dbg & (1u << 21))) {
-    if (SMAX_WT & 1) st_wt_u64(&a.slots[tile * (uint64_t) SMAX_SSLOT + lane], rec);
-    else a.slots[tile * (uint64_t) SMAX_SSLOT + lane] = rec;
-  }
+  if ((uint32_t) lane < cnt && !(a.dbg & (1u << 21))) a.slots[tile * (uint64_t) SMAX_SSLOT + lane] = rec;
   if (lane == 0) {
-    if (!(a.dbg & (1u << 22))) {
-      if (SMAX_WT & 1) st_wt_u32(&a.tile_count[tile], cnt);
-      else a.tile_count[tile] = cnt;
-    }
+    if (!(a.dbg & (1u << 22))) a.tile_count[tile] = cnt;
   }
 }
 
@@ -2376,11 +2352,7 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
         rec.lb = g00 + tile * (uint64_t) SMAX_TILE + (v[u] & 0x7ffu) - 1;   // g00: global row of tile 0
         rec.width = (uint32_t) (v[u] >> 11) & SMAX_PK_WMAX;
         rec.lcp = (uint32_t) (v[u] >> 32);
-        if (SMAX_WT & 2)
-          st_wt_u128(out + base + r, make_uint4((uint32_t) rec.lb, (uint32_t) (rec.lb >> 32), rec.lcp,
-                                                rec.width));
-        else
-          out[base + r] = rec;
+        out[base + r] = rec;
       }
     }
   }

@@ -124,12 +124,15 @@ uint64_t stage_bytes() {
 }
 #define kStage stage_bytes()
 
-// pinned chunks in the H2D ring: 2, GT_SMAX_RING (2..4) overrides
+// pinned chunks in the H2D ring: 3 (with the interleaved upload the planes'
+// CPU-bound fill overlaps two queued LCP chunks; warm h2d of the C3 tables
+// 76-79 ms against 83+ with 2, profiles/r04o/e2e_ring_sweep_c3.json),
+// GT_SMAX_RING (2..4) overrides
 constexpr int kRingMax = 4;
 int ring_depth() {
   static const int r = [] {
     const char *v = getenv("GT_SMAX_RING");
-    const long d = v ? strtol(v, NULL, 0) : 2;
+    const long d = v ? strtol(v, NULL, 0) : 3;
     return (int) (d < 2 ? 2 : d > kRingMax ? kRingMax : d);
   }();
   return r;
@@ -141,10 +144,12 @@ struct DevCtx {
   hipStream_t stream = nullptr;
   void *pin[kRingMax] = {};
   hipEvent_t ev[kRingMax] = {};
-  // the ring's chunks are pinned on helper threads, one per chunk, beside
-  // the stream creation (a first call pays about one chunk's pinning, not
-  // one per chunk in turn); chunk_ready(c, i) waits for chunk i, ring_ready
-  // for all of them
+  // chunk 0 is pinned with the context, the others one after another on a
+  // helper thread while the first chunks fill and drain (a first call pays
+  // one chunk's pinning up front); chunk_ready(c, i) waits for chunk i,
+  // ring_ready for all of them.  (Pinning beside the stream creation, one
+  // thread per chunk, made the context 45-68 ms instead of 24-36:
+  // profiles/r04o/e2e_ring_sweep_c3.json)
   std::promise<hipError_t> pinned[kRingMax];
   std::shared_future<hipError_t> pin_done[kRingMax];
 };
@@ -171,24 +176,22 @@ hipError_t ctx_get(int device, DevCtx **out) {
   DevCtx *c = new DevCtx;
   c->device = device;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) {
-    // every ring chunk pinned on its own helper thread from the start, beside
-    // this thread's stream creation (pinned one after another, a first call
-    // waited ~14 ms per chunk)
-    for (int i = 0; i < ring_depth(); i++) {
-      c->pin_done[i] = c->pinned[i].get_future().share();
-      std::thread([c, device, i] {
-        hipError_t r = hipSetDevice(device);
-        if (r == hipSuccess) r = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
-        c->pinned[i].set_value(r);
-      }).detach();
-    }
-  }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
     e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
+  if (e == hipSuccess) {
+    for (int i = 1; i < ring_depth(); i++) c->pin_done[i] = c->pinned[i].get_future().share();
+    std::thread([c, device] {
+      hipError_t r = hipSetDevice(device);
+      for (int i = 1; i < ring_depth(); i++) {
+        if (r == hipSuccess) r = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
+        c->pinned[i].set_value(r);
+      }
+    }).detach();
+  }
   if (e != hipSuccess) {
-    (void) ring_ready(c);   // the helpers may still write pin[]
+    (void) ring_ready(c);   // the helper may still write pin[]
     for (int i = 0; i < kRingMax; i++) {
       if (c->pin[i]) (void) hipHostFree(c->pin[i]);
       if (c->ev[i]) (void) hipEventDestroy(c->ev[i]);
