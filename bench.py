@@ -336,9 +336,10 @@ def main():
     for _ in range(args.warmup):
         step()
     # K1's duration by HIP events around every 4th launch of the timed
-    # region: each timed launch pays two event records (measured ~1 % of a
-    # C3 step, ~3 % of an 8-way shard's, profiles/r02z_event_overhead.txt)
-    ev_stride = 4
+    # region (every 8th on N > 1 ranks): each timed launch pays two event
+    # records, ~5.7 us each on the box (~1 % of a C3 step, ~7 % of a 3/8
+    # shard's: profiles/r02z_event_overhead.txt, profiles/r04r/timeline_*)
+    ev_stride = 4 if world == 1 else 8
     plan.enable_timing((args.steps + ev_stride - 1) // ev_stride, ev_stride)
     torch.cuda.synchronize()
     if dist:

@@ -175,11 +175,15 @@ hipError_t ctx_get(int device, DevCtx **out) {
   if (it != g_ctx.end()) { *out = it->second; return hipSuccess; }
   DevCtx *c = new DevCtx;
   c->device = device;
+  double tc = smax_phase_clock();
   hipError_t e = hipSetDevice(device);
+  smax_phase_mark(" ctx.device", &tc);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
     e = hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming);
+  smax_phase_mark(" ctx.stream", &tc);
   if (e == hipSuccess) e = hipHostMalloc(&c->pin[0], kStage, hipHostMallocDefault);
+  smax_phase_mark(" ctx.pin0", &tc);
   if (e == hipSuccess) {
     for (int i = 1; i < ring_depth(); i++) c->pin_done[i] = c->pinned[i].get_future().share();
     std::thread([c, device] {

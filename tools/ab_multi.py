@@ -45,17 +45,24 @@ k1 = {n: [] for n in names}
 
 
 def timed(L, p, n=30):
+    """(step, K1) in ms: K1 from the plan's own events around every K1 of a
+    first pass; the step from a second pass with those events off (an event
+    record between K1 and K1b costs ~5.7 us on the box, profiles/r04r/)."""
     for _ in range(3):
         L.gt_smax_plan_run(p.plan, sp)
     L.gt_smax_plan_timing(p.plan, n)
+    for _ in range(n):
+        L.gt_smax_plan_run(p.plan, sp)
+    torch.cuda.synchronize()
+    ms, k = ctypes.c_double(), ctypes.c_int()
+    L.gt_smax_plan_timing_read(p.plan, ctypes.byref(ms), ctypes.byref(k))
+    L.gt_smax_plan_timing(p.plan, 0)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(n):
         L.gt_smax_plan_run(p.plan, sp)
     e1.record(s)
     torch.cuda.synchronize()
-    ms, k = ctypes.c_double(), ctypes.c_int()
-    L.gt_smax_plan_timing_read(p.plan, ctypes.byref(ms), ctypes.byref(k))
     return e0.elapsed_time(e1) / n, ms.value / max(k.value, 1)
 
 

@@ -25,7 +25,15 @@ for r in range(W):
     p = esa.plan(minlen, begin, end)
     for _ in range(5):
         p.run(s.cuda_stream)
+    # K1 from the plan's events around every K1 of one pass; the step from
+    # a second pass without them (an event record between K1 and K1b costs
+    # ~5.7 us, profiles/r04r/)
     p.enable_timing(50)
+    for _ in range(50):
+        p.run(s.cuda_stream)
+    torch.cuda.synchronize()
+    k1, n = p.kernel_ms()
+    p.enable_timing(0)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record(s)
@@ -33,7 +41,7 @@ for r in range(W):
         p.run(s.cuda_stream)
     e1.record(s)
     torch.cuda.synchronize()
-    k1, n = p.kernel_ms()
-    print("shard %d/%d rows %d: step %.4f ms, K1 %.4f ms, deferred %d"
-          % (r, W, end - begin, e0.elapsed_time(e1) / 50, k1 / n, p.deferred_tiles()), flush=True)
+    st = e0.elapsed_time(e1) / 50
+    print("shard %d/%d rows %d: step %.4f ms, K1 %.4f ms, rest %.4f ms, deferred %d"
+          % (r, W, end - begin, st, k1 / n, st - k1 / n, p.deferred_tiles()), flush=True)
     p.close()
