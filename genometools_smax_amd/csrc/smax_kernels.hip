@@ -511,10 +511,6 @@ __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, 
 // per-run resets (pending-plateau slot, pool cursor, deferral count) and the
 // boundary head.  Non-empty shards never launch it: K1 clears the pending
 // slot, the previous run's K3 resets the rest and K1b computes the head.
-// diagnostic (GT_SMAX_GAP_PROBE): nothing, between K1 and K1b -- does the
-// time between them belong to K1's end or to K1b's start?
-__global__ void __launch_bounds__(64) smax_empty_kernel() {}
-
 __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   a.bnd->pend_valid = 0;
@@ -2582,7 +2578,6 @@ struct GtSmaxPlan {
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   uint32_t *err;
   uint32_t dbg;
-  uint32_t gap_probe;         // diagnostic (GT_SMAX_GAP_PROBE): an empty kernel between K1 and K1b
   // optional K1 timing: event pairs recorded around the scan kernel
   hipEvent_t *ev;
   unsigned long long *stamps;    // GT_SMAX_STAMPS: K1 section cycles (diag build)
@@ -2719,7 +2714,6 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   {
     const char *d = getenv("GT_SMAX_DEBUG");
     p->dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
-    p->gap_probe = getenv("GT_SMAX_GAP_PROBE") != NULL;
     // section stamps need the diagnostic build (a no-op ablation bit selects it)
     if (getenv("GT_SMAX_STAMPS")) p->dbg |= 1u << 30;
   }
@@ -3105,7 +3099,6 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
   }
-  if (p->gap_probe) hipLaunchKernelGGL(smax_empty_kernel, dim3(1), dim3(64), 0, s);
   {
     // K1b over the static list and K1's deferrals, one launch; its first
     // workgroup computes the boundary head, its last ones the block sums
