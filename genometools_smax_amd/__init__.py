@@ -176,6 +176,8 @@ def lib():
         L.gt_smax_build_id.restype = ctypes.c_char_p
         L.gt_smax_plan_scan_kernel.restype = ctypes.c_char_p
         L.gt_smax_plan_scan_kernel.argtypes = [vp]
+        L.gt_smax_plan_k1b_waves.restype = ctypes.c_uint32
+        L.gt_smax_plan_k1b_waves.argtypes = [vp]
         L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
         L.gt_smax_dev_free_table.argtypes = [ci, vp]
         L.gt_smax_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtSmaxDevShard), u32, u64,
@@ -823,6 +825,10 @@ class SmaxPlan:
     def scan_kernel(self):
         """Name of the K1 variant this plan launches (gt_smax_plan_scan_kernel)."""
         return lib().gt_smax_plan_scan_kernel(self.plan).decode()
+
+    def k1b_waves(self):
+        """Waves per K1b workgroup of this plan (gt_smax_plan_k1b_waves)."""
+        return lib().gt_smax_plan_k1b_waves(self.plan)
 
     def deferred_tiles(self):
         return lib().gt_smax_plan_deferred_tiles(self.plan)

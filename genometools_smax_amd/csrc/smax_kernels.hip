@@ -93,7 +93,6 @@ typedef uint8_t SmaxRank;
 // K1b), K1b writes GtSmaxRecord (16 bytes) and flags its tile count
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
-#define SMAX_BSW 4                                    // block sums per K1b block-sum workgroup
 #define SMAX_SBB 64                                   // blocks per superblock sum (K3's two-level prefix)
 // one run's block-sum buffer (block sums added up in K1b's launch): the
 // blocks' sums, then the superblocks' sums
@@ -1686,7 +1685,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
 // plateau end from the ballot words, local maximum, left diversity over the
 // window's BWT bytes, the pending plateau at the shard end.  Plateaus that
 // run past the window take the generic global path (eval_start).
-#define SMAX_XQ 512                                   // rows per compaction round
 #define SMAX_XSTEPS ((SMAX_TILE + 64 + 63) / 64)      // ballot steps incl. right halo
 
 struct SmaxWindowX {
@@ -1695,7 +1693,6 @@ struct SmaxWindowX {
   uint32_t X[SMAX_LDSB];        // exact LCP of window row o (0 outside [1, N))
   uint64_t ne[SMAX_XSTEPS];     // bit b: LCP[row b + 1] != LCP[row b] (tile rows b)
   uint64_t st[SMAX_TILE / 64];  // bit b: row b is an owned plateau start
-  uint16_t list[SMAX_XQ];
 };
 
 // Loads tile l0's window (rows g0-LH .. g0+TILE+RH-1) into W and expands the
@@ -1875,23 +1872,25 @@ __device__ static bool eval_start_x(const SmaxScanArgs &a, const Win &t, const S
   return true;
 }
 
-// load_exact_window for a whole workgroup (256 threads): one 16-row chunk
+// load_exact_window for a whole workgroup (TH threads): one 16-row chunk
 // per thread and every .llv entry of the window (<= SMAX_LDSB) fetched in
-// one round of at most 9 per thread, instead of one wave doing 3 chunks per
-// lane and up to 4 dependent .llv rounds.  *nff is a workgroup counter the
-// caller zeroes.
+// one round of at most 9 (256 threads) or 5 (512) per thread, instead of one
+// wave doing 3 chunks per lane and up to 4 dependent .llv rounds.  *nff is
+// a workgroup counter the caller zeroes.
+template <int TH>
 __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, uint2 info,
                                             SmaxWindowX *W, uint32_t *nff, uint64_t *tmark) {
+  static_assert(TH >= SMAX_NCHUNK, "one window chunk per thread");
   const int tid = threadIdx.x;
   const uint64_t g0 = a.base + l0;
   const uint32_t lo = info.x, n = SMAX_WIN_N(info.y);
   const uint64_t wb = g0 - SMAX_LH;
-  constexpr int EPT = (SMAX_LDSB + 255) / 256;        // .llv entries per thread (9)
+  constexpr int EPT = (SMAX_LDSB + TH - 1) / TH;      // .llv entries per thread
   uint2 ep[EPT];
   uint32_t ev[EPT];
 #pragma unroll
   for (int r = 0; r < EPT; r++) {
-    const uint32_t e = (uint32_t) tid + 256u * r;
+    const uint32_t e = (uint32_t) tid + (uint32_t) TH * r;
     const uint32_t *rec = reinterpret_cast<const uint32_t *>(&a.llv[lo + (e < n ? e : 0)]);
     const uint32_t r0 = __builtin_nontemporal_load(rec), r1 = __builtin_nontemporal_load(rec + 1);
     const uint32_t r2 = __builtin_nontemporal_load(rec + 2);
@@ -1939,7 +1938,7 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
   if ((a.dbg & 1048576u) && *tmark == 0) *tmark = __builtin_readcyclecounter();
 #pragma unroll
   for (int r = 0; r < EPT; r++) {
-    const uint32_t e = (uint32_t) tid + 256u * r;
+    const uint32_t e = (uint32_t) tid + (uint32_t) TH * r;
     const uint64_t pos = ((uint64_t) ep[r].y << 32) | ep[r].x;
     const uint64_t o = pos - wb;
     if (e < n && o < SMAX_LDSB && pos < a.N) W->X[o] = ev[r];
@@ -1951,49 +1950,55 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
 
 // K1b, one workgroup per tile (the combined placement's kernel): a K1b
 // launch covers few tiles (the static list and K1's rare deferrals; about
-// 130 per shard of an 8-way C3 split), so its time is the slowest tile's,
+// 300 per shard of an 8-way C3 split), so its time is the slowest tile's,
 // and one wave per tile left three of every four waves idle.  Here the
-// whole workgroup loads the exact window (load_exact_window_wg), the four
-// waves share the ballot steps, and each takes one 512-row round of starts:
-// evaluated once into LDS (value, width,
-// accepted), the rounds' record counts are scanned across the waves and
-// the records written in row order.
+// whole workgroup loads the exact window (load_exact_window_wg), the NW
+// waves share the ballot steps, and each takes one round of 2048 / NW rows'
+// starts: evaluated once into LDS (value, width, accepted), the rounds'
+// record counts are scanned across the waves and the records written in
+// row order.  NW = 4 (one tile in 24k cycles, 5 workgroups per CU) or, when
+// the launch fits one generation of them, NW = 8 (two per CU, a tile's
+// ballots and evaluation split twice as fine).
+template <int NW>
 struct SmaxDeferWG {
+  static constexpr int XQ = SMAX_TILE / NW;   // rows per wave's round
   SmaxWindowX win;
-  uint16_t list[4][SMAX_XQ];        // per wave: its round's starts (row order)
-  // per wave: its accepted records, compacted (a 512-row round holds at most
-  // 256: consecutive accepted starts are >= 2 rows apart) -- half the LDS of
-  // per-start results (28 KB per workgroup; registers, not LDS, hold the
-  // kernel at 4 workgroups per CU: forcing 5 spilled to scratch and measured
-  // slower, profiles/r02v_k1b_variants.txt)
-  uint2 rec[4][SMAX_XQ / 2];        // {LCP value, width}
-  uint16_t row[4][SMAX_XQ / 2];     // start row in the tile
-  uint32_t cnt[4];
+  uint16_t list[NW][XQ];            // per wave: its round's starts (row order)
+  // per wave: its accepted records, compacted (a round of XQ rows holds at
+  // most XQ / 2: consecutive accepted starts are >= 2 rows apart) -- half
+  // the LDS of per-start results (27 KB per workgroup; registers, not LDS,
+  // hold the 4-wave kernel at 5 workgroups per CU: forcing more spilled to
+  // scratch and measured slower, profiles/r02v_k1b_variants.txt)
+  uint2 rec[NW][XQ / 2];            // {LCP value, width}
+  uint16_t row[NW][XQ / 2];         // start row in the tile
+  uint32_t cnt[NW];
   uint32_t nff;                     // 255 bytes of the window (load_exact_window_wg)
   uint64_t off;                     // the tile's first record in the pool (~0: none)
 };
 
-__global__ void __launch_bounds__(SMAX_THREADS)
+template <int NW>
+__global__ void __launch_bounds__(64 * NW)
 smax_defer_wg_kernel(SmaxScanArgs a) {
-  __shared__ __attribute__((aligned(16))) SmaxDeferWG sD;
+  constexpr int XQ = SmaxDeferWG<NW>::XQ;
+  __shared__ __attribute__((aligned(16))) SmaxDeferWG<NW> sD;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   SmaxWindowX *W = &sD.win;
   Win t;
   win_init(t, a);
   // the last bs_wgs workgroups: K3's block sums (K2's work, without its
-  // launch), SMAX_BSW blocks each, from the counts K1 wrote; tiles K1 left
+  // launch), NW blocks each, from the counts K1 wrote; tiles K1 left
   // to K1b hold the wide bit and are added by their K1b workgroup below.
   // Both add into the run's zeroed buffer (K3 clears the other one).
   const uint32_t tile_wgs = gridDim.x - a.bs_wgs;
   if (blockIdx.x >= tile_wgs) {
     // wave w sums block b0 + w (4 counts per lane), one atomic per block;
-    // the workgroup's 4 blocks share a superblock: one atomic for it
+    // the workgroup's NW blocks share a superblock: one atomic for it
     // (atomics are issued at about one wave-instruction per 50 ns per CU:
     // one per wave and block instead of per wave, block and level)
-    static_assert(SMAX_BSW == SMAX_THREADS / 64 && SMAX_SBB % SMAX_BSW == 0, "a block per wave");
+    static_assert(SMAX_SBB % NW == 0, "a block per wave, one superblock per workgroup");
     const uint32_t nb = (a.num_tiles + SMAX_CPB - 1) / SMAX_CPB;
-    const uint32_t b0 = (blockIdx.x - tile_wgs) * SMAX_BSW, b = b0 + (uint32_t) wave;
+    const uint32_t b0 = (blockIdx.x - tile_wgs) * NW, b = b0 + (uint32_t) wave;
     uint32_t v[SMAX_CPB / 64];
 #pragma unroll
     for (int u = 0; u < SMAX_CPB / 64; u++) {
@@ -2011,7 +2016,9 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      const uint32_t sc = sD.cnt[0] + sD.cnt[1] + sD.cnt[2] + sD.cnt[3];
+      uint32_t sc = 0;
+#pragma unroll
+      for (int w = 0; w < NW; w++) sc += sD.cnt[w];
       if (sc != 0) atomicAdd(&a.block_sum[nb + b0 / SMAX_SBB], sc);   // their superblock
     }
     return;
@@ -2043,7 +2050,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     // loads of thread 0 have landed, |1048576 after the LDS writes
     const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
     uint64_t tmark = 0;
-    load_exact_window_wg(a, l0, info, W, &sD.nff, &tmark);
+    load_exact_window_wg<64 * NW>(a, l0, info, W, &sD.nff, &tmark);
     if (a.dbg & 65536u) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
     t.L = to_lds<uint8_t>(W->L);
@@ -2053,8 +2060,8 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     t.val = nullptr;
     t.val16 = nullptr;
     t.nval = -1;
-    // ballots: the waves take every 4th 64-row step
-    for (uint32_t st = (uint32_t) wave; st < SMAX_XSTEPS; st += 4) {
+    // ballots: the waves take every NW-th 64-row step
+    for (uint32_t st = (uint32_t) wave; st < SMAX_XSTEPS; st += NW) {
       const uint32_t b = st * 64 + lane, o = b + SMAX_LH;
       bool ne = true, sm = false;
       if (o + 1 < SMAX_LDSB) {
@@ -2071,11 +2078,11 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     }
     __syncthreads();
     if ((a.dbg & 131072u) && tmark == 0) tmark = __builtin_readcyclecounter();
-    // wave w: the starts of rows [512 w, 512 w + 512), evaluated; accepted
+    // wave w: the starts of rows [XQ w, XQ w + XQ), evaluated; accepted
     // records compacted into LDS in row order
-    const uint32_t q0 = (uint32_t) wave * SMAX_XQ;
+    const uint32_t q0 = (uint32_t) wave * XQ;
     uint32_t ns = 0;
-    for (uint32_t s2 = q0 / 64; s2 < (q0 + SMAX_XQ) / 64; s2++) {
+    for (uint32_t s2 = q0 / 64; s2 < (q0 + XQ) / 64; s2++) {
       const uint64_t m = W->st[s2];
       if ((m >> lane) & 1u) sD.list[wave][ns + (uint32_t) __popcll(m & ltm)] = (uint16_t) (s2 * 64 + lane);
       ns += (uint32_t) __popcll(m);
@@ -2094,22 +2101,26 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
       }
       const uint64_t am = __ballot(acc);
       const uint32_t w = wc + (uint32_t) __popcll(am & ltm);
-      if (acc && w < SMAX_XQ / 2) {
+      if (acc && w < XQ / 2) {
         sD.rec[wave][w] = make_uint2(cur, (uint32_t) (j - (g0 + b) + 2));
         sD.row[wave][w] = (uint16_t) b;
       }
       wc += (uint32_t) __popcll(am);
     }
-    if (wc > SMAX_XQ / 2) {   // impossible in a consistent index (see SmaxDeferWG)
+    if (wc > XQ / 2) {   // impossible in a consistent index (see SmaxDeferWG)
       if (lane == 0) atomicOr(a.err, SMAX_ERR_LLV);
-      wc = SMAX_XQ / 2;
+      wc = XQ / 2;
     }
     if (lane == 0) sD.cnt[wave] = wc;
     __syncthreads();
     if ((a.dbg & 262144u) && tmark == 0) tmark = __builtin_readcyclecounter();
-    const uint32_t c0 = sD.cnt[0], c1 = sD.cnt[1], c2 = sD.cnt[2], c3 = sD.cnt[3];
-    const uint32_t total = c0 + c1 + c2 + c3;
-    const uint32_t base = wave == 0 ? 0u : wave == 1 ? c0 : wave == 2 ? c0 + c1 : c0 + c1 + c2;
+    uint32_t total = 0, base = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      const uint32_t cw = sD.cnt[w];
+      base += w < wave ? cw : 0u;
+      total += cw;
+    }
     const bool nowrite = (a.dbg & (4096u | 32768u)) != 0;
     if (threadIdx.x == 0) {
       // the tile's records: list entry i owns wide slot wide_slot0 + i (a
@@ -2574,6 +2585,7 @@ struct GtSmaxPlan {
   bool nt;                   // window stream with the non-temporal policy (smax_scan_kernel_b2*_nt)
   uint32_t k1b_grid;         // K1b's tile workgroups (+1: the boundary head)
   uint32_t bs_wgs;           // block-sum workgroups appended to K1b's grid
+  uint32_t k1b_nw;           // waves per K1b workgroup (4 or 8)
   uint32_t k3_split;         // K3 workgroups per block of 256 tiles (GT_SMAX_K3_SPLIT)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   uint32_t *err;
@@ -2950,10 +2962,25 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
             hipSuccess || ncu < 1)
       ncu = 256;
     p->k1b_grid = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u, (uint32_t) ncu * 8u) + 1;
+    // 8 waves per tile (each tile's ballots and evaluation split twice as
+    // fine) when the launch -- tiles, the head and the block-sum workgroups
+    // -- fits one generation of the 8-wave kernel (two per CU), else 4 (five
+    // per CU).  GT_SMAX_K1B_WAVES=4/8 overrides.
+    {
+      int per8 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per8, smax_defer_wg_kernel<8>, 512, 0) !=
+          hipSuccess)
+        per8 = 0;
+      const uint64_t need8 = (uint64_t) p->k1b_grid + (p->compact_grid + 7u) / 8u;
+      const char *kw = getenv("GT_SMAX_K1B_WAVES");
+      p->k1b_nw = kw ? (strtol(kw, NULL, 0) == 8 ? 8u : 4u)
+                     : (per8 > 0 && need8 <= (uint64_t) per8 * (uint64_t) ncu ? 8u : 4u);
+    }
     // K3's block sums in the same launch (K2's work without its launch):
-    // K1b's last workgroups (measured against a separate block-sum kernel:
-    // C3 step -0.3 %, 3/8 shard -1.4 %, C2 -4.2 %, profiles/r03zb/fuse_bs_*.txt)
-    p->bs_wgs = (p->compact_grid + SMAX_BSW - 1) / SMAX_BSW;
+    // K1b's last workgroups, one block per wave (measured against a separate
+    // block-sum kernel: C3 step -0.3 %, 3/8 shard -1.4 %, C2 -4.2 %,
+    // profiles/r03zb/fuse_bs_*.txt)
+    p->bs_wgs = (p->compact_grid + p->k1b_nw - 1) / p->k1b_nw;
     // the first run's state (later runs: reset by the previous run's K3)
     const unsigned long long pc = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
     HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
@@ -3104,7 +3131,10 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
     // workgroup computes the boundary head, its last ones the block sums
     SmaxScanArgs c = a;
     c.k1b_head = 1;
-    hipLaunchKernelGGL(smax_defer_wg_kernel, dim3(p->k1b_grid + p->bs_wgs), dim3(SMAX_THREADS), 0, s, c);
+    if (p->k1b_nw == 8)
+      hipLaunchKernelGGL(smax_defer_wg_kernel<8>, dim3(p->k1b_grid + p->bs_wgs), dim3(512), 0, s, c);
+    else
+      hipLaunchKernelGGL(smax_defer_wg_kernel<4>, dim3(p->k1b_grid + p->bs_wgs), dim3(256), 0, s, c);
     HIPCHK(hipGetLastError());
   }
   return 0;
@@ -3290,6 +3320,8 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
 // diagnostic: K1's per-section cycle sums (GT_SMAX_STAMPS plans; 8 values:
 // wait, flush+issue, filter, classify+queue, exact starts, output, staging,
 // tiles); -1 if the plan has none
+extern "C" uint32_t gt_smax_plan_k1b_waves(const GtSmaxPlan *p) { return p->k1b_nw; }
+
 extern "C" const char *gt_smax_plan_scan_kernel(const GtSmaxPlan *p) {
   // the selection of plan_run_scan
   if (!p->pk) return "smax_scan_kernel_bytes";

@@ -290,6 +290,10 @@ int gt_smax_plan_stamps(GtSmaxPlan *plan, unsigned long long *out8);
  * _bytes = byte BWT windows); a static string. */
 const char *gt_smax_plan_scan_kernel(const GtSmaxPlan *plan);
 
+/* Waves per workgroup of the plan's K1b launch (4, or 8 when the launch
+ * fits one generation of the 8-wave kernel; GT_SMAX_K1B_WAVES overrides). */
+uint32_t gt_smax_plan_k1b_waves(const GtSmaxPlan *plan);
+
 /* Diagnostic: tiles the last run handed from K1 to the generic kernel K1b
  * (shard edges and tiles with more exact-evaluation starts than K1 queues). */
 uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *plan);

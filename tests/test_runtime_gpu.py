@@ -238,6 +238,37 @@ def test_window_stream_policy(human10, nt, dense, bw2):
         x.close()
 
 
+@pytest.mark.parametrize("waves", ["4", "8"])
+def test_k1b_workgroup_widths(human10, waves):
+    """K1b with 4 or 8 waves per tile workgroup (the plan picks 8 when the
+    launch fits one generation of them; GT_SMAX_K1B_WAVES forces either):
+    the oracle's records, whole table and a middle shard, two consecutive
+    runs each (the block-sum workgroups then sum 4 or 8 blocks)."""
+    esa, host = human10
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    old = os.environ.get("GT_SMAX_K1B_WAVES")
+    os.environ["GT_SMAX_K1B_WAVES"] = waves
+    try:
+        p = esa.plan(20)
+        q = esa.plan(20, N // 3, 2 * N // 3)
+    finally:
+        if old is None:
+            os.environ.pop("GT_SMAX_K1B_WAVES", None)
+        else:
+            os.environ["GT_SMAX_K1B_WAVES"] = old
+    r = esa.plan(20, N // 3, 2 * N // 3)
+    assert p.k1b_waves() == int(waves) and q.k1b_waves() == int(waves)
+    for _ in range(2):
+        p.run()
+        assert np.array_equal(p.fetch_triples(), want)
+        q.run()
+        r.run()
+        assert np.array_equal(q.fetch_triples(), r.fetch_triples())
+    for x in (p, q, r):
+        x.close()
+
+
 def test_block_sums_in_k1b_launch(human10):
     """K3's block sums added up by K1b's last workgroups (two buffers: each
     run adds into one, its K3 clears the other): the oracle's records over
