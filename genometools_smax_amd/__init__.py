@@ -176,8 +176,9 @@ def lib():
         L.gt_smax_build_id.restype = ctypes.c_char_p
         L.gt_smax_plan_scan_kernel.restype = ctypes.c_char_p
         L.gt_smax_plan_scan_kernel.argtypes = [vp]
-        L.gt_smax_plan_k1b_waves.restype = ctypes.c_uint32
-        L.gt_smax_plan_k1b_waves.argtypes = [vp]
+        if hasattr(L, "gt_smax_plan_k1b_waves"):   # (older builds loaded by the A/B tools lack it)
+            L.gt_smax_plan_k1b_waves.restype = ctypes.c_uint32
+            L.gt_smax_plan_k1b_waves.argtypes = [vp]
         L.gt_smax_dev_alloc_table.argtypes = [ci, u64, ctypes.POINTER(vp), cs, sz]
         L.gt_smax_dev_free_table.argtypes = [ci, vp]
         L.gt_smax_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtSmaxDevShard), u32, u64,

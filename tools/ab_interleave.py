@@ -45,19 +45,26 @@ sp = s.cuda_stream
 
 
 def timed(L, p, n=30):
+    """The step in ms, from a pass without K1 events (an event record between
+    K1 and K1b costs ~5.7 us, profiles/r04r/); K1 from the plan's events
+    around every K1 of a pass before it."""
+    import ctypes
     for _ in range(3):
         L.gt_smax_plan_run(p.plan, sp)
-    L.gt_smax_plan_timing(p.plan, n)           # K1 events of the timed runs
+    L.gt_smax_plan_timing(p.plan, n)           # K1 events of this pass
+    for _ in range(n):
+        L.gt_smax_plan_run(p.plan, sp)
+    torch.cuda.synchronize()
+    ms, k = ctypes.c_double(), ctypes.c_int()
+    L.gt_smax_plan_timing_read(p.plan, ctypes.byref(ms), ctypes.byref(k))
+    k1.setdefault(id(L), []).append(ms.value / max(k.value, 1))
+    L.gt_smax_plan_timing(p.plan, 0)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(n):
         L.gt_smax_plan_run(p.plan, sp)
     e1.record(s)
     torch.cuda.synchronize()
-    import ctypes
-    ms, k = ctypes.c_double(), ctypes.c_int()
-    L.gt_smax_plan_timing_read(p.plan, ctypes.byref(ms), ctypes.byref(k))
-    k1.setdefault(id(L), []).append(ms.value / max(k.value, 1))
     return e0.elapsed_time(e1) / n
 
 
