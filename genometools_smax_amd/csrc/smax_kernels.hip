@@ -510,8 +510,6 @@ __global__ void __launch_bounds__(256) smax_static_defer_kernel(SmaxScanArgs a, 
 // per-run resets (pending-plateau slot, pool cursor, deferral count) and the
 // boundary head.  Non-empty shards never launch it: K1 clears the pending
 // slot, the previous run's K3 resets the rest and K1b computes the head.
-__global__ void __launch_bounds__(64) smax_nop_kernel() {}
-
 __global__ void __launch_bounds__(64) smax_head_kernel(SmaxScanArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   a.bnd->pend_valid = 0;
@@ -2588,11 +2586,6 @@ struct GtSmaxPlan {
   uint32_t k1b_grid;         // K1b's tile workgroups (+1: the boundary head)
   uint32_t bs_wgs;           // block-sum workgroups appended to K1b's grid
   uint32_t k1b_nw;           // waves per K1b workgroup (4 or 8)
-  // diagnostic (GT_SMAX_FORK_PROBE): a one-lane kernel on a side stream
-  // forked before K1 and joined after it (untimed events) -- what a fork /
-  // join around K1 costs the step
-  hipStream_t side;
-  hipEvent_t evf, evj;
   uint32_t k3_split;         // K3 workgroups per block of 256 tiles (GT_SMAX_K3_SPLIT)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   uint32_t *err;
@@ -2738,11 +2731,6 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   }
   double tpc = smax_phase_clock();
   HIPCHK(hipSetDevice(shard->device));
-  if (getenv("GT_SMAX_FORK_PROBE")) {
-    HIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&p->evf, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&p->evj, hipEventDisableTiming));
-  }
   {
     int dev_cus = 0, per_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
@@ -3016,9 +3004,6 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
     if (bufs[i]) smax_dev_free(bufs[i]);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
   free(p->ev);
-  if (p->evf) (void) hipEventDestroy(p->evf);
-  if (p->evj) (void) hipEventDestroy(p->evj);
-  if (p->side) (void) hipStreamDestroy(p->side);
   free(p);
 }
 
@@ -3127,12 +3112,6 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
     const int slot = p->nslots && p->runs % ts == 0 ? (int) ((p->runs / ts) % (uint64_t) p->nslots)
                                                     : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
-    if (p->side) {
-      HIPCHK(hipEventRecord(p->evf, s));
-      HIPCHK(hipStreamWaitEvent(p->side, p->evf, 0));
-      hipLaunchKernelGGL(smax_nop_kernel, dim3(1), dim3(64), 0, p->side);
-      HIPCHK(hipEventRecord(p->evj, p->side));
-    }
     const dim3 g(p->grid), b(SMAX_K1_THREADS);
     if (!p->pk)
       hipLaunchKernelGGL(smax_scan_kernel_bytes, g, b, 0, s, a);
@@ -3146,7 +3125,6 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
       hipLaunchKernelGGL(p->dense ? smax_scan_kernel_dense : smax_scan_kernel, g, b, 0, s, a);
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
-    if (p->side) HIPCHK(hipStreamWaitEvent(s, p->evj, 0));
   }
   {
     // K1b over the static list and K1's deferrals, one launch; its first
