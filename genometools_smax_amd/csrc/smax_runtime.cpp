@@ -345,6 +345,10 @@ struct StageSeg {
 hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) {
   hipError_t e = hipSuccess;
   const uint64_t R = (uint64_t) ring_depth();
+  // GT_SMAX_TIMING: where the pass waits -- for a ring slot (its DMA, or a
+  // chunk still being pinned) or in the fills; the first chunks apart
+  static const bool timing = env_on("GT_SMAX_TIMING");
+  double t_wait = 0, t_fill = 0, t_wait4 = 0, t_fill4 = 0, tq = timing ? smax_phase_clock() : 0;
   for (auto &sg : segs) {
     sg.done = 0;
     sg.stop = false;
@@ -368,6 +372,12 @@ hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) 
     const uint64_t off = sg.done, n = std::min(kStage, sg.len - off);
     if (k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
     if (k >= R && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
+    if (timing) {
+      const double t = smax_phase_clock();
+      t_wait += t - tq;
+      if (k < 4) t_wait4 += t - tq;
+      tq = t;
+    }
     char *buf = (char *) c->pin[b];
     std::atomic<bool> ok{true};
     const uint64_t units = (n + 63) / 64;   // 64-byte units (whole packed groups)
@@ -375,6 +385,12 @@ hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) 
       const uint64_t lo = ulo * 64, hi = std::min(n, uhi * 64);
       if (lo < hi && !sg.fill(off + lo, hi - lo, buf + lo)) ok = false;
     });
+    if (timing) {
+      const double t = smax_phase_clock();
+      t_fill += t - tq;
+      if (k < 4) t_fill4 += t - tq;
+      tq = t;
+    }
     if (!ok) {
       sg.stop = true;
       if (sg.aborted) {
@@ -389,6 +405,14 @@ hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) 
     sg.done += n;
   }
   hipError_t e2 = hipStreamSynchronize(c->stream);
+  if (timing) {
+    const double t = smax_phase_clock();
+    fprintf(stderr, "[gt_smax timing]  h2d.waits   %8.2f ms (first 4 chunks %.2f)\n", t_wait * 1e3,
+            t_wait4 * 1e3);
+    fprintf(stderr, "[gt_smax timing]  h2d.fills   %8.2f ms (first 4 chunks %.2f)\n", t_fill * 1e3,
+            t_fill4 * 1e3);
+    fprintf(stderr, "[gt_smax timing]  h2d.drain   %8.2f ms\n", (t - tq) * 1e3);
+  }
   return e == hipSuccess ? e2 : e;
 }
 
@@ -707,12 +731,16 @@ void device_phase1(Call *C, int d) {
       const uint64_t blen = S.len;
       bool nondna = env_on("GT_SMAX_BYTE_BWT");
       void *planes = nullptr;
-      DCHK(alloc_table(&S.lcp, S.len));
+      // the LCP table's zero pads travel with its bytes in the upload (no
+      // memset kernels ahead of the first DMA: in a fresh process the first
+      // fill launch cost tens of ms before the ring started)
+      DCHK(smax_dev_alloc(&S.lcp, S.len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
       if (!nondna) {
         DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
         DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
       }
       DCHK(smax_dev_alloc(&S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo + 1)));
+      if (d == 0) smax_phase_mark(" h2d.alloc", &th);
       {
         // the plan's own buffers into the cache beside the upload
         GtSmaxDevShard g;
@@ -736,9 +764,18 @@ void device_phase1(Call *C, int d) {
         std::mutex smu;
         const char *lsrc = (const char *) in->lcptab + S.base;
         std::vector<StageSeg> segs;
-        segs.push_back({(char *) S.lcp + GT_SMAX_PAD_FRONT, S.len,
-                        [lsrc](uint64_t off, uint64_t n, char *buf) {
-                          memcpy(buf, lsrc + off, n);
+        const uint64_t llen = S.len;
+        segs.push_back({S.lcp, GT_SMAX_PAD_FRONT + S.len + GT_SMAX_PAD_BACK,
+                        [lsrc, llen](uint64_t off, uint64_t n, char *buf) {
+                          // [0, PAD_FRONT) zeros, the table, then PAD_BACK zeros
+                          const uint64_t t0 = GT_SMAX_PAD_FRONT, t1 = t0 + llen;
+                          const uint64_t a = std::max(off, t0), b = std::min(off + n, t1);
+                          if (off < t0) memset(buf, 0, std::min(off + n, t0) - off);
+                          if (a < b) memcpy(buf + (a - off), lsrc + (a - t0), b - a);
+                          if (off + n > t1) {
+                            const uint64_t z = std::max(off, t1);
+                            memset(buf + (z - off), 0, off + n - z);
+                          }
                           return true;
                         }, nullptr, 0, false});
         if (!nondna)
