@@ -677,6 +677,31 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
           "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
         : "memory");
+    } else if (a.dbg & (1u << 25)) {
+    // diagnostic ablation (diagnostic kernel only; records are wrong): the
+    // tile's LCP rows [l0, l0+TILE) aligned, without the two halo pieces
+    // and their extra 128-B lines -- the FETCH_SIZE and time they cost
+    const uint8_t *la = uni_ptr(a.lcp + l0);
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:0\n\t"
+        "global_load_lds_dwordx4 %2, %8 offset:1024\n\t"
+        "s_mov_b32 m0, %5\n\t"
+        "s_mov_b64 exec, %14\n\t"
+        "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
+        "s_mov_b64 exec, %11\n\t"
+        "s_mov_b32 m0, %6\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
+        SMAX_ASM_INFO
+        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep), "=&s"(ex)
+        : "v"(v16), "v"(v4), "s"(wl + SMAX_LH), "s"(wp), "s"(wv), "s"(iaddr), "s"(la), "s"(pb), "s"(vb),
+          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+        : "memory");
     } else {
     asm volatile(
         "s_mov_b32 %0, m0\n\t"

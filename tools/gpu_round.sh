@@ -22,6 +22,7 @@
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
 #   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
+#   fetchablate:V,... K1 FETCH_SIZE under GT_SMAX_DEBUG ablation bits at C3
 #   tilestats:CONFIG tools/tile_stats.py (active segments and records per K1 tile)
 #   abm:KIND:BASES:MINLEN:SHARD:LIB,... the in-tree library and several others, one process
 #   ab:LIB:KIND:BASES:MINLEN:SHARD   A/B of the in-tree library against LIB
@@ -123,6 +124,15 @@ for S in "$@"; do
           > "$O/pmca_$V.log" 2>&1)
         python3 tools/rocpd_summary.py pmc "$O/pmca_$V.json" smax_scan "c3" "$O/pmca_$V/p_results.db"
         rm -rf "$O/pmca_$V"
+      done ;;
+    fetchablate:*)
+      # fetchablate:V1,V2,... -- K1 FETCH_SIZE under GT_SMAX_DEBUG ablation bits (C3)
+      for V in $(echo "${S#fetchablate:}" | tr , ' '); do
+        (cd /tmp && GT_SMAX_DEBUG=$V TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE \
+          --kernel-include-regex smax_scan -d "$O/pmcf_$V" -o p -- python3 "$R/tools/k1_once.py" c3 2 \
+          > "$O/pmcf_$V.log" 2>&1)
+        python3 tools/rocpd_summary.py pmc "$O/pmcf_$V.json" smax_scan "c3" "$O/pmcf_$V/p_results.db"
+        rm -rf "$O/pmcf_$V"
       done ;;
     tilestats:*)
       timeout -k 10 600 python -u tools/tile_stats.py "${S#tilestats:}" > "$O/tilestats_${S#tilestats:}.txt" 2>&1 ;;
