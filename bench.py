@@ -21,7 +21,7 @@ by range (strong scaling): value = nonspecials / max-over-ranks step time.
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 "roofline" for K1 (algorithmic bytes = 2 B per suffix row + 16 B per .llv
 entry + 16 B per emitted record, SURVEY.md §8(d), over the average K1 duration from HIP events recorded
-on K1's stream around every 4th K1 launch of the timed region) and, at N = 1, "cpu_baseline": the
+on K1's stream around every 8th K1 launch of the timed region) and, at N = 1, "cpu_baseline": the
 oracle's single-core linear scan (oracle/smax_oracle.c orc_linsmax, the
 repo's CPU esa_linsmax restatement) timed on this host over the same tables.
 """
@@ -335,11 +335,11 @@ def main():
     t_prime = time.perf_counter() - t_pr
     for _ in range(args.warmup):
         step()
-    # K1's duration by HIP events around every 4th launch of the timed
-    # region (every 8th on N > 1 ranks): each timed launch pays two event
-    # records, ~5.7 us each on the box (~1 % of a C3 step, ~7 % of a 3/8
-    # shard's: profiles/r02z_event_overhead.txt, profiles/r04r/timeline_*)
-    ev_stride = 4 if world == 1 else 8
+    # K1's duration by HIP events around every 8th launch of the timed
+    # region: each timed launch pays two event records, ~5.7 us each on the
+    # box (~1 % of a C3 step, ~7 % of a 3/8 shard's when every launch is
+    # timed: profiles/r02z_event_overhead.txt, profiles/r04r/timeline_*)
+    ev_stride = 8
     plan.enable_timing((args.steps + ev_stride - 1) // ev_stride, ev_stride)
     torch.cuda.synchronize()
     if dist:
