@@ -16,7 +16,9 @@
 // K1b; the boundary record is final after it) and part 1 (compaction: K3):
 //   K1  smax_scan_kernel     the streaming kernel; its block 0 also clears
 //                            the pending-plateau slot of this run
-//   K1b smax_defer_wg_kernel one workgroup per deferred tile: the plan-time
+//   K1b smax_defer_wg_kernel<4|8> one workgroup of 4 or 8 waves per
+//                            deferred tile (8 when the launch fits one
+//                            generation of them): the plan-time
 //                            static list (shard edges, windows with more
 //                            .llv values than K1 stages), then K1's runtime
 //                            deferrals (exact-queue overflow, tiles with more
@@ -33,8 +35,8 @@
 // (smax_head_kernel -- "K0" -- runs only for an empty shard.)
 //
 // K1: every wave is an independent worker on 2048-row tiles (tile = wave id
-// + k * waves in grid; 8 generations of resident one-wave workgroups), no
-// workgroup barrier.  Per tile:
+// + k * waves in grid; 8-16 generations of resident one-wave workgroups, 6
+// per SIMD for the 2-plane windows), no workgroup barrier.  Per tile:
 //   window   LCP bytes (+16-row halos), packed BWT bit planes (DNA) or BWT
 //            bytes, and the window's .llv values (u16) go global -> LDS by
 //            LDS-DMA into one of the wave's two windows; the next tile's
@@ -46,7 +48,7 @@
 //            relations: 2- and 3-row intervals are decided in place (local
 //            maximum + left diversity from the bit planes); plateaus of
 //            >= 3 rows and 255 bytes (.llv values by rank) go to an exact
-//            queue, evaluated 64 starts at a time;
+//            queue of 56 starts, evaluated one per lane;
 //   output   owning lanes put packed 8-byte records in row order into an
 //            LDS staging slot; lane r then holds record r, and the tile's
 //            slot store (one coalesced instruction) and count are issued at
@@ -75,7 +77,7 @@ typedef uint8_t SmaxRank;
   "s_mov_b32 m0, %7\n\t"                    \
   "s_nop 0\n\t"                             \
   "global_load_lds_dword %3, %12 offset:0\n\t"
-#define SMAX_THREADS 256                              // 4 waves per K1b / K2 / K3 workgroup
+#define SMAX_THREADS 256                              // 4 waves per K3 workgroup (and the 4-wave K1b)
 // K1 workgroup: ONE wave.  K1's waves share nothing (no barrier, each its own
 // LDS windows), so a one-wave workgroup frees its LDS and wave slot as soon
 // as that wave is done -- with four waves per workgroup, a wave that ran out
@@ -142,7 +144,7 @@ struct SmaxScanArgs {
   unsigned long long *pool_cursor;   // reset by K0
   uint64_t *tile_off;        // per K1b tile: its first pool record (~0: pool full)
   uint32_t *tile_count;      // [tile][wave] record counts
-  uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), written by K2
+  uint32_t *block_sum;       // records per SMAX_CPB tiles (K3's workgroups), summed in K1b's launch
   GtSmaxBoundary *bnd;
   uint32_t *defer_list;      // tiles left to K1b (num_tiles capacity)
   uint2 *defer_info;         // beside each entry: the tile's llv_win word pair (K1b's
@@ -154,7 +156,7 @@ struct SmaxScanArgs {
   uint32_t k1_reset;         // combined placement without K0: K1 clears the pending slot
   uint32_t wide_cap;         // wide slots (SMAX_TILE / 2 records each) at the pool's start
   uint32_t dbg;              // diagnostic ablation bits (GT_SMAX_DEBUG), 0 in use
-  uint32_t bs_wgs;           // block-sum workgroups at the end of the K1b grid (0: K2 runs);
+  uint32_t bs_wgs;           // block-sum workgroups at the end of the K1b grid;
                              // K1 then marks its deferred and static tiles' counts
   unsigned long long *stamps; // diagnostic (GT_SMAX_STAMPS, diag build only): per-section
                               // s_memtime cycles of K1 summed over waves, [7] = tiles
@@ -3077,7 +3079,7 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s);
 static int plan_run_compact(GtSmaxPlan *p, hipStream_t s);
 
 // parts: bit 0 = the scan (K1 and K1b; the boundary record is final after
-// it), bit 1 = the ordered compaction (K2 block sums, K3).  gt_smax_plan_run
+// it), bit 1 = the ordered compaction (K3).  gt_smax_plan_run
 // enqueues both; a sharded caller can enqueue part 0, start the boundary
 // all-gather on its communication stream, then part 1 beside it.
 static int plan_run_parts(GtSmaxPlan *p, hipStream_t s, unsigned parts) {
