@@ -151,6 +151,179 @@ def cold_e2e(G, host, n, N, minlen, want, log, calls=2):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def main_maxpairs(args):
+    """F2 leg: maximal pairs, `gt repfind -l minlen` -- the
+    reference's default repfind path (/root/reference/src/match/esa-maxpairs.c:
+    476-513, hot loop esa-bottomup-maxpairs.inc:155-243) -- over tables
+    resident in HBM (the GPU suffixerator, suffix array kept).  A step is one
+    count pass + one emission pass in the reference's emission order
+    (gt_maxpairs_plan_count + gt_maxpairs_plan_emit_ordered: the pairs and
+    their order equal the reference's GtProcessmaxpairs calls).  One GPU:
+    maximal pairs do not shard by suffix-array range without a cross-shard
+    pair exchange (pairs span blocks of any length), so --gpus N runs N
+    independent replicas.  C3/C5 are refused: a 40-80 % repeat genome of
+    3-12 Gbp has ~1e11+ maximal pairs at minlen 20 (copies of a family pair
+    quadratically), TBs of output for the reference as for this path.
+
+    Algorithmic bytes per pass (the roofline's "achieved"): the two candidate
+    scans over the LCP bytes (count, then ordered write: 2 B/row), and per
+    candidate row (LCP >= minlen) its walk in both passes (exact LCP u32 +
+    BWT byte, + the 4-byte suffix in the emission pass: 13 B) and list/count/
+    offset entries (8 + 4 + 8 B), plus per pair its triple (24 B) and its
+    emission-order sort keys (3-4 x 8 B written, LSD passes: + 2 x 16 B per
+    key pass)."""
+    import numpy as np
+    import torch
+    import genometools_smax_amd as G
+
+    if args.config not in ("c2",) and not args.bases:
+        sys.exit("bench.py --path maxpairs: config %s has ~1e11+ maximal pairs (quadratic in the "
+                 "repeat copies); use --config c2 (or --bases for a uniform genome)" % args.config)
+    cfg = dict(CONFIGS[args.config])
+    if args.bases:
+        cfg["bases"] = args.bases
+        cfg["workload"] = cfg["workload"].replace(
+            cfg["workload"].split(" synthetic")[0], "%.3g bp" % args.bases)
+    if args.minlen:
+        cfg["minlen"] = args.minlen
+    minlen = cfg["minlen"]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(0 if args.one_gpu else local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # replicas: the barrier only
+    t0 = time.time()
+    text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    esa = G.DeviceEsa(text, device=torch.cuda.current_device(), keep_suftab=True)
+    t_esa = time.time() - t0
+    n, N = esa.totallength, esa.nonspecials
+    t0 = time.perf_counter()
+    plan = esa.maxpairs_plan(minlen)
+    torch.cuda.synchronize()
+    t_plan = time.perf_counter() - t0
+    plan.count()
+    total = plan.total()
+    ncand = plan.candidates()
+    out = torch.empty(max(3 * total, 3), dtype=torch.int64, device="cuda")
+    outr = torch.empty(max(3 * total, 3), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        plan.count(s)
+        plan.emit_ordered(out.data_ptr(), total, s)
+
+    def step_rows():
+        plan.count(s)
+        plan.emit(outr.data_ptr(), total, s)
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / args.steps
+
+    # priming (clock ramp), as the smax bench
+    t_pr = time.perf_counter()
+    while time.perf_counter() - t_pr < args.prime_s:
+        step_rows()
+        torch.cuda.synchronize()
+    el = timed(step)
+    el_rows = timed(step_rows)
+    if dist:
+        mx = torch.tensor([el, el_rows], dtype=torch.float64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        el, el_rows = float(mx[0]), float(mx[1])
+    nkeys = 4 if (N.bit_length() + 32) > 64 else 3
+    alg = (2 * N + ncand * (5 + 9 + 8 + 4 + 8) + total * (24 + 8 * nkeys + 2 * 16 * nkeys))
+    alg_rows = 2 * N + ncand * (5 + 9 + 8 + 4 + 8) + total * 24
+    in_mall = N < (256 << 20)      # the LCP bytes stay in the Infinity Cache across passes
+    parity = None
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O  # noqa: E402  (the checker, CPU baseline leg only)
+        h = esa.download(suftab=True)
+        lcp = h["lcptab"].astype(np.uint64)
+        if len(h["llvtab"]):
+            lcp[h["llvtab"][:, 0].astype(np.int64)] = h["llvtab"][:, 1]
+
+        class _E:
+            pass
+        e = _E()
+        e.lcp, e.suftab, e.text, e.nonspecials = lcp, h["suftab"], text, N
+        t0 = time.perf_counter()
+        ref = O.maxpairs(e, minlen)
+        t_cpu = time.perf_counter() - t0
+        got = out[: 3 * total].cpu().numpy().view(np.uint64).reshape(-1, 3)
+        gotr = outr[: 3 * total].cpu().numpy().view(np.uint64).reshape(-1, 3)
+
+        def norm(p):
+            q = np.stack([p[:, 0], np.minimum(p[:, 1], p[:, 2]), np.maximum(p[:, 1], p[:, 2])], 1)
+            return q[np.lexsort((q[:, 2], q[:, 1], q[:, 0]))]
+        # the ordered pass: the reference's calls, argument order included
+        same_order = len(ref) == total and bool(np.array_equal(ref, got))
+        same_set = len(ref) == total and bool(np.array_equal(norm(ref), norm(gotr)))
+        parity = {"reference_order_identical": same_order, "row_order_pass_same_pair_set": same_set}
+        cpu = {"value": N / t_cpu, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
+               "sample": "oracle orc_maxpairs (the gt_esa_bottomup_maxpairs stack walk restated, "
+                         "src/match/esa-bottomup-maxpairs.inc:136-264, 1 core) over all %d rows: %.2fs"
+                         % (N, t_cpu), "seconds": round(t_cpu, 3)}
+        cpu.update(host_cpu())
+        cpu["cgroup_cpus"] = cgroup_cpus()
+        del lcp, h, ref, got, gotr
+        if not (same_order and same_set):
+            log("FAIL: maxpairs differ from the oracle: %s" % parity)
+            plan.close()
+            esa.release()
+            sys.exit(1)
+    if rank == 0:
+        achieved = alg / el / 1e9
+        print(json.dumps({
+            "metric": "suffix-positions/s (maximal pairs, gt repfind -l %d)" % minlen,
+            "value": world * N / el, "unit": "suffix-positions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3,
+            "higher_is_better": True, "scaling": "weak" if world > 1 else None,
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": cfg["workload"], "minlen": minlen, "totallength": n,
+                       "nonspecials": N, "path": "maxpairs (F2)",
+                       "parallelism": "replicas x%d" % world if world > 1 else "single GPU"},
+            "step": "count pass + emission in the reference's order (gt_maxpairs_plan_count + "
+                    "gt_maxpairs_plan_emit_ordered)",
+            "maximal_pairs": total, "maximal_pairs_per_s": total / el, "candidate_rows": ncand,
+            "ms_per_step_row_order": el_rows * 1e3,
+            "roofline": {"bound": "mall" if in_mall else "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": None if in_mall else achieved / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_step": alg,
+                         "algorithmic_bytes_per_step_row_order": alg_rows,
+                         "achieved_row_order": alg_rows / el_rows / 1e9,
+                         "note": "whole-pass bytes over the pass time; per-kernel times: the "
+                                 "rocprofv3 kernel stats under profiles/"},
+            "parity": parity, "cpu_baseline": cpu,
+            "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2),
+                        "plan": round(t_plan, 3)}}), flush=True)
+    plan.close()
+    esa.release()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,7 +332,11 @@ def main():
     ap.add_argument("--prime-s", type=float, default=0.2,
                     help="untimed device priming before the warmup steps: passes for this many "
                          "seconds (clock ramp after the setup's idle periods)")
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="workload (default: c3 for --path smax, c2 for --path maxpairs)")
+    ap.add_argument("--path", default="smax", choices=["smax", "maxpairs"],
+                    help="smax: the hot path (BASELINE metric); maxpairs: the F2 leg, "
+                         "`gt repfind -l minlen` maximal pairs in the reference's emission order")
     ap.add_argument("--bases", type=lambda x: int(float(x)), default=None, help="override genome size")
     ap.add_argument("--minlen", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -186,6 +363,10 @@ def main():
                     help="plan from the byte BWT (plan-time packing) instead of the builder's "
                          "packed BWT")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "c2" if args.path == "maxpairs" else "c3"
+    if args.path == "maxpairs":
+        return main_maxpairs(args)
 
     import numpy as np
     import torch

@@ -157,6 +157,12 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise SmaxError("HIP library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+        if (os.environ.get("GT_SMAX_DEBUG") or os.environ.get("GT_SMAX_STAMPS")) and \
+                os.path.abspath(LIB_PATH) == os.path.join(_HERE, "lib", "libgtsmax_hip.so"):
+            # the production library reads no diagnostic switch: say so rather
+            # than run the production kernels under a diagnostic's name
+            raise SmaxError("GT_SMAX_DEBUG/GT_SMAX_STAMPS need the diagnostic build: "
+                            "GT_SMAX_LIB=genometools_smax_amd/lib/diag/libgtsmax_hip.so")
         # torch first: its bundled HIP runtime (soname libamdhip64.so.7) then
         # also serves this library.  Loaded the other way round, torch's
         # libtorch_hip (NEEDED libamdhip64.so, RPATH $ORIGIN) would map a
@@ -219,6 +225,8 @@ def lib():
         L.gt_maxpairs_plan_total.argtypes = [vp, ctypes.POINTER(u64)]
         L.gt_maxpairs_plan_emit.argtypes = [vp, vp, u64, vp]
         L.gt_maxpairs_plan_emit_ordered.argtypes = [vp, vp, u64, vp]
+        L.gt_maxpairs_plan_candidates.argtypes = [vp]
+        L.gt_maxpairs_plan_candidates.restype = u64
         L.gt_seqpos_map_dev.argtypes = [vp, u64, vp, u64, vp, ci, vp]
         L.gt_repfind_pairs_lines_dev.argtypes = [vp, u64, vp, u64, ci, _TEXT_CB, vp, cs, sz]
         L.gt_repfind_smax_lines.argtypes = [vp, u64, vp, u64, vp, u64, _TEXT_CB, vp, cs, sz]
@@ -548,6 +556,10 @@ class MaxpairsPlan:
         if lib().gt_maxpairs_plan_total(self._p, ctypes.byref(t)) != 0:
             raise SmaxError("gt_maxpairs_plan_total failed")
         return t.value
+
+    def candidates(self):
+        """Rows with a non-empty walk (LCP >= minlen), fixed at plan creation."""
+        return int(lib().gt_maxpairs_plan_candidates(self._p))
 
     def emit(self, out_ptr, capacity, stream=0):
         if lib().gt_maxpairs_plan_emit(self._p, out_ptr, int(capacity), stream) != 0:

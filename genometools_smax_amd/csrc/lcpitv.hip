@@ -554,6 +554,9 @@ struct LiHostTables {
 };
 
 static void li_host_free(LiHostTables *h) {
+  // the plan's kernels ran on the null stream (the staging ring synchronised
+  // its own stream): after them the tables go back to the runtime's cache
+  (void) hipStreamSynchronize(nullptr);
   smax_dev_free(h->lcp);
   smax_dev_free(h->llv);
   smax_dev_free(h->suf);

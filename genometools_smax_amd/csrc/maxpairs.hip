@@ -668,6 +668,8 @@ fail:
   return -1;
 }
 
+extern "C" uint64_t gt_maxpairs_plan_candidates(const GtMaxpairsPlan *p) { return p->ncand; }
+
 extern "C" int gt_maxpairs_plan_emit(GtMaxpairsPlan *p, uint64_t *out_dev, uint64_t capacity,
                                      void *stream) {
   char *errbuf = NULL;
@@ -758,11 +760,14 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   K.lbits = mp_bits(p->xmax);
   K.split = K.rowbits + K.lbits > 64;
   if (K.rowbits > 48) return -1;
-  MPCHK(hipMalloc(&tri, sizeof (uint64_t) * 3 * T));
-  MPCHK(hipMalloc(&keys, sizeof (uint64_t) * (K.split ? 4 : 3) * T));
-  MPCHK(hipMalloc(&ktmp, sizeof (uint64_t) * T));
-  MPCHK(hipMalloc(&pa, sizeof (uint64_t) * T));
-  MPCHK(hipMalloc(&pb, sizeof (uint64_t) * T));
+  // per-call temporaries from the runtime's caching allocator: repeated
+  // passes reuse them (a hipMalloc/hipFree of each per pass was most of a
+  // small table's ordered pass)
+  MPCHK(smax_dev_alloc((void **) &tri, sizeof (uint64_t) * 3 * T));
+  MPCHK(smax_dev_alloc((void **) &keys, sizeof (uint64_t) * (K.split ? 4 : 3) * T));
+  MPCHK(smax_dev_alloc((void **) &ktmp, sizeof (uint64_t) * T));
+  MPCHK(smax_dev_alloc((void **) &pa, sizeof (uint64_t) * T));
+  MPCHK(smax_dev_alloc((void **) &pb, sizeof (uint64_t) * T));
   K.k1 = keys;
   K.k2 = keys + T;
   K.k3 = keys + 2 * T;
@@ -779,7 +784,7 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   hipLaunchKernelGGL(mp_iota_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, pa, T);
   MPCHK(hipGetLastError());
   MPCHK(rocprim::radix_sort_pairs(nullptr, sb, ktmp, ktmp, pa, pb, (size_t) T, 0, 64, s));
-  MPCHK(hipMalloc(&st, sb ? sb : 16));
+  MPCHK(smax_dev_alloc(&st, sb ? sb : 16));
   {
     // stable LSD passes: r2, then (classes, r1), then the event [depth, then t]
     const int nk = K.split ? 4 : 3;
@@ -805,15 +810,15 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   MPCHK(hipGetLastError());
   MPCHK(hipStreamSynchronize(s));
   {
-    void *bufs[] = {tri, keys, ktmp, pa, pb, st};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) (void) hipFree(bufs[i]);
+    void *bufs[] = {tri, keys, ktmp, pa, pb, st};   // the pass is complete: back to the cache
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   return 0;
 fail:
   {
+    (void) hipStreamSynchronize(s);
     void *bufs[] = {tri, keys, ktmp, pa, pb, st};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   return -1;
 }
@@ -922,6 +927,7 @@ static int mp_host_run(const GtSmaxInput *in, unsigned int minlen, uint64_t **pa
   gt_maxpairs_plan_delete(plan);
   {
     void *bufs[] = {lcp, bwt, suf, llv, out, dsep};
+    (void) hipStreamSynchronize(nullptr);   // the plan's kernels (null stream) are done
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   return 0;
@@ -930,6 +936,7 @@ fail_quiet:
   gt_maxpairs_plan_delete(plan);
   {
     void *bufs[] = {lcp, bwt, suf, llv, out, dsep};
+    (void) hipStreamSynchronize(nullptr);   // the plan's kernels (null stream) are done
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   free(*pairs);

@@ -13,12 +13,22 @@
 // Per-device caching allocator of the host runtime: plan buffers and staged
 // tables come from it, so back-to-back calls in one process reuse device
 // memory instead of hipMalloc/hipFree of multi-GB buffers per call.
-// smax_dev_free returns a block to the cache (or frees it when caching is
-// off, GT_SMAX_NO_CACHE=1); gt_smax_release_cache() frees everything cached.
+// Blocks are stream-ordered: smax_dev_free returns a block whose work the
+// caller has already synchronised (a blocking copy, a stream or event wait)
+// to the cache at once; smax_dev_free_fenced returns one that work on some
+// streams may still use, with a fence (events recorded on those streams) that
+// the next smax_dev_alloc handing the block out waits for -- no call waits on
+// the whole device.  With caching off (GT_SMAX_NO_CACHE=1) a block is freed.
+// gt_smax_release_cache() frees everything cached.
 hipError_t smax_dev_alloc(void **ptr, size_t bytes);   // on the current device
 void smax_dev_free(void *ptr);                          // any device; NULL ok
-// in_use = false: the block never had work enqueued on it (no device wait)
-void smax_dev_free_ex(void *ptr, bool in_use);
+struct SmaxFence;
+// events on `streams` of the current device now (nstreams < 0: the whole
+// device, for callers that lost track of their streams); released with the
+// last block that holds it
+SmaxFence *smax_fence_create(const hipStream_t *streams, int nstreams);
+void smax_dev_free_fenced(void *ptr, SmaxFence *fence);  // NULL ptr ok
+void smax_fence_release(SmaxFence *fence);               // the creator's reference
 
 // Device records of a plan -> host (lcp, lb, rb) triples through the
 // device's pinned ring (the plan's work must be complete).

@@ -162,6 +162,17 @@ struct SmaxScanArgs {
                               // s_memtime cycles of K1 summed over waves, [7] = tiles
 };
 
+// Diagnostic ablation bits (GT_SMAX_DEBUG) exist only in the diagnostic build
+// (-DGT_SMAX_DIAG: lib/diag/libgtsmax_hip.so beside the production library,
+// loaded through GT_SMAX_LIB); the production library reads no such switch and
+// every diagnostic branch is a compile-time constant there.  Its test hooks
+// are plan-time choices (GT_SMAX_ALL_STATIC, GT_SMAX_BYTE_WINDOWS, ...).
+#ifdef GT_SMAX_DIAG
+#define SMAX_DBG(a) ((a).dbg)
+#else
+#define SMAX_DBG(a) (0u)
+#endif
+
 // K1 section stamps (diagnostic build): cycles since the previous stamp
 // into acc[k]; the production build compiles them away
 struct SmaxStamps {
@@ -489,7 +500,7 @@ __device__ static void compute_head(const SmaxScanArgs &a) {
 // 8-aligned index at or below the first, or a value >= 2^16) -- decided by
 // smax_llv_index_kernel into bit 31 of the tile's llv_win word.
 __host__ __device__ __forceinline__ bool static_deferred(const SmaxScanArgs &a, uint32_t wnf) {
-  return (wnf & SMAX_WIN_STATIC) != 0 || (a.dbg & 64u);
+  return (wnf & SMAX_WIN_STATIC) != 0 || (SMAX_DBG(a) & 64u);
 }
 
 // the llv_win words of the combined list's static entries (plan time)
@@ -679,7 +690,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
           "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
         : "memory");
-    } else if (a.dbg & (1u << 25)) {
+    } else if (SMAX_DBG(a) & (1u << 25)) {
     // diagnostic ablation (diagnostic kernel only; records are wrong): the
     // tile's LCP rows [l0, l0+TILE) aligned, without the two halo pieces
     // and their extra 128-B lines -- the FETCH_SIZE and time they cost
@@ -948,7 +959,7 @@ __device__ static bool eval_start(const Win &t, const SmaxScanArgs &a, uint64_t 
       }
     }
   }
-  if (slow && !(a.dbg & 32u)) {
+  if (slow && !(SMAX_DBG(a) & 32u)) {
     acc = false;
     cur = lcp_exact(t, cc);
     const bool start = !interior || lcp_exact(t, cc - 1) < cur;
@@ -1339,22 +1350,23 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   }
   SMAX_STAMP(st, 3);
   if (nL > DL) return UINT32_MAX;
-  if (a.dbg & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
+  if (SMAX_DBG(a) & 8u) return (Dm0 ^ Dm1 ^ Lm0 ^ Lm1) == 0x12345u ? 1u : 0u;   // ablation: classify only
   // exact evaluation of the queued starts (one per lane); accepted ones set
   // their row bit in their segment's mask
   bool wide = false;
-  if (nL != 0 && !(a.dbg & 4u)) {
+  if (nL != 0 && !(SMAX_DBG(a) & 4u)) {
     accw[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     static_assert(DL <= 64, "one exact start per lane");
     const uint32_t i = lane;
     uint32_t cur = 0, width = 0;
+    bool acc = false;
     if (i < nL) {
       const uint32_t e = ent[i];
       const uint32_t ro = e & 0x7ffu, si = (e >> 11) & 0x7fu;
       uint64_t j;
-      const bool acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
+      acc = eval_start(t, a, g0, sL, ro, e >> 18, true, &cur, &j);
       width = (uint32_t) (j - (g0 + ro) + 2);
       if (acc) atomicOr(&accw[si >> 1], 1u << ((ro & 15u) + 16u * (si & 1u)));
       wide = acc && j - (g0 + ro) + 2 > SMAX_PK_WMAX;
@@ -1364,7 +1376,9 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     __builtin_amdgcn_wave_barrier();
     if (i < nL) {
       res[i] = cur | (width << 16);
-      wide = wide || (cur | width) >= 65536u;
+      // only accepted starts' results are read back (rejected ones, e.g. a
+      // long plateau that is not a local maximum, need not defer the tile)
+      wide = wide || (acc && (cur | width) >= 65536u);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1385,7 +1399,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     const uint32_t Lpre = k == 0 ? Lpre0 : Lpre1, ro = k == 0 ? ro0 : ro1;
     const uint32_t si = k * 64 + lane;
     uint32_t acc = D;
-    if (Lq != 0 && !(a.dbg & 4u)) acc |= (accw[si >> 1] >> (16u * (si & 1u))) & 0xffffu;
+    if (Lq != 0 && !(SMAX_DBG(a) & 4u)) acc |= (accw[si >> 1] >> (16u * (si & 1u))) & 0xffffu;
     uint32_t tot;
     uint32_t pos = wcount + wave_excl((uint32_t) __popc(acc), &tot);
     uint32_t bits = acc;
@@ -1404,7 +1418,7 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
         lcp = rw & 0xffffu;
         width = rw >> 16;
       }
-      if (!(a.dbg & (4096u | (1u << 21))))
+      if (!(SMAX_DBG(a) & (4096u | (1u << 21))))
         stg[min(pos, (uint32_t) SMAX_SSLOT - 1u)] = (uint64_t) (ro + q) | ((uint64_t) width << 11) | ((uint64_t) lcp << 32);
       pos++;
     }
@@ -1480,7 +1494,7 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
   const uint4 v0 = lds_ld16(&t.L[so]);
   const uint4 v1 = lds_ld16(&t.L[so + 1024]);
   uint32_t segpre_bits = (seg_ge(v0, mf) ? 1u : 0u) | (seg_ge(v1, mf) ? 2u : 0u);
-  if (t.B == nullptr && !(a.dbg & 1u) &&
+  if (t.B == nullptr && !(SMAX_DBG(a) & 1u) &&
       __popcll(__ballot(segpre_bits & 1u)) + __popcll(__ballot(segpre_bits & 2u)) > 64) {
     // more active segments than one classification step holds (packed
     // windows): keep only segments where some row c can start a record --
@@ -1508,10 +1522,10 @@ __device__ __forceinline__ uint32_t prepare_window(Win &t, const SmaxScanArgs &a
 __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t tile, uint64_t rec,
                                                 uint32_t cnt) {
   const int lane = threadIdx.x & 63;
-  if (a.dbg & 4096u) return;
-  if ((uint32_t) lane < cnt && !(a.dbg & (1u << 21))) a.slots[tile * (uint64_t) SMAX_SSLOT + lane] = rec;
+  if (SMAX_DBG(a) & 4096u) return;
+  if ((uint32_t) lane < cnt && !(SMAX_DBG(a) & (1u << 21))) a.slots[tile * (uint64_t) SMAX_SSLOT + lane] = rec;
   if (lane == 0) {
-    if (!(a.dbg & (1u << 22))) a.tile_count[tile] = cnt;
+    if (!(SMAX_DBG(a) & (1u << 22))) a.tile_count[tile] = cnt;
   }
 }
 
@@ -1624,7 +1638,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
-    if (next < a.num_tiles && !((a.dbg & (1u << 23)) && it > 0)) {   // diagnostic: compute only
+    if (next < a.num_tiles && !((SMAX_DBG(a) & (1u << 23)) && it > 0)) {   // diagnostic: compute only
       const uint32_t n2 = next + stride <= last ? next + stride : last;
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
@@ -1635,8 +1649,8 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     t.halo_ff = SMAX_WIN_HALO(wnf);
     uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
     if constexpr (DIAG) SMAX_STAMP(st, 2);
-    if (a.dbg & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
-      if (a.dbg & (1u << 17)) {
+    if (SMAX_DBG(a) & (3u << 17)) {   // diagnostic: 64 extra dependent VALU / SALU per tile (cost model)
+      if (SMAX_DBG(a) & (1u << 17)) {
         uint32_t x = segpre_bits;
 #pragma unroll
         for (int q = 0; q < 64; q++) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x));
@@ -1648,7 +1662,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
         if (y == 12345) segpre_bits = 0;
       }
     }
-    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(a.dbg & 2u);
+    const bool wave_pre = __ballot(segpre_bits != 0) != 0 && !(SMAX_DBG(a) & 2u);
 
     // ---- detection, diversity, records (row order)
     uint32_t wcount = 0;
@@ -1657,7 +1671,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // run concurrently on the plan's side stream): K1 leaves them alone and
     // never waits on a global .llv read
     const bool stat = static_deferred(a, wnf);
-    bool defer = !stat && wave_pre && (a.dbg & 128u);
+    bool defer = !stat && wave_pre && (SMAX_DBG(a) & 128u);
     if (!stat && !defer && wave_pre) {
       wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave],
                                                     window_scratch(W), segpre_bits,
@@ -1934,7 +1948,7 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
     const uint4 lv = make_uint4(lq.x, lq.y, lq.z, lq.w);
     const uint4 bv = a.bwtpk != nullptr ? pk_expand(__builtin_nontemporal_load(&a.bwtpk[l0 / 16 + i]))
                                         : *reinterpret_cast<const uint4 *>(a.bwt + r0);
-    if (a.dbg & 524288u) {   // diagnostic stamp: every load of the thread has landed
+    if (SMAX_DBG(a) & 524288u) {   // diagnostic stamp: every load of the thread has landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (*tmark == 0) *tmark = __builtin_readcyclecounter();
     }
@@ -1962,7 +1976,7 @@ __device__ static void load_exact_window_wg(const SmaxScanArgs &a, uint64_t l0, 
   (void) wave_excl(f, &ftot);
   if ((threadIdx.x & 63) == 0 && ftot) atomicAdd(nff, ftot);
   __syncthreads();
-  if ((a.dbg & 1048576u) && *tmark == 0) *tmark = __builtin_readcyclecounter();
+  if ((SMAX_DBG(a) & 1048576u) && *tmark == 0) *tmark = __builtin_readcyclecounter();
 #pragma unroll
   for (int r = 0; r < EPT; r++) {
     const uint32_t e = (uint32_t) tid + (uint32_t) TH * r;
@@ -2075,10 +2089,10 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     // count; |65536 stops the clock after the window load, |131072 after the
     // ballots, |262144 after the evaluation; inside the load: |524288 when the
     // loads of thread 0 have landed, |1048576 after the LDS writes
-    const uint64_t t0 = (a.dbg & 32768u) ? __builtin_readcyclecounter() : 0;
+    const uint64_t t0 = (SMAX_DBG(a) & 32768u) ? __builtin_readcyclecounter() : 0;
     uint64_t tmark = 0;
     load_exact_window_wg<64 * NW>(a, l0, info, W, &sD.nff, &tmark);
-    if (a.dbg & 65536u) tmark = __builtin_readcyclecounter();
+    if (SMAX_DBG(a) & 65536u) tmark = __builtin_readcyclecounter();
     t.g0 = g0;
     t.L = to_lds<uint8_t>(W->L);
     t.B = to_lds<uint8_t>(W->B);
@@ -2104,7 +2118,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
       }
     }
     __syncthreads();
-    if ((a.dbg & 131072u) && tmark == 0) tmark = __builtin_readcyclecounter();
+    if ((SMAX_DBG(a) & 131072u) && tmark == 0) tmark = __builtin_readcyclecounter();
     // wave w: the starts of rows [XQ w, XQ w + XQ), evaluated; accepted
     // records compacted into LDS in row order
     const uint32_t q0 = (uint32_t) wave * XQ;
@@ -2140,7 +2154,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
     }
     if (lane == 0) sD.cnt[wave] = wc;
     __syncthreads();
-    if ((a.dbg & 262144u) && tmark == 0) tmark = __builtin_readcyclecounter();
+    if ((SMAX_DBG(a) & 262144u) && tmark == 0) tmark = __builtin_readcyclecounter();
     uint32_t total = 0, base = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -2148,7 +2162,7 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
       base += w < wave ? cw : 0u;
       total += cw;
     }
-    const bool nowrite = (a.dbg & (4096u | 32768u)) != 0;
+    const bool nowrite = (SMAX_DBG(a) & (4096u | 32768u)) != 0;
     if (threadIdx.x == 0) {
       // the tile's records: list entry i owns wide slot wide_slot0 + i (a
       // tile has at most SMAX_TILE / 2 records), else a run from the pool
@@ -2164,9 +2178,9 @@ smax_defer_wg_kernel(SmaxScanArgs a) {
         a.tile_off[tile] = off;
       }
       sD.off = off;
-      if (a.dbg & 32768u)
+      if (SMAX_DBG(a) & 32768u)
         a.tile_count[tile] = (uint32_t) (((tmark ? tmark : __builtin_readcyclecounter()) - t0) >> 4);
-      else if (!(a.dbg & 4096u))
+      else if (!(SMAX_DBG(a) & 4096u))
         a.tile_count[tile] = total | SMAX_SLOT_WIDE;   // 16-byte records
       if (a.bs_wgs && total != 0) {
         const uint32_t nb = (a.num_tiles + SMAX_CPB - 1) / SMAX_CPB;
@@ -2224,9 +2238,11 @@ __global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_b2_nt(Sma
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_b2_dense_nt(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowB2, false, true, true, true>(a);
 }
+#ifdef GT_SMAX_DIAG
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 6) smax_scan_kernel_diag(SmaxScanArgs a) {
   smax_scan_body<SmaxWindowB2, true, false, false, true>(a);
 }
+#endif
 __global__ void __launch_bounds__(SMAX_K1_THREADS, 4) smax_scan_kernel_bytes(SmaxScanArgs a) {
   smax_scan_body<SmaxWindow, false>(a);
 }
@@ -2479,7 +2495,7 @@ smax_llv16_kernel(const GtSmaxLlv *llv, uint64_t numllv, uint16_t *out) {
 __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
                                       uint64_t base, uint64_t tile_first, uint64_t begin,
                                       uint64_t end, uint32_t num_tiles, uint2 *win_out,
-                                      uint32_t *err) {
+                                      uint32_t *err, uint32_t all_static) {
   const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (t < numllv) {
     if (llv[t].value > 0xffffffffull) atomicOr(err, 1u);
@@ -2508,8 +2524,10 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
   const uint32_t wn = (uint32_t) (lo2 - lo);   // <= SMAX_LDSB rows
   // g0 < begin: the shard's first tile when begin is not tile-aligned (K1
   // assumes every row of its tiles is owned)
+  // all_static (GT_SMAX_ALL_STATIC, a test hook): every tile through K1b's
+  // exact path
   const bool stat = g0 < SMAX_LH || g0 < begin || g0 + SMAX_TILE + SMAX_RH > end || wide ||
-                    wn + ((uint32_t) lo & 7u) > SMAX_LLV_CAP;
+                    wn + ((uint32_t) lo & 7u) > SMAX_LLV_CAP || all_static;
   win_out[t] = make_uint2((uint32_t) lo, wn | (halo << 12) | (stat ? SMAX_WIN_STATIC : 0u));
 }
 
@@ -2578,6 +2596,7 @@ static void seterr(char *errbuf, size_t errlen, const char *fmt, ...) {
     }                                                                        \
   } while (0)
 
+#define SMAX_PLAN_STREAMS 4
 struct GtSmaxPlan {
   GtSmaxDevShard shard;
   unsigned int minlen;
@@ -2616,7 +2635,16 @@ struct GtSmaxPlan {
   uint32_t k3_split;         // K3 workgroups per block of 256 tiles (GT_SMAX_K3_SPLIT)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   uint32_t *err;
-  uint32_t dbg;
+  uint32_t dbg;              // GT_SMAX_DEBUG (diagnostic build only; 0 otherwise)
+  bool all_static;           // GT_SMAX_ALL_STATIC: every tile through K1b (test hook)
+  bool byte_windows;         // GT_SMAX_BYTE_WINDOWS: byte BWT windows, never packed (test hook)
+  uint32_t dev_cus;
+  // streams this plan's work was enqueued on (the fence of its buffers at
+  // delete: a freed block is reused only after that work, smax_dev_free_fenced);
+  // more than SMAX_PLAN_STREAMS distinct ones: the device is synchronised
+  hipStream_t streams[SMAX_PLAN_STREAMS];
+  int nstreams;
+  bool streams_overflow;
   // optional K1 timing: event pairs recorded around the scan kernel
   hipEvent_t *ev;
   unsigned long long *stamps;    // GT_SMAX_STAMPS: K1 section cycles (diag build)
@@ -2706,10 +2734,75 @@ hipError_t smax_plan_reserve(const GtSmaxDevShard *shard, uint64_t capacity) {
   void *blk[K] = {};
   hipError_t e = hipSuccess;
   for (size_t i = 0; i < K && e == hipSuccess; i++) e = smax_dev_alloc(&blk[i], sizes[i]);
-  for (size_t i = 0; i < K; i++) smax_dev_free_ex(blk[i], false);
+  for (size_t i = 0; i < K; i++) smax_dev_free(blk[i]);   // no work was enqueued on them
   int per_cu = 0;   // loads the code object (the first query or launch of a kernel does)
   if (e == hipSuccess)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, smax_scan_kernel_b2, SMAX_K1_THREADS, 0);
+  return e;
+}
+
+typedef void (*SmaxScanFn)(SmaxScanArgs);
+
+// The K1 variant a plan launches (its choices: packed or byte windows,
+// 2-plane or u64-group stream, dense .llv, non-temporal) and its name
+static SmaxScanFn plan_scan_fn(const GtSmaxPlan *p, const char **name) {
+  const char *nm;
+  SmaxScanFn f;
+  if (!p->pk) { nm = "smax_scan_kernel_bytes"; f = smax_scan_kernel_bytes; }
+#ifdef GT_SMAX_DIAG
+  else if (p->dbg) { nm = "smax_scan_kernel_diag"; f = smax_scan_kernel_diag; }
+#endif
+  else if (p->bw2 && p->dense && p->nt) { nm = "smax_scan_kernel_b2_dense_nt"; f = smax_scan_kernel_b2_dense_nt; }
+  else if (p->bw2 && p->dense) { nm = "smax_scan_kernel_b2_dense"; f = smax_scan_kernel_b2_dense; }
+  else if (p->bw2 && p->nt) { nm = "smax_scan_kernel_b2_nt"; f = smax_scan_kernel_b2_nt; }
+  else if (p->bw2) { nm = "smax_scan_kernel_b2"; f = smax_scan_kernel_b2; }
+  else if (p->dense) { nm = "smax_scan_kernel_dense"; f = smax_scan_kernel_dense; }
+  else { nm = "smax_scan_kernel"; f = smax_scan_kernel; }
+  if (name) *name = nm;
+  return f;
+}
+
+// K1's grid: 8 generations of resident workgroups of the launched variant --
+// the dispatcher hands a finished slot the next workgroup, which balances
+// tiles of uneven cost (measured 9 % faster than one persistent generation
+// on repeat-rich input) -- up to 16 for tables of more than ~18 tiles per
+// wave of one generation (the whole C3 table, profiles/r03i_*: 16 measured
+// 0.9 % shorter there, 6 % longer on an 8-way shard's 181 k tiles)
+static hipError_t plan_size_grid(GtSmaxPlan *p) {
+  int per_cu = 0;
+  const char *name = nullptr;
+  const SmaxScanFn f = plan_scan_fn(p, &name);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, SMAX_K1_THREADS, 0);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1) per_cu = 1;
+  const uint64_t resident = (uint64_t) p->dev_cus * (uint64_t) per_cu;
+  uint64_t gens = resident ? (uint64_t) p->num_tiles / (resident * (SMAX_K1_THREADS / 64) * 18) : 8;
+  gens = gens < 8 ? 8 : gens > 16 ? 16 : gens;
+  uint64_t g = resident * gens;
+  const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
+  if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
+  const uint64_t wg = ((uint64_t) p->num_tiles + SMAX_K1_THREADS / 64 - 1) /
+                      (SMAX_K1_THREADS / 64);                // workgroups with a tile per wave
+  p->grid = (uint32_t) (g < wg ? g : wg);
+  if (p->grid < 1) p->grid = 1;
+  if (getenv("GT_SMAX_VERBOSE"))
+    fprintf(stderr, "gt_smax: K1 %s, %u CUs x %d blocks/CU -> grid %u, %u tiles\n", name,
+            p->dev_cus, per_cu, p->grid, p->num_tiles);
+  return hipSuccess;
+}
+
+static void plan_note_stream(GtSmaxPlan *p, hipStream_t s) {
+  for (int i = 0; i < p->nstreams; i++)
+    if (p->streams[i] == s) return;
+  if (p->nstreams < SMAX_PLAN_STREAMS) p->streams[p->nstreams++] = s;
+  else p->streams_overflow = true;
+}
+
+// waits for the work this plan enqueued (its streams), not for the device
+static hipError_t plan_sync(GtSmaxPlan *p) {
+  hipError_t e = hipSetDevice(p->shard.device);
+  if (e == hipSuccess && p->streams_overflow) return hipDeviceSynchronize();
+  for (int i = 0; e == hipSuccess && i < p->nstreams; i++) e = hipStreamSynchronize(p->streams[i]);
   return e;
 }
 
@@ -2750,27 +2843,37 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   p->num_tiles = plan_tiles(shard, &p->tile_first);
   if (capacity == 0) capacity = (shard->end - shard->begin) / 64 + 4096;
   p->capacity = capacity;
+  p->dbg = 0;
+#ifdef GT_SMAX_DIAG
   {
     const char *d = getenv("GT_SMAX_DEBUG");
     p->dbg = d ? (uint32_t) strtoul(d, NULL, 0) : 0u;
-    // section stamps need the diagnostic build (a no-op ablation bit selects it)
+    // section stamps need the diagnostic kernel (a no-op ablation bit selects it)
     if (getenv("GT_SMAX_STAMPS")) p->dbg |= 1u << 30;
   }
+#endif
+  {
+    const char *v = getenv("GT_SMAX_ALL_STATIC");
+    p->all_static = (v && strtol(v, NULL, 0) != 0) || (p->dbg & 64u);
+    v = getenv("GT_SMAX_BYTE_WINDOWS");
+    p->byte_windows = (v && strtol(v, NULL, 0) != 0) || (p->dbg & 8192u);
+  }
+  plan_note_stream(p, nullptr);   // plan-time kernels: the null stream
   double tpc = smax_phase_clock();
   HIPCHK(hipSetDevice(shard->device));
   {
-    int dev_cus = 0, per_cu = 0;
+    int dev_cus = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount,
                                  shard->device));
     // packed BWT: the caller's (ESA builder, host staging), or packed here
     // from the byte table when the shard's alphabet is DNA ({0..3} plus
     // specials) -- a plan-time pass over the .bwt bytes
-    if (shard->bwtpk_dev != NULL && !((p->dbg & 8192u) && shard->bwt_dev != NULL)) {
+    if (shard->bwtpk_dev != NULL && !(p->byte_windows && shard->bwt_dev != NULL)) {
       p->bwtpk = const_cast<uint64_t *>(shard->bwtpk_dev);
       p->pk = true;
       p->pk_owned = false;
     } else if (shard->bwt_dev == NULL) {
-      seterr(errbuf, errlen, "byte BWT requested (GT_SMAX_DEBUG 8192) but the shard has none");
+      seterr(errbuf, errlen, "byte BWT windows requested (GT_SMAX_BYTE_WINDOWS) but the shard has none");
       goto fail;
     } else {
       p->pk_owned = true;
@@ -2785,32 +2888,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
       HIPCHK(hipMemcpy(&hflag, flag, sizeof hflag, hipMemcpyDeviceToHost));
       smax_dev_free(flag);
       smax_phase_mark(" pack_bwt", &tpc);
-      p->pk = hflag == 0 && !(p->dbg & 8192u);
+      p->pk = hflag == 0 && !p->byte_windows;
       if (!p->pk) { smax_dev_free(p->bwtpk); p->bwtpk = NULL; }
     }
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, !p->pk ? smax_scan_kernel_bytes : p->dbg ? smax_scan_kernel_diag
-                                                          : smax_scan_kernel_b2,
-        SMAX_K1_THREADS, 0));
-    if (per_cu < 1) per_cu = 1;
-    // 8 generations of resident workgroups: the dispatcher hands a finished
-    // slot the next workgroup, which balances tiles of uneven cost (measured
-    // 9 % faster than one persistent generation on repeat-rich input)
-    // (generations: 8, up to 16 for tables of more than ~18 tiles per wave of
-    // one generation -- the whole C3 table, profiles/r03i_*: 16 measured
-    // 0.9 % shorter there, 6 % longer on an 8-way shard's 181 k tiles)
-    const uint64_t resident = (uint64_t) dev_cus * (uint64_t) per_cu;
-    uint64_t gens = resident ? (uint64_t) p->num_tiles / (resident * (SMAX_K1_THREADS / 64) * 18) : 8;
-    gens = gens < 8 ? 8 : gens > 16 ? 16 : gens;
-    uint64_t g = resident * gens;
-    const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
-    if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
-    const uint64_t wg = ((uint64_t) p->num_tiles + SMAX_K1_THREADS / 64 - 1) /
-                        (SMAX_K1_THREADS / 64);                // workgroups with a tile per wave
-    p->grid = (uint32_t) (g < wg ? g : wg);
-    if (getenv("GT_SMAX_VERBOSE"))
-      fprintf(stderr, "gt_smax: K1 %s BWT, %d CUs x %d blocks/CU -> grid %u, %u tiles\n",
-              p->pk ? "packed" : "byte", dev_cus, per_cu, p->grid, p->num_tiles);
+    p->dev_cus = (uint32_t) (dev_cus > 0 ? dev_cus : 256);
     p->compact_grid = (uint32_t) (((uint64_t) p->num_tiles + SMAX_CPB - 1) / SMAX_CPB);
     {
       // K3: each block of 256 tiles split over two workgroups (each copies
@@ -2858,10 +2939,12 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(dalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
+#ifdef GT_SMAX_DIAG
   if (getenv("GT_SMAX_STAMPS")) {
     HIPCHK(dalloc(&p->stamps, sizeof (unsigned long long) * 8));
     HIPCHK(hipMemset(p->stamps, 0, sizeof (unsigned long long) * 8));
   }
+#endif
   // K1's runtime list; in the combined placement (mode 4) the static list is
   // copied to its front and K1 appends behind it
   HIPCHK(dalloc(&p->defer_list, sizeof (uint32_t) * (2 * (uint64_t) p->num_tiles + 1)));
@@ -2886,7 +2969,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                          dim3(256), 0, 0, shard->llv_dev, shard->numllv, p->llv16);
     hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
                        shard->llv_dev, shard->numllv, shard->base, p->tile_first, shard->begin,
-                       shard->end, p->num_tiles, p->llv_win, derr);
+                       shard->end, p->num_tiles, p->llv_win, derr, p->all_static ? 1u : 0u);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
   }
@@ -2917,8 +3000,11 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     HIPCHK(hipMemcpy(&nsp, cnt, sizeof nsp, hipMemcpyDeviceToHost));
     smax_dev_free(cnt);
     // a special group flags at most two windows
-    p->bw2 = b2 ? strtol(b2, NULL, 0) != 0
-                 : p->dbg != 0 || 2ull * nsp <= std::max<uint32_t>(p->num_tiles / 256u, 64u);
+    // (the diagnostic kernel streams the 2-plane form: bw2 whatever
+    // GT_SMAX_BW2 says while GT_SMAX_DEBUG/STAMPS select it)
+    p->bw2 = p->dbg != 0 ? true
+           : b2 ? strtol(b2, NULL, 0) != 0
+                : 2ull * nsp <= std::max<uint32_t>(p->num_tiles / 256u, 64u);
     if (p->bw2) {
       const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
       HIPCHK(dalloc(&p->bwt2, sizeof (uint32_t) * ngroups));
@@ -2980,6 +3066,9 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     p->nt = p->bw2 && (ntv ? strtol(ntv, NULL, 0) != 0
                            : stream_bytes > (256ull << 20) && p->num_tiles <= (1u << 19));
   }
+  // K1's grid, from the occupancy of the variant this plan launches (the
+  // u64-group kernels hold 5 waves per SIMD, the 2-plane ones 6)
+  HIPCHK(plan_size_grid(p));
   {
     // K1b: a workgroup per tile -- the static list plus K1's deferrals
     // (about one tile in 10^4) -- in one generation on all CUs where they fit;
@@ -3027,8 +3116,14 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
+  // stream-ordered: the buffers go back to the cache behind events on the
+  // streams this plan's work ran on (a plan closed right after run() must
+  // not hand them to the next allocation while K1..K3 still write them);
+  // nothing here waits, and no other stream of the device is involved
+  SmaxFence *fence = smax_fence_create(p->streams, p->streams_overflow ? -1 : p->nstreams);
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-    if (bufs[i]) smax_dev_free(bufs[i]);
+    if (bufs[i]) smax_dev_free_fenced(bufs[i], fence);
+  smax_fence_release(fence);
   for (int i = 0; i < 2 * p->nslots; i++) (void) hipEventDestroy(p->ev[i]);
   free(p->ev);
   free(p);
@@ -3086,6 +3181,7 @@ static int plan_run_parts(GtSmaxPlan *p, hipStream_t s, unsigned parts) {
   char *errbuf = NULL;
   size_t errlen = 0;
   HIPCHK(hipSetDevice(p->shard.device));
+  plan_note_stream(p, s);
   // K3 of part 1 resets the deferral list and pool cursor the next part 0's
   // K1/K1b start from: a second part 0 before that part 1 would run on stale
   // state (and part 1 without a part 0 would compact stale tiles)
@@ -3140,16 +3236,8 @@ static int plan_run_scan(GtSmaxPlan *p, hipStream_t s) {
                                                     : -1;
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot], s));
     const dim3 g(p->grid), b(SMAX_K1_THREADS);
-    if (!p->pk)
-      hipLaunchKernelGGL(smax_scan_kernel_bytes, g, b, 0, s, a);
-    else if (p->dbg)
-      hipLaunchKernelGGL(smax_scan_kernel_diag, g, b, 0, s, a);
-    else if (p->bw2 && p->dense)
-      hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_dense_nt : smax_scan_kernel_b2_dense, g, b, 0, s, a);
-    else if (p->bw2)
-      hipLaunchKernelGGL(p->nt ? smax_scan_kernel_b2_nt : smax_scan_kernel_b2, g, b, 0, s, a);
-    else
-      hipLaunchKernelGGL(p->dense ? smax_scan_kernel_dense : smax_scan_kernel, g, b, 0, s, a);
+    void *kargs_[] = {&a};
+    HIPCHK(hipLaunchKernel(reinterpret_cast<const void *>(plan_scan_fn(p, nullptr)), g, b, kargs_, 0, s));
     HIPCHK(hipGetLastError());
     if (slot >= 0) HIPCHK(hipEventRecord(p->ev[2 * slot + 1], s));
   }
@@ -3210,6 +3298,7 @@ extern "C" int gt_smax_plan_stitch(GtSmaxPlan *p, const GtSmaxBoundary *all_dev,
   char *errbuf = NULL;
   size_t errlen = 0;
   HIPCHK(hipSetDevice(p->shard.device));
+  plan_note_stream(p, (hipStream_t) stream);
   hipLaunchKernelGGL(smax_stitch_kernel, dim3(1), dim3(64), 0,
                      (hipStream_t) stream, all_dev, nshards, shard_index,
                      p->minlen, p->out, p->capacity, p->count);
@@ -3276,6 +3365,7 @@ extern "C" int gt_smax_plan_copy_boundary(GtSmaxPlan *p, void *dst_dev, void *st
   char *errbuf = NULL;
   size_t errlen = 0;
   HIPCHK(hipSetDevice(p->shard.device));
+  plan_note_stream(p, (hipStream_t) stream);
   HIPCHK(hipMemcpyAsync(dst_dev, p->bnd, sizeof (GtSmaxBoundary),
                         hipMemcpyDeviceToDevice, (hipStream_t) stream));
   return 0;
@@ -3287,8 +3377,7 @@ extern "C" int gt_smax_plan_fetch_count(GtSmaxPlan *p, uint64_t *count) {
   char *errbuf = NULL;
   size_t errlen = 0;
   uint32_t e = 0;
-  HIPCHK(hipSetDevice(p->shard.device));
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(plan_sync(p));
   HIPCHK(hipMemcpy(count, p->count, sizeof (uint64_t), hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(&e, p->err, sizeof e, hipMemcpyDeviceToHost));
   if (e != 0) {
@@ -3326,7 +3415,7 @@ extern "C" uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *p) {
 
 extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_t *deferred,
                                         uint32_t *ndeferred) {
-  if (hipSetDevice(p->shard.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
+  if (plan_sync(p) != hipSuccess) return -1;
   if (counts && hipMemcpy(counts, p->tile_count, sizeof (uint32_t) * (uint64_t) p->num_tiles,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
@@ -3351,16 +3440,14 @@ extern "C" uint32_t gt_smax_plan_k1b_waves(const GtSmaxPlan *p) { return p->k1b_
 
 extern "C" const char *gt_smax_plan_scan_kernel(const GtSmaxPlan *p) {
   // the selection of plan_run_scan
-  if (!p->pk) return "smax_scan_kernel_bytes";
-  if (p->dbg) return "smax_scan_kernel_diag";
-  if (p->bw2 && p->dense) return p->nt ? "smax_scan_kernel_b2_dense_nt" : "smax_scan_kernel_b2_dense";
-  if (p->bw2) return p->nt ? "smax_scan_kernel_b2_nt" : "smax_scan_kernel_b2";
-  return p->dense ? "smax_scan_kernel_dense" : "smax_scan_kernel";
+  const char *name = nullptr;
+  (void) plan_scan_fn(p, &name);
+  return name;
 }
 
 extern "C" int gt_smax_plan_stamps(GtSmaxPlan *p, unsigned long long *out8) {
   if (p->stamps == nullptr) return -1;
-  if (hipSetDevice(p->shard.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
+  if (plan_sync(p) != hipSuccess) return -1;
   return hipMemcpy(out8, p->stamps, sizeof (unsigned long long) * 8, hipMemcpyDeviceToHost) ==
                  hipSuccess ? 0 : -1;
 }

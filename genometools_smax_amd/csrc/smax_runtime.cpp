@@ -38,6 +38,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -80,10 +81,56 @@ bool env_on(const char *name) {
 
 // ------------------------------------------------------------ device cache
 
+}  // namespace
+
+// A freed block's fence: events recorded on the streams whose work may still
+// use it (or the whole device); the allocation that hands the block out
+// again waits for them once.  Reference-counted by the blocks holding it.
+struct SmaxFence {
+  int device = -1;
+  bool whole_device = false;
+  std::vector<hipEvent_t> ev;
+  std::atomic<int> refs{1};
+  std::mutex mu;
+  bool waited = false;
+  hipError_t result = hipSuccess;
+  hipError_t wait() {   // on any thread; restores its device
+    std::lock_guard<std::mutex> g(mu);
+    if (waited) return result;
+    int cur = -1;
+    (void) hipGetDevice(&cur);
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess && whole_device) e = hipDeviceSynchronize();
+    for (size_t i = 0; e == hipSuccess && i < ev.size(); i++) e = hipEventSynchronize(ev[i]);
+    if (cur >= 0) (void) hipSetDevice(cur);
+    result = e;
+    waited = true;
+    return e;
+  }
+  ~SmaxFence() {
+    int cur = -1;
+    (void) hipGetDevice(&cur);
+    (void) hipSetDevice(device);
+    for (hipEvent_t e : ev) (void) hipEventDestroy(e);
+    if (cur >= 0) (void) hipSetDevice(cur);
+  }
+};
+
+namespace {
+
+struct IdleBlock {
+  void *ptr;
+  SmaxFence *fence;   // null: no work pending on it
+};
+
+void fence_unref(SmaxFence *f) {
+  if (f != nullptr && f->refs.fetch_sub(1) == 1) delete f;
+}
+
 struct Pool {
   std::mutex mu;
   std::unordered_map<void *, std::pair<int, size_t>> live;   // ptr -> (device, bytes)
-  std::multimap<std::pair<int, size_t>, void *> idle;        // (device, bytes) -> ptr
+  std::multimap<std::pair<int, size_t>, IdleBlock> idle;     // (device, bytes) -> block
 };
 Pool &pool() {
   static Pool *p = new Pool;   // never destroyed: frees may come from atexit paths
@@ -103,7 +150,9 @@ void release_idle(int device) {   // pool.mu held
   for (auto it = P.idle.begin(); it != P.idle.end();) {
     if (device >= 0 && it->first.first != device) { ++it; continue; }
     (void) hipSetDevice(it->first.first);
-    (void) hipFree(it->second);
+    if (it->second.fence) (void) it->second.fence->wait();
+    (void) hipFree(it->second.ptr);
+    fence_unref(it->second.fence);
     it = P.idle.erase(it);
   }
   if (cur >= 0) (void) hipSetDevice(cur);
@@ -280,16 +329,51 @@ void par_for(uint64_t n, unsigned nt, F f) {
   cv.wait(g, [&] { return left == 0; });
 }
 
+// CPUs this process may actually run on: the cgroup's CPU quota
+// (/sys/fs/cgroup/cpu.max, "quota period"; v1: cpu.cfs_quota_us /
+// cpu.cfs_period_us) and the affinity mask, not hardware_concurrency()
+// (256 on the GPU box, whose cgroup allows 16)
+unsigned usable_cpus() {
+  static const unsigned n = [] {
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) hw = std::max(1, CPU_COUNT(&set));
+    double quota = -1.0;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = "";
+      long per = 0;
+      if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+        quota = strtod(q, NULL) / (double) per;
+      fclose(f);
+    } else if (FILE *f1 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+      long q = -1, per = 0;
+      if (fscanf(f1, "%ld", &q) == 1 && q > 0)
+        if (FILE *f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+          if (fscanf(f2, "%ld", &per) == 1 && per > 0) quota = (double) q / (double) per;
+          fclose(f2);
+        }
+      fclose(f1);
+    }
+    if (quota > 0) hw = std::min(hw, std::max(1u, (unsigned) (quota + 0.5)));
+    return hw;
+  }();
+  return n;
+}
+
+// Staging threads per device thread of a call over ndev devices.  One
+// device: 12 (h2d of the C3 tables 92-95 ms with 8, 83-88 ms with 12 or 16,
+// 124 ms with 4: profiles/r03zt/e2e_threads.txt).  Several devices fill
+// their rings at once, so they share the CPUs the cgroup allows
+// (usable_cpus): 16 on the GPU box -> 2 per device at 8 devices, where
+// 12 x 2 / 8 = 3 each had oversubscribed the quota 24 : 16.
+// GT_SMAX_COPY_THREADS: the total over all devices.
 unsigned copy_threads(int ndev) {
   const char *v = getenv("GT_SMAX_COPY_THREADS");
+  const unsigned nd = (unsigned) std::max(1, ndev);
+  const unsigned cpus = usable_cpus();
   unsigned total = v ? (unsigned) strtoul(v, NULL, 0) : 0u;
-  // 12 per device: h2d of the C3 tables 92-95 ms with 8, 83-88 ms with 12
-  // or 16, 124 ms with 4 (profiles/r03zt/e2e_threads.txt; the box's cgroup
-  // allows 16 CPUs)
-  if (total == 0) total = 12u * (unsigned) std::max(1, std::min(ndev, 2));
-  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  unsigned per = std::max(1u, std::min(total, hw) / (unsigned) std::max(1, ndev));
-  return std::min(per, 16u);
+  if (total == 0) total = nd == 1 ? std::min(12u, cpus) : cpus;
+  return std::min(16u, std::max(1u, total / nd));
 }
 
 // Host -> device through the context's ring of pinned chunks: fill(off, n,
@@ -912,6 +996,9 @@ void device_phase1(Call *C, int d) {
   }
 out:
   if (!voted) call_barrier(C);   // a failed slot still meets the others (no collective then)
+  // a failed slot may leave work queued on its stream: done before the
+  // exchange buffers go back to the cache
+  if (c != nullptr) (void) hipStreamSynchronize(c->stream);
   smax_dev_free(send);
   smax_dev_free(recv);
   smax_dev_free(all);
@@ -986,6 +1073,9 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
     C.first[d + 1] = C.first[d] + C.nshards / C.ndev + (d < C.nshards % C.ndev ? 1 : 0);
   C.err.assign(C.ndev, std::string());
   C.nt = copy_threads(C.ndev);
+  if (env_on("GT_SMAX_TIMING"))
+    fprintf(stderr, "[gt_smax timing] staging    %d device(s) x %u fill threads (usable CPUs %u), "
+            "%d shard(s)\n", C.ndev, C.nt, usable_cpus(), C.nshards);
   C.sh.resize(C.nshards);
   for (int s = 0; s < C.nshards; s++) {
     Shard &S = C.sh[s];
@@ -1051,6 +1141,14 @@ int run_call(const GtSmaxInput *in, unsigned minlen, int num_gpus, uint64_t **tr
       if (!m.empty()) { seterr(errbuf, errlen, "%s", m.c_str()); break; }
   free(C.trip);
   double tr = smax_phase_clock();
+  // every table was used on its device context's stream (uploads, plans):
+  // after those streams (idle already unless a slot failed) the blocks
+  // return to the cache
+  for (int d : C.devs) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    auto it = g_ctx.find(d);
+    if (it != g_ctx.end() && hipSetDevice(d) == hipSuccess) (void) hipStreamSynchronize(it->second->stream);
+  }
   for (auto &S : C.sh) {
     if (S.plan) gt_smax_plan_delete(S.plan);
     smax_dev_free(S.lcp);
@@ -1072,29 +1170,51 @@ hipError_t smax_dev_alloc(void **ptr, size_t bytes) {
   if (e != hipSuccess) return e;
   const size_t sz = round_block(bytes);
   Pool &P = pool();
-  std::lock_guard<std::mutex> g(P.mu);
-  // reuse an idle block of this device of at most twice the size
-  auto it = P.idle.lower_bound({dev, sz});
-  if (it != P.idle.end() && it->first.first == dev && it->first.second <= 2 * sz) {
-    *ptr = it->second;
-    P.live[*ptr] = it->first;
-    P.idle.erase(it);
+  for (;;) {
+    IdleBlock b{nullptr, nullptr};
+    std::pair<int, size_t> key;
+    {
+      std::lock_guard<std::mutex> g(P.mu);
+      // reuse an idle block of this device of at most twice the size
+      auto it = P.idle.lower_bound({dev, sz});
+      if (it != P.idle.end() && it->first.first == dev && it->first.second <= 2 * sz) {
+        b = it->second;
+        key = it->first;
+        P.idle.erase(it);
+      }
+    }
+    if (b.ptr == nullptr) break;
+    // the work still using the block (its fence) first; a fence that
+    // reports an error (a faulted kernel) retires the block
+    const hipError_t fe = b.fence ? b.fence->wait() : hipSuccess;
+    fence_unref(b.fence);
+    if (fe != hipSuccess) {
+      (void) hipGetLastError();
+      (void) hipFree(b.ptr);
+      continue;
+    }
+    std::lock_guard<std::mutex> g(P.mu);
+    *ptr = b.ptr;
+    P.live[b.ptr] = key;
     return hipSuccess;
   }
   e = hipMalloc(ptr, sz);
   if (e == hipErrorOutOfMemory) {   // give the cached blocks back and retry
     (void) hipGetLastError();
-    release_idle(dev);
+    {
+      std::lock_guard<std::mutex> g(P.mu);
+      release_idle(dev);
+    }
     e = hipMalloc(ptr, sz);
   }
   if (e != hipSuccess) { *ptr = nullptr; return e; }
+  std::lock_guard<std::mutex> g(P.mu);
   P.live[*ptr] = {dev, sz};
   return hipSuccess;
 }
 
-void smax_dev_free(void *ptr) { smax_dev_free_ex(ptr, true); }
-
-void smax_dev_free_ex(void *ptr, bool in_use) {
+namespace {
+void dev_free_impl(void *ptr, SmaxFence *fence) {
   if (ptr == nullptr) return;
   Pool &P = pool();
   std::pair<int, size_t> key;
@@ -1106,30 +1226,47 @@ void smax_dev_free_ex(void *ptr, bool in_use) {
     P.live.erase(it);
   }
   static const bool nocache = env_on("GT_SMAX_NO_CACHE");
-  int cur = -1;
-  (void) hipGetDevice(&cur);
-  (void) hipSetDevice(key.first);
   if (nocache) {
+    // hipFree waits for the device's work itself
+    int cur = -1;
+    (void) hipGetDevice(&cur);
+    (void) hipSetDevice(key.first);
     (void) hipFree(ptr);
-  } else {
-    // a block goes back to the cache only once every kernel that may still
-    // use it has finished (hipFree synchronised implicitly; a plan closed
-    // right after run() must not hand its buffers to the next allocation
-    // while K1..K3 still write them).  Outside the pool lock: other device
-    // threads keep allocating meanwhile.
-    // A device that reports an error (a faulted kernel) gets its block
-    // freed, not cached: nothing is known about what still touches it.
-    // (in_use false: a block no work was ever enqueued on -- no wait.)
-    if (in_use && hipDeviceSynchronize() != hipSuccess) {
-      (void) hipGetLastError();
-      (void) hipFree(ptr);
-    } else {
-      std::lock_guard<std::mutex> g(P.mu);
-      P.idle.insert({key, ptr});
-    }
+    if (cur >= 0) (void) hipSetDevice(cur);
+    return;
   }
-  if (cur >= 0) (void) hipSetDevice(cur);
+  if (fence) fence->refs.fetch_add(1);
+  std::lock_guard<std::mutex> g(P.mu);
+  P.idle.insert({key, IdleBlock{ptr, fence}});
 }
+}  // namespace
+
+void smax_dev_free(void *ptr) { dev_free_impl(ptr, nullptr); }
+
+void smax_dev_free_fenced(void *ptr, SmaxFence *fence) { dev_free_impl(ptr, fence); }
+
+SmaxFence *smax_fence_create(const hipStream_t *streams, int nstreams) {
+  SmaxFence *f = new SmaxFence;
+  (void) hipGetDevice(&f->device);
+  if (nstreams < 0) {
+    f->whole_device = true;
+    return f;
+  }
+  for (int i = 0; i < nstreams; i++) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(e, streams[i]) != hipSuccess) {
+      (void) hipGetLastError();
+      if (e) (void) hipEventDestroy(e);
+      f->whole_device = true;   // could not fence the stream: wait for everything
+      continue;
+    }
+    f->ev.push_back(e);
+  }
+  return f;
+}
+
+void smax_fence_release(SmaxFence *fence) { fence_unref(fence); }
 
 double smax_phase_clock() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();

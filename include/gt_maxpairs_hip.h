@@ -92,6 +92,12 @@ int gt_maxpairs_plan_count(GtMaxpairsPlan *plan, void *stream);
 /* Synchronises and returns the number of pairs of the last count pass. */
 int gt_maxpairs_plan_total(GtMaxpairsPlan *plan, uint64_t *total);
 
+/* Candidate rows of the plan (rows j >= 1 with LCP[j] >= minlen: the rows
+ * whose walk is not empty -- the rows the reference's traversal pushes into
+ * an lcp-interval of depth >= minlen, src/match/esa-bottomup-maxpairs.inc:
+ * 155-243); fixed at plan creation (the tables are immutable). */
+uint64_t gt_maxpairs_plan_candidates(const GtMaxpairsPlan *plan);
+
 /* Enqueue the emission pass: out_dev receives 3*total uint64
  * (len, pos1 < pos2) triples in suffix-array row order (by the later row,
  * then descending earlier row); capacity is in triples (pairs beyond it are

@@ -374,3 +374,33 @@ def test_host_entry_across_devices(human10, shards):
     got = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], esa.totallength,
                            esa.nonspecials, 20, shards)
     assert np.array_equal(got, want)
+
+
+DIAG_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "genometools_smax_amd", "lib", "diag", "libgtsmax_hip.so")
+
+
+@pytest.mark.skipif(not os.path.exists(DIAG_LIB), reason="diagnostic build not present")
+def test_diag_build_forces_two_plane_stream():
+    """The diagnostic kernel (diag build only) streams the 2-plane BWT:
+    GT_SMAX_STAMPS with GT_SMAX_BW2=0 must still plan the 2-plane buffers
+    (it once passed a null plane pointer to the diagnostic kernel), and the
+    records equal the oracle's.  Own process: the library is chosen at load."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, sys
+sys.path.insert(0, "tests")
+import genometools_smax_amd as G, oracle_lib as O
+from conftest import oracle_esa
+e = oracle_esa("at1MB")
+for m in (5, 20, 256):
+    got = G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, m, 2)
+    assert np.array_equal(got, O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, m)), m
+print("diag ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GT_SMAX_LIB=DIAG_LIB, GT_SMAX_BW2="0", GT_SMAX_STAMPS="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "diag ok" in r.stdout, r.stdout + r.stderr

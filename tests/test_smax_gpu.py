@@ -177,12 +177,12 @@ def test_exact_queue_overflow_falls_back():
             assert np.array_equal(_gpu(e, minlen, shards), want), (minlen, shards)
 
 
-@pytest.mark.parametrize("dbg", [64, 128, 8192])
-def test_detection_paths_agree(monkeypatch, dbg):
-    # GT_SMAX_DEBUG=128: every interior tile through the start-list path;
-    # 64: every tile through the exact edge path; 8192: byte BWT windows
-    # instead of packed ones.  Same answers required.
-    monkeypatch.setenv("GT_SMAX_DEBUG", str(dbg))
+@pytest.mark.parametrize("hook", ["GT_SMAX_ALL_STATIC", "GT_SMAX_BYTE_WINDOWS"])
+def test_detection_paths_agree(monkeypatch, hook):
+    # plan-time test hooks of the production library: GT_SMAX_ALL_STATIC
+    # sends every tile through K1b's exact path, GT_SMAX_BYTE_WINDOWS keeps
+    # byte BWT windows instead of packed ones.  Same answers required.
+    monkeypatch.setenv(hook, "1")
     e = oracle_esa("at1MB")
     for minlen in (5, 20, 256):
         assert np.array_equal(_gpu(e, minlen, 2), _cpu(e, minlen)), minlen
@@ -190,6 +190,33 @@ def test_detection_paths_agree(monkeypatch, dbg):
     e2 = O.Esa(_repetitive_text(rng, 60000, 0.001))
     for minlen in (3, 20, 300):
         assert np.array_equal(_gpu(e2, minlen), _cpu(e2, minlen)), minlen
+
+
+def test_runtime_deferrals_past_the_wide_slots():
+    """K1's runtime deferral list (exact-queue overflow) beyond the plan's
+    wide slots (max(256, tiles/256) of them): those K1b tiles take their
+    record runs from the pool cursor.  A triplicated-word text defers most of
+    its ~500 tiles at minlen 2; records equal the oracle's through the plan
+    and through the host entry point."""
+    rng = np.random.default_rng(12)
+    t = _triplicated_text(rng, 12000)
+    esa = G.DeviceEsa(t, device=0)
+    host = esa.download()
+    N = esa.nonspecials
+    for minlen in (2, 20):
+        want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen)
+        p = esa.plan(minlen)
+        p.run()
+        got = p.fetch_triples()
+        deferred = p.deferred_tiles()
+        p.close()
+        assert np.array_equal(got, want), minlen
+        if minlen == 2:
+            assert deferred > 256, deferred
+        got = G.enumerate_smax(host["lcptab"], host["llvtab"], host["bwttab"], esa.totallength, N,
+                               minlen, 3)
+        assert np.array_equal(got, want), minlen
+    esa.release()
 
 
 def test_protein_alphabet_uses_byte_windows():

@@ -18,7 +18,8 @@
 #   shards:W         tools/shard_step.py: per-rank step of a W-way C3 split
 #   e2ecold:CONFIG   tools/e2e_cold.py: first drop-in call of a fresh process (+ phases)
 #   e2esweep:CONFIG:K=V,..;..  e2ecold per runtime setting (fresh process each)
-#   mp:KIND          tools/bench_maxpairs.py (F2/F3, 100 Mbp of KIND, minlen 20)
+#   mp:CONFIG[:BASES]  bench.py --path maxpairs (F2, reference emission order)
+#   mpprof:CONFIG[:BASES] rocprofv3 --kernel-trace --stats of that run
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
 #   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
@@ -38,6 +39,9 @@ TAG=$1
 shift
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
+# the diagnostic build of the library (GT_SMAX_DEBUG / GT_SMAX_STAMPS exist
+# only there): make -C genometools_smax_amd builds it beside the production one
+DIAGLIB=$R/genometools_smax_amd/lib/diag/libgtsmax_hip.so
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
 SQ2="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS"
 for S in "$@"; do
@@ -98,7 +102,7 @@ for S in "$@"; do
         > "$O/abm_${KIND}_${SHARD//\//of}.txt" 2>&1 ;;
     ablate:*)
       # ablate:V1,V2,...  K1 time under GT_SMAX_DEBUG ablation bits at C3 (diag build)
-      timeout -k 10 600 python -u tools/k1_ablate.py human 3e9 "${S#ablate:}" > "$O/ablate.txt" 2>&1 ;;
+      GT_SMAX_LIB=$DIAGLIB timeout -k 10 600 python -u tools/k1_ablate.py human 3e9 "${S#ablate:}" > "$O/ablate.txt" 2>&1 ;;
     abenv:*)
       # abenv:K=V[;K=V]:KIND:BASES:MINLEN:SHARD -- plan A created under the
       # environment K=V (plan-time switches), B without; same library
@@ -106,7 +110,7 @@ for S in "$@"; do
       AB_ENV_A="${ENVA//;/,}" timeout -k 10 600 python -u tools/ab_interleave.py "$KIND" "$BASES" "$MINLEN" \
         genometools_smax_amd/lib/libgtsmax_hip.so 8 "$SHARD" > "$O/abenv_${KIND}_${ENVA//[=;]/_}_${SHARD//\//of}.txt" 2>&1 ;;
     stamps:*)
-      timeout -k 10 600 python -u tools/k1_stamps.py "${S#stamps:}" 5 > "$O/stamps_${S#stamps:}.txt" 2>&1 ;;
+      GT_SMAX_LIB=$DIAGLIB timeout -k 10 600 python -u tools/k1_stamps.py "${S#stamps:}" 5 > "$O/stamps_${S#stamps:}.txt" 2>&1 ;;
     rehearse:*)
       # rehearse:W[:BASES] -- bench.py --gpus W as W torchrun ranks on this
       # one GPU, boundary exchange staged through gloo (parity checked)
@@ -119,7 +123,7 @@ for S in "$@"; do
       # pmcablate:V1,V2,... -- K1 SQ counters under GT_SMAX_DEBUG ablation bits (C3)
       P="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM"
       for V in $(echo "${S#pmcablate:}" | tr , ' '); do
-        (cd /tmp && GT_SMAX_DEBUG=$V TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc $P \
+        (cd /tmp && GT_SMAX_LIB=$DIAGLIB GT_SMAX_DEBUG=$V TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc $P \
           --kernel-include-regex smax_scan -d "$O/pmca_$V" -o p -- python3 "$R/tools/k1_once.py" c3 2 \
           > "$O/pmca_$V.log" 2>&1)
         python3 tools/rocpd_summary.py pmc "$O/pmca_$V.json" smax_scan "c3" "$O/pmca_$V/p_results.db"
@@ -128,7 +132,7 @@ for S in "$@"; do
     fetchablate:*)
       # fetchablate:V1,V2,... -- K1 FETCH_SIZE under GT_SMAX_DEBUG ablation bits (C3)
       for V in $(echo "${S#fetchablate:}" | tr , ' '); do
-        (cd /tmp && GT_SMAX_DEBUG=$V TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE \
+        (cd /tmp && GT_SMAX_LIB=$DIAGLIB GT_SMAX_DEBUG=$V TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE \
           --kernel-include-regex smax_scan -d "$O/pmcf_$V" -o p -- python3 "$R/tools/k1_once.py" c3 2 \
           > "$O/pmcf_$V.log" 2>&1)
         python3 tools/rocpd_summary.py pmc "$O/pmcf_$V.json" smax_scan "c3" "$O/pmcf_$V/p_results.db"
@@ -136,6 +140,11 @@ for S in "$@"; do
       done ;;
     tilestats:*)
       timeout -k 10 600 python -u tools/tile_stats.py "${S#tilestats:}" > "$O/tilestats_${S#tilestats:}.txt" 2>&1 ;;
+    designstats:*)
+      # designstats:KIND:BASES:MINLEN -- classification steps per tile by filter / tile size
+      IFS=: read -r _ KIND BASES MINLEN <<< "$S"
+      timeout -k 10 600 python -u tools/tile_design_stats.py "$KIND" "$BASES" "$MINLEN" \
+        > "$O/designstats_${KIND}_$BASES.txt" 2>&1 ;;
     llvstats)
       for C in c3 c5; do
         timeout -k 10 300 python -u tools/llv_window_stats.py $C > "$O/llvstats_$C.txt" 2>&1
@@ -147,9 +156,19 @@ for S in "$@"; do
       python3 tools/rocpd_summary.py stats "$O/profshards_$W/p_results.db" "$O/kernel_stats_shards_$W.csv"
       rm -rf "$O/profshards_$W" ;;
     mp:*)
-      # F2/F3 secondary bench line (tools/bench_maxpairs.py): device steps + host entry points
-      timeout -k 10 600 python -u tools/bench_maxpairs.py --kind "${S#mp:}" > "$O/bench_maxpairs_${S#mp:}.json" \
-        2> "$O/bench_maxpairs_${S#mp:}.err" ;;
+      # mp:CONFIG[:BASES] -- the F2 leg, bench.py --path maxpairs (reference emission order)
+      IFS=: read -r _ C BASES <<< "$S"
+      timeout -k 10 600 python -u bench.py --path maxpairs --config "$C" ${BASES:+--bases $BASES} \
+        > "$O/bench_maxpairs_$C${BASES:+_$BASES}.json" 2> "$O/bench_maxpairs_$C${BASES:+_$BASES}.err" ;;
+    mpprof:*)
+      # mpprof:CONFIG[:BASES] -- rocprofv3 kernel stats of the F2 leg
+      IFS=: read -r _ C BASES <<< "$S"
+      T=$C${BASES:+_$BASES}
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/mpprof_$T" -o p -- \
+        python3 "$R/bench.py" --path maxpairs --config "$C" ${BASES:+--bases $BASES} --no-cpu-baseline \
+        > "$O/mpprof_bench_$T.json" 2> "$O/mpprof_bench_$T.err")
+      python3 tools/rocpd_summary.py stats "$O/mpprof_$T/p_results.db" "$O/kernel_stats_maxpairs_$T.csv"
+      rm -rf "$O/mpprof_$T" ;;
     e2ecold:*)
       # cold end-to-end: first call of the drop-in entry point in a fresh process
       timeout -k 10 900 python -u tools/e2e_cold.py "${S#e2ecold:}" 3 > "$O/e2e_cold_${S#e2ecold:}.json" \
@@ -163,6 +182,14 @@ for S in "$@"; do
         > "$O/tl_${SH//\//of}.log" 2>&1)
       python3 tools/step_timeline.py "$O/tl_${SH//\//of}" > "$O/timeline_${SH//\//of}.txt"
       rm -rf "$O/tl_${SH//\//of}" ;;
+    coldprobe)
+      # a fresh process's first HIP stream vs the memory the previous one held
+      timeout -k 10 600 bash tools/probe/cold_probe.sh "$O/cold_probe.jsonl" > "$O/cold_probe.log" 2>&1 ;;
+    e2eshards:*)
+      # e2eshards:W -- gt_smax_hip_enumerate_to_buffer(num_gpus=W) on this one
+      # device, 3 calls, GT_SMAX_TIMING phases per shard, records vs the oracle
+      SHARDS=${S#e2eshards:} CALLS=3 timeout -k 10 600 python -u tools/e2e_breakdown.py 3e9 \
+        > "$O/e2e_shards_${S#e2eshards:}.txt" 2>&1 ;;
     e2esweep:*)
       # e2esweep:CONFIG:K=V,..;K=V,.. -- first/second call per runtime setting
       IFS=: read -r _ C SETS <<< "$S"
