@@ -193,19 +193,20 @@ def test_detection_paths_agree(monkeypatch, hook):
 
 
 def test_runtime_deferrals_past_the_wide_slots():
-    """K1's runtime deferral list (exact-queue overflow) beyond the plan's
-    wide slots (max(256, tiles/256) of them): those K1b tiles take their
-    record runs from the pool cursor.  A triplicated-word text defers most of
-    its ~500 tiles at minlen 2; records equal the oracle's through the plan
-    and through the host entry point."""
+    """K1's runtime deferral list beyond the plan's wide slots (max(256,
+    tiles/256) of them): those K1b tiles take their record runs from the pool
+    cursor.  A uniform random text at minlen 2 has hundreds of short
+    supermaximal repeats per 2048-row tile, more than a K1 slot holds, so
+    every one of its ~730 tiles is deferred at run time; records equal the
+    oracle's through the plan and through the host entry point."""
     rng = np.random.default_rng(12)
-    t = _triplicated_text(rng, 12000)
+    t = rng.integers(0, 4, 1_500_000, dtype=np.uint8)
     esa = G.DeviceEsa(t, device=0)
     host = esa.download()
     N = esa.nonspecials
     for minlen in (2, 20):
         want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, minlen)
-        p = esa.plan(minlen)
+        p = esa.plan(minlen, capacity=len(want) + 4096)
         p.run()
         got = p.fetch_triples()
         deferred = p.deferred_tiles()

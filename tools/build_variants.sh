@@ -12,7 +12,7 @@ while [ $# -ge 2 ]; do
   NAME=$1; FLAGS=$2; shift 2
   mkdir -p "$R/abl/$NAME" "$M/build/var"
   ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I"$R/include" -I"$M/host" \
-      -DGT_SMAX_BUILD_ID="\"var-$NAME\"" $FLAGS -c -o "$M/build/var/$NAME.o" "$M/csrc/smax_kernels.hip" &&
+      -DGT_SMAX_BUILD_ID="\"var-$NAME\"" -mllvm -amdgpu-atomic-optimizer-strategy=None $FLAGS -c -o "$M/build/var/$NAME.o" "$M/csrc/smax_kernels.hip" &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o "$R/abl/$NAME/libgtsmax_hip.so" \
       "$M/build/var/$NAME.o" $OBJS -lpthread -ldl && echo "built abl/$NAME ($FLAGS)" ) &
   pids+=($!)
