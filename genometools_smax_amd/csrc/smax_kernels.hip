@@ -61,6 +61,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <chrono>
 #include <vector>
 
@@ -110,6 +111,10 @@ __host__ __device__ __forceinline__ uint64_t smax_bs_stride(uint64_t nblocks) {
 // (5 bits, <= 16), bit 31: K1 leaves the tile to the static K1b list
 #define SMAX_WIN_N(y) ((y) & 0xfffu)
 #define SMAX_WIN_HALO(y) (((y) >> 12) & 0x1fu)
+// (6 bits): the 16-byte lanes of u16 .llv values K1's window DMA moves (from
+// the 8-aligned index at or below the first entry, at most SMAX_LLV_CAP / 8),
+// computed at plan time -- K1 turns it into an EXEC mask with two scalar ops
+#define SMAX_WIN_LANES(y) (((y) >> 17) & 0x3fu)
 #define SMAX_WIN_STATIC 0x80000000u
 #define SMAX_SSLOT 64                                 // packed records per K1 tile slot
 #define SMAX_FFPV_DENSITY 0.006                       // .llv entries per row: dense K1 above
@@ -669,14 +674,13 @@ __device__ __forceinline__ const T *uni_ptr(const T *p) {
 
 template <bool NT, bool BW2 = false, typename WinT = SmaxWindowPk>
 __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t l0, uint32_t wl,
-                                                uint32_t lo, uint32_t n, const void *ibase,
+                                                uint32_t lo, uint32_t nyw, const void *ibase,
                                                 uint32_t iaddr, uint32_t v16, uint32_t v4) {
   const uint32_t wp = wl + (uint32_t) offsetof(WinT, P);
   const uint32_t wv = wl + (uint32_t) offsetof(WinT, val16);
   const uint8_t *vb = uni_ptr(reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u)));
-  const uint32_t nl8 = n == 0 ? 0u : (n + (lo & 7u) + 7) / 8;   // 16-byte lanes of values
-  const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;   // < 64
-  const uint64_t vmask = (1ull << nl) - 1;
+  // 16-byte lanes of values (plan time, llv_win word nyw)
+  const uint64_t vmask = (1ull << SMAX_WIN_LANES(nyw)) - 1;
   const uint64_t imask = 3ull;
   const uint8_t *ib = uni_ptr(reinterpret_cast<const uint8_t *>(ibase));
   uint32_t keep;
@@ -1650,7 +1654,7 @@ template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindow *w,
                                            uint32_t wl, uint32_t lo, uint32_t n, const uint2 *info,
                                            uint32_t iaddr, uint32_t v16, uint32_t v4) {
-  issue_window(a, l0, w, lo, n);
+  issue_window(a, l0, w, lo, SMAX_WIN_N(n));
   if ((threadIdx.x & 63) < 2) glds4(reinterpret_cast<const uint32_t *>(info) + (threadIdx.x & 63), iaddr);
 }
 
@@ -1830,7 +1834,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // the same value)
   issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase,
                       __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
-                      SMAX_WIN_N(__builtin_amdgcn_readfirstlane(sInfo[wave][0][1])),
+                      __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]),
                       a.llv_win + first_next, info1, v16, v4);
   // the previous tile's records (lane r holds record r) and count: stored
   // one iteration late, right after the window wait, so that those stores
@@ -1848,8 +1852,13 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       stv.prev = __builtin_amdgcn_s_memtime();
     }
   }
-  for (uint32_t it = 0;; it++) {
-    const uint32_t cur = it & 1u;
+  // the loop body twice per trip, once per window buffer: the buffer
+  // parity is a compile-time constant in each (no per-tile selects of the
+  // window, ring slot and LDS addresses; the scalar pipe, which the four
+  // SIMDs of a CU share, issues about 220 instructions per tile)
+  bool first = true;
+  auto step = [&](auto curc) -> bool {
+    constexpr uint32_t cur = decltype(curc)::value;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
     const uint32_t next = DYN ? t1 : tile + stride;
@@ -1891,12 +1900,12 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const uint32_t wnf = cur ? iw : iy;
     const uint32_t wn = SMAX_WIN_N(wnf);
     const uint32_t nlo = cur ? ix : iz;
-    const uint32_t nn = SMAX_WIN_N(cur ? iy : iw);
+    const uint32_t nn = cur ? iy : iw;   // the next tile's llv_win word (count, DMA lanes)
 
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
-    if (next < a.num_tiles && !((SMAX_DBG(a) & (1u << 23)) && it > 0)) {   // diagnostic: compute only
+    if (next < a.num_tiles && !((SMAX_DBG(a) & (1u << 23)) && !first)) {   // diagnostic: compute only
       const uint32_t n2 = DYN ? (t2 != SMAX_NO_TILE ? t2 : last)
                               : (next + stride <= last ? next + stride : last);
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
@@ -1980,7 +1989,12 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       t1 = t2;
       t2 = SMAX_NO_TILE;   // filled from the claim in flight (pend) at the next wait
     }
-    if (tile >= a.num_tiles) break;
+    first = false;
+    return tile < a.num_tiles;
+  };
+  for (;;) {
+    if (!step(std::integral_constant<uint32_t, 0>())) break;
+    if (!step(std::integral_constant<uint32_t, 1>())) break;
   }
   if (ptile != ~0u) smax_flush_tile(a, ptile, prec, pcnt);
   glds_wait();
@@ -2807,7 +2821,10 @@ __global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
   // exact path
   const bool stat = g0 < SMAX_LH || g0 < begin || g0 + SMAX_TILE + SMAX_RH > end || wide ||
                     wn + ((uint32_t) lo & 7u) > SMAX_LLV_CAP || all_static;
-  win_out[t] = make_uint2((uint32_t) lo, wn | (halo << 12) | (stat ? SMAX_WIN_STATIC : 0u));
+  const uint32_t nl8 = wn == 0 ? 0u : (wn + ((uint32_t) lo & 7u) + 7u) / 8u;
+  const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;
+  static_assert(SMAX_LLV_CAP / 8 < 64, "lane count fits SMAX_WIN_LANES");
+  win_out[t] = make_uint2((uint32_t) lo, wn | (halo << 12) | (nl << 17) | (stat ? SMAX_WIN_STATIC : 0u));
 }
 
 // ------------------------------------------------------------ stitch
