@@ -1209,10 +1209,12 @@ __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r
   uint32_t UP = r.UP, EQ = r.EQ;
   uint32_t FFP = r.F18 & ((r.F18 << 1) | (r.pb == 255u ? 1u : 0u));    // 255 after 255
   bool unresolved = false;
-  if (r.F18 != 0 && t.rank == nullptr) {
-    unresolved = true;                      // no ranks (inconsistent index): exact queue
-  } else if (FFPV && FFP != 0 && t.staged_all) {
-    ffp_resolve(relm, r.F18, FFP, crank, &UP, &EQ);
+  // (the rank tests first: wave-uniform, so a tile without .llv values skips
+  // the per-row loop's exec bookkeeping)
+  if (t.rank == nullptr) {
+    unresolved = r.F18 != 0;                // no ranks (inconsistent index): exact queue
+  } else if (FFPV && t.staged_all) {
+    if (FFP != 0) ffp_resolve(relm, r.F18, FFP, crank, &UP, &EQ);
   } else {
     while (FFP) {
       const int q = __builtin_ctz(FFP);
@@ -1229,6 +1231,8 @@ __device__ __forceinline__ void classify_fin(const Win &t, uint32_t so, SegRel r
   const uint32_t eqn1 = EQ >> 2, dn1 = ~((UP | EQ) >> 2);          // c+1 vs c+2
   const uint32_t D = A & dn & 0xffffu;
   const uint32_t D3 = A & eqn & dn1 & 0xffffu;
+  // (the early exit pays for its exec bookkeeping on the plant genome, whose
+  // active segments often hold no start: profiles/s5/output_loop_ab_*.txt)
   if (A == 0) {
     *Dm = 0;
     *D3m = 0;
@@ -1333,45 +1337,50 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   for (int k = 0; k < 2; k++) {
     if ((uint32_t) k >= nsteps) break;
     const uint32_t i = k * 64 + lane;
-    uint32_t D = 0, D3 = 0, Lq = 0, ro = 0;
-    SegRel rel;                     // fields other than FF read only for i < nseg
-    rel.FF = 0;
-    if (i < nseg) {
-      const uint32_t sid = (k == 0 && (uint32_t) lane < n0) ? segA : segB;
-      ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
-      classify_rel(t, SMAX_LH + ro, mf, rel);
-    }
+    uint32_t D = 0, D3 = 0, Lq = 0;
+    // every lane classifies a segment (no exec-mask bookkeeping): lanes
+    // past the active ones hold an inactive segment or, in the second step,
+    // one the first step already took -- their masks are cleared, so they
+    // add no start, record or rank, and their rank entry goes to the left
+    // halo chunk (set after the steps)
+    const bool act = i < nseg;
+    const uint32_t sid = (k == 0 && (uint32_t) lane < n0) ? segA : segB;
+    const uint32_t ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
+    SegRel rel;
+    classify_rel(t, SMAX_LH + ro, mf, rel);
+    rel.GE = act ? rel.GE : 0u;
+    rel.FF = act ? rel.FF : 0u;
+    rel.F18 = act ? rel.F18 : 0u;
     uint32_t crank = 0;
     if (rank != nullptr) {
       uint32_t ftot;
       crank = fbase + wave_excl((uint32_t) __popc(rel.FF), &ftot);
-      if (i < nseg) rank[(SMAX_LH + ro) >> 4] = (SmaxRank) crank;
+      rank[act ? (SMAX_LH + ro) >> 4 : 0u] = (SmaxRank) crank;
       fbase += ftot;
     }
     if constexpr (FFPV) {
-      const uint32_t ffp = i < nseg ? rel.F18 & ((rel.F18 << 1) | (rel.pb == 255u ? 1u : 0u)) : 0u;
+      const uint32_t ffp = rel.F18 & ((rel.F18 << 1) | (rel.pb == 255u ? 1u : 0u));
       if (!relm_ready && rank != nullptr && __ballot(ffp != 0) != 0) {
         ffp_masks(t, relm);
         relm_ready = true;
       }
     }
-    if (i < nseg) {
-      // every row is owned: tiles holding rows before `begin` are static K1b
-      classify_fin<FFPV>(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq, relm);
-    }
+    // every row is owned: tiles holding rows before `begin` are static K1b
+    classify_fin<FFPV>(t, SMAX_LH + ro, rel, crank, all_exact, &D, &D3, &Lq, relm);
     const uint32_t F = rel.FF;
     // one scan for the queue positions (low half) and the decided records
     // before this lane (high half): <= 1024 each, no carry between them
     uint32_t tot2;
     const uint32_t excl2 = wave_excl((uint32_t) __popc(Lq) | ((uint32_t) __popc(D) << 16), &tot2);
     const uint32_t excl = excl2 & 0xffffu, tot = tot2 & 0xffffu;
-    if (nL + tot <= DL && Lq != 0) {
+    if (nL + tot <= DL) {
+      // queue entry: row in the tile (11 bits) | its .llv rank << 18
       uint32_t pos = nL + excl, bits = Lq;
       while (bits) {
         const int q = __builtin_ctz(bits);
         bits &= bits - 1;
         const uint32_t rk = ((F >> q) & 1u) ? crank + (uint32_t) __popc(F & ((1u << q) - 1)) : 0u;
-        ent[pos++] = (ro + (uint32_t) q) | (i << 11) | (rk << 18);
+        ent[pos++] = (ro + (uint32_t) q) | (rk << 18);
       }
     }
     if (k == 0) { Dm0 = D; W30 = D3; F0 = F; R0 = crank; Lm0 = Lq; Lpre0 = nL + excl; Dpre0 = nD + (excl2 >> 16); ro0 = ro; }
@@ -1435,7 +1444,6 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
     while (bits) {
       const int q = __builtin_ctz(bits);
       bits &= bits - 1;
-      // packed slot record: row in the tile + 1 (11 bits) | width (21) | lcp (32)
       uint32_t lcp, width;
       if ((D >> q) & 1u) {
         const uint32_t b = sL[SMAX_LH + ro + q];
@@ -1786,7 +1794,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // per wave: wave_detect_direct's queue of exact starts (then their
   // packed results) and accepted masks (the tile's staged records go to
   // the current window's BWT region once it is dead: window_scratch)
-  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_K1_SQ ? SMAX_SQ_CAP / 2 + 16 : SMAX_DLIST + 64];
+  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_K1_SQ ? SMAX_SQ_CAP / 2 + 16 : SMAX_DLIST + 16];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1961,15 +1969,21 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
     }
-    if (lane == 0 && defer) {
-      const uint32_t k = atomicAdd(a.defer_count, 1u);
-      a.defer_list[k] = (uint32_t) tile;
-      a.defer_info[k] = make_uint2(wlo, wnf);
+    // (uniform tests first, then lane 0: a `lane == 0 && flag` condition
+    // costs exec-mask bookkeeping on every tile, taken or not)
+    if (defer) {
+      if (lane == 0) {
+        const uint32_t k = atomicAdd(a.defer_count, 1u);
+        a.defer_list[k] = (uint32_t) tile;
+        a.defer_info[k] = make_uint2(wlo, wnf);
+      }
     }
     // K1b's tiles: their count words carry the wide bit (K1b writes
     // count | wide), so the block sums in K1b's launch skip them and K1b adds
     // their records itself
-    if (lane == 0 && (stat || defer) && a.bs_wgs) a.tile_count[tile] = SMAX_SLOT_WIDE;
+    if ((stat || defer) && a.bs_wgs) {
+      if (lane == 0) a.tile_count[tile] = SMAX_SLOT_WIDE;
+    }
     if (!stat && !defer) {
       // the tile's records move from the LDS staging to one lane each; they
       // are stored at the start of the next iteration (see above)

@@ -214,6 +214,31 @@ hipError_t ring_ready(DevCtx *c) {
   }
   return e;
 }
+// A chunk whose pinning failed (pinned-memory pressure) shrinks the ring to
+// the chunks pinned before it instead of failing every later transfer on
+// the device: chunk 0 is pinned with the context, the helper stops at its
+// first failure, so the usable chunks are always a prefix.
+bool chunk_usable(DevCtx *c, int i) { return chunk_ready(c, i) == hipSuccess && c->pin[i] != nullptr; }
+// ring slot of the k-th chunk of an upload: the first R chunks take fresh
+// slots as their pinning completes (R drops to the pinned prefix on a
+// failure), later ones wait for the slot's previous DMA
+hipError_t ring_slot(DevCtx *c, uint64_t k, uint64_t &R, int *slot) {
+  if (k < R) {
+    if (chunk_usable(c, (int) k)) {
+      *slot = (int) k;
+      return hipSuccess;
+    }
+    R = k;   // >= 1
+  }
+  *slot = (int) (k % R);
+  return hipEventSynchronize(c->ev[*slot]);
+}
+// download buffers: 2 (chunk k+1's DMA beside chunk k's copy-out), 1 when
+// the second chunk could not be pinned
+int d2h_buffers(DevCtx *c, uint64_t nch) {
+  if (nch <= 1 || ring_depth() < 2) return 1;
+  return chunk_usable(c, 1) ? 2 : 1;
+}
 
 std::mutex g_ctx_mu;
 std::map<int, DevCtx *> g_ctx;
@@ -237,8 +262,14 @@ hipError_t ctx_get(int device, DevCtx **out) {
     for (int i = 1; i < ring_depth(); i++) c->pin_done[i] = c->pinned[i].get_future().share();
     std::thread([c, device] {
       hipError_t r = hipSetDevice(device);
+      // GT_SMAX_PIN_FAIL_AT=i: chunk i and later report a pinning failure
+      // (tests: the ring degrades instead of failing the device)
+      const char *fa = getenv("GT_SMAX_PIN_FAIL_AT");
+      const int fail_at = fa ? (int) strtol(fa, NULL, 0) : kRingMax;
       for (int i = 1; i < ring_depth(); i++) {
+        if (r == hipSuccess && i >= fail_at) r = hipErrorOutOfMemory;
         if (r == hipSuccess) r = hipHostMalloc(&c->pin[i], kStage, hipHostMallocDefault);
+        if (r != hipSuccess) c->pin[i] = nullptr;
         c->pinned[i].set_value(r);
       }
     }).detach();
@@ -384,12 +415,11 @@ hipError_t stage_h2d(DevCtx *c, void *dst, uint64_t len, unsigned nt, Fill fill,
                      bool *aborted) {
   hipError_t e = hipSuccess;
   if (aborted) *aborted = false;
-  const uint64_t R = (uint64_t) ring_depth();
+  uint64_t R = (uint64_t) ring_depth();
   for (uint64_t off = 0, k = 0; e == hipSuccess && off < len; off += kStage, k++) {
-    const int b = (int) (k % R);
+    int b;
     const uint64_t n = std::min(kStage, len - off);
-    if (k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
-    if (k >= R && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
+    if ((e = ring_slot(c, k, R, &b)) != hipSuccess) break;
     char *buf = (char *) c->pin[b];
     std::atomic<bool> ok{true};
     // split at 64-byte units (whole packed groups for the BWT fill)
@@ -428,7 +458,7 @@ struct StageSeg {
 
 hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) {
   hipError_t e = hipSuccess;
-  const uint64_t R = (uint64_t) ring_depth();
+  uint64_t R = (uint64_t) ring_depth();
   // GT_SMAX_TIMING: where the pass waits -- for a ring slot (its DMA, or a
   // chunk still being pinned) or in the fills; the first chunks apart
   static const bool timing = env_on("GT_SMAX_TIMING");
@@ -452,10 +482,9 @@ hipError_t stage_h2d_multi(DevCtx *c, std::vector<StageSeg> &segs, unsigned nt) 
     }
     if (pick < 0) break;
     StageSeg &sg = segs[(size_t) pick];
-    const int b = (int) (k % R);
+    int b;
     const uint64_t off = sg.done, n = std::min(kStage, sg.len - off);
-    if (k < R && (e = chunk_ready(c, b)) != hipSuccess) break;
-    if (k >= R && (e = hipEventSynchronize(c->ev[b])) != hipSuccess) break;
+    if ((e = ring_slot(c, k, R, &b)) != hipSuccess) break;
     if (timing) {
       const double t = smax_phase_clock();
       t_wait += t - tq;
@@ -560,19 +589,19 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
                        unsigned nt) {
   const uint64_t CH = kStage / sizeof (GtSmaxRecord);
   const uint64_t nch = (cnt + CH - 1) / CH;
-  hipError_t e = nch > 1 ? ring_ready(c) : chunk_ready(c, 0);
-  if (e != hipSuccess) return e;
+  const uint64_t nb = (uint64_t) d2h_buffers(c, nch);
+  hipError_t e = hipSuccess;
   auto issue = [&](uint64_t j) {
     const uint64_t n = std::min(CH, cnt - j * CH);
-    hipError_t r = hipMemcpyAsync(c->pin[j & 1], dev + j * CH, sizeof (GtSmaxRecord) * n,
+    hipError_t r = hipMemcpyAsync(c->pin[j % nb], dev + j * CH, sizeof (GtSmaxRecord) * n,
                                   hipMemcpyDeviceToHost, c->stream);
-    return r == hipSuccess ? hipEventRecord(c->ev[j & 1], c->stream) : r;
+    return r == hipSuccess ? hipEventRecord(c->ev[j % nb], c->stream) : r;
   };
   if (nch > 0) e = issue(0);
   for (uint64_t k = 0; e == hipSuccess && k < nch; k++) {
-    if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
-    if ((e = hipEventSynchronize(c->ev[k & 1])) != hipSuccess) break;
-    const GtSmaxRecord *h = (const GtSmaxRecord *) c->pin[k & 1];
+    if (nb > 1 && k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
+    if ((e = hipEventSynchronize(c->ev[k % nb])) != hipSuccess) break;
+    const GtSmaxRecord *h = (const GtSmaxRecord *) c->pin[k % nb];
     uint64_t *t0 = dst + 3 * k * CH;
     par_for(std::min(CH, cnt - k * CH), nt, [=](uint64_t lo, uint64_t hi) {
       for (uint64_t i = lo; i < hi; i++) {
@@ -582,6 +611,7 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
       }
     });
     // chunk k+2 reuses this buffer: issued only after this conversion
+    if (nb == 1 && k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
   }
   hipError_t e2 = hipStreamSynchronize(c->stream);
   return e == hipSuccess ? e2 : e;
@@ -591,25 +621,26 @@ hipError_t d2h_triples(DevCtx *c, uint64_t *dst, const GtSmaxRecord *dev, uint64
 // threaded copy-out of chunk k)
 hipError_t d2h_bytes(DevCtx *c, void *dst, const void *dev, uint64_t bytes, unsigned nt) {
   const uint64_t nch = (bytes + kStage - 1) / kStage;
-  hipError_t e = nch > 1 ? ring_ready(c) : chunk_ready(c, 0);
-  if (e != hipSuccess) return e;
+  const uint64_t nb = (uint64_t) d2h_buffers(c, nch);
+  hipError_t e = hipSuccess;
   auto issue = [&](uint64_t j) {
     const uint64_t n = std::min(kStage, bytes - j * kStage);
-    hipError_t r = hipMemcpyAsync(c->pin[j & 1], (const char *) dev + j * kStage, n,
+    hipError_t r = hipMemcpyAsync(c->pin[j % nb], (const char *) dev + j * kStage, n,
                                   hipMemcpyDeviceToHost, c->stream);
-    return r == hipSuccess ? hipEventRecord(c->ev[j & 1], c->stream) : r;
+    return r == hipSuccess ? hipEventRecord(c->ev[j % nb], c->stream) : r;
   };
   if (nch > 0) e = issue(0);
   for (uint64_t k = 0; e == hipSuccess && k < nch; k++) {
-    if (k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
-    if ((e = hipEventSynchronize(c->ev[k & 1])) != hipSuccess) break;
-    const char *h = (const char *) c->pin[k & 1];
+    if (nb > 1 && k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
+    if ((e = hipEventSynchronize(c->ev[k % nb])) != hipSuccess) break;
+    const char *h = (const char *) c->pin[k % nb];
     char *t0 = (char *) dst + k * kStage;
     const uint64_t n = std::min(kStage, bytes - k * kStage);
     par_for((n + 4095) / 4096, nt, [=](uint64_t lo, uint64_t hi) {
       const uint64_t a = lo * 4096, b = std::min(n, hi * 4096);
       if (a < b) memcpy(t0 + a, h + a, b - a);
     });
+    if (nb == 1 && k + 1 < nch && (e = issue(k + 1)) != hipSuccess) break;
   }
   hipError_t e2 = hipStreamSynchronize(c->stream);
   return e == hipSuccess ? e2 : e;

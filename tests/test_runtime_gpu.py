@@ -404,3 +404,30 @@ print("diag ok")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "diag ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("fail_at", [1, 2])
+def test_pin_failure_shrinks_ring(fail_at):
+    """A staging chunk whose pinning fails (GT_SMAX_PIN_FAIL_AT: chunk i and
+    later report hipErrorOutOfMemory) shrinks the device's upload/download
+    ring to the chunks pinned before it; the calls still succeed, again and
+    again, with 1 MiB chunks so that every transfer spans many of them.  Own
+    process: the ring is created once per device."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, sys
+sys.path.insert(0, "tests")
+import genometools_smax_amd as G, oracle_lib as O
+from conftest import oracle_esa
+e = oracle_esa("at1MB")
+for shards in (1, 2, 1):
+    got = G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 5, shards)
+    assert np.array_equal(got, O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 5)), shards
+print("pin ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GT_SMAX_PIN_FAIL_AT=str(fail_at), GT_SMAX_STAGE_MB="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "pin ok" in r.stdout, r.stdout + r.stderr
