@@ -175,6 +175,8 @@ def lib():
                                                       ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
         L.gt_smax_free.argtypes = [vp]
         L.gt_smax_release_cache.argtypes = []
+        L.gt_smax_hip_prepare.argtypes = [u64, u64, ci]
+        L.gt_smax_hip_prepare.restype = ci
         L.gt_smax_pack_bwt.argtypes = [vp, u64, vp]
         L.gt_smax_encode_fasta.argtypes = [ctypes.c_char_p, u64, vp, ctypes.POINTER(u64),
                                            ctypes.POINTER(u64), cs, sz]
@@ -914,6 +916,14 @@ def encode_fasta(buf):
 def release_cache():
     """Frees the runtime's cached device and pinned buffers."""
     lib().gt_smax_release_cache()
+
+
+def prepare(totallength, nonspecials, num_gpus=1):
+    """gt_smax_hip_prepare: asynchronous warm-up of the devices, staging ring
+    and device buffers for a first enumerate_smax call over an index of
+    these sizes; the next call waits for it."""
+    if lib().gt_smax_hip_prepare(int(totallength), int(nonspecials), int(num_gpus)) != 0:
+        raise SmaxError("gt_smax_hip_prepare: cannot start the warm-up thread")
 
 
 def stitch_host(boundaries, shard_index, minlen):

@@ -115,6 +115,19 @@ void gt_smax_free(void *ptr);
  * device-to-device copies when one device holds all shards. */
 void gt_smax_release_cache(void);
 
+/* Warm-up for the first host-table call of a process, asynchronous: returns
+ * at once and, on a helper thread, initialises the HIP runtime, creates the
+ * device contexts and pinned staging ring of the devices a call with
+ * num_gpus would use, starts the staging workers, loads the scan kernels and
+ * puts the device buffers of an index with this totallength / nonspecials
+ * into the cache.  The next host-table call (or gt_smax_release_cache)
+ * waits for it to finish.  A `gt repfind -smax` runner issues it as soon as
+ * it has read the index's .prj (src/match/esa-map.c:331-342: the sizes are known
+ * before the tables are mapped), so the warm-up overlaps reading the
+ * .lcp/.llv/.bwt files.  Returns 0, or -1 when no thread can be started.
+ * Optional: without it the first call does the same work itself. */
+int gt_smax_hip_prepare(uint64_t totallength, uint64_t nonspecials, int num_gpus);
+
 /* Number of HIP devices visible (0 if the runtime has none). */
 int gt_smax_device_count(void);
 

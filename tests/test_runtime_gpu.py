@@ -431,3 +431,36 @@ print("pin ok")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "pin ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_prepare_then_calls():
+    """gt_smax_hip_prepare (asynchronous warm-up) ahead of host-table calls:
+    the calls wait for it and stay bit-exact, whatever sizes or shard count
+    it announced; release_cache waits for a warm-up in flight.  Fresh process
+    (the warm-up then creates the contexts), and again in this one."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, sys
+sys.path.insert(0, "tests")
+import genometools_smax_amd as G, oracle_lib as O
+from conftest import oracle_esa
+e = oracle_esa("at1MB")
+want = O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 12)
+G.prepare(e.n, e.nonspecials, 2)
+assert np.array_equal(G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 12, 2), want)
+G.prepare(10 * e.n, 10 * e.nonspecials, 3)          # other sizes: only the cache differs
+assert np.array_equal(G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 12, 1), want)
+G.prepare(e.n, e.nonspecials, 1)
+G.release_cache()
+assert np.array_equal(G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 12, 1), want)
+print("prepare ok")
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "prepare ok" in r.stdout, r.stdout + r.stderr
+    e = oracle_esa("at1MB")
+    G.prepare(e.n, e.nonspecials, 1)
+    got = G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 20, 1)
+    assert np.array_equal(got, O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 20))
