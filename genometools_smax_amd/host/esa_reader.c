@@ -153,6 +153,17 @@ static int map_table(SmaxEsa *esa, int slot, const char *indexname,
   return 0;
 }
 
+int smax_esa_sizes(const char *indexname, uint64_t *totallength, uint64_t *nonspecials,
+                   char *errbuf, size_t errlen)
+{
+  SmaxEsa esa;
+  memset(&esa, 0, sizeof esa);
+  if (parse_prj(&esa, indexname, errbuf, errlen) != 0) return -1;
+  *totallength = esa.totallength;
+  *nonspecials = esa.totallength - esa.specialcharacters;
+  return 0;
+}
+
 int smax_esa_open(SmaxEsa *esa, const char *indexname, int need_suftab,
                   int scanfile, char *errbuf, size_t errlen)
 {

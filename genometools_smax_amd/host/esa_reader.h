@@ -33,6 +33,10 @@ typedef struct {
   int scanned;
 } SmaxEsa;
 
+/* The .prj's totallength and nonspecials (totallength - specialcharacters)
+ * alone, before any table is mapped: 0, or -1 with a message. */
+int smax_esa_sizes(const char *indexname, uint64_t *totallength, uint64_t *nonspecials,
+                   char *errbuf, size_t errlen);
 /* 0 on success, -1 with a gt-style message in errbuf. */
 int smax_esa_open(SmaxEsa *esa, const char *indexname, int need_suftab,
                   int scanfile, char *errbuf, size_t errlen);

@@ -244,6 +244,13 @@ int main(int argc, char **argv)
 
   setvbuf(stdout, outbuf, _IOFBF, sizeof outbuf);
   t0 = now_s();
+  if (smax) {
+    /* the device warm-up from the .prj sizes, beside the table reads and
+     * the separator scan below (gt_smax_hip_prepare) */
+    uint64_t pn = 0, pN = 0;
+    if (smax_esa_sizes(indexname, &pn, &pN, errbuf, sizeof errbuf) == 0)
+      (void) gt_smax_hip_prepare(pn, pN, gpus);
+  }
   if (smax_esa_open(&esa, indexname, !intervals || !smax, scan, errbuf, sizeof errbuf) != 0)
     return fail(errbuf);
   smax_esa_input(&esa, &in);
