@@ -680,8 +680,11 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
   const uint32_t wv = wl + (uint32_t) offsetof(WinT, val16);
   const uint8_t *vb = uni_ptr(reinterpret_cast<const uint8_t *>(a.llv16 + (lo & ~7u)));
   // 16-byte lanes of values (plan time, llv_win word nyw)
-  const uint64_t vmask = (1ull << SMAX_WIN_LANES(nyw)) - 1;
-  const uint64_t imask = 3ull;
+  // (s_bfm: the mask of the low SMAX_WIN_LANES(nyw) lanes in one instruction,
+  // its width operand's bits 5:0 being the lane-count field)
+  uint64_t vmask;
+  static_assert(SMAX_WIN_LANES(~0u) == 0x3fu, "lane count: bits 17..22 of the llv_win word");
+  asm("s_bfm_b64 %0, %1, 0" : "=s"(vmask) : "s"(nyw >> 17));
   const uint8_t *ib = uni_ptr(reinterpret_cast<const uint8_t *>(ibase));
   uint32_t keep;
   uint64_t ex;
@@ -696,11 +699,10 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %4\n\t"
-        "s_mov_b64 %1, exec\n\t"
         "global_load_lds_dwordx4 %2, %8 offset:0 nt\n\t"
         "global_load_lds_dwordx4 %2, %8 offset:1024 nt\n\t"
         "s_mov_b32 m0, %5\n\t"
-        "s_mov_b64 exec, %14\n\t"
+        "s_mov_b32 exec_hi, 1\n\t"   // 33 lanes (exec_lo is all ones)
         "global_load_lds_dwordx4 %2, %9 offset:0 nt\n\t"
         "s_mov_b64 exec, 3\n\t"
         "s_mov_b32 m0, %4\n\t"
@@ -711,11 +713,11 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
         SMAX_ASM_INFO
-        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b64 exec, -1\n\t"   // (issued with every lane active)
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
         : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+          "s"(vmask), "s"(ib), "i"(3), "i"(0)
         : "memory");
     } else if (SMAX_DBG(a) & (1u << 25)) {
     // diagnostic ablation (diagnostic kernel only; records are wrong): the
@@ -740,17 +742,16 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
         : "v"(v16), "v"(v4), "s"(wl + SMAX_LH), "s"(wp), "s"(wv), "s"(iaddr), "s"(la), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+          "s"(vmask), "s"(ib), "i"(3), "s"(p2mask)
         : "memory");
     } else {
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %4\n\t"
-        "s_mov_b64 %1, exec\n\t"
         "global_load_lds_dwordx4 %2, %8 offset:0\n\t"
         "global_load_lds_dwordx4 %2, %8 offset:1024\n\t"
         "s_mov_b32 m0, %5\n\t"
-        "s_mov_b64 exec, %14\n\t"
+        "s_mov_b32 exec_hi, 1\n\t"   // 33 lanes (exec_lo is all ones)
         "global_load_lds_dwordx4 %2, %9 offset:0\n\t"
         "s_mov_b64 exec, 3\n\t"
         "s_mov_b32 m0, %4\n\t"
@@ -761,11 +762,11 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %2, %10 offset:0\n\t"
         SMAX_ASM_INFO
-        "s_mov_b64 exec, %1\n\t"
+        "s_mov_b64 exec, -1\n\t"   // (issued with every lane active)
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
         : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask), "s"(p2mask)
+          "s"(vmask), "s"(ib), "i"(3), "i"(0)
         : "memory");
     }
     return;
@@ -796,7 +797,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
         : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask)
+          "s"(vmask), "s"(ib), "i"(3)
         : "memory");
   } else {
   asm volatile(
@@ -822,7 +823,7 @@ __device__ __forceinline__ void issue_window_pk(const SmaxScanArgs &a, uint64_t 
         "s_mov_b32 m0, %0"
         : "=&s"(keep), "=&s"(ex)
         : "v"(v16), "v"(v4), "s"(wl), "s"(wp), "s"(wv), "s"(iaddr), "s"(lb), "s"(pb), "s"(vb),
-          "s"(vmask), "s"(ib), "s"(imask)
+          "s"(vmask), "s"(ib), "i"(3)
         : "memory");
   }
 }
@@ -1755,7 +1756,7 @@ __device__ __forceinline__ uint32_t dyn_tile(uint32_t v, uint32_t h, uint32_t g3
 }
 // head h is exhausted: claim from the next heads in turn, waiting for each
 // answer (the tail of the run only); SMAX_NO_TILE when every head is
-__device__ static uint32_t claim_next_heads(const SmaxScanArgs &a, uint32_t &h, uint32_t &left,
+[[maybe_unused]] __device__ static uint32_t claim_next_heads(const SmaxScanArgs &a, uint32_t &h, uint32_t &left,
                                             uint32_t g3) {
   while (left > 1) {
     left--;
