@@ -1798,7 +1798,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_K1_SQ ? SMAX_SQ_CAP / 2 + 16 : SMAX_DLIST + 16];
 
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // one-wave workgroups: wave 0, so every LDS address below is a constant
+  // (no SGPRs held for them across the loop)
+  const int wave = SMAX_K1_THREADS == 64 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // tile indices are 32-bit (num_tiles < 2^32): one scalar op each
   const uint32_t stride = gridDim.x * (SMAX_K1_THREADS / 64);
   const uint32_t last = a.num_tiles - 1;
