@@ -220,3 +220,38 @@ def test_real_esa_with_long_duplicates_and_homopolymer():
     big = np.flatnonzero(lcp == 255)
     e1, e2 = int(big[len(big) // 3]), int(big[2 * len(big) // 3])
     _check_all(lcp, llv, bwt, n, N, (e1, e2), "real")
+
+
+def test_plateau_wider_than_65535_rows(tmp_path):
+    """An interval of 70,000 rows: 70,000 sequences that are the same
+    30-mer, each between two separators (unique left and right symbols), so
+    [lb, lb+69,999] with lcp-value 30 is one supermaximal repeat whose width
+    does not fit K1's 16-bit result field -- K1 flags the tile wide and K1b
+    decides it.  Whole plan, three range plans with shard ends inside the
+    plateau (device stitch), host entry with 1 and 3 shards."""
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    motif = acgt[rng.integers(0, 4, 30)].tobytes().decode()
+    recs = [">r%d\n%s\n" % (i, acgt[rng.integers(0, 4, 3000)].tobytes().decode()) for i in range(3)]
+    recs += [">m%d\n%s\n" % (i, motif) for i in range(70000)]
+    recs += [">t\n%s\n" % acgt[rng.integers(0, 4, 5000)].tobytes().decode()]
+    text, _ = G.encode_fasta("".join(recs).encode())
+    esa = G.DeviceEsa(text, device=0)
+    host = esa.download()
+    n, N = esa.totallength, esa.nonspecials
+    esa.release()
+    lcp, llv, bwt = host["lcptab"], host["llvtab"], host["bwttab"]
+    want20 = O.linsmax(lcp, llv, bwt, N, 20)
+    wid = want20[:, 2] - want20[:, 1] + 1
+    assert int(wid.max()) == 70000 and int(want20[wid.argmax(), 0]) == 30
+    lb = int(want20[wid.argmax(), 1])
+    e1, e2 = lb + 20000, lb + 50000
+    for minlen in (20, 30, 31):
+        want = O.linsmax(lcp, llv, bwt, N, minlen)
+        got = _plan_runs(lcp, llv, bwt, N, minlen, [(1, N)])
+        assert np.array_equal(got, want), ("plan", minlen, len(got), len(want))
+        got = _plan_runs(lcp, llv, bwt, N, minlen, [(1, e1), (e1, e2), (e2, N)])
+        assert np.array_equal(got, want), ("3 plans", minlen, len(got), len(want))
+        for shards in (1, 3):
+            got = G.enumerate_smax(lcp, llv, bwt, n, N, minlen, shards)
+            assert np.array_equal(got, want), ("host", shards, minlen, len(got), len(want))
