@@ -106,7 +106,7 @@ def _dev_padded(a, length):
 def _plan_runs(lcp, llv, bwt, N, minlen, ranges):
     """Range plans over the whole device tables: part 0, boundary into the
     gathered buffer, part 1, device stitch; records concatenated."""
-    length = N + 1
+    length = max(N + 1, len(lcp))   # multi-sequence tables: n + 1 > N + 1
     lcp_t, lcp_p = _dev_padded(lcp, length)
     bwt_t, bwt_p = _dev_padded(bwt, length)
     llv_t = torch.from_numpy(np.ascontiguousarray(
