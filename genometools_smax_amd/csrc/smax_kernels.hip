@@ -127,6 +127,15 @@ static_assert(GT_SMAX_PAD_BACK >= SMAX_TILE + SMAX_RH,
 static_assert(GT_SMAX_PAD_FRONT >= SMAX_LH, "front padding covers the halo");
 static_assert(SMAX_LDSB % 16 == 0, "window is whole 16-byte chunks");
 
+// K1 grid generations with their own tile counts (guided schedule)
+#define SMAX_SCHED_MAX 12
+#ifndef SMAX_K1_GUIDED
+#define SMAX_K1_GUIDED 1
+#endif
+#ifndef SMAX_GUIDE_NUM                                // a generation takes NUM/DEN of the tiles left
+#define SMAX_GUIDE_NUM 2
+#define SMAX_GUIDE_DEN 3
+#endif
 struct SmaxScanArgs {
   const uint8_t *lcp;        // local tables: index i <-> global base+i
   const uint8_t *bwt;
@@ -167,6 +176,9 @@ struct SmaxScanArgs {
                               // s_memtime cycles of K1 summed over waves, [7] = tiles
   uint32_t *heads;            // K1's tile-claim heads (SMAX_HEADS, one 128-B line each),
                               // zero at the start of every run (K3 resets them)
+  // K1's tile schedule (plan time, plan_size_grid), or null: per workgroup
+  // {first tile, stride, end of its generation's tile range}
+  const uint4 *sched_wg;
 };
 
 // K1 tile order.  The first three tiles of every wave are static (wave w:
@@ -1801,22 +1813,33 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // one-wave workgroups: wave 0, so every LDS address below is a constant
   // (no SGPRs held for them across the loop)
   const int wave = SMAX_K1_THREADS == 64 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // tile indices are 32-bit (num_tiles < 2^32): one scalar op each
-  const uint32_t stride = gridDim.x * (SMAX_K1_THREADS / 64);
-  const uint32_t last = a.num_tiles - 1;
+  // tile indices are 32-bit (num_tiles < 2^32): one scalar op each.  This
+  // workgroup's generation of the schedule: its tiles are those of the
+  // generation's range, strided by the generation's workgroup count
+  // (one plan-time entry per workgroup: {first tile, stride, end}; without
+  // the table every workgroup strides the whole range)
+  uint32_t t0 = blockIdx.x * (SMAX_K1_THREADS / 64), stride = gridDim.x * (SMAX_K1_THREADS / 64),
+           tend = a.num_tiles;
+  if (a.sched_wg != nullptr) {
+    const uint4 w = a.sched_wg[blockIdx.x];
+    t0 = __builtin_amdgcn_readfirstlane(w.x);
+    stride = __builtin_amdgcn_readfirstlane(w.y);
+    tend = __builtin_amdgcn_readfirstlane(w.z);
+  }
+  const uint32_t last = tend - 1;
 
-  uint32_t tile = blockIdx.x * (SMAX_K1_THREADS / 64) + (uint32_t) wave;
+  uint32_t tile = t0 + (uint32_t) wave;
   // no K0 (combined placement): K1 never fills the pending slot and K1b runs
   // after it, so clearing the slot here is K0's only remaining reset (the
   // deferral count and pool cursor are reset by the previous run's K3)
   if (a.k1_reset && blockIdx.x == 0 && threadIdx.x == 0) a.bnd->pend_valid = 0;
-  if (tile >= a.num_tiles) return;
+  if (tile >= tend) return;
   // dynamic tile order (SMAX_K1_DYN): the wave's next two tiles t1, t2 and
   // the claim in flight for the one after (pv, lane 0; pend)
   constexpr bool DYN = SMAX_K1_DYN != 0;
   const uint32_t g3 = 3u * stride;
-  uint32_t t1 = tile + stride < a.num_tiles ? tile + stride : SMAX_NO_TILE;
-  uint32_t t2 = tile + 2u * stride < a.num_tiles ? tile + 2u * stride : SMAX_NO_TILE;
+  uint32_t t1 = tile + stride < tend ? tile + stride : SMAX_NO_TILE;
+  uint32_t t2 = tile + 2u * stride < tend ? tile + 2u * stride : SMAX_NO_TILE;
   uint32_t hd = 0, hleft = 0, pv = 0;
   bool pend = false;
   if constexpr (DYN) {
@@ -1916,7 +1939,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // ---- DMA of the next tile's window (and the .llv window of the tile
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
-    if (next < a.num_tiles && !((SMAX_DBG(a) & (1u << 23)) && !first)) {   // diagnostic: compute only
+    if (next < tend && !((SMAX_DBG(a) & (1u << 23)) && !first)) {   // diagnostic: compute only
       const uint32_t n2 = DYN ? (t2 != SMAX_NO_TILE ? t2 : last)
                               : (next + stride <= last ? next + stride : last);
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
@@ -2007,7 +2030,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
       t2 = SMAX_NO_TILE;   // filled from the claim in flight (pend) at the next wait
     }
     first = false;
-    return tile < a.num_tiles;
+    return tile < tend;
   };
   for (;;) {
     if (!step(std::integral_constant<uint32_t, 0>())) break;
@@ -2917,6 +2940,9 @@ struct GtSmaxPlan {
   uint32_t num_tiles;
   uint64_t tile_first;
   uint32_t grid, compact_grid;
+  uint32_t sched_n;                               // K1's tile schedule (plan_size_grid)
+  uint32_t sched_blk[SMAX_SCHED_MAX + 1], sched_tile[SMAX_SCHED_MAX + 1];
+  uint4 *sched_wg;                                // its per-workgroup entries (device)
   GtSmaxRecord *out;         // capacity records, ascending lb
   uint64_t *slots;           // num_tiles * SMAX_SSLOT packed records (K1)
   GtSmaxRecord *pool;        // wide_cap wide slots + capacity records (K1b tiles' runs)
@@ -3105,9 +3131,47 @@ static hipError_t plan_size_grid(GtSmaxPlan *p) {
                       (SMAX_K1_THREADS / 64);                // workgroups with a tile per wave
   p->grid = (uint32_t) (g < wg ? g : wg);
   if (p->grid < 1) p->grid = 1;
-  if (getenv("GT_SMAX_VERBOSE"))
-    fprintf(stderr, "gt_smax: K1 %s, %u CUs x %d blocks/CU -> grid %u, %u tiles\n", name,
+  // one generation: every workgroup strides the whole tile range
+  p->sched_n = 1;
+  p->sched_blk[0] = 0;
+  p->sched_blk[1] = p->grid;
+  p->sched_tile[0] = 0;
+  p->sched_tile[1] = p->num_tiles;
+#if SMAX_K1_GUIDED
+  // guided: generation g of resident workgroups takes 2/3 of the tiles left
+  // (ceil(2R / 3W) per wave), the last ones a tile or two each, so the
+  // launch ends on short workgroups instead of a generation of equal ones
+  // started late
+  if (!(gs && strtoul(gs, NULL, 0) > 0) && resident > 0 && SMAX_K1_THREADS == 64) {
+    const uint64_t W = resident;
+    uint64_t R = p->num_tiles, t0 = 0, b0 = 0;
+    uint32_t n = 0;
+    while (R > 0 && n < SMAX_SCHED_MAX) {
+      uint64_t c = (SMAX_GUIDE_NUM * R + SMAX_GUIDE_DEN * W - 1) / (SMAX_GUIDE_DEN * W);
+      if (c < 2 || n + 1 == SMAX_SCHED_MAX) c = (R + W - 1) / W;   // the rest, in one generation
+      const uint64_t w = std::min<uint64_t>(W, (R + c - 1) / c);
+      const uint64_t take = std::min<uint64_t>(R, w * c);
+      p->sched_blk[n] = (uint32_t) b0;
+      p->sched_tile[n] = (uint32_t) t0;
+      b0 += w;
+      t0 += take;
+      R -= take;
+      n++;
+    }
+    p->sched_n = n;
+    p->sched_blk[n] = (uint32_t) b0;
+    p->sched_tile[n] = (uint32_t) t0;
+    p->grid = (uint32_t) b0;
+  }
+#endif
+  if (getenv("GT_SMAX_VERBOSE")) {
+    fprintf(stderr, "gt_smax: K1 %s, %u CUs x %d blocks/CU -> grid %u, %u tiles, schedule", name,
             p->dev_cus, per_cu, p->grid, p->num_tiles);
+    for (uint32_t k = 0; k < p->sched_n; k++)
+      fprintf(stderr, " [%u wgs: %u tiles]", p->sched_blk[k + 1] - p->sched_blk[k],
+              p->sched_tile[k + 1] - p->sched_tile[k]);
+    fprintf(stderr, "\n");
+  }
   return hipSuccess;
 }
 
@@ -3391,6 +3455,17 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   // K1's grid, from the occupancy of the variant this plan launches (the
   // u64-group kernels hold 5 waves per SIMD, the 2-plane ones 6)
   HIPCHK(plan_size_grid(p));
+  if (p->sched_n > 1) {
+    // the schedule's per-workgroup entries {first tile, stride, end}
+    std::vector<uint4> wg(p->grid);
+    for (uint32_t g = 0; g < p->sched_n; g++) {
+      const uint32_t b0 = p->sched_blk[g], w = p->sched_blk[g + 1] - b0;
+      for (uint32_t j = 0; j < w; j++)
+        wg[b0 + j] = make_uint4(p->sched_tile[g] + j, w, p->sched_tile[g + 1], 0u);
+    }
+    HIPCHK(dalloc(&p->sched_wg, sizeof (uint4) * wg.size()));
+    HIPCHK(hipMemcpy(p->sched_wg, wg.data(), sizeof (uint4) * wg.size(), hipMemcpyHostToDevice));
+  }
   {
     // K1b: a workgroup per tile -- the static list plus K1's deferrals
     // (about one tile in 10^4) -- in one generation on all CUs where they fit;
@@ -3435,7 +3510,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2, p->heads,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2, p->heads, p->sched_wg,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   // stream-ordered: the buffers go back to the cache behind events on the
@@ -3490,6 +3565,7 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.dbg = p->dbg;
   a.stamps = p->stamps;
   a.heads = p->heads;
+  a.sched_wg = p->sched_n > 1 ? p->sched_wg : nullptr;
   return a;
 }
 
