@@ -174,33 +174,10 @@ struct SmaxScanArgs {
                              // K1 then marks its deferred and static tiles' counts
   unsigned long long *stamps; // diagnostic (GT_SMAX_STAMPS, diag build only): per-section
                               // s_memtime cycles of K1 summed over waves, [7] = tiles
-  uint32_t *heads;            // K1's tile-claim heads (SMAX_HEADS, one 128-B line each),
-                              // zero at the start of every run (K3 resets them)
   // K1's tile schedule (plan time, plan_size_grid), or null: per workgroup
   // {first tile, stride, end of its generation's tile range}
   const uint4 *sched_wg;
 };
-
-// K1 tile order.  The first three tiles of every wave are static (wave w:
-// w, w + G, w + 2G over a grid of G resident waves); the rest are claimed at
-// run time from SMAX_HEADS counters, so the waves finish together instead
-// of after the last generation of workgroups (whose tiles started late).
-// Head h hands out the tiles of chunks h, h + SMAX_HEADS, h + 2 SMAX_HEADS,
-// ... (SMAX_CHUNK consecutive tiles each) after the static prefix; a wave
-// claims from the head of its XCD (HW_REG_XCC_ID, four heads per XCD) and,
-// once that is exhausted, from the others in turn.  One claim per tile
-// (a returning device-scope atomicAdd, ~1 us under load), issued a tile
-// before its result is needed; 32 heads keep each below the ~88 claims/us
-// at which one word saturates (MI355X_MICROARCH.md, "dequeue").
-#ifndef SMAX_K1_DYN
-#define SMAX_K1_DYN 0
-#endif
-#define SMAX_HEADS 32
-#ifndef SMAX_HEAD_STRIDE
-#define SMAX_HEAD_STRIDE 32                           // u32 per head (128 B)
-#endif
-#define SMAX_CHUNK 16                                 // consecutive tiles per chunk of a head
-#define SMAX_NO_TILE 0xffffffffu
 
 // Diagnostic ablation bits (GT_SMAX_DEBUG) exist only in the diagnostic build
 // (-DGT_SMAX_DIAG: lib/diag/libgtsmax_hip.so beside the production library,
@@ -1479,184 +1456,6 @@ __device__ static uint32_t wave_detect_direct(const Win &t, const SmaxScanArgs &
   return wcount;   // > SMAX_SSLOT: the caller defers the tile
 }
 
-// ---- start-queue classification (SMAX_K1_SQ)
-//
-// Rows that can start a record at all are few: at C3 about 33 of a tile's
-// 2048 rows (LCP[c] >= min(minlen, 128), LCP[c] > LCP[c-1], BWT[c-1] !=
-// BWT[c] or a special; tools/tile_design_stats.py, profiles/s5e/).  So each
-// compacted segment computes only that test -- two byte relations (UP, >=)
-// and the 255 bytes, and the 2-row left diversity from the bit planes --
-// and every candidate start goes to one queue, evaluated one per lane by
-// the exact path (eval_start: value, plateau end, local maximum, diversity).
-// An accepted start is one record, at the position the acceptance ballot
-// gives it: no per-segment record masks, no per-bit output loop.
-#ifndef SMAX_K1_SQ
-#define SMAX_K1_SQ 0
-#endif
-#define SMAX_SQ_CAP 128                               // queued starts per tile (two rounds)
-
-// 2-row left diversity of the 16 rows c of segment `so` (packed windows):
-// {BWT[c-1], BWT[c]} distinct or one of them special
-__device__ __forceinline__ uint32_t segment_div2(const Win &t, uint32_t so) {
-  if (t.B == nullptr) {
-    const uint64_t w = pk_word(t, so >> 4), pw = pk_word(t, (so >> 4) - 1);
-    const uint32_t c = (uint32_t) w, pc = (uint32_t) pw;
-    const uint32_t sp = (uint32_t) (w >> 32) & 0xffffu;
-    const uint32_t spm1 = ((sp << 1) | ((uint32_t) (pw >> 47) & 1u)) & 0xffffu;
-    const uint32_t cp = ((c << 1) & 0xfffefffeu) | ((pc >> 15) & 0x00010001u);
-    const uint32_t x1 = c ^ cp;
-    return ((x1 | (x1 >> 16)) & 0xffffu) | sp | spm1;
-  }
-  uint32_t d2, d3;
-  segment_div(t, so, &d2, &d3);
-  return d2;
-}
-
-// The candidate starts of segment `so` (16-bit row mask) and its 255 bytes
-// (*F): rows with LCP >= mf and LCP above the predecessor's, left-diverse
-// over two rows; a 255 byte after a 255 byte is a candidate unless the rank
-// relation masks (dense variant, relm) say its value is not larger
-template <bool FFPV>
-__device__ __forceinline__ uint32_t classify_start(const Win &t, uint32_t so, uint32_t mf,
-                                                   uint32_t *F, uint32_t *FFPo) {
-  const LDSP uint8_t *L = t.L;
-  const uint4 v = lds_ld16(&L[so]);
-  const uint32_t pb = L[so - 1];
-  const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
-  uint32_t st[4], ff[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t cur = k == 0 ? w0 : k == 1 ? w1 : k == 2 ? w2 : w3;
-    const uint32_t prv = k == 0 ? ((w0 << 8) | pb)
-                       : __builtin_amdgcn_alignbyte(cur, k == 1 ? w0 : k == 2 ? w1 : w2, 3);
-    st[k] = bytes_lt(prv, cur) & bytes_ge(cur, mf);
-    ff[k] = bytes_ff(cur);
-  }
-  const uint32_t FF = pack16(ff);
-  *F = FF;
-  *FFPo = FF & ((FF << 1) | (pb == 255u ? 1u : 0u));   // 255 after 255: relation by value
-  return pack16(st);
-}
-
-// Returns the tile's record count (records staged in stg, row order), or
-// UINT32_MAX when the tile goes to K1b (more than SMAX_SQ_CAP candidates, a
-// record wider than the packed slot format).
-template <bool FFPV>
-__device__ static uint32_t wave_detect_sq(const Win &t, const SmaxScanArgs &a, uint64_t g0,
-                                          const uint8_t *sL, uint32_t *ent, uint64_t *stg,
-                                          uint32_t segpre) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t mf = a.minlen < 128 ? a.minlen : 128;
-  // queue: candidate rows (u16, row order); the dense variant's rank
-  // relation masks after it
-  LDSP uint16_t *q16 = (LDSP uint16_t *) ent;
-  LDSP uint32_t *relm = (LDSP uint32_t *) (ent + SMAX_SQ_CAP / 2);
-  const uint64_t m0 = __ballot(segpre & 1u), m1 = __ballot((segpre >> 1) & 1u);
-  const uint32_t n0 = (uint32_t) __popcll(m0), n1 = (uint32_t) __popcll(m1), nseg = n0 + n1;
-  const bool a0 = (segpre & 1u) != 0, a1 = (segpre & 2u) != 0;
-  const uint32_t c0 = __builtin_amdgcn_mbcnt_hi((uint32_t) (m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m0, 0u));
-  const uint32_t c1 = __builtin_amdgcn_mbcnt_hi((uint32_t) (m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m1, 0u));
-  const uint32_t d0 = a0 ? c0 : n0 + (uint32_t) lane - c0;
-  const uint32_t d1 = (a1 ? n0 + c1 : n0 + n1 + (uint32_t) lane - c1) & 63u;
-  const uint32_t segA = (uint32_t) __builtin_amdgcn_ds_permute((int) (d0 * 4u), lane);
-  const uint32_t segB = (uint32_t) __builtin_amdgcn_ds_permute((int) (d1 * 4u), 64 + lane);
-  const uint32_t nsteps = (nseg + 63) >> 6;      // 1 or 2
-  LDSP SmaxRank *rank = const_cast<LDSP SmaxRank *>(t.rank);
-  uint32_t fbase = rank != nullptr ? t.halo_ff : 0u;
-  uint32_t nq = 0;
-  bool relm_ready = false;
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    if ((uint32_t) k >= nsteps) break;
-    const uint32_t i = k * 64 + lane;
-    uint32_t S = 0, F = 0, FFP = 0, ro = 0;
-    if (i < nseg) {
-      const uint32_t sid = (k == 0 && (uint32_t) lane < n0) ? segA : segB;
-      ro = (sid >> 6) * 1024 + (sid & 63) * 16;   // segment's first row in the tile
-      S = classify_start<FFPV>(t, SMAX_LH + ro, mf, &F, &FFP);
-    }
-    uint32_t crank = 0;
-    if (rank != nullptr) {
-      uint32_t ftot;
-      crank = fbase + wave_excl((uint32_t) __popc(F), &ftot);
-      if (i < nseg) rank[(SMAX_LH + ro) >> 4] = (SmaxRank) crank;
-      fbase += ftot;
-      if (FFPV && t.staged_all) {
-        if (!relm_ready && __ballot(FFP != 0) != 0) {
-          ffp_masks(t, relm);
-          relm_ready = true;
-        }
-        if (FFP != 0) {
-          uint32_t UP = 0, EQ = 0;
-          ffp_resolve(relm, F, FFP, crank, &UP, &EQ);
-          S |= UP & FFP;
-          FFP = 0;
-        }
-      }
-    } else {
-      FFP = 0;   // no .llv value in the window: no 255 byte (the slow path resolves a stray one)
-    }
-    S |= FFP;                                      // unresolved 255-after-255 rows
-    if (S != 0) S &= segment_div2(t, SMAX_LH + ro);
-    uint32_t tot;
-    const uint32_t ex = wave_excl((uint32_t) __popc(S), &tot);
-    if (nq + tot <= SMAX_SQ_CAP) {
-      uint32_t pos = nq + ex, bits = S;
-      while (bits) {
-        const uint32_t q = (uint32_t) __builtin_ctz(bits);
-        bits &= bits - 1;
-        q16[pos++] = (uint16_t) (ro + q);
-      }
-    }
-    nq += tot;
-  }
-  if (rank != nullptr && lane == 0) {   // halo chunks (ranks of rows the slow paths may read)
-    rank[0] = 0;
-    rank[1 + SMAX_TILE / 16] = (SmaxRank) fbase;
-  }
-  if (nq > SMAX_SQ_CAP) return UINT32_MAX;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  // exact evaluation, one candidate per lane and round; each accepted one is
-  // a record, kept in registers until every round has read the BWT planes
-  // (the records are staged in the window's BWT region)
-  uint64_t rec0 = 0, rec1 = 0;
-  uint32_t pos0 = 0, pos1 = 0, nrec = 0;
-  bool ok0 = false, ok1 = false, wide = false;
-  // (not unrolled: one copy of the exact path; a second round is rare)
-#pragma unroll 1
-  for (int r = 0; r < SMAX_SQ_CAP / 64; r++) {
-    if ((uint32_t) (64 * r) >= nq) break;
-    const uint32_t e = 64u * r + lane;
-    bool acc = false;
-    uint64_t rec = 0;
-    if (e < nq) {
-      const uint32_t ro = q16[e];
-      const uint32_t o = SMAX_LH + ro;
-      const uint32_t rk = (rank != nullptr && sL[o] == 255) ? rank_at(t, o) : 0u;
-      uint32_t cur;
-      uint64_t j;
-      acc = eval_start(t, a, g0, sL, ro, rk, true, &cur, &j);
-      const uint64_t width = j - (g0 + ro) + 2;
-      wide = wide || (acc && width > SMAX_PK_WMAX);
-      // packed slot record: row in the tile + 1 (11 bits) | width (21) | lcp (32)
-      rec = (uint64_t) ro | (width << 11) | ((uint64_t) cur << 32);
-    }
-    const uint64_t am = __ballot(acc);
-    const uint32_t p = nrec + __builtin_amdgcn_mbcnt_hi((uint32_t) (am >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t) am, 0u));
-    if (r == 0) { rec0 = rec; pos0 = p; ok0 = acc; }
-    else { rec1 = rec; pos1 = p; ok1 = acc; }
-    nrec += (uint32_t) __popcll(am);
-  }
-  if (__ballot(wide) != 0) return UINT32_MAX;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if (ok0) stg[min(pos0, (uint32_t) SMAX_SSLOT - 1u)] = rec0;
-  if (ok1) stg[min(pos1, (uint32_t) SMAX_SSLOT - 1u)] = rec1;
-  return nrec;   // > SMAX_SSLOT: the caller defers the tile
-}
-
 // next tile's window + the llv_win entry of the tile after it (ring slot iaddr)
 template <bool NT, bool BW2 = false>
 __device__ __forceinline__ void issue_next(const SmaxScanArgs &a, uint64_t l0, SmaxWindowPk *w,
@@ -1758,37 +1557,6 @@ __device__ __forceinline__ void smax_flush_tile(const SmaxScanArgs &a, uint64_t 
   }
 }
 
-// The tile a claim on head h returned (its v-th): chunk v / SMAX_CHUNK of
-// the head is chunk (v / SMAX_CHUNK) * SMAX_HEADS + h of the dynamic region
-// [g3, num_tiles); SMAX_NO_TILE past the table
-__device__ __forceinline__ uint32_t dyn_tile(uint32_t v, uint32_t h, uint32_t g3, uint32_t nt) {
-  const uint64_t t = (uint64_t) g3 +
-                     ((uint64_t) (v / SMAX_CHUNK) * SMAX_HEADS + h) * SMAX_CHUNK + (v % SMAX_CHUNK);
-  return t < nt ? (uint32_t) t : SMAX_NO_TILE;
-}
-// head h is exhausted: claim from the next heads in turn, waiting for each
-// answer (the tail of the run only); SMAX_NO_TILE when every head is
-[[maybe_unused]] __device__ static uint32_t claim_next_heads(const SmaxScanArgs &a, uint32_t &h, uint32_t &left,
-                                            uint32_t g3) {
-  while (left > 1) {
-    left--;
-    h = (h + 1) % SMAX_HEADS;
-    uint32_t v = 0;
-    if ((threadIdx.x & 63) == 0)
-      v = __hip_atomic_fetch_add(&a.heads[h * SMAX_HEAD_STRIDE], 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t t = dyn_tile(__builtin_amdgcn_readfirstlane(v), h, g3, a.num_tiles);
-    if (t != SMAX_NO_TILE) return t;
-  }
-  left = 0;
-  return SMAX_NO_TILE;
-}
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-  return x;
-}
-
 // K1 body.  Interior tiles whose starts the direct path covers are finished
 // here; shard-edge tiles and tiles with more exact starts than the direct
 // path queues are deferred to K1b (their generic path is kept out of K1,
@@ -1807,7 +1575,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // per wave: wave_detect_direct's queue of exact starts (then their
   // packed results) and accepted masks (the tile's staged records go to
   // the current window's BWT region once it is dead: window_scratch)
-  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_K1_SQ ? SMAX_SQ_CAP / 2 + 16 : SMAX_DLIST + 16];
+  __shared__ uint32_t sQueue[SMAX_K1_THREADS / 64][SMAX_DLIST + 16];
 
   const int lane = threadIdx.x & 63;
   // one-wave workgroups: wave 0, so every LDS address below is a constant
@@ -1834,19 +1602,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // deferral count and pool cursor are reset by the previous run's K3)
   if (a.k1_reset && blockIdx.x == 0 && threadIdx.x == 0) a.bnd->pend_valid = 0;
   if (tile >= tend) return;
-  // dynamic tile order (SMAX_K1_DYN): the wave's next two tiles t1, t2 and
-  // the claim in flight for the one after (pv, lane 0; pend)
-  constexpr bool DYN = SMAX_K1_DYN != 0;
-  const uint32_t g3 = 3u * stride;
-  uint32_t t1 = tile + stride < tend ? tile + stride : SMAX_NO_TILE;
-  uint32_t t2 = tile + 2u * stride < tend ? tile + 2u * stride : SMAX_NO_TILE;
-  uint32_t hd = 0, hleft = 0, pv = 0;
-  bool pend = false;
-  if constexpr (DYN) {
-    hd = ((xcc_id() & 7u) * 4u + ((blockIdx.x >> 3) & 3u)) % SMAX_HEADS;
-    hleft = g3 < a.num_tiles ? SMAX_HEADS : 0u;
-  }
-
   Win t;
   win_init(t, a);
   t.staged_all = true;   // non-static tiles: all window values staged
@@ -1857,8 +1612,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   const uint32_t info0 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][0][0]));
   const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
-  const uint32_t first_next = DYN ? (t1 != SMAX_NO_TILE ? t1 : last)
-                                  : (tile + stride <= last ? tile + stride : last);
+  const uint32_t first_next = tile + stride <= last ? tile + stride : last;
   if (lane < 2) {
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
     glds4(reinterpret_cast<const uint32_t *>(a.llv_win + first_next) + lane, info1);
@@ -1895,7 +1649,7 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     constexpr uint32_t cur = decltype(curc)::value;
     const uint64_t l0 = (a.tile_first + tile) * (uint64_t) SMAX_TILE;   // local index
     const uint64_t g0 = a.base + l0;                                      // global row
-    const uint32_t next = DYN ? t1 : tile + stride;
+    const uint32_t next = tile + stride;
     WinT *W = &sWin[wave][cur];
     t.g0 = g0;
     t.L = to_lds<uint8_t>(W->L);
@@ -1907,17 +1661,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // ---- this tile's window has landed (the wave's own DMA: no barrier)
     glds_wait();
     if constexpr (DIAG) SMAX_STAMP(st, 0);
-    if constexpr (DYN) {
-      // the claim issued a tile ago has landed (the wait above; read before the
-      // previous tile's stores are issued, so no wait covers them): the tile
-      // after next; an exhausted head sends the wave to the others
-      if (pend) {
-        uint32_t tt = dyn_tile(__builtin_amdgcn_readfirstlane(pv), hd, g3, a.num_tiles);
-        if (tt == SMAX_NO_TILE) tt = claim_next_heads(a, hd, hleft, g3);
-        t2 = tt;
-        pend = false;
-      }
-    }
     if (ptile != ~0u) {
       smax_flush_tile(a, ptile, prec, pcnt);
       ptile = ~0u;
@@ -1940,23 +1683,11 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     // after it, into the ring slot just read): in flight during all of this
     // tile's work
     if (next < tend && !((SMAX_DBG(a) & (1u << 23)) && !first)) {   // diagnostic: compute only
-      const uint32_t n2 = DYN ? (t2 != SMAX_NO_TILE ? t2 : last)
-                              : (next + stride <= last ? next + stride : last);
+      const uint32_t n2 = next + stride <= last ? next + stride : last;
       issue_next<NT, BW2>(a, (a.tile_first + next) * (uint64_t) SMAX_TILE, &sWin[wave][cur ^ 1u],
                  wbase + (cur ^ 1u) * (uint32_t) sizeof(WinT), nlo, nn,
                  a.llv_win + n2, cur ? info1 : info0, v16, v4);
     }
-    if constexpr (DYN) {
-      // claim the tile after the one whose .llv window was just requested:
-      // its answer has this whole tile's work to come back
-      if (hleft != 0 && t2 != SMAX_NO_TILE) {
-        if (lane == 0)
-          pv = __hip_atomic_fetch_add(&a.heads[hd * SMAX_HEAD_STRIDE], 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-        pend = true;
-      }
-    }
-
     if constexpr (DIAG) SMAX_STAMP(st, 1);
     t.halo_ff = SMAX_WIN_HALO(wnf);
     uint32_t segpre_bits = prepare_window(t, a, rank, wlo, wn);
@@ -1985,12 +1716,9 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     const bool stat = static_deferred(a, wnf);
     bool defer = !stat && wave_pre && (SMAX_DBG(a) & 128u);
     if (!stat && !defer && wave_pre) {
-      if constexpr (SMAX_K1_SQ != 0)
-        wcount = wave_detect_sq<FFPV>(t, a, g0, W->L, sQueue[wave], window_scratch(W), segpre_bits);
-      else
-        wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave],
-                                                      window_scratch(W), segpre_bits,
-                                                      DIAG ? st : nullptr);
+      wcount = wave_detect_direct<SMAX_DLIST, FFPV>(t, a, g0, W->L, sQueue[wave],
+                                                    window_scratch(W), segpre_bits,
+                                                    DIAG ? st : nullptr);
       // exact-queue overflow (UINT32_MAX) or more records than the tile's
       // slot holds: runtime K1b list
       defer = wcount > SMAX_SSLOT;
@@ -2025,10 +1753,6 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
     }
 
     tile = next;
-    if constexpr (DYN) {
-      t1 = t2;
-      t2 = SMAX_NO_TILE;   // filled from the claim in flight (pend) at the next wait
-    }
     first = false;
     return tile < tend;
   };
@@ -2612,7 +2336,6 @@ struct SmaxNextRun {                  // the next run's resets, done by K3
   unsigned long long *pool_cursor;
   uint32_t defer_base;
   unsigned long long pool_start;
-  uint32_t *heads;                    // K1's tile-claim heads (null: static order)
 };
 
 // One workgroup per SMAX_CPB consecutive tile slots: the slots' counts are
@@ -2645,8 +2368,6 @@ smax_compact_kernel(const uint64_t *slots, const uint32_t *slot_count,
     *nr.defer_count = nr.defer_base;
     *nr.pool_cursor = nr.pool_start;
   }
-  if (nr.heads != nullptr && blockIdx.x == 0 && threadIdx.x < SMAX_HEADS)
-    nr.heads[threadIdx.x * SMAX_HEAD_STRIDE] = 0u;
   __shared__ uint32_t sPre[SMAX_CPB + 1];
   __shared__ uint32_t sWave[4];
   __shared__ uint8_t sWide[SMAX_CPB];
@@ -2974,7 +2695,6 @@ struct GtSmaxPlan {
   uint32_t k3_split;         // K3 workgroups per block of 256 tiles (GT_SMAX_K3_SPLIT)
   bool part1_pending;        // part 0 enqueued, its part 1 not yet (the next part 0 must wait)
   uint32_t *err;
-  uint32_t *heads;           // K1's tile-claim heads (SMAX_HEADS lines; K3 zeroes them per run)
   uint32_t dbg;              // GT_SMAX_DEBUG (diagnostic build only; 0 otherwise)
   bool all_static;           // GT_SMAX_ALL_STATIC: every tile through K1b (test hook)
   bool byte_windows;         // GT_SMAX_BYTE_WINDOWS: byte BWT windows, never packed (test hook)
@@ -3068,8 +2788,7 @@ hipError_t smax_plan_reserve(const GtSmaxDevShard *shard, uint64_t capacity) {
       sizeof (uint2) * (nt + 2), sizeof (uint32_t), sizeof (uint32_t) * (2 * nt + 1),
       sizeof (uint2) * (2 * nt + 1), sizeof (uint32_t), sizeof (uint32_t), sizeof (uint32_t),
       sizeof (uint16_t) * (shard->numllv + 16), sizeof (uint32_t), sizeof (uint32_t) * (ngroups + 4),
-      64 * nt, sizeof (uint32_t) * (nt + 1), sizeof (uint32_t),
-      sizeof (uint32_t) * SMAX_HEADS * SMAX_HEAD_STRIDE};
+      64 * nt, sizeof (uint32_t) * (nt + 1), sizeof (uint32_t)};
   // (not K1b's record pool: its size depends on the static list, an
   // estimate parked a block of up to ~2x the plan's need in the cache)
   (void) wide_est;
@@ -3105,12 +2824,16 @@ static SmaxScanFn plan_scan_fn(const GtSmaxPlan *p, const char **name) {
   return f;
 }
 
-// K1's grid: 8 generations of resident workgroups of the launched variant --
+// K1's grid: generations of resident workgroups of the launched variant --
 // the dispatcher hands a finished slot the next workgroup, which balances
 // tiles of uneven cost (measured 9 % faster than one persistent generation
-// on repeat-rich input) -- up to 16 for tables of more than ~18 tiles per
-// wave of one generation (the whole C3 table, profiles/r03i_*: 16 measured
-// 0.9 % shorter there, 6 % longer on an 8-way shard's 181 k tiles)
+// on repeat-rich input).  The guided schedule (SMAX_K1_GUIDED) gives each
+// generation 2/3 of the tiles left, so the launch ends on workgroups of one
+// or two tiles (C3 -1.4 %, 1/8 shards -2.2 to -2.6 %, C5 -2.7 % against 8-16
+// equal generations, profiles/s5/guided_ab_*; 1/2 and 3/4 measured in
+// guided_fraction_ab_*).  Without it (or under GT_SMAX_GRID): 8 equal
+// generations, up to 16 for tables of more than ~18 tiles per wave of one
+// generation (profiles/r03i_*)
 static hipError_t plan_size_grid(GtSmaxPlan *p) {
   int per_cu = 0;
   const char *name = nullptr;
@@ -3121,9 +2844,6 @@ static hipError_t plan_size_grid(GtSmaxPlan *p) {
   const uint64_t resident = (uint64_t) p->dev_cus * (uint64_t) per_cu;
   uint64_t gens = resident ? (uint64_t) p->num_tiles / (resident * (SMAX_K1_THREADS / 64) * 18) : 8;
   gens = gens < 8 ? 8 : gens > 16 ? 16 : gens;
-  // claimed tiles (SMAX_K1_DYN): one generation of resident waves, the
-  // claims balance them
-  if (SMAX_K1_DYN) gens = 1;
   uint64_t g = resident * gens;
   const char *gs = getenv("GT_SMAX_GRID");     // diagnostic / test override
   if (gs && strtoul(gs, NULL, 0) > 0) g = strtoul(gs, NULL, 0);
@@ -3323,8 +3043,6 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->llv_win, 0, sizeof (uint2) * (p->num_tiles + 2)));
   HIPCHK(dalloc(&p->err, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->err, 0, sizeof (uint32_t)));
-  HIPCHK(dalloc(&p->heads, sizeof (uint32_t) * SMAX_HEADS * SMAX_HEAD_STRIDE));
-  HIPCHK(hipMemset(p->heads, 0, sizeof (uint32_t) * SMAX_HEADS * SMAX_HEAD_STRIDE));
 #ifdef GT_SMAX_DIAG
   if (getenv("GT_SMAX_STAMPS")) {
     HIPCHK(dalloc(&p->stamps, sizeof (unsigned long long) * 8));
@@ -3510,7 +3228,7 @@ fail:
 extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->shard.device);
-  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2, p->heads, p->sched_wg,
+  void *bufs[] = {p->out, p->slots, p->pool, p->pool_cursor, p->tile_off, p->tile_count, p->block_sum, p->count, p->bnd, p->defer_last, p->stamps, p->bwt2, p->sched_wg,
                   p->llv_win, p->err, p->pk_owned ? p->bwtpk : NULL, p->llv16, p->defer_list, p->defer_info,
                   p->defer_count, p->static_list, p->static_count};
   // stream-ordered: the buffers go back to the cache behind events on the
@@ -3564,7 +3282,6 @@ static SmaxScanArgs plan_args(GtSmaxPlan *p) {
   a.k1_reset = 0;
   a.dbg = p->dbg;
   a.stamps = p->stamps;
-  a.heads = p->heads;
   a.sched_wg = p->sched_n > 1 ? p->sched_wg : nullptr;
   return a;
 }
@@ -3671,7 +3388,6 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s) {
     nr.pool_cursor = p->pool_cursor;
     nr.defer_base = p->n_static;
     nr.pool_start = (unsigned long long) p->wide_cap * (SMAX_TILE / 2);
-    nr.heads = p->heads;
     hipLaunchKernelGGL(smax_compact_kernel, dim3(p->compact_grid * p->k3_split), dim3(256), 0, s,
                        p->slots, p->tile_count, bs, (uint64_t) p->num_tiles,
                        p->pool, (uint64_t) p->wide_cap * (SMAX_TILE / 2) + p->capacity,
