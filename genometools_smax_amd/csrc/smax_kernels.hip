@@ -2834,6 +2834,35 @@ static SmaxScanFn plan_scan_fn(const GtSmaxPlan *p, const char **name) {
 // guided_fraction_ab_*).  Without it (or under GT_SMAX_GRID): 8 equal
 // generations, up to 16 for tables of more than ~18 tiles per wave of one
 // generation (profiles/r03i_*)
+// The guided schedule of num_tiles tiles over `resident` workgroup slots:
+// generation g = workgroups [blk[g], blk[g+1]) over tiles [tile[g],
+// tile[g+1]), each taking ceil(2R / 3W) of the R tiles left per workgroup
+// (the rest in one generation once that is below 2, or at the last of
+// SMAX_SCHED_MAX); returns the generation count.  Exported for the host
+// tests (tests/test_host_logic.py): every tile once, in order, each
+// generation at most `resident` workgroups.
+extern "C" uint32_t gt_smax_k1_schedule(uint32_t num_tiles, uint32_t resident, uint32_t *blk,
+                                        uint32_t *tile) {
+  const uint64_t W = resident ? resident : 1;
+  uint64_t R = num_tiles, t0 = 0, b0 = 0;
+  uint32_t n = 0;
+  while (R > 0 && n < SMAX_SCHED_MAX) {
+    uint64_t c = (SMAX_GUIDE_NUM * R + SMAX_GUIDE_DEN * W - 1) / (SMAX_GUIDE_DEN * W);
+    if (c < 2 || n + 1 == SMAX_SCHED_MAX) c = (R + W - 1) / W;   // the rest, in one generation
+    const uint64_t w = std::min<uint64_t>(W, (R + c - 1) / c);
+    const uint64_t take = std::min<uint64_t>(R, w * c);
+    blk[n] = (uint32_t) b0;
+    tile[n] = (uint32_t) t0;
+    b0 += w;
+    t0 += take;
+    R -= take;
+    n++;
+  }
+  blk[n] = (uint32_t) b0;
+  tile[n] = (uint32_t) t0;
+  return n;
+}
+
 static hipError_t plan_size_grid(GtSmaxPlan *p) {
   int per_cu = 0;
   const char *name = nullptr;
@@ -2862,26 +2891,10 @@ static hipError_t plan_size_grid(GtSmaxPlan *p) {
   // (ceil(2R / 3W) per wave), the last ones a tile or two each, so the
   // launch ends on short workgroups instead of a generation of equal ones
   // started late
-  if (!(gs && strtoul(gs, NULL, 0) > 0) && resident > 0 && SMAX_K1_THREADS == 64) {
-    const uint64_t W = resident;
-    uint64_t R = p->num_tiles, t0 = 0, b0 = 0;
-    uint32_t n = 0;
-    while (R > 0 && n < SMAX_SCHED_MAX) {
-      uint64_t c = (SMAX_GUIDE_NUM * R + SMAX_GUIDE_DEN * W - 1) / (SMAX_GUIDE_DEN * W);
-      if (c < 2 || n + 1 == SMAX_SCHED_MAX) c = (R + W - 1) / W;   // the rest, in one generation
-      const uint64_t w = std::min<uint64_t>(W, (R + c - 1) / c);
-      const uint64_t take = std::min<uint64_t>(R, w * c);
-      p->sched_blk[n] = (uint32_t) b0;
-      p->sched_tile[n] = (uint32_t) t0;
-      b0 += w;
-      t0 += take;
-      R -= take;
-      n++;
-    }
-    p->sched_n = n;
-    p->sched_blk[n] = (uint32_t) b0;
-    p->sched_tile[n] = (uint32_t) t0;
-    p->grid = (uint32_t) b0;
+  if (!(gs && strtoul(gs, NULL, 0) > 0) && resident > 0 && p->num_tiles > 0 &&
+      SMAX_K1_THREADS == 64) {
+    p->sched_n = gt_smax_k1_schedule(p->num_tiles, (uint32_t) resident, p->sched_blk, p->sched_tile);
+    p->grid = p->sched_blk[p->sched_n];
   }
 #endif
   if (getenv("GT_SMAX_VERBOSE")) {
