@@ -1257,6 +1257,10 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t *tot) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
   x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  // (opaque to the optimiser: otherwise x - c is rewritten as the sum of the
+  // five shifted partials, which keeps them live and splits every step into
+  // a DPP move and an add -- ~15 more VALU per scan)
+  asm("" : "+v"(x));
   *tot = (uint32_t) __builtin_amdgcn_readlane(x, 63);
   return (uint32_t) x - c;
 }
@@ -1588,8 +1592,10 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   // the table every workgroup strides the whole range)
   uint32_t t0 = blockIdx.x * (SMAX_K1_THREADS / 64), stride = gridDim.x * (SMAX_K1_THREADS / 64),
            tend = a.num_tiles;
+  uint4 wi = make_uint4(0u, 0u, 0u, 0u);   // llv_win words of the first two tiles
   if (a.sched_wg != nullptr) {
-    const uint4 w = a.sched_wg[blockIdx.x];
+    const uint4 w = a.sched_wg[2 * blockIdx.x];
+    wi = a.sched_wg[2 * blockIdx.x + 1];
     t0 = __builtin_amdgcn_readfirstlane(w.x);
     stride = __builtin_amdgcn_readfirstlane(w.y);
     tend = __builtin_amdgcn_readfirstlane(w.z);
@@ -1613,17 +1619,29 @@ __device__ __forceinline__ void smax_scan_body(const SmaxScanArgs &a_in) {
   const uint32_t info1 = __builtin_amdgcn_readfirstlane(lds_addr(&sInfo[wave][1][0]));
   const uint32_t v16 = (uint32_t) lane * 16u, v4 = (uint32_t) lane * 4u;
   const uint32_t first_next = tile + stride <= last ? tile + stride : last;
-  if (lane < 2) {
-    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
-    glds4(reinterpret_cast<const uint32_t *>(a.llv_win + first_next) + lane, info1);
+  uint32_t lo0, n0;
+  if (a.sched_wg != nullptr) {
+    // the words came with the schedule entry: into their ring slots (LDS
+    // stores, ordered before the loop's reads), and the first window at once
+    lo0 = __builtin_amdgcn_readfirstlane(wi.x);
+    n0 = __builtin_amdgcn_readfirstlane(wi.y);
+    if (lane < 4) {
+      const uint32_t v = lane == 0 ? wi.x : lane == 1 ? wi.y : lane == 2 ? wi.z : wi.w;
+      (&sInfo[wave][0][0])[lane] = v;
+    }
+  } else {
+    if (lane < 2) {
+      glds4(reinterpret_cast<const uint32_t *>(a.llv_win + tile) + lane, info0);
+      glds4(reinterpret_cast<const uint32_t *>(a.llv_win + first_next) + lane, info1);
+    }
+    glds_wait();
+    lo0 = __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]);
+    n0 = __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]);
   }
-  glds_wait();
   // (the llv_win word of the tile after is loaded again into its slot:
   // the same value)
-  issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase,
-                      __builtin_amdgcn_readfirstlane(sInfo[wave][0][0]),
-                      __builtin_amdgcn_readfirstlane(sInfo[wave][0][1]),
-                      a.llv_win + first_next, info1, v16, v4);
+  issue_next<NT, BW2>(a, (a.tile_first + tile) * (uint64_t) SMAX_TILE, &sWin[wave][0], wbase, lo0,
+                      n0, a.llv_win + first_next, info1, v16, v4);
   // the previous tile's records (lane r holds record r) and count: stored
   // one iteration late, right after the window wait, so that those stores
   // (and the block-sum atomic) have a whole tile of work to complete before
@@ -2834,6 +2852,18 @@ static SmaxScanFn plan_scan_fn(const GtSmaxPlan *p, const char **name) {
 // guided_fraction_ab_*).  Without it (or under GT_SMAX_GRID): 8 equal
 // generations, up to 16 for tables of more than ~18 tiles per wave of one
 // generation (profiles/r03i_*)
+// The schedule table's second entry per workgroup: the llv_win words of its
+// first tile and of the one after (the last of its range if none)
+__global__ void __launch_bounds__(256)
+smax_sched_info_kernel(uint4 *wg, uint32_t grid, const uint2 *llv_win) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= grid) return;
+  const uint4 e = wg[2 * (size_t) b];
+  const uint32_t t1 = e.x + e.y <= e.z - 1 ? e.x + e.y : e.z - 1;
+  const uint2 w0 = llv_win[e.x], w1 = llv_win[t1];
+  wg[2 * (size_t) b + 1] = make_uint4(w0.x, w0.y, w1.x, w1.y);
+}
+
 // The guided schedule of num_tiles tiles over `resident` workgroup slots:
 // generation g = workgroups [blk[g], blk[g+1]) over tiles [tile[g],
 // tile[g+1]), each taking ceil(2R / 3W) of the R tiles left per workgroup
@@ -3187,15 +3217,21 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   // u64-group kernels hold 5 waves per SIMD, the 2-plane ones 6)
   HIPCHK(plan_size_grid(p));
   if (p->sched_n > 1) {
-    // the schedule's per-workgroup entries {first tile, stride, end}
-    std::vector<uint4> wg(p->grid);
+    // the schedule's per-workgroup entries: {first tile, stride, end, 0},
+    // then the llv_win words of the workgroup's first two tiles (filled on
+    // the device from llv_win): a workgroup's prologue is one scalar load
+    // and its first window DMA, not three dependent round trips
+    std::vector<uint4> wg(2 * (size_t) p->grid, make_uint4(0u, 0u, 0u, 0u));
     for (uint32_t g = 0; g < p->sched_n; g++) {
       const uint32_t b0 = p->sched_blk[g], w = p->sched_blk[g + 1] - b0;
       for (uint32_t j = 0; j < w; j++)
-        wg[b0 + j] = make_uint4(p->sched_tile[g] + j, w, p->sched_tile[g + 1], 0u);
+        wg[2 * (size_t) (b0 + j)] = make_uint4(p->sched_tile[g] + j, w, p->sched_tile[g + 1], 0u);
     }
     HIPCHK(dalloc(&p->sched_wg, sizeof (uint4) * wg.size()));
     HIPCHK(hipMemcpy(p->sched_wg, wg.data(), sizeof (uint4) * wg.size(), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(smax_sched_info_kernel, dim3((p->grid + 255) / 256), dim3(256), 0, 0,
+                       p->sched_wg, p->grid, (const uint2 *) p->llv_win);
+    HIPCHK(hipGetLastError());
   }
   {
     // K1b: a workgroup per tile -- the static list plus K1's deferrals
