@@ -10,6 +10,12 @@
 
 #include "gt_smax_hip.h"
 
+// Offset of the library's own LCP/BWT tables past a 128-byte line: K1's
+// window of tile l0 reads LCP[l0-16 .. l0+2064), 2080 bytes, which fit in 17
+// lines when l0-16 starts 16 bytes into one and take 18 when the table is
+// line-aligned (C3 step -0.5 %, 3/8 shard -0.7 %, profiles/s5/lcp_align_ab_*)
+#define SMAX_TABLE_SHIFT 32
+
 // Per-device caching allocator of the host runtime: plan buffers and staged
 // tables come from it, so back-to-back calls in one process reuse device
 // memory instead of hipMalloc/hipFree of multi-GB buffers per call.

@@ -2758,12 +2758,13 @@ extern "C" const char *gt_smax_build_id(void) { return GT_SMAX_BUILD_ID; }
 extern "C" int gt_smax_dev_alloc_table(int device, uint64_t len,
                                        uint8_t **table, char *errbuf,
                                        size_t errlen) {
+  // the table starts SMAX_TABLE_SHIFT bytes past a 128-byte line (smax_internal.h)
   uint8_t *p = NULL;
   HIPCHK(hipSetDevice(device));
-  HIPCHK(hipMalloc(&p, len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
-  HIPCHK(hipMemset(p, 0, GT_SMAX_PAD_FRONT));
-  HIPCHK(hipMemset(p + GT_SMAX_PAD_FRONT + len, 0, GT_SMAX_PAD_BACK));
-  *table = p + GT_SMAX_PAD_FRONT;
+  HIPCHK(hipMalloc(&p, len + SMAX_TABLE_SHIFT + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
+  HIPCHK(hipMemset(p, 0, SMAX_TABLE_SHIFT + GT_SMAX_PAD_FRONT));
+  HIPCHK(hipMemset(p + SMAX_TABLE_SHIFT + GT_SMAX_PAD_FRONT + len, 0, GT_SMAX_PAD_BACK));
+  *table = p + SMAX_TABLE_SHIFT + GT_SMAX_PAD_FRONT;
   return 0;
 fail:
   if (p) (void) hipFree(p);
@@ -2773,7 +2774,7 @@ fail:
 extern "C" int gt_smax_dev_free_table(int device, uint8_t *table) {
   if (table == NULL) return 0;
   if (hipSetDevice(device) != hipSuccess) return -1;
-  return hipFree(table - GT_SMAX_PAD_FRONT) == hipSuccess ? 0 : -1;
+  return hipFree(table - GT_SMAX_PAD_FRONT - SMAX_TABLE_SHIFT) == hipSuccess ? 0 : -1;
 }
 
 // tiles of the local grid [first, last] that hold owned rows [begin, end)

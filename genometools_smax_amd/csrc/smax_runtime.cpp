@@ -849,7 +849,7 @@ void device_phase1(Call *C, int d) {
       // the LCP table's zero pads travel with its bytes in the upload (no
       // memset kernels ahead of the first DMA: in a fresh process the first
       // fill launch cost tens of ms before the ring started)
-      DCHK(smax_dev_alloc(&S.lcp, S.len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
+      DCHK(smax_dev_alloc(&S.lcp, SMAX_TABLE_SHIFT + S.len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
       if (!nondna) {
         DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
         DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
@@ -880,7 +880,7 @@ void device_phase1(Call *C, int d) {
         const char *lsrc = (const char *) in->lcptab + S.base;
         std::vector<StageSeg> segs;
         const uint64_t llen = S.len;
-        segs.push_back({S.lcp, GT_SMAX_PAD_FRONT + S.len + GT_SMAX_PAD_BACK,
+        segs.push_back({(char *) S.lcp + SMAX_TABLE_SHIFT, GT_SMAX_PAD_FRONT + S.len + GT_SMAX_PAD_BACK,
                         [lsrc, llen](uint64_t off, uint64_t n, char *buf) {
                           // [0, PAD_FRONT) zeros, the table, then PAD_BACK zeros
                           const uint64_t t0 = GT_SMAX_PAD_FRONT, t1 = t0 + llen;
@@ -936,7 +936,7 @@ void device_phase1(Call *C, int d) {
                        }, nullptr));
         S.sh.bwt_dev = (const uint8_t *) S.bwt + GT_SMAX_PAD_FRONT;
       }
-      S.sh.lcp_dev = (const uint8_t *) S.lcp + GT_SMAX_PAD_FRONT;
+      S.sh.lcp_dev = (const uint8_t *) S.lcp + SMAX_TABLE_SHIFT + GT_SMAX_PAD_FRONT;
       S.sh.llv_dev = (const GtSmaxLlv *) S.llv;
       S.sh.numllv = S.hi - S.lo;
       S.sh.base = S.base;
@@ -1175,7 +1175,8 @@ void prepare_run(uint64_t n, uint64_t N, int num_gpus) {
         g.device = d;
         const uint64_t ng = GT_SMAX_PK_GROUPS(g.local_len);
         void *b[3] = {};
-        hipError_t e = smax_dev_alloc(&b[0], g.local_len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK);
+        hipError_t e = smax_dev_alloc(&b[0], SMAX_TABLE_SHIFT + g.local_len + GT_SMAX_PAD_FRONT +
+                                             GT_SMAX_PAD_BACK);
         if (e == hipSuccess) e = smax_dev_alloc(&b[1], sizeof (uint64_t) * ng);
         if (e == hipSuccess) e = smax_dev_alloc(&b[2], sizeof (uint32_t) * ng);
         if (e == hipSuccess) (void) smax_plan_reserve(&g, 0);

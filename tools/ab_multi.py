@@ -19,8 +19,13 @@ import genometools_smax_amd as G  # noqa: E402
 kind, bases, minlen = sys.argv[1], int(float(sys.argv[2])), int(sys.argv[3])
 si, sw = (int(x) for x in sys.argv[4].split("/"))
 rounds = int(sys.argv[5])
-paths = [G.LIB_PATH] + sys.argv[6:]
-names = ["in-tree"] + [os.path.basename(os.path.dirname(p)) for p in sys.argv[6:]]
+# a LIB argument "shift:S" is the in-tree build over a copy of the LCP table
+# placed so that its device address is S mod 128 (window-stream alignment)
+args = sys.argv[6:]
+paths = [G.LIB_PATH] + [G.LIB_PATH if a.startswith("shift:") else a for a in args]
+names = ["in-tree"] + [a if a.startswith("shift:") else os.path.basename(os.path.dirname(a))
+                       for a in args]
+shifts = [None] + [int(a.split(":")[1]) if a.startswith("shift:") else None for a in args]
 libs = []
 for p in paths:
     G._lib, G.LIB_PATH = None, p
@@ -33,10 +38,25 @@ del text
 N = esa.nonspecials
 begin, end = 1 + (N - 1) * si // sw, 1 + (N - 1) * (si + 1) // sw
 print("rows [%d, %d) (shard %d/%d), builds: %s" % (begin, end, si, sw, ", ".join(names)), flush=True)
+print("LCP table at %d mod 128" % (esa.esa.lcptab_dev % 128), flush=True)
 plans = []
-for L in libs:
+copies = []
+for L, sh in zip(libs, shifts):
     G._lib = L
-    plans.append(esa.plan(minlen, begin, end))
+    if sh is None:
+        plans.append(esa.plan(minlen, begin, end))
+        continue
+    n1 = esa.totallength + 1
+    buf = torch.zeros(G.PAD_FRONT + n1 + G.PAD_BACK + 256, dtype=torch.uint8, device="cuda")
+    off = G.PAD_FRONT + ((sh - (buf.data_ptr() + G.PAD_FRONT)) % 128)
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy(ctypes.c_void_p(buf.data_ptr() + off), ctypes.c_void_p(esa.esa.lcptab_dev),
+                  ctypes.c_size_t(n1), 3)   # hipMemcpyDeviceToDevice
+    copies.append(buf)
+    plans.append(G.SmaxPlan(buf.data_ptr() + off, esa.esa.bwttab_dev, esa.esa.llvtab_dev, esa.numllv,
+                            0, n1, begin, end, N, minlen, esa.device, 0,
+                            bwtpk_ptr=esa.esa.bwtpk_dev))
 G._lib = libs[0]
 s = torch.cuda.current_stream()
 sp = s.cuda_stream
