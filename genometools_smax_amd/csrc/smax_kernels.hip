@@ -97,6 +97,10 @@ typedef uint8_t SmaxRank;
 #define SMAX_PK_WMAX ((1u << 21) - 1)
 #define SMAX_CPB 256                                  // tiles per K3 workgroup / block sum
 #define SMAX_SBB 64                                   // blocks per superblock sum (K3's two-level prefix)
+// K1b workgroups for K1's runtime deferrals: 64 + one per this many tiles
+// (about one tile in 10^4 defers; more loop; 4096 against 1024: 1/8 shards
+// of C3 -0.1 to -1.8 %, profiles/s5/k1b_slack_ab_*)
+#define SMAX_K1B_SLACK 4096u
 // one run's block-sum buffer (block sums added up in K1b's launch): the
 // blocks' sums, then the superblocks' sums
 __host__ __device__ __forceinline__ uint64_t smax_bs_stride(uint64_t nblocks) {
@@ -3242,7 +3246,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, shard->device) !=
             hipSuccess || ncu < 1)
       ncu = 256;
-    p->k1b_grid = std::min<uint32_t>(p->n_static + p->num_tiles / 1024u + 64u, (uint32_t) ncu * 8u) + 1;
+    p->k1b_grid = std::min<uint32_t>(p->n_static + p->num_tiles / SMAX_K1B_SLACK + 64u, (uint32_t) ncu * 8u) + 1;
     // 8 waves per tile (each tile's ballots and evaluation split twice as
     // fine) when the launch -- tiles, the head and the block-sum workgroups
     // -- fits one generation of the 8-wave kernel (two per CU), else 4 (five
