@@ -464,3 +464,42 @@ print("prepare ok")
     G.prepare(e.n, e.nonspecials, 1)
     got = G.enumerate_smax(e.lcpbytes, e.llv, e.bwt, e.n, e.nonspecials, 20, 1)
     assert np.array_equal(got, O.linsmax(e.lcpbytes, e.llv, e.bwt, e.nonspecials, 20))
+
+
+def test_guided_schedule_against_static_grids():
+    """K1's guided tile schedule (several generations, per-workgroup table
+    with the first tiles' .llv words) against static grids (GT_SMAX_GRID:
+    every workgroup strides the whole range), on a table large enough for
+    several generations (40 Mbp, ~20 k tiles), whole and a middle shard:
+    all equal the oracle's records."""
+    text = G.synth_genome("human", 40_000_000, 7)
+    esa = G.DeviceEsa(text)
+    del text
+    host = esa.download()
+    N = esa.nonspecials
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], N, 20)
+    mid = (N // 3, 2 * N // 3)
+    ref_mid = None
+    for grid in (None, "6144", "97"):
+        old = os.environ.get("GT_SMAX_GRID")
+        if grid is not None:
+            os.environ["GT_SMAX_GRID"] = grid
+        try:
+            p = esa.plan(20)
+            q = esa.plan(20, *mid)
+        finally:
+            if old is None:
+                os.environ.pop("GT_SMAX_GRID", None)
+            else:
+                os.environ["GT_SMAX_GRID"] = old
+        for _ in range(2):
+            p.run()
+            assert np.array_equal(p.fetch_triples(), want), grid
+            q.run()
+            got = q.fetch_triples()
+            if ref_mid is None:
+                ref_mid = got
+            assert np.array_equal(got, ref_mid), grid
+        p.close()
+        q.close()
+    esa.release()
