@@ -83,6 +83,9 @@ bool env_on(const char *name) {
 
 }  // namespace
 
+// helper threads' own plans (warm_kernels) keep out of the call's phase list
+static thread_local bool t_phase_mute = false;
+
 // A freed block's fence: events recorded on the streams whose work may still
 // use it (or the whole device); the allocation that hands the block out
 // again waits for them once.  Reference-counted by the blocks holding it.
@@ -162,11 +165,15 @@ void release_idle(int device) {   // pool.mu held
 
 // ------------------------------------------------------------ per device
 
-// pinned staging chunk (bytes): 64 MiB, GT_SMAX_STAGE_MB overrides
+// pinned staging chunk (bytes): 16 MiB, GT_SMAX_STAGE_MB overrides.  A
+// first call waits for the ring's chunks to be pinned (~4-5 GB/s): at C3 its
+// median over five fresh processes was 0.137 s with 16 MiB chunks against
+// 0.170 s with 64, the warm second call the same (0.096 / 0.097 s,
+// profiles/s7/stage_mb_sweep_c3.txt)
 uint64_t stage_bytes() {
   static const uint64_t b = [] {
     const char *v = getenv("GT_SMAX_STAGE_MB");
-    const uint64_t mb = v ? strtoull(v, NULL, 0) : 64;
+    const uint64_t mb = v ? strtoull(v, NULL, 0) : 16;
     return (mb < 1 ? 1 : mb > 1024 ? 1024 : mb) << 20;
   }();
   return b;
@@ -201,6 +208,8 @@ struct DevCtx {
   // profiles/r04o/e2e_ring_sweep_c3.json)
   std::promise<hipError_t> pinned[kRingMax];
   std::shared_future<hipError_t> pin_done[kRingMax];
+  // every kernel of a plan launched once in this process (warm_kernels)
+  std::atomic<bool> kernels_warm{false};
 };
 
 hipError_t chunk_ready(DevCtx *c, int i) {
@@ -814,6 +823,8 @@ hipError_t alloc_table(void **raw, uint64_t bytes) {
 }
 
 // Phase 1 of device slot d: upload, plan, run, exchange, stitch, counts.
+void warm_kernels(int dev, hipStream_t st);
+
 void device_phase1(Call *C, int d) {
   const GtSmaxInput *in = C->in;
   DevCtx *c = nullptr;
@@ -835,6 +846,7 @@ void device_phase1(Call *C, int d) {
       // loaded) on a helper thread while this thread stages the tables: a
       // first call otherwise pays ~30 ms of cold allocations in plan creation
       std::thread reserve;
+      hipError_t reserve_err = hipSuccess;
       struct JoinT {
         std::thread &t;
         ~JoinT() { if (t.joinable()) t.join(); }
@@ -850,10 +862,7 @@ void device_phase1(Call *C, int d) {
       // memset kernels ahead of the first DMA: in a fresh process the first
       // fill launch cost tens of ms before the ring started)
       DCHK(smax_dev_alloc(&S.lcp, SMAX_TABLE_SHIFT + S.len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK));
-      if (!nondna) {
-        DCHK(smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng));
-        DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
-      }
+      if (!nondna) DCHK(smax_dev_alloc(&planes, sizeof (uint32_t) * ng));
       DCHK(smax_dev_alloc(&S.llv, sizeof (GtSmaxLlv) * (S.hi - S.lo + 1)));
       if (d == 0) smax_phase_mark(" h2d.alloc", &th);
       {
@@ -867,8 +876,23 @@ void device_phase1(Call *C, int d) {
         g.end = S.end;
         g.nonspecials = in->nonspecials;
         g.device = dev;
-        reserve = std::thread([g, dev] {
-          if (hipSetDevice(dev) == hipSuccess) (void) smax_plan_reserve(&g, 0);
+        // the u64 groups are first written after the ring: allocated here
+        // (a cold allocation costs ~5 ms per GB), then every plan kernel's
+        // first launch in the process and the null stream plan creation
+        // uses (~10 ms in a fresh process, profiles/s5/bench_c3.json)
+        const bool want_groups = !nondna;
+        reserve = std::thread([g, dev, c, want_groups, ng, &S, &reserve_err] {
+          // after the ring's chunks are pinned (beside the pinning, the
+          // first chunks waited 22-27 ms instead of 8: profiles/s5/)
+          // (a chunk that failed to pin is the ring's concern, not an error)
+          (void) ring_ready(c);
+          hipError_t e = hipSetDevice(dev);
+          if (e == hipSuccess && want_groups) e = smax_dev_alloc(&S.bwt, sizeof (uint64_t) * ng);
+          reserve_err = e;
+          if (e != hipSuccess) return;
+          (void) smax_plan_reserve(&g, 0);
+          t_phase_mute = true;
+          if (!c->kernels_warm.exchange(true)) warm_kernels(dev, nullptr);
         });
       }
       {
@@ -909,6 +933,9 @@ void device_phase1(Call *C, int d) {
         }
         hipError_t pe = stage_h2d_multi(c, segs, C->nt);
         if (d == 0) smax_phase_mark(" h2d.ring", &th);
+        if (reserve.joinable()) reserve.join();
+        if (pe == hipSuccess) pe = reserve_err;
+        if (d == 0) smax_phase_mark(" h2d.helper", &th);
         void *dspec = nullptr;
         if (pe == hipSuccess && !nondna && !spec.empty()) {
           pe = smax_dev_alloc(&dspec, sizeof (uint64_t) * spec.size());
@@ -950,7 +977,6 @@ void device_phase1(Call *C, int d) {
         fail_dev(C, d, C->valid_msg);
         goto out;
       }
-      if (reserve.joinable()) reserve.join();
       if (gt_smax_plan_create(&S.plan, &S.sh, C->minlen, 0, eb, sizeof eb)) {
         fail_dev(C, d, eb);
         goto out;
@@ -1096,12 +1122,11 @@ std::vector<int> shard_blocks(int nshards, int ndev) {
   return first;
 }
 
-// One pass over a 64 Ki-row all-zero index on the context's stream: a
-// kernel's first launch in a process pays its code-object load (~10 ms for
-// the .llv index kernel, profiles/s5/), and the stream's first copies in
-// each direction set up their DMA path; one small copy out of every pinned
-// chunk, one back.
-void warm_pass(DevCtx *c, int dev) {
+// One plan over a 64 Ki-row all-zero index on stream st: the first plan in a
+// process pays ~10 ms in its .llv index phase (the null stream plan creation
+// uses for its memsets and copies, and the kernels' first launches:
+// profiles/s5/bench_c3.json, llv_index 10-11 ms in a first call, 1 ms after)
+void warm_kernels(int dev, hipStream_t st) {
   const uint64_t len = 1u << 16, ng = GT_SMAX_PK_GROUPS(len);
   const uint64_t lbytes = len + GT_SMAX_PAD_FRONT + GT_SMAX_PAD_BACK;
   void *lcp = nullptr, *grp = nullptr, *pl = nullptr, *llv = nullptr;
@@ -1109,16 +1134,11 @@ void warm_pass(DevCtx *c, int dev) {
   if (e == hipSuccess) e = smax_dev_alloc(&grp, sizeof (uint64_t) * ng);
   if (e == hipSuccess) e = smax_dev_alloc(&pl, sizeof (uint32_t) * ng);
   if (e == hipSuccess) e = smax_dev_alloc(&llv, sizeof (GtSmaxLlv));
-  for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
-    if (chunk_usable(c, i))
-      e = hipMemcpyAsync(lcp, c->pin[i], std::min<uint64_t>(kStage, lbytes), hipMemcpyHostToDevice,
-                         c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->pin[0], lcp, 4096, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(lcp, 0, lbytes, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(pl, 0, sizeof (uint32_t) * ng, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(lcp, 0, lbytes, st);
+  if (e == hipSuccess) e = hipMemsetAsync(pl, 0, sizeof (uint32_t) * ng, st);
   if (e == hipSuccess)
-    e = smax_groups_from_planes((uint64_t *) grp, (const uint32_t *) pl, ng, nullptr, 0, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    e = smax_groups_from_planes((uint64_t *) grp, (const uint32_t *) pl, ng, nullptr, 0, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e == hipSuccess) {
     GtSmaxDevShard g;
     memset(&g, 0, sizeof g);
@@ -1134,13 +1154,27 @@ void warm_pass(DevCtx *c, int dev) {
     GtSmaxPlan *plan = nullptr;
     char eb[256];
     if (gt_smax_plan_create(&plan, &g, 20, 0, eb, sizeof eb) == 0) {
-      (void) gt_smax_plan_run(plan, c->stream);
-      (void) hipStreamSynchronize(c->stream);
+      (void) gt_smax_plan_run(plan, st);
+      (void) hipStreamSynchronize(st);
       gt_smax_plan_delete(plan);
     }
   }
-  (void) hipStreamSynchronize(c->stream);
+  (void) hipStreamSynchronize(st);
   for (void *p : {lcp, grp, pl, llv}) smax_dev_free(p);
+}
+
+// the stream's first copies in each direction set up their DMA path: one
+// small copy out of every pinned chunk, one back; then the kernels
+void warm_pass(DevCtx *c, int dev) {
+  void *buf = nullptr;
+  const uint64_t n = std::min<uint64_t>(kStage, 1u << 16);
+  hipError_t e = smax_dev_alloc(&buf, n);
+  for (int i = 0; i < ring_depth() && e == hipSuccess; i++)
+    if (chunk_usable(c, i)) e = hipMemcpyAsync(buf, c->pin[i], n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->pin[0], buf, 4096, hipMemcpyDeviceToHost, c->stream);
+  (void) hipStreamSynchronize(c->stream);
+  smax_dev_free(buf);
+  if (!c->kernels_warm.exchange(true)) warm_kernels(dev, c->stream);
 }
 
 void prepare_run(uint64_t n, uint64_t N, int num_gpus) {
@@ -1430,7 +1464,7 @@ double smax_phase_clock() {
 void smax_phase_mark(const char *what, double *t) {
   static const bool on = env_on("GT_SMAX_TIMING");
   const double now = smax_phase_clock();
-  if (on) fprintf(stderr, "[gt_smax timing] %-12s %8.2f ms\n", what, (now - *t) * 1e3);
+  if (on && !t_phase_mute) fprintf(stderr, "[gt_smax timing] %-12s %8.2f ms\n", what, (now - *t) * 1e3);
   *t = now;
 }
 
