@@ -182,6 +182,7 @@ struct MpKeys {
   uint64_t *k1, *k2, *k3, *k4;   // r2 | (classes, r1) | event | t (split)
   int rowbits, lbits;            // rows < 2^rowbits, depths < 2^lbits
   int split;                     // rowbits + lbits > 64: t in k4, depth in k3
+  uint32_t *rank0;               // when set: zeroed beside the keys (mp_rank_kernel's counts)
 };
 
 // Walk of row j: counts (EMIT = false) or writes at out[o..] (EMIT = true)
@@ -268,6 +269,7 @@ __device__ __forceinline__ uint32_t mp_walk(const uint8_t *lcp, const uint32_t *
             K->k2[e] = (cls << rb) | r1;
             K->k3[e] = ev_key3;
             if (K->split) K->k4[e] = ev_key4;
+            if (K->rank0) K->rank0[e] = 0;
           }
         }
         c++;
@@ -338,25 +340,120 @@ __device__ __forceinline__ uint32_t mp_candidates(const uint8_t *lcp, uint64_t j
 }
 
 __global__ void __launch_bounds__(256)
-mp_cand_count_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, uint64_t *wg_cand) {
+mp_cand_count_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, uint64_t *wg_cand,
+                     uint16_t *masks) {
   const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) MP_ROWS;
+  const uint32_t m = mp_candidates(lcp, j0, N, mf);
+  masks[blockIdx.x * (uint64_t) 256 + threadIdx.x] = (uint16_t) m;
   uint64_t tot;
-  (void) mp_block_excl((uint64_t) __popc(mp_candidates(lcp, j0, N, mf)), &tot);
+  (void) mp_block_excl((uint64_t) __popc(m), &tot);
   if (threadIdx.x == 0) wg_cand[blockIdx.x] = tot;
 }
 
+// pass B reads pass A's 16-row masks (2 B per 16 rows), not the LCP bytes;
+// one workgroup per MP_WR_GROUP of pass A's workgroups, 4 masks (64 rows)
+// per thread: one 8-byte load each (a workgroup per pass-A workgroup, one
+// mask per thread: 15.5 us for C2's 12.5 MB)
+#define MP_WR_GROUP 4
 __global__ void __launch_bounds__(256)
-mp_cand_write_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, const uint64_t *wg_cand_off,
-                     uint64_t *list) {
-  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) MP_ROWS;
-  uint32_t m = mp_candidates(lcp, j0, N, mf);
+mp_cand_write_kernel(const uint16_t *masks, const uint64_t *wg_cand_off, uint64_t *list) {
+  const uint64_t k0 = (uint64_t) blockIdx.x * (256 * MP_WR_GROUP) + 4u * threadIdx.x;
+  uint64_t m = *reinterpret_cast<const uint64_t *>(masks + k0);
   uint64_t tot;
-  uint64_t pos = wg_cand_off[blockIdx.x] + mp_block_excl((uint64_t) __popc(m), &tot);
+  uint64_t pos = wg_cand_off[(uint64_t) blockIdx.x * MP_WR_GROUP] +
+                 mp_block_excl((uint64_t) __popcll(m), &tot);
+  const uint64_t j0 = k0 * MP_ROWS;
   while (m) {
-    const int q = __builtin_ctz(m);
+    const int q = __builtin_ctzll(m);
     m &= m - 1;
     list[pos++] = j0 + q;
   }
+}
+
+// Single-pass pass C + scan (small candidate lists): each workgroup
+// publishes its total in a status word, then looks back over its
+// predecessors' words for the nearest inclusive prefix, adding the
+// aggregates before it, and publishes its own inclusive prefix (decoupled
+// look-back); the whole workgroup looks back, 1024 words per round trip.  A
+// status word is [tag:16 | flag:2 | value:46], the tag the pass's number, so
+// no pass clears the words of the last.  Used only where every workgroup of
+// the grid looks back within one window (mp_count_grid <= MP_LB_MAX_WG): for
+// the 6,104-workgroup candidate list of C2 the same look-back cost 66-78 us
+// on top of the 25 us stream, even with no waiting at all (the status
+// loads and write-through stores themselves; profiles/s7/f2_lookback.txt),
+// against 5 us for rocprim's scan between two passes.
+#define MP_ST_AGG (1ull << 46)
+#define MP_ST_INC (2ull << 46)
+#define MP_ST_VAL (MP_ST_AGG - 1)
+#define MP_LB_PER 4   // status words per thread per look-back step
+#define MP_LB_MAX_WG 64   // (measured at C2's 18 workgroups: 8.9-11.6 us against 16.1)
+
+// all 256 threads of workgroup bid: the exclusive prefix of its total tot
+__device__ uint64_t mp_lookback(uint64_t *status, uint64_t bid, uint64_t tot, uint64_t tag) {
+  __shared__ uint32_t sNear;
+  const uint64_t tg = tag << 48;
+  if (bid == 0) {
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&status[0], tg | MP_ST_INC | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&status[bid], tg | MP_ST_AGG | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  int64_t base = (int64_t) bid;
+  for (;;) {
+    // one poller per workgroup, backing off, on the nearest word of the
+    // window before the window's 1024 loads (every thread of ~2000 resident
+    // workgroups re-polling its words saturated the L2s: 103 us)
+    if (threadIdx.x == 0) {
+      uint32_t nap = 1;
+      while ((__hip_atomic_load(&status[base - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 48) != tag) {
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(8);
+        nap = nap < 32 ? 2 * nap : 32;
+      }
+    }
+    __syncthreads();
+    uint64_t st[MP_LB_PER];
+#pragma unroll
+    for (int u = 0; u < MP_LB_PER; u++) {   // word u of thread t: predecessor base-1-(t*PER+u)
+      const int64_t idx = base - 1 - (int64_t) (threadIdx.x * MP_LB_PER + u);
+      st[u] = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : (tg | MP_ST_INC);
+    }
+#pragma unroll
+    for (int u = 0; u < MP_LB_PER; u++) {
+      const int64_t idx = base - 1 - (int64_t) (threadIdx.x * MP_LB_PER + u);
+      uint32_t nap = 1;
+      while ((st[u] >> 48) != tag) {
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(8);
+        nap = nap < 32 ? 2 * nap : 32;
+        st[u] = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    uint32_t near = 0xffffffffu;   // this thread's nearest inclusive word
+#pragma unroll
+    for (int u = MP_LB_PER - 1; u >= 0; u--)
+      if (st[u] & MP_ST_INC) near = threadIdx.x * MP_LB_PER + u;
+    if (threadIdx.x == 0) sNear = 0xffffffffu;
+    __syncthreads();
+    if (near != 0xffffffffu) atomicMin(&sNear, near);
+    __syncthreads();
+    const uint32_t k = sNear;
+    uint64_t v = 0;
+#pragma unroll
+    for (int u = 0; u < MP_LB_PER; u++)
+      if (threadIdx.x * MP_LB_PER + u <= k) v += st[u] & MP_ST_VAL;
+    uint64_t sum;
+    (void) mp_block_excl(v, &sum);
+    excl += sum;
+    __syncthreads();   // sNear and mp_block_excl's LDS before the next step
+    if (k != 0xffffffffu) break;
+    base -= 256 * MP_LB_PER;
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&status[bid], tg | MP_ST_INC | (excl + tot), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
 }
 
 // Pass C: pairs per candidate row.
@@ -367,6 +464,49 @@ mp_count_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const u
                 uint32_t *cnt) {
   MP_FOR(e, ncand)
     cnt[e] = mp_walk<false, SufT>(lcp, X, B, RM, RO, nullptr, list[e], minlen, 0, nullptr, 0);
+}
+
+// passes C + scan + total in one: workgroup b owns candidates
+// [b * 256 * R, (b + 1) * 256 * R) (R > 1 only past 2^30 candidates, the grid
+// cap), their counts, exclusive offsets and, from the last workgroup, the
+// total
+template <typename SufT>
+__global__ void __launch_bounds__(256)
+mp_count_scan_kernel(const uint8_t *lcp, const uint32_t *X, const uint8_t *B, const uint32_t *RM,
+                     const uint32_t *RO, const uint64_t *list, uint64_t ncand, uint32_t minlen,
+                     uint32_t R, uint64_t *status, uint64_t tag, uint32_t *cnt, uint64_t *off,
+                     uint64_t *total) {
+  const uint64_t e0 = (uint64_t) blockIdx.x * 256u * R;
+  uint64_t run = 0, loc0 = 0;
+  uint32_t c0 = 0;
+  for (uint32_t r = 0; r < R; r++) {   // the first 256 stay in registers
+    const uint64_t e = e0 + (uint64_t) r * 256u + threadIdx.x;
+    const uint32_t c = e < ncand ? mp_walk<false, SufT>(lcp, X, B, RM, RO, nullptr, list[e], minlen, 0,
+                                                        nullptr, 0)
+                                 : 0u;
+    uint64_t t;
+    const uint64_t loc = mp_block_excl((uint64_t) c, &t);
+    if (r == 0) {
+      c0 = c;
+      loc0 = loc;
+    } else if (e < ncand) {
+      cnt[e] = c;
+      off[e] = run + loc;
+    }
+    run += t;
+    __syncthreads();   // mp_block_excl's LDS before its next use
+  }
+  const uint64_t pre = mp_lookback(status, blockIdx.x, run, tag);
+  if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) *total = pre + run;
+  if (e0 + threadIdx.x < ncand) {
+    cnt[e0 + threadIdx.x] = c0;
+    off[e0 + threadIdx.x] = pre + loc0;
+  }
+  if (pre)
+    for (uint32_t r = 1; r < R; r++) {
+      const uint64_t e = e0 + (uint64_t) r * 256u + threadIdx.x;
+      if (e < ncand) off[e] += pre;
+    }
 }
 
 // Pass D: the pairs of every candidate row at its scanned offset,
@@ -423,6 +563,64 @@ __global__ void __launch_bounds__(256) mp_gather_kernel(const uint64_t *src, con
   }
 }
 
+// Small ordered passes (T <= mp_rank_max()): the stable LSD passes below
+// are one rank count instead -- the final order is the composite key
+// (k_{NK-1}, ..., k_1, emission index) in lexicographic order, so an
+// entry's place is the number of entries before it under that order.  Each
+// workgroup counts, for 256 entries i, the entries of one MP_RANK_J-slice j
+// that precede i (the slice staged in LDS, the loop unrolled so its LDS
+// reads overlap) and adds them into rank[i]; one scatter moves the triples.
+// At C2 (3,365 pairs) that is 14 x 53 workgroups, against three rocprim
+// sorts of ~5 kernels each.
+#define MP_RANK_J 64
+template <int NK>
+__global__ void __launch_bounds__(256) mp_rank_kernel(const uint64_t *keys, uint64_t T,
+                                                      uint32_t *rank) {
+  __shared__ uint64_t kj[NK][MP_RANK_J];
+  const uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  const uint64_t j0 = (uint64_t) blockIdx.y * MP_RANK_J;
+  const uint32_t jn = T - j0 < MP_RANK_J ? (uint32_t) (T - j0) : MP_RANK_J;
+  if (threadIdx.x < MP_RANK_J)
+#pragma unroll
+    for (int k = 0; k < NK; k++)   // past T: all ones, after every entry
+      kj[k][threadIdx.x] = threadIdx.x < jn ? keys[(uint64_t) k * T + j0 + threadIdx.x] : ~0ull;
+  uint64_t ki[NK];
+#pragma unroll
+  for (int k = 0; k < NK; k++) ki[k] = i < T ? keys[(uint64_t) k * T + i] : 0;
+  __syncthreads();
+  if (i >= T) return;
+  uint32_t cnt = 0;
+#pragma unroll 16
+  for (uint32_t t = 0; t < MP_RANK_J; t++) {
+    // lt: entry j0+t sorts before i; eq: equal keys (then emission order)
+    bool lt = false, eq = true;
+#pragma unroll
+    for (int k = NK - 1; k >= 0; k--) {
+      const uint64_t a = kj[k][t];
+      lt = lt || (eq && a < ki[k]);
+      eq = eq && a == ki[k];
+    }
+    cnt += (t < jn && (lt || (eq && j0 + t < i))) ? 1u : 0u;
+  }
+  if (cnt) atomicAdd(&rank[i], cnt);
+}
+
+__global__ void __launch_bounds__(256) mp_rank_scatter_kernel(const uint64_t *tri,
+                                                              const uint32_t *rank, uint64_t T,
+                                                              uint64_t *out) {
+  MP_FOR(i, T) {
+    const uint64_t r = rank[i];
+#pragma unroll
+    for (int w = 0; w < 3; w++) out[3 * r + w] = tri[3 * i + w];
+  }
+}
+
+// largest ordered pass sorted by ranks (GT_MP_RANK_MAX overrides; 0 = never)
+static uint64_t mp_rank_max() {
+  const char *e = getenv("GT_MP_RANK_MAX");
+  return e ? strtoull(e, NULL, 0) : (uint64_t) 16384;
+}
+
 __global__ void mp_total_kernel(const uint32_t *cnt, const uint64_t *off, uint64_t n,
                                 uint64_t *total) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *total = n == 0 ? 0 : off[n - 1] + cnt[n - 1];
@@ -466,6 +664,9 @@ struct GtMaxpairsPlan {
   uint32_t *cnt;                 // ncand pair counts
   uint64_t *off;                 // ncand exclusive offsets
   uint64_t *total;               // 1
+  uint16_t *masks;               // nwg * 256 candidate masks of 16 rows (pass A -> B)
+  uint64_t *st_cnt;              // look-back status words (count workgroups)
+  uint32_t epoch;                // count passes so far (the status words' tag)
   void *scan_tmp;
   size_t scan_tmp_bytes;
   bool counted;
@@ -482,11 +683,27 @@ static unsigned mp_blocks(uint64_t n) {
   return (unsigned) (b > MP_MAX_BLOCKS ? MP_MAX_BLOCKS : (b ? b : 1));
 }
 
+// the single-pass count's grid: 256 * R candidates per workgroup, R > 1
+// only where one per workgroup would exceed the grid cap
+static uint64_t mp_count_grid(uint64_t ncand, uint32_t *R) {
+  const uint64_t per = (ncand + 256u * MP_MAX_BLOCKS - 1) / (256u * MP_MAX_BLOCKS);
+  const uint64_t r = per ? per : 1;
+  if (R) *R = (uint32_t) r;
+  const uint64_t g = (ncand + 256u * r - 1) / (256u * r);
+  return g ? g : 1;
+}
+
+// GT_MP_LOOKBACK=0: pass C, its scan and the total as three kernels always
+static bool mp_lookback_on() {
+  const char *e = getenv("GT_MP_LOOKBACK");
+  return !(e && e[0] == '0');
+}
+
 extern "C" void gt_maxpairs_plan_delete(GtMaxpairsPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
   void *bufs[] = {p->X, p->RM, p->RO, p->wg_cand, p->wg_cand_off, p->list, p->cnt, p->off,
-                  p->total, p->scan_tmp, p->hier};
+                  p->total, p->scan_tmp, p->hier, p->masks, p->st_cnt};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) (void) hipFree(bufs[i]);
   free(p);
@@ -530,6 +747,10 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
   p->nwg = (N + MP_WG_ROWS - 1) / MP_WG_ROWS;
   MPCHK(hipMalloc(&p->wg_cand, sizeof (uint64_t) * (p->nwg + 1)));
   MPCHK(hipMalloc(&p->wg_cand_off, sizeof (uint64_t) * (p->nwg + 1)));
+  // whole groups of MP_WR_GROUP pass-A workgroups; the masks past the last
+  // one stay zero
+  MPCHK(hipMalloc(&p->masks, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
+  MPCHK(hipMemset(p->masks, 0, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
   MPCHK(hipMalloc(&p->total, sizeof (uint64_t)));
   MPCHK(hipMemset(p->total, 0, sizeof (uint64_t)));
   MPCHK(hipMalloc(&derr, sizeof (uint32_t)));
@@ -584,7 +805,7 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
                                   (size_t) p->nwg, rocprim::plus<uint64_t>(), (hipStream_t) 0));
     p->scan_tmp_bytes = b1;
     hipLaunchKernelGGL(mp_cand_count_kernel, dim3((unsigned) p->nwg), dim3(256), 0, 0, in->lcp_dev,
-                       N, minlen < 255u ? minlen : 255u, p->wg_cand);
+                       N, minlen < 255u ? minlen : 255u, p->wg_cand, p->masks);
     MPCHK(hipGetLastError());
     MPCHK(hipMalloc(&p->scan_tmp, b1 ? b1 : 16));
     MPCHK(rocprim::exclusive_scan(p->scan_tmp, b1, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
@@ -597,6 +818,8 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
   MPCHK(hipMalloc(&p->list, sizeof (uint64_t) * (p->ncand + 1)));
   MPCHK(hipMalloc(&p->cnt, sizeof (uint32_t) * (p->ncand + 1)));
   MPCHK(hipMalloc(&p->off, sizeof (uint64_t) * (p->ncand + 1)));
+  MPCHK(hipMalloc(&p->st_cnt, sizeof (uint64_t) * (MP_LB_MAX_WG + 1)));
+  MPCHK(hipMemset(p->st_cnt, 0, sizeof (uint64_t) * (MP_LB_MAX_WG + 1)));
   if (p->ncand > 0) {
     size_t b2 = 0;
     MPCHK(rocprim::exclusive_scan(nullptr, b2, p->cnt, p->off, (uint64_t) 0, (size_t) p->ncand,
@@ -634,22 +857,33 @@ extern "C" int gt_maxpairs_plan_count(GtMaxpairsPlan *p, void *stream) {
   } else {
     size_t bytes = p->scan_tmp_bytes;
     hipLaunchKernelGGL(mp_cand_count_kernel, dim3((unsigned) p->nwg), dim3(256), 0, s,
-                       p->in.lcp_dev, N, mf, p->wg_cand);
+                       p->in.lcp_dev, N, mf, p->wg_cand, p->masks);
     MPCHK(hipGetLastError());
+    // (one 1024-thread workgroup scanning the 24,414 counts of C2 took 34.8 us)
     MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
                                   (size_t) p->nwg, rocprim::plus<uint64_t>(), s));
-    hipLaunchKernelGGL(mp_cand_write_kernel, dim3((unsigned) p->nwg), dim3(256), 0, s,
-                       p->in.lcp_dev, N, mf, p->wg_cand_off, p->list);
+    hipLaunchKernelGGL(mp_cand_write_kernel, dim3((unsigned) ((p->nwg + MP_WR_GROUP - 1) / MP_WR_GROUP)),
+                       dim3(256), 0, s, p->masks, p->wg_cand_off, p->list);
     MPCHK(hipGetLastError());
-    hipLaunchKernelGGL((mp_count_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
-                       p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->list, nc, p->minlen,
-                       p->cnt);
-    MPCHK(hipGetLastError());
-    bytes = p->scan_tmp_bytes;
-    MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->cnt, p->off, (uint64_t) 0, (size_t) nc,
-                                  rocprim::plus<uint64_t>(), s));
-    hipLaunchKernelGGL(mp_total_kernel, dim3(1), dim3(64), 0, s, p->cnt, p->off, nc, p->total);
-    MPCHK(hipGetLastError());
+    uint32_t R = 1;
+    const uint64_t g = mp_count_grid(nc, &R);
+    if (g <= MP_LB_MAX_WG && mp_lookback_on()) {
+      p->epoch = p->epoch % 0xffffu + 1u;   // tags 1 .. 65535: never the last pass's
+      hipLaunchKernelGGL((mp_count_scan_kernel<uint32_t>), dim3((unsigned) g), dim3(256), 0, s,
+                         p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->list, nc, p->minlen, R,
+                         p->st_cnt, (uint64_t) p->epoch, p->cnt, p->off, p->total);
+      MPCHK(hipGetLastError());
+    } else {
+      hipLaunchKernelGGL((mp_count_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
+                         p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->list, nc, p->minlen,
+                         p->cnt);
+      MPCHK(hipGetLastError());
+      bytes = p->scan_tmp_bytes;
+      MPCHK(rocprim::exclusive_scan(p->scan_tmp, bytes, p->cnt, p->off, (uint64_t) 0, (size_t) nc,
+                                    rocprim::plus<uint64_t>(), s));
+      hipLaunchKernelGGL(mp_total_kernel, dim3(1), dim3(64), 0, s, p->cnt, p->off, nc, p->total);
+      MPCHK(hipGetLastError());
+    }
   }
   p->counted = true;
   return 0;
@@ -749,6 +983,7 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   void *st = NULL;
   size_t sb = 0;
   MpKeys K;
+  bool by_rank = false;
   if (!p->counted) return -1;
   MPCHK(hipSetDevice(p->in.device));
   MPCHK(hipStreamSynchronize(s));
@@ -766,12 +1001,13 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   MPCHK(smax_dev_alloc((void **) &tri, sizeof (uint64_t) * 3 * T));
   MPCHK(smax_dev_alloc((void **) &keys, sizeof (uint64_t) * (K.split ? 4 : 3) * T));
   MPCHK(smax_dev_alloc((void **) &ktmp, sizeof (uint64_t) * T));
-  MPCHK(smax_dev_alloc((void **) &pa, sizeof (uint64_t) * T));
-  MPCHK(smax_dev_alloc((void **) &pb, sizeof (uint64_t) * T));
   K.k1 = keys;
   K.k2 = keys + T;
   K.k3 = keys + 2 * T;
   K.k4 = K.split ? keys + 3 * T : nullptr;
+  // small passes are ordered by rank counts (mp_rank_kernel) in ktmp
+  by_rank = T <= mp_rank_max() && (T + MP_RANK_J - 1) / MP_RANK_J <= 65535;
+  K.rank0 = by_rank ? (uint32_t *) ktmp : nullptr;
   if (p->in.suf_bytes == 8)
     hipLaunchKernelGGL((mp_emit_ord_kernel<uint64_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
                        p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
@@ -781,6 +1017,24 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
                        p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
                        p->minlen, p->cnt, p->off, tri, T, p->h, K);
   MPCHK(hipGetLastError());
+  if (by_rank) {
+    uint32_t *rank = K.rank0;   // T u64 hold T u32 ranks, zeroed by the emission
+    const dim3 grid((unsigned) ((T + 255) / 256), (unsigned) ((T + MP_RANK_J - 1) / MP_RANK_J));
+    if (K.split)
+      hipLaunchKernelGGL(mp_rank_kernel<4>, grid, dim3(256), 0, s, keys, T, rank);
+    else
+      hipLaunchKernelGGL(mp_rank_kernel<3>, grid, dim3(256), 0, s, keys, T, rank);
+    MPCHK(hipGetLastError());
+    hipLaunchKernelGGL(mp_rank_scatter_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, tri, rank, T,
+                       out_dev);
+    MPCHK(hipGetLastError());
+    MPCHK(hipStreamSynchronize(s));
+    void *bufs[] = {tri, keys, ktmp};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
+    return 0;
+  }
+  MPCHK(smax_dev_alloc((void **) &pa, sizeof (uint64_t) * T));
+  MPCHK(smax_dev_alloc((void **) &pb, sizeof (uint64_t) * T));
   hipLaunchKernelGGL(mp_iota_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, pa, T);
   MPCHK(hipGetLastError());
   MPCHK(rocprim::radix_sort_pairs(nullptr, sb, ktmp, ktmp, pa, pb, (size_t) T, 0, 64, s));

@@ -18,6 +18,8 @@ algorithms read only the LCP array, the BWT and the suffix array).
     orc_maxpairs_blocks (the definition, block by block); the suffix array
     is suftab[r] = N - r, so positions map back to rows.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -123,6 +125,20 @@ def test_maxpairs_past_2_32(tables):
     plan.emit_ordered(out.data_ptr(), T)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint64).reshape(-1, 3).copy()
+    # the other ordering path (rank counting with the 4-key split, or the
+    # radix passes) on the same pass: the same calls in the same order
+    other = "0" if T <= 16384 else str(T)
+    old = os.environ.get("GT_MP_RANK_MAX")
+    os.environ["GT_MP_RANK_MAX"] = other
+    try:
+        plan.emit_ordered(out.data_ptr(), T)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("GT_MP_RANK_MAX")
+        else:
+            os.environ["GT_MP_RANK_MAX"] = old
+    assert np.array_equal(out.cpu().numpy().view(np.uint64).reshape(-1, 3), got)
     plan.close()
     del lcp_t, llv_t, bwt_t, suf_t, out       # the plan borrowed them until here
     # positions -> rows (suftab[r] = N - r); each pair comes in the reference's

@@ -93,6 +93,52 @@ def test_random_repetitive(seed):
         assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen)), minlen
 
 
+@pytest.mark.parametrize("rank_max", ["0", "1000000000"])
+def test_ordered_pass_rank_and_radix_paths(monkeypatch, rank_max):
+    # emit_ordered sorts a small pass (T <= GT_MP_RANK_MAX, 16384 by default)
+    # by rank counting and a larger one by stable LSD radix passes; both must
+    # give the reference's calls exactly, forced either way here
+    monkeypatch.setenv("GT_MP_RANK_MAX", rank_max)
+    e = oracle_esa("at1MB")
+    for minlen in (8, 20):
+        assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen)), minlen
+    rng = np.random.default_rng(303)
+    e = O.Esa(_repetitive(rng, 60000, 0.01))
+    for minlen in (12, 30):
+        assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen)), minlen
+
+
+def test_count_pass_separate_scan_path(monkeypatch):
+    # GT_MP_LOOKBACK=0: the count pass as count, scan and write kernels (the
+    # default fuses each pair with a decoupled look-back)
+    monkeypatch.setenv("GT_MP_LOOKBACK", "0")
+    e = oracle_esa("at1MB")
+    for minlen in (8, 20, 300):
+        assert np.array_equal(_gpu(e, minlen), O.maxpairs(e, minlen)), minlen
+    e = O.Esa(_repetitive(np.random.default_rng(304), 50000, 0.01))
+    assert np.array_equal(_gpu(e, 12), O.maxpairs(e, 12))
+
+
+def test_count_passes_past_the_status_tag_wrap():
+    # the look-back status words carry the pass number mod 65535: 70,000
+    # count passes on one plan (the tag wraps once) keep the same list,
+    # offsets and total
+    import torch
+    e = oracle_esa("at1MB")
+    d = G.DeviceEsa(e.text, keep_suftab=True)
+    p = d.maxpairs_plan(20)
+    want = O.maxpairs(e, 20)
+    out = torch.empty(3 * len(want), dtype=torch.int64, device="cuda")
+    for k in range(70000):
+        p.count()
+        if k in (0, 65534, 65535, 65536, 69999):
+            assert p.total() == len(want), k
+            p.emit_ordered(out.data_ptr(), len(want))
+            assert np.array_equal(out.cpu().numpy().view(np.uint64).reshape(-1, 3), want), k
+    p.close()
+    d.release()
+
+
 def test_long_lcp_values():
     # an exact 1200-symbol duplication: pairs of length >= 255 need the .llv
     rng = np.random.default_rng(9)
