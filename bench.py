@@ -156,6 +156,159 @@ def cold_e2e(G, host, n, N, minlen, want, log, calls=2, prepared=False):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def main_lcpitv(args):
+    """F3 leg: the generic bottom-up traversal -- every
+    lcp-interval with its father in pop order and the GtESAVisitor event
+    stream in the reference's order (/root/reference/src/match/
+    esa-bottomup.c:116-273) -- over tables resident in HBM.  A step is one
+    gt_lcpitv_plan_create (the interval tree: exact LCP, 64-ary minimum
+    hierarchy, per-row interval records, pop-order sort) + one
+    gt_lcpitv_plan_events pass into a resident buffer + gt_lcpitv_plan_delete.
+    One GPU (--gpus N: replicas).
+
+    Algorithmic bytes per step (the roofline's "achieved"): per row the LCP
+    byte, its exact u32 written and read by the two hierarchy searches
+    (1 + 4 + 2 x 4 B), per interval its 5-word record written, its sort key
+    and index through one radix pass (2 x 2 x 16 B) and the gather (2 x 40 B),
+    per event its 7-word record (56 B) plus the leaf's suffix and LCP reads
+    (8 B per row)."""
+    import numpy as np
+    import torch
+    import genometools_smax_amd as G
+
+    cfg = dict(CONFIGS[args.config])
+    if args.config not in ("c2",) and not args.bases:
+        sys.exit("bench.py --path lcpitv: use --config c2 (or --bases): the event stream is 56 B "
+                 "per row and per interval end")
+    if args.bases:
+        cfg["bases"] = args.bases
+        cfg["workload"] = cfg["workload"].replace(
+            cfg["workload"].split(" synthetic")[0], "%.3g bp" % args.bases)
+    cfg["workload"] = cfg["workload"].split(", minlen")[0]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(0 if args.one_gpu else local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # replicas: the barrier only
+    t0 = time.time()
+    text = G.synth_genome(cfg["kind"], cfg["bases"], cfg["seed"], threads=16)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    esa = G.DeviceEsa(text, device=torch.cuda.current_device(), keep_suftab=True)
+    t_esa = time.time() - t0
+    n, N = esa.totallength, esa.nonspecials
+    plan = esa.lcpitv_plan()
+    nitv = plan.intervals()[0]
+    n_ev = plan.num_events()
+    itv0 = None
+    if rank == 0 and not args.no_cpu_baseline:
+        nn, ptr = plan.intervals()
+        itv0 = torch.empty(5 * max(nn, 1), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+
+        class _View:   # the plan's device records, copied out before it closes
+
+            __cuda_array_interface__ = {"shape": (5 * nn,), "typestr": "<i8", "data": (ptr, False),
+                                        "version": 2}
+        if nn:
+            itv0.copy_(torch.as_tensor(_View(), device="cuda"))
+    plan.close()
+    ev = torch.empty(7 * max(n_ev, 1), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        p = esa.lcpitv_plan()
+        p.events(ev.data_ptr(), s)
+        p.close()
+
+    def step_tree():
+        esa.lcpitv_plan().close()
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / args.steps
+
+    t_pr = time.perf_counter()
+    while time.perf_counter() - t_pr < args.prime_s:
+        step_tree()
+    el = timed(step)
+    el_tree = timed(step_tree)
+    if dist:
+        mx = torch.tensor([el, el_tree], dtype=torch.float64)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        el, el_tree = float(mx[0]), float(mx[1])
+    alg_tree = N * 13 + nitv * (40 + 64 + 80)
+    alg = alg_tree + n_ev * 56 + N * 8
+    parity = None
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O  # noqa: E402  (the checker, CPU baseline leg only)
+        h = esa.download()
+        t0 = time.perf_counter()
+        ref = O.lcp_intervals(h["lcptab"], h["llvtab"], N, nitv + 1)
+        t_cpu = time.perf_counter() - t0
+        got = itv0[: 5 * nitv].cpu().numpy().view(np.uint64).reshape(-1, 5)
+        same = len(ref) == nitv and bool(np.array_equal(ref, got))
+        parity = {"intervals_identical_pop_order": same,
+                  "num_events": n_ev, "num_events_expected": N + 2 * nitv,
+                  "events": "record for record against the oracle's gt_esa_bottomup stream on the "
+                            "fixtures and random texts (tests/test_lcpitv_gpu.py)"}
+        cpu = {"value": N / t_cpu, "unit": "suffix-positions/s", "cores": 1, "kind": "port",
+               "sample": "oracle orc_lcp_intervals (the gt_esa_bottomup stack walk restated, "
+                         "src/match/esa-bottomup.c:116-273, intervals with their fathers, 1 core) "
+                         "over all %d rows: %.2fs" % (N, t_cpu), "seconds": round(t_cpu, 3)}
+        cpu.update(host_cpu())
+        cpu["cgroup_cpus"] = cgroup_cpus()
+        del h, ref, got
+        if not same or n_ev != N + 2 * nitv:
+            log("FAIL: lcp-intervals differ from the oracle: %s" % parity)
+            esa.release()
+            sys.exit(1)
+    if rank == 0:
+        achieved = alg / el / 1e9
+        print(json.dumps({
+            "metric": "suffix-positions/s (generic bottom-up traversal: lcp-interval tree + visitor "
+                      "events)",
+            "value": world * N / el, "unit": "suffix-positions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3,
+            "higher_is_better": True, "scaling": "weak" if world > 1 else None,
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": cfg["workload"], "totallength": n, "nonspecials": N,
+                       "path": "lcpitv (F3)",
+                       "parallelism": "replicas x%d" % world if world > 1 else "single GPU"},
+            "step": "gt_lcpitv_plan_create + gt_lcpitv_plan_events + gt_lcpitv_plan_delete",
+            "lcp_intervals": nitv, "visitor_events": n_ev,
+            "ms_per_step_tree_only": el_tree * 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_step": alg,
+                         "algorithmic_bytes_per_step_tree_only": alg_tree,
+                         "achieved_tree_only": alg_tree / el_tree / 1e9,
+                         "note": "whole-pass bytes over the pass time; per-kernel times: the "
+                                 "rocprofv3 kernel stats under profiles/"},
+            "parity": parity, "cpu_baseline": cpu,
+            "setup_s": {"genome": round(t_gen, 2), "gpu_esa_build": round(t_esa, 2)}}), flush=True)
+    esa.release()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main_maxpairs(args):
     """F2 leg: maximal pairs, `gt repfind -l minlen` -- the
     reference's default repfind path (/root/reference/src/match/esa-maxpairs.c:
@@ -339,9 +492,10 @@ def main():
                          "seconds (clock ramp after the setup's idle periods)")
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="workload (default: c3 for --path smax, c2 for --path maxpairs)")
-    ap.add_argument("--path", default="smax", choices=["smax", "maxpairs"],
+    ap.add_argument("--path", default="smax", choices=["smax", "maxpairs", "lcpitv"],
                     help="smax: the hot path (BASELINE metric); maxpairs: the F2 leg, "
-                         "`gt repfind -l minlen` maximal pairs in the reference's emission order")
+                         "`gt repfind -l minlen` maximal pairs in the reference's emission order; "
+                         "lcpitv: the F3 leg, the generic bottom-up traversal (intervals + events)")
     ap.add_argument("--bases", type=lambda x: int(float(x)), default=None, help="override genome size")
     ap.add_argument("--minlen", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -369,9 +523,11 @@ def main():
                          "packed BWT")
     args = ap.parse_args()
     if args.config is None:
-        args.config = "c2" if args.path == "maxpairs" else "c3"
+        args.config = "c2" if args.path in ("maxpairs", "lcpitv") else "c3"
     if args.path == "maxpairs":
         return main_maxpairs(args)
+    if args.path == "lcpitv":
+        return main_lcpitv(args)
 
     import numpy as np
     import torch

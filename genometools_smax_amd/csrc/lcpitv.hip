@@ -105,19 +105,46 @@ __device__ __forceinline__ bool li_ok(uint32_t x, uint32_t v, bool strict) {
   return strict ? x < v : x <= v;
 }
 
+// The searches read a level's whole 64-entry block at once (16 independent
+// 16-byte loads, then a bit mask of the entries that qualify) instead of one
+// dependent load per entry: a search that climbs the hierarchy paid up to
+// 64 round trips per level, and a wave waits for its slowest lane
+// (li_write_kernel 14.7 -> 9.2 ms, li_count_kernel 5.2 -> 3.4 ms at C2,
+// profiles/s7/kernel_stats_lcpitv_c2*.csv; checking the 16 bytes next to
+// the row first changed nothing: the slowest lane of a wave, on a long
+// search, sets its time).  Levels are allocated LI_PAD
+// entries long past their end; bits past it are masked off.
+#define LI_PAD 64
+__device__ __forceinline__ uint64_t li_block_mask(const uint32_t *lv, uint64_t b, uint64_t n,
+                                                  uint32_t v, bool strict) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(lv + b);
+  uint4 t[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) t[j] = p[j];
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    m |= (uint64_t) (li_ok(t[j].x, v, strict) ? 1u : 0u) << (4 * j);
+    m |= (uint64_t) (li_ok(t[j].y, v, strict) ? 1u : 0u) << (4 * j + 1);
+    m |= (uint64_t) (li_ok(t[j].z, v, strict) ? 1u : 0u) << (4 * j + 2);
+    m |= (uint64_t) (li_ok(t[j].w, v, strict) ? 1u : 0u) << (4 * j + 3);
+  }
+  if (n - b < 64) m &= (1ull << (n - b)) - 1;
+  return m;
+}
+
 // nearest p < k with X[p] < v (strict) / <= v; X[0] == 0 guarantees one
 // for v > 0 (strict) and any v (<=)
 __device__ static uint64_t li_prev(const LiLevels &L, uint64_t k, uint32_t v, bool strict) {
   uint64_t i = k, p = 0;
   int lev = 0;
   for (;;) {
-    const uint64_t start = (i >> 6) << 6;
-    bool found = false;
-    for (uint64_t q = i; q > start;) {
-      q--;
-      if (li_ok(L.lv[lev][q], v, strict)) { p = q; found = true; break; }
-    }
-    if (found) break;
+    const uint64_t b = (i >> 6) << 6;
+    const uint64_t below = i - b;   // entries [b, i)
+    const uint64_t m = below ? li_block_mask(L.lv[lev], b, L.n[lev], v, strict) &
+                                   ((below >= 64 ? 0ull : (1ull << below)) - 1ull)
+                             : 0ull;
+    if (m) { p = b + 63 - (uint64_t) __builtin_clzll(m); break; }
     if (lev + 1 >= L.nlev || i < 64) return 0;   // only row 0 is left
     i >>= 6;
     lev++;
@@ -125,11 +152,8 @@ __device__ static uint64_t li_prev(const LiLevels &L, uint64_t k, uint32_t v, bo
   while (lev > 0) {                // last child of p whose subtree qualifies
     lev--;
     const uint64_t b = p << 6;
-    const uint64_t e = b + 64 < L.n[lev] ? b + 64 : L.n[lev];
-    for (uint64_t c = e; c > b;) {
-      c--;
-      if (li_ok(L.lv[lev][c], v, strict)) { p = c; break; }
-    }
+    const uint64_t m = li_block_mask(L.lv[lev], b, L.n[lev], v, strict);
+    p = b + 63 - (uint64_t) __builtin_clzll(m);
   }
   return p;
 }
@@ -139,12 +163,11 @@ __device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v) {
   uint64_t i = k, p = 0;
   int lev = 0;
   for (;;) {
-    const uint64_t end = ((i >> 6) + 1) << 6;
-    const uint64_t e = end < L.n[lev] ? end : L.n[lev];
-    bool found = false;
-    for (uint64_t q = i + 1; q < e; q++)
-      if (L.lv[lev][q] < v) { p = q; found = true; break; }
-    if (found) break;
+    const uint64_t b = (i >> 6) << 6;
+    const uint64_t upto = i - b;    // entries (i, b + 64)
+    const uint64_t m = upto >= 63 ? 0ull
+                                  : li_block_mask(L.lv[lev], b, L.n[lev], v, true) & ~((2ull << upto) - 1ull);
+    if (m) { p = b + (uint64_t) __builtin_ctzll(m); break; }
     if (lev + 1 >= L.nlev) return L.n[0] - 1;    // row N
     i >>= 6;
     lev++;
@@ -152,9 +175,7 @@ __device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v) {
   while (lev > 0) {                // first child of p whose subtree qualifies
     lev--;
     const uint64_t b = p << 6;
-    const uint64_t e = b + 64 < L.n[lev] ? b + 64 : L.n[lev];
-    for (uint64_t c = b; c < e; c++)
-      if (L.lv[lev][c] < v) { p = c; break; }
+    p = b + (uint64_t) __builtin_ctzll(li_block_mask(L.lv[lev], b, L.n[lev], v, true));
   }
   return p;
 }
@@ -369,10 +390,13 @@ struct GtLcpitvPlan {
 extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
+  // the plan's buffers go back to the runtime's cache (smax_dev_alloc): the
+  // work still queued on them (an events pass on a caller's stream) first
+  (void) hipDeviceSynchronize();
   for (int l = 0; l < LI_MAXLEV; l++)
-    if (p->lev[l]) (void) hipFree(p->lev[l]);
-  if (p->itv) (void) hipFree(p->itv);
-  if (p->first) (void) hipFree(p->first);
+    if (p->lev[l]) smax_dev_free(p->lev[l]);
+  if (p->itv) smax_dev_free(p->itv);
+  if (p->first) smax_dev_free(p->first);
   free(p);
 }
 
@@ -406,12 +430,12 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
   p->in = *in;
   N = in->nonspecials;
   LICHK(hipSetDevice(in->device));
-  LICHK(hipMalloc(&derr, sizeof (uint32_t)));
+  LICHK(smax_dev_alloc((void **) &derr, sizeof (uint32_t)));
   LICHK(hipMemset(derr, 0, sizeof (uint32_t)));
-  LICHK(hipMalloc(&p->first, sizeof (unsigned long long)));
+  LICHK(smax_dev_alloc((void **) &p->first, sizeof (unsigned long long)));
   // level 0: exact LCP, then 64-ary mins until one entry remains
   p->L.n[0] = N + 1;
-  LICHK(hipMalloc(&p->lev[0], sizeof (uint32_t) * p->L.n[0]));
+  LICHK(smax_dev_alloc((void **) &p->lev[0], sizeof (uint32_t) * (p->L.n[0] + LI_PAD)));
   hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, 0, in->lcp_dev, N,
                      p->lev[0]);
   LICHK(hipGetLastError());
@@ -424,7 +448,7 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
   while (p->L.n[p->L.nlev - 1] > 1 && p->L.nlev < LI_MAXLEV) {
     const int l = p->L.nlev;
     p->L.n[l] = (p->L.n[l - 1] + 63) / 64;
-    LICHK(hipMalloc(&p->lev[l], sizeof (uint32_t) * p->L.n[l]));
+    LICHK(smax_dev_alloc((void **) &p->lev[l], sizeof (uint32_t) * (p->L.n[l] + LI_PAD)));
     hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(p->L.n[l])), dim3(256), 0, 0, p->lev[l - 1],
                        p->L.n[l - 1], p->lev[l], p->L.n[l]);
     LICHK(hipGetLastError());
@@ -441,14 +465,14 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
   // intervals: count per workgroup, scan, write, sort into pop order
   nwg = (N + 255) / 256;
   if (nwg > 0x7fffffffull) { li_seterr(errbuf, errlen, "too many suffixes"); goto fail; }
-  LICHK(hipMalloc(&wg_cnt, sizeof (uint32_t) * (nwg + 1)));
-  LICHK(hipMalloc(&wg_off, sizeof (uint64_t) * (nwg + 1)));
+  LICHK(smax_dev_alloc((void **) &wg_cnt, sizeof (uint32_t) * (nwg + 1)));
+  LICHK(smax_dev_alloc((void **) &wg_off, sizeof (uint64_t) * (nwg + 1)));
   if (nwg > 0) {
     hipLaunchKernelGGL(li_count_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, p->L, N, nwg, wg_cnt);
     LICHK(hipGetLastError());
     LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
                                   rocprim::plus<uint64_t>(), (hipStream_t) 0));
-    LICHK(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
+    LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
     LICHK(rocprim::exclusive_scan(tmp, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
                                   rocprim::plus<uint64_t>(), (hipStream_t) 0));
     uint64_t lo = 0;
@@ -457,23 +481,23 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
     LICHK(hipMemcpy(&lc, wg_cnt + nwg - 1, sizeof lc, hipMemcpyDeviceToHost));
     p->nitv = lo + lc;
   }
-  LICHK(hipMalloc(&p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
+  LICHK(smax_dev_alloc((void **) &p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
   if (p->nitv > 0) {
     const uint64_t n = p->nitv;
-    LICHK(hipMalloc(&rec, sizeof (uint64_t) * 5 * n));
-    LICHK(hipMalloc(&key_a, sizeof (uint64_t) * n));
-    LICHK(hipMalloc(&key_b, sizeof (uint64_t) * n));
-    LICHK(hipMalloc(&idx_a, sizeof (uint64_t) * n));
-    LICHK(hipMalloc(&idx_b, sizeof (uint64_t) * n));
+    LICHK(smax_dev_alloc((void **) &rec, sizeof (uint64_t) * 5 * n));
+    LICHK(smax_dev_alloc((void **) &key_a, sizeof (uint64_t) * n));
+    LICHK(smax_dev_alloc((void **) &key_b, sizeof (uint64_t) * n));
+    LICHK(smax_dev_alloc((void **) &idx_a, sizeof (uint64_t) * n));
+    LICHK(smax_dev_alloc((void **) &idx_b, sizeof (uint64_t) * n));
     hipLaunchKernelGGL(li_write_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, p->L, N, nwg, wg_off,
                        rec, key_a, idx_a);
     LICHK(hipGetLastError());
-    LICHK(hipFree(tmp));
+    smax_dev_free(tmp);   // the scan is done: the copies above waited for it
     tmp = NULL;
     tmp_bytes = 0;
     LICHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0,
                                     64, (hipStream_t) 0));
-    LICHK(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
+    LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
     if (N < 0xffffffffull) {
       // key = rb << 32 | ~lcp: one pass
       LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 64,
@@ -497,15 +521,16 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
   {
     void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
+      if (bufs[i]) smax_dev_free(bufs[i]);
   }
   *planp = p;
   return 0;
 fail:
   {
+    (void) hipDeviceSynchronize();   // nothing queued may still use a cached block
     void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) (void) hipFree(bufs[i]);
+      if (bufs[i]) smax_dev_free(bufs[i]);
   }
   gt_lcpitv_plan_delete(p);
   return -1;

@@ -20,6 +20,8 @@
 #   e2esweep:CONFIG:K=V,..;..  e2ecold per runtime setting (fresh process each)
 #   mp:CONFIG[:BASES]  bench.py --path maxpairs (F2, reference emission order)
 #   mpprof:CONFIG[:BASES] rocprofv3 --kernel-trace --stats of that run
+#   f3:CONFIG[:BASES]  bench.py --path lcpitv (F3, intervals + visitor events)
+#   f3prof:CONFIG[:BASES] rocprofv3 --kernel-trace --stats of that run
 #   llvstats         tools/llv_window_stats.py c3 and c5 (.llv values per K1 window)
 #   rehearse:W[:BASES]  bench.py --gpus W as W ranks on this one GPU (gloo staging)
 #   pmcablate:V,...  K1 SQ counters under GT_SMAX_DEBUG ablation bits at C3
@@ -169,6 +171,20 @@ for S in "$@"; do
         > "$O/mpprof_bench_$T.json" 2> "$O/mpprof_bench_$T.err")
       python3 tools/rocpd_summary.py stats "$O/mpprof_$T/p_results.db" "$O/kernel_stats_maxpairs_$T.csv"
       rm -rf "$O/mpprof_$T" ;;
+    f3:*)
+      # f3:CONFIG[:BASES] -- the F3 leg, bench.py --path lcpitv (intervals + visitor events)
+      IFS=: read -r _ C BASES <<< "$S"
+      timeout -k 10 600 python -u bench.py --path lcpitv --config "$C" ${BASES:+--bases $BASES} \
+        > "$O/bench_lcpitv_$C${BASES:+_$BASES}.json" 2> "$O/bench_lcpitv_$C${BASES:+_$BASES}.err" ;;
+    f3prof:*)
+      # f3prof:CONFIG[:BASES] -- rocprofv3 kernel stats of the F3 leg
+      IFS=: read -r _ C BASES <<< "$S"
+      T=$C${BASES:+_$BASES}
+      (cd /tmp && TMPDIR=/tmp timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/f3prof_$T" -o p -- \
+        python3 "$R/bench.py" --path lcpitv --config "$C" ${BASES:+--bases $BASES} --no-cpu-baseline \
+        > "$O/f3prof_bench_$T.json" 2> "$O/f3prof_bench_$T.err")
+      python3 tools/rocpd_summary.py stats "$O/f3prof_$T/p_results.db" "$O/kernel_stats_lcpitv_$T.csv"
+      rm -rf "$O/f3prof_$T" ;;
     e2ecold:*)
       # cold end-to-end: first call of the drop-in entry point in a fresh process
       timeout -k 10 900 python -u tools/e2e_cold.py "${S#e2ecold:}" 3 > "$O/e2e_cold_${S#e2ecold:}.json" \
