@@ -292,27 +292,47 @@ __device__ __forceinline__ uint64_t li_lower_rb(const uint64_t *itv, uint64_t n,
   return lo;
 }
 
+// intervals with rb < v: the plan's prefix array (one load) when it has
+// one, else a binary search over the pop-ordered records (26 dependent
+// loads at C2, in four kernels: 16.5 ms of the events pass, profiles/s7/)
+__device__ __forceinline__ uint64_t li_before(const uint32_t *C, const uint64_t *itv, uint64_t n,
+                                              uint64_t v) {
+  return C != nullptr ? (uint64_t) C[v] : li_lower_rb(itv, n, v);
+}
+
+// the prefix array's input: at rb + 1 of the last interval of each run of
+// equal rb, the number of intervals up to it (a max-scan fills the rest)
+__global__ void __launch_bounds__(256) li_rb_marks_kernel(const uint64_t *itv, uint64_t n,
+                                                          uint32_t *D) {
+  LI_FOR(j, n) {
+    const uint64_t rb = itv[5 * j + 2];
+    if (j + 1 == n || itv[5 * (j + 1) + 2] != rb) D[rb + 1] = (uint32_t) (j + 1);
+  }
+}
+
 // event positions of root edges that consume the reference's
 // firstedgefromroot flag (leaf edges to the root attached in step 1 and
 // branching edges to the root of pops); the first one in stream order gets
 // firstsucc = 1 (src/match/esa-bottomup.c:134-141)
 __global__ void __launch_bounds__(256) li_rootfirst_leaf_kernel(LiLevels L, uint64_t N,
                                                                 const uint64_t *itv, uint64_t nitv,
+                                                                const uint32_t *C,
                                                                 unsigned long long *first) {
   LI_FOR(idx, N) {
     const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
     if (X != 0 || Y > X) continue;
-    const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
+    const uint64_t pos = idx + 2 * li_before(C, itv, nitv, idx);
     atomicMin(first, (unsigned long long) pos);
   }
 }
 
 __global__ void __launch_bounds__(256) li_rootfirst_itv_kernel(const uint64_t *itv, uint64_t nitv,
+                                                               const uint32_t *C,
                                                                unsigned long long *first) {
   LI_FOR(j, nitv) {
     const uint64_t *r = itv + 5 * j;
     if (r[3] != 0) continue;
-    const uint64_t g = li_lower_rb(itv, nitv, r[2]);
+    const uint64_t g = li_before(C, itv, nitv, r[2]);
     const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g) + 1;
     atomicMin(first, (unsigned long long) pos);
   }
@@ -322,12 +342,12 @@ __global__ void __launch_bounds__(256) li_rootfirst_itv_kernel(const uint64_t *i
 template <typename SufT>
 __global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_t N,
                                                              const uint64_t *itv, uint64_t nitv,
-                                                             const void *suf,
+                                                             const uint32_t *C, const void *suf,
                                                              const unsigned long long *first,
                                                              uint64_t *ev) {
   LI_FOR(idx, N) {
     const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
-    const uint64_t pos = idx + 2 * li_lower_rb(itv, nitv, idx);
+    const uint64_t pos = idx + 2 * li_before(C, itv, nitv, idx);
     uint64_t *w = ev + 7 * pos;
     w[0] = 0;
     if (Y <= X) {            // attached to the interval of depth X holding idx
@@ -349,11 +369,12 @@ __global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_
 // (1, firstsucc, fd, flb, sd, slb, srb); a father that is new at rb (same
 // lb, pushed after the pops) gets the firstsucc edge with its own lb
 __global__ void __launch_bounds__(256) li_events_itv_kernel(const uint64_t *itv, uint64_t nitv,
+                                                            const uint32_t *C,
                                                             const unsigned long long *first,
                                                             uint64_t *ev) {
   LI_FOR(j, nitv) {
     const uint64_t *r = itv + 5 * j;
-    const uint64_t g = li_lower_rb(itv, nitv, r[2]);
+    const uint64_t g = li_before(C, itv, nitv, r[2]);
     const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g);
     uint64_t *w = ev + 7 * pos;
     w[0] = 2; w[1] = 0; w[2] = r[0]; w[3] = r[1]; w[4] = r[2]; w[5] = 0; w[6] = 0;
@@ -384,6 +405,7 @@ struct GtLcpitvPlan {
   LiLevels L;
   uint64_t nitv;
   uint64_t *itv;                 // 5 * nitv, pop order
+  uint32_t *before;              // N + 1: intervals with rb < v (NULL past 2^32 rows)
   unsigned long long *first;     // position of the first root edge
 };
 
@@ -396,6 +418,7 @@ extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
   for (int l = 0; l < LI_MAXLEV; l++)
     if (p->lev[l]) smax_dev_free(p->lev[l]);
   if (p->itv) smax_dev_free(p->itv);
+  if (p->before) smax_dev_free(p->before);
   if (p->first) smax_dev_free(p->first);
   free(p);
 }
@@ -403,7 +426,7 @@ extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
 extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInput *in,
                                      char *errbuf, size_t errlen) {
   GtLcpitvPlan *p = NULL;
-  uint32_t *derr = NULL, herr = 0, *wg_cnt = NULL;
+  uint32_t *derr = NULL, herr = 0, *wg_cnt = NULL, *dmarks = NULL;
   uint64_t *wg_off = NULL, *rec = NULL, *key_a = NULL, *key_b = NULL, *idx_a = NULL,
            *idx_b = NULL;
   void *tmp = NULL;
@@ -516,10 +539,35 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
     }
     hipLaunchKernelGGL(li_gather_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, p->itv);
     LICHK(hipGetLastError());
+    if (N < 0xffffffffull) {   // (past 2^32 rows: the binary search; one scan of < 2^32 items)
+      // the events pass's positions: before[v] = intervals with rb < v, a
+      // max-scan over the run ends (rec's space is free after the gather)
+      uint32_t *D = (uint32_t *) rec;
+      LICHK(smax_dev_alloc((void **) &p->before, sizeof (uint32_t) * (N + 1)));
+      if (sizeof (uint64_t) * 5 * n < sizeof (uint32_t) * (N + 1)) {
+        LICHK(smax_dev_alloc((void **) &dmarks, sizeof (uint32_t) * (N + 1)));
+        D = dmarks;
+      }
+      LICHK(hipMemsetAsync(D, 0, sizeof (uint32_t) * (N + 1), 0));
+      hipLaunchKernelGGL(li_rb_marks_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, p->itv, n, D);
+      LICHK(hipGetLastError());
+      size_t sb = 0;
+      LICHK(rocprim::inclusive_scan(nullptr, sb, D, p->before, (size_t) (N + 1),
+                                    rocprim::maximum<uint32_t>(), (hipStream_t) 0));
+      if (sb > tmp_bytes) {
+        LICHK(hipDeviceSynchronize());   // the sort is done with tmp
+        smax_dev_free(tmp);
+        tmp = NULL;
+        LICHK(smax_dev_alloc((void **) &tmp, sb));
+        tmp_bytes = sb;
+      }
+      LICHK(rocprim::inclusive_scan(tmp, sb, D, p->before, (size_t) (N + 1),
+                                    rocprim::maximum<uint32_t>(), (hipStream_t) 0));
+    }
   }
   LICHK(hipDeviceSynchronize());
   {
-    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp};
+    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp, dmarks};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
       if (bufs[i]) smax_dev_free(bufs[i]);
   }
@@ -528,7 +576,7 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
 fail:
   {
     (void) hipDeviceSynchronize();   // nothing queued may still use a cached block
-    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp};
+    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp, dmarks};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
       if (bufs[i]) smax_dev_free(bufs[i]);
   }
@@ -553,19 +601,19 @@ extern "C" int gt_lcpitv_plan_events(GtLcpitvPlan *p, uint64_t *events_dev, void
   if (N == 0) return 0;
   if (hipMemcpyAsync(p->first, &none, sizeof none, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
   hipLaunchKernelGGL(li_rootfirst_leaf_kernel, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N, p->itv,
-                     n, p->first);
+                     n, p->before, p->first);
   if (n > 0)
     hipLaunchKernelGGL(li_rootfirst_itv_kernel, dim3(li_blocks(n)), dim3(256), 0, s, p->itv, n,
-                       p->first);
+                       p->before, p->first);
   if (p->in.suf_bytes == 4)
     hipLaunchKernelGGL(li_events_leaf_kernel<uint32_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N,
-                       p->itv, n, p->in.suf_dev, p->first, events_dev);
+                       p->itv, n, p->before, p->in.suf_dev, p->first, events_dev);
   else
     hipLaunchKernelGGL(li_events_leaf_kernel<uint64_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N,
-                       p->itv, n, p->in.suf_dev, p->first, events_dev);
+                       p->itv, n, p->before, p->in.suf_dev, p->first, events_dev);
   if (n > 0)
     hipLaunchKernelGGL(li_events_itv_kernel, dim3(li_blocks(n)), dim3(256), 0, s, p->itv, n,
-                       p->first, events_dev);
+                       p->before, p->first, events_dev);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
