@@ -348,20 +348,29 @@ __global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_
   LI_FOR(idx, N) {
     const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
     const uint64_t pos = idx + 2 * li_before(C, itv, nitv, idx);
-    uint64_t *w = ev + 7 * pos;
-    w[0] = 0;
+    uint64_t e1, e2, e3;
     if (Y <= X) {            // attached to the interval of depth X holding idx
-      w[1] = (X == 0 && pos == *first) ? 1u : 0u;
-      w[2] = X;
-      w[3] = X == 0 ? 0 : li_prev(L, idx, X, true);
+      e1 = (X == 0 && pos == *first) ? 1u : 0u;
+      e2 = X;
+      e3 = X == 0 ? 0 : li_prev(L, idx, X, true);
     } else {                 // firstsucc leaf of the new interval (Y, idx)
-      w[1] = 1;
-      w[2] = Y;
-      w[3] = idx;
+      e1 = 1;
+      e2 = Y;
+      e3 = idx;
     }
-    w[4] = suf == nullptr ? 0 : (uint64_t) reinterpret_cast<const SufT *>(suf)[idx];
-    w[5] = 0;
-    w[6] = 0;
+    const uint64_t e4 = suf == nullptr ? 0 : (uint64_t) reinterpret_cast<const SufT *>(suf)[idx];
+    uint64_t *w = ev + 7 * pos;   // 16-byte pieces, as li_events_itv_kernel
+    if ((pos & 1) == 0) {
+      reinterpret_cast<ulonglong2 *>(w)[0] = make_ulonglong2(0, e1);
+      reinterpret_cast<ulonglong2 *>(w)[1] = make_ulonglong2(e2, e3);
+      reinterpret_cast<ulonglong2 *>(w)[2] = make_ulonglong2(e4, 0);
+      w[6] = 0;
+    } else {
+      w[0] = 0;
+      reinterpret_cast<ulonglong2 *>(w + 1)[0] = make_ulonglong2(e1, e2);
+      reinterpret_cast<ulonglong2 *>(w + 1)[1] = make_ulonglong2(e3, e4);
+      reinterpret_cast<ulonglong2 *>(w + 1)[2] = make_ulonglong2(0, 0);
+    }
   }
 }
 
