@@ -239,7 +239,7 @@ __device__ __forceinline__ void li_write_one(const LiLevels &L, uint64_t k, uint
   r[2] = q - 1;
   r[3] = fl;
   r[4] = flb;
-  key[pos] = ((q - 1) << 32) | (uint64_t) (0xffffffffu - v);   // rb < 2^32 (else li_key_kernel)
+  key[pos] = q - 1;   // rb (past 2^32 rows li_key_kernel rewrites the keys)
   idx[pos] = pos;
 }
 
@@ -267,6 +267,24 @@ __global__ void __launch_bounds__(256) li_key_kernel(const uint64_t *rec, const 
   LI_FOR(i, n) {
     const uint64_t *r = rec + 5 * perm[i];
     key[i] = pass == 0 ? (uint64_t) (0xffffffffu - (uint32_t) r[0]) : r[2];
+  }
+}
+
+// the records sorted by rb alone into pop order: each run of equal rb is in
+// row order of its intervals' first l-index, i.e. lcp ascending (an outer
+// interval's l-indices lie at or before an inner one's lb), and the pops
+// take the deepest first -- the run reversed
+__global__ void __launch_bounds__(256) li_gather_rev_kernel(const uint64_t *rec, const uint64_t *idx,
+                                                            const uint64_t *rb,
+                                                            const uint32_t *before, uint64_t n,
+                                                            uint64_t *out) {
+  LI_FOR(i, n) {
+    const uint64_t v = rb[i];
+    const uint64_t dst = (uint64_t) before[v] + before[v + 1] - 1 - i;
+    const uint64_t *r = rec + 5 * (uint64_t) idx[i];
+    uint64_t *w = out + 5 * dst;
+#pragma unroll
+    for (int f = 0; f < 5; f++) w[f] = r[f];
   }
 }
 
@@ -301,12 +319,12 @@ __device__ __forceinline__ uint64_t li_before(const uint32_t *C, const uint64_t 
 }
 
 // the prefix array's input: at rb + 1 of the last interval of each run of
-// equal rb, the number of intervals up to it (a max-scan fills the rest)
-__global__ void __launch_bounds__(256) li_rb_marks_kernel(const uint64_t *itv, uint64_t n,
+// equal rb (rb sorted), the number of intervals up to it (a max-scan fills
+// the rest)
+__global__ void __launch_bounds__(256) li_rb_marks_kernel(const uint64_t *rb, uint64_t n,
                                                           uint32_t *D) {
   LI_FOR(j, n) {
-    const uint64_t rb = itv[5 * j + 2];
-    if (j + 1 == n || itv[5 * (j + 1) + 2] != rb) D[rb + 1] = (uint32_t) (j + 1);
+    if (j + 1 == n || rb[j + 1] != rb[j]) D[rb[j] + 1] = (uint32_t) (j + 1);
   }
 }
 
@@ -541,34 +559,22 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
                                     64, (hipStream_t) 0));
     LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
     if (N < 0xffffffffull) {
-      // key = rb << 32 | ~lcp: one pass
-      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 64,
-                                      (hipStream_t) 0));
-    } else {
-      // rb >= 2^32 possible: stable passes by ~lcp, then by rb
-      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_a, n, 0, key_a);
-      LICHK(hipGetLastError());
-      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 32,
-                                      (hipStream_t) 0));
-      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, 1, key_a);
-      LICHK(hipGetLastError());
-      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_b, idx_a, (size_t) n, 0, 64,
-                                      (hipStream_t) 0));
-      uint64_t *t = idx_a; idx_a = idx_b; idx_b = t;
-    }
-    hipLaunchKernelGGL(li_gather_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, p->itv);
-    LICHK(hipGetLastError());
-    if (N < 0xffffffffull) {   // (past 2^32 rows: the binary search; one scan of < 2^32 items)
-      // the events pass's positions: before[v] = intervals with rb < v, a
-      // max-scan over the run ends (rec's space is free after the gather)
-      uint32_t *D = (uint32_t *) rec;
+      // by rb alone: bits(N) radix bits instead of 64 (rb << 32 | ~lcp, 8
+      // onesweep passes, 4.1 ms of the C2 step), then the run reversal
+      const int rbits = 64 - __builtin_clzll((unsigned long long) N);
+      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0,
+                                      rbits, (hipStream_t) 0));
+      // before[v] = intervals with rb < v (the events pass's positions, and
+      // the runs here): a max-scan over the run ends, staged in key_a's
+      // space (free after the sort) where it fits
+      uint32_t *D = (uint32_t *) key_a;
       LICHK(smax_dev_alloc((void **) &p->before, sizeof (uint32_t) * (N + 1)));
-      if (sizeof (uint64_t) * 5 * n < sizeof (uint32_t) * (N + 1)) {
+      if (sizeof (uint64_t) * n < sizeof (uint32_t) * (N + 1)) {
         LICHK(smax_dev_alloc((void **) &dmarks, sizeof (uint32_t) * (N + 1)));
         D = dmarks;
       }
       LICHK(hipMemsetAsync(D, 0, sizeof (uint32_t) * (N + 1), 0));
-      hipLaunchKernelGGL(li_rb_marks_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, p->itv, n, D);
+      hipLaunchKernelGGL(li_rb_marks_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, key_b, n, D);
       LICHK(hipGetLastError());
       size_t sb = 0;
       LICHK(rocprim::inclusive_scan(nullptr, sb, D, p->before, (size_t) (N + 1),
@@ -582,6 +588,22 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
       }
       LICHK(rocprim::inclusive_scan(tmp, sb, D, p->before, (size_t) (N + 1),
                                     rocprim::maximum<uint32_t>(), (hipStream_t) 0));
+      hipLaunchKernelGGL(li_gather_rev_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, key_b,
+                         p->before, n, p->itv);
+      LICHK(hipGetLastError());
+    } else {
+      // rb >= 2^32 possible: stable passes by ~lcp, then by rb (past 2^32
+      // rows the events pass finds positions by binary search)
+      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_a, n, 0, key_a);
+      LICHK(hipGetLastError());
+      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 32,
+                                      (hipStream_t) 0));
+      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, 1, key_a);
+      LICHK(hipGetLastError());
+      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_b, idx_a, (size_t) n, 0, 64,
+                                      (hipStream_t) 0));
+      hipLaunchKernelGGL(li_gather_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_a, n, p->itv);
+      LICHK(hipGetLastError());
     }
   }
   LICHK(hipDeviceSynchronize());
