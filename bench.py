@@ -185,9 +185,7 @@ def main_lcpitv(args):
         cfg["workload"] = cfg["workload"].replace(
             cfg["workload"].split(" synthetic")[0], "%.3g bp" % args.bases)
     cfg["workload"] = cfg["workload"].split(", minlen")[0]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = rank_env(args)
     torch.cuda.set_device(0 if args.one_gpu else local)
     dist = None
     if world > 1:
@@ -345,9 +343,7 @@ def main_maxpairs(args):
     if args.minlen:
         cfg["minlen"] = args.minlen
     minlen = cfg["minlen"]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = rank_env(args)
     torch.cuda.set_device(0 if args.one_gpu else local)
     dist = None
     if world > 1:
@@ -482,6 +478,60 @@ def main_maxpairs(args):
         dist.destroy_process_group()
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` started as a plain process (no WORLD_SIZE): start
+    the N ranks here, one child process per GPU, before anything in this
+    process touches HIP or torch.cuda (the parent never imports torch).  Each
+    child re-runs this script with RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, exactly what
+    `python -m torch.distributed.run --nproc-per-node N` hands its workers,
+    and inherits stdout/stderr (rank 0 prints the one JSON line).  Returns
+    the first non-zero child exit code (the surviving ranks are terminated),
+    else 0."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    log("launching %d ranks (127.0.0.1:%d)" % (n, port))
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log("rank %d exited with %d; stopping the other ranks" % (procs.index(p), code))
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def rank_env(args):
+    """(world, rank, local) from the launcher's environment; --gpus must
+    agree with a set WORLD_SIZE (a mismatch is an error, not a note: the
+    line's n_gpus would otherwise not be the count asked for)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        log("error: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+        sys.exit(2)
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -521,7 +571,20 @@ def main():
     ap.add_argument("--byte-bwt", action="store_true",
                     help="plan from the byte BWT (plan-time packing) instead of the builder's "
                          "packed BWT")
+    ap.add_argument("--launch-probe", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world, rank, _ = rank_env(args)
+    if args.launch_probe:
+        # launcher check (tests/test_bench_launch_cpu.py): what this rank was
+        # handed, before any GPU or torch import
+        print(json.dumps({k: os.environ.get(k) for k in
+                          ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                           "MASTER_PORT")}), flush=True)
+        sys.exit(3 if args.launch_probe == "fail%d" % rank else 0)
     if args.config is None:
         args.config = "c2" if args.path in ("maxpairs", "lcpitv") else "c3"
     if args.path == "maxpairs":
@@ -542,11 +605,7 @@ def main():
         cfg["minlen"] = args.minlen
     minlen = cfg["minlen"]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world))
+    world, rank, local = rank_env(args)
     if args.one_gpu:
         local = 0
     torch.cuda.set_device(local)

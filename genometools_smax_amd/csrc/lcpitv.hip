@@ -244,7 +244,10 @@ __device__ __forceinline__ void li_write_one(const LiLevels &L, uint64_t k, uint
 }
 
 // records (lcp, lb, rb, fatherlcp, fatherlb) in row order of their
-// leftmost l-index, and the pop-order sort key rb << 32 | ~lcp
+// leftmost l-index, and the pop-order sort key rb alone: within a run of
+// equal rb the records stay in row order (lcp ascending) through the stable
+// sort, and li_gather_rev_kernel reverses each run into pop order -- so this
+// kernel must keep writing in row order
 __global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N, uint64_t ngroups,
                                                        const uint64_t *wg_off, uint64_t *rec,
                                                        uint64_t *key, uint64_t *idx) {

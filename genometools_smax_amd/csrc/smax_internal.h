@@ -33,6 +33,9 @@ struct SmaxFence;
 // device, for callers that lost track of their streams); released with the
 // last block that holds it
 SmaxFence *smax_fence_create(const hipStream_t *streams, int nstreams);
+// a fence over events the caller already recorded (it takes ownership and
+// destroys them); whole_device: also wait for the whole device
+SmaxFence *smax_fence_adopt(const hipEvent_t *events, int nevents, bool whole_device);
 void smax_dev_free_fenced(void *ptr, SmaxFence *fence);  // NULL ptr ok
 void smax_fence_release(SmaxFence *fence);               // the creator's reference
 

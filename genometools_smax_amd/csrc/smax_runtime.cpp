@@ -946,7 +946,12 @@ void device_phase1(Call *C, int d) {
         if (pe == hipSuccess && !nondna)
           pe = smax_groups_from_planes((uint64_t *) S.bwt, (const uint32_t *) planes, ng,
                                        (const uint64_t *) dspec, spec.size(), c->stream);
-        if (pe == hipSuccess) pe = hipStreamSynchronize(c->stream);
+        {
+          // unconditionally: on an error above, work enqueued before it may
+          // still read dspec / planes, which go back to the cache here
+          const hipError_t se = hipStreamSynchronize(c->stream);
+          if (pe == hipSuccess) pe = se;
+        }
         smax_dev_free(dspec);
         smax_dev_free(planes);
         DCHK(pe);
@@ -1452,6 +1457,14 @@ SmaxFence *smax_fence_create(const hipStream_t *streams, int nstreams) {
     }
     f->ev.push_back(e);
   }
+  return f;
+}
+
+SmaxFence *smax_fence_adopt(const hipEvent_t *events, int nevents, bool whole_device) {
+  SmaxFence *f = new SmaxFence;
+  (void) hipGetDevice(&f->device);
+  f->whole_device = whole_device;
+  for (int i = 0; i < nevents; i++) f->ev.push_back(events[i]);
   return f;
 }
 

@@ -222,7 +222,9 @@ int gt_smax_plan_create(GtSmaxPlan **plan, const GtSmaxDevShard *shard,
                         char *errbuf, size_t errlen);
 /* Frees the plan; its device buffers return to the runtime's cache only
  * after the device has finished the work already enqueued (safe right after
- * an asynchronous gt_smax_plan_run). */
+ * an asynchronous gt_smax_plan_run).  Nothing here waits: the fence is made
+ * of events the plan recorded when it enqueued the work, so the caller's
+ * streams may already be destroyed. */
 void gt_smax_plan_delete(GtSmaxPlan *plan);
 
 /* Enqueue one smax pass (scan + ordered compaction + boundary record) on

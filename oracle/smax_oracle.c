@@ -991,3 +991,75 @@ uint64_t orc_maxpairs_blocks(const uint8_t *lcpbytes, const OrcLlv *llv,
   }
   return found;
 }
+
+/* ---------------------------------------------------- spmitvs visitor (F3)
+ *
+ * orc_spmitv -- the GtESAVisitor of `gt dev sfxmap -spmitv`
+ * (src/match/esa_spmitvs_visitor.c:59-152, driven by gt_esa_bottomup in
+ * src/match/esa-spmitvs.c:25-69) restated over a gt_esa_bottomup event
+ * stream in the 7-word form of orc_bottomup_events (which the GPU's
+ * gt_lcpitv_plan_events writes too):
+ *   leaf edge (:59-89): leaf number 0, or one right after a separator, is a
+ *     "whole leaf" (:50-57) and becomes lastwholeleaf (its leaf index, the
+ *     running count of leaf edges); any other leaf whose suffix continues
+ *     past the father's depth without hitting a separator (leaf + fd <
+ *     totallength, text[leaf + fd] != SEPARATOR) is an unnecessary leaf;
+ *   branching edge (:91-125): for every depth fd < idx < sd the child
+ *     interval [slb, srb] counts as a whole-leaf one at depth idx if
+ *     lastwholeleaf lies in it (lastwholeleaf >= slb), else as a no-whole-leaf
+ *     one, width srb - slb + 1 either way;
+ *   lcp-interval (:127-152): the same count for the interval at its own lcp.
+ * counts: 4 words per depth 0..maxlen (wholeleaf, wholeleafwidth,
+ * nowholeleaf, nowholeleafwidth), zeroed here.  Returns -1 where the
+ * reference asserts (a depth above maxlen, lastwholeleaf past rb, a whole
+ * leaf at leaf index totallength), else 0.  text: the encoded sequence
+ * (255 = separator). */
+int orc_spmitv(const uint64_t *ev, uint64_t nev, const uint8_t *text, uint64_t totallength,
+               uint64_t maxlen, uint64_t *counts, uint64_t *unnecessary)
+{
+  const uint64_t undef = totallength;            /* lastwholeleaf "undefined" (:193) */
+  uint64_t current = 0, lastwhole = undef, unnec = 0;
+  memset(counts, 0, sizeof (uint64_t) * 4 * (maxlen + 1));
+  for (uint64_t k = 0; k < nev; k++) {
+    const uint64_t *r = ev + 7 * k;
+    if (r[0] == 0) {
+      const uint64_t fd = r[2], leaf = r[4];
+      if (leaf == 0 || text[leaf - 1] == 255) {
+        if (current == totallength) return -1;
+        lastwhole = current;
+      } else if (leaf + fd < totallength && text[leaf + fd] != 255) {
+        unnec++;
+      }
+      current++;
+    } else if (r[0] == 1) {
+      const uint64_t fd = r[2], sd = r[4], slb = r[5], srb = r[6];
+      for (uint64_t idx = fd + 1; idx < sd; idx++) {
+        uint64_t *c = counts + 4 * idx;
+        if (idx > maxlen) return -1;
+        if (lastwhole != undef && lastwhole >= slb) {
+          if (lastwhole > srb) return -1;
+          c[0]++;
+          c[1] += srb - slb + 1;
+        } else {
+          c[2]++;
+          c[3] += srb - slb + 1;
+        }
+      }
+    } else {
+      const uint64_t lcp = r[2], lb = r[3], rb = r[4];
+      uint64_t *c;
+      if (lcp > maxlen) return -1;
+      c = counts + 4 * lcp;
+      if (lastwhole != undef && lastwhole >= lb) {
+        if (lastwhole > rb) return -1;
+        c[0]++;
+        c[1] += rb - lb + 1;
+      } else {
+        c[2]++;
+        c[3] += rb - lb + 1;
+      }
+    }
+  }
+  *unnecessary = unnec;
+  return 0;
+}

@@ -58,6 +58,9 @@ def lib():
         L.orc_bottomup_events_slots.restype = ctypes.c_uint64
         L.orc_dfs_events.argtypes = [_u64p, _u64p, ctypes.c_uint64, ctypes.c_void_p]
         L.orc_dfs_events.restype = ctypes.c_uint64
+        L.orc_spmitv.argtypes = [_u64p, ctypes.c_uint64, _u8p, ctypes.c_uint64, ctypes.c_uint64,
+                                 _u64p, _u64p]
+        L.orc_spmitv.restype = ctypes.c_int
         L.orc_format_pair.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _u64p,
                                       ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int]
         _lib = L
@@ -299,3 +302,32 @@ def pack_bwt_ref(bwt):
            | ((s * w).sum(1).astype(np.uint64) << np.uint64(32)))
     is_dna = not np.any((bwt > 3) & (bwt < 254))
     return out, is_dna
+
+
+def spmitv_lines(events, text, nonspecials):
+    """`gt dev sfxmap -spmitv` output (src/match/esa-spmitvs.c:25-69) from a
+    gt_esa_bottomup event stream (7-word records: the oracle's or the GPU's):
+    the spmitvs visitor restated in orc_spmitv, printed as
+    gt_esa_spmitvs_visitor_print_results does (src/match/esa_spmitvs_visitor.c:
+    203-226).  maxlen = the longest sequence (gt_encseq_max_seq_length),
+    totallength = the text length with separators."""
+    text = np.ascontiguousarray(text, dtype=np.uint8)
+    ev = np.ascontiguousarray(events, dtype=np.uint64).reshape(-1, 7)
+    n = len(text)
+    seps = np.flatnonzero(text == 255)
+    bounds = np.concatenate([[-1], seps, [n]])
+    maxlen = int((np.diff(bounds) - 1).max()) if n else 0
+    counts = np.zeros(4 * (maxlen + 1), dtype=np.uint64)
+    unnec = ctypes.c_uint64()
+    rc = lib().orc_spmitv(_p(ev, _u64p), len(ev), _p(text, _u8p), n, maxlen, _p(counts, _u64p),
+                          ctypes.byref(unnec))
+    if rc != 0:
+        raise AssertionError("orc_spmitv: a reference assertion fails on this event stream")
+    c = counts.reshape(-1, 4).astype(np.int64)
+    lines = ["unnecessaryleaves=%d (%.2f)" % (unnec.value, unnec.value / nonspecials)]
+    for idx in range(maxlen + 1):
+        w, ww, nw = int(c[idx, 0]), int(c[idx, 1]), int(c[idx, 2])
+        if w != 0 or nw != 0:
+            lines.append("wholeleaf[%d]:num=%d (%.2f), width=%d (%.2f)"
+                         % (idx, w, w / (w + nw), ww, ww / n))
+    return lines

@@ -219,3 +219,43 @@ def test_nccl_ranks_one_per_device(world):
     r = _spawn(_worker_nccl, world, "human", 30_000_000, 5, 20)
     assert len(r["want"]) > 100
     assert np.array_equal(r["got"], r["want"]), (len(r["got"]), len(r["want"]))
+
+
+# ------------------------------------------------ bench.py's own rank launch
+# `python bench.py --gpus N` from a plain process (no torchrun): the parent
+# starts the N ranks itself; the line must report N ranks that all took part
+# in the collective, with the stitched records bit-exact.
+
+def _bench_line(args, timeout=600):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                        "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args,
+                       capture_output=True, text=True, env=env, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_two_ranks_one_gpu():
+    out = _bench_line(["--gpus", "2", "--one-gpu", "--dist-backend", "gloo", "--bases", "2e7",
+                       "--steps", "3", "--warmup", "1", "--prime-s", "0"])
+    assert out["n_gpus"] == 2
+    assert out["dist"]["world_size"] == 2 and out["dist"]["allreduce_ranks"] == 2
+    assert out["parity"].startswith("bit-exact")
+    assert out["smax_intervals"] > 100
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 visible GPUs")
+def test_bench_self_launch_nccl_one_rank_per_device():
+    out = _bench_line(["--gpus", "2", "--bases", "3e7", "--steps", "3", "--warmup", "1",
+                       "--prime-s", "0"])
+    assert out["n_gpus"] == 2
+    assert out["dist"]["backend"] == "nccl" and out["dist"]["allreduce_ranks"] == 2
+    assert out["dist"]["distinct_devices"] == 2
+    assert out["parity"].startswith("bit-exact")

@@ -192,3 +192,72 @@ def test_info_visitor_leaf_counts_deep_stack():
     G.esa_bottomup_info(e.lcpbytes, e.llv, e.suftab, e.n, e.nonspecials, new, None, leaf, branch, itv)
     assert made[0] > 32 and seen[0] > 1000
     assert bad == []
+
+
+# ---------------------------------------- spmitv: a reference golden for F3
+# `gt dev sfxmap -spmitv` (src/match/esa-spmitvs.c:25-69) is gt_esa_bottomup
+# driving the spmitvs visitor (src/match/esa_spmitvs_visitor.c:59-226); its
+# output on Reads2.fna is reference testdata (testdata/Reads2-spmitv.txt,
+# testsuite/gt_suffixerator_include.rb:587-592).  Here the GPU traversal
+# (gt_esa_bottomup_hip over the index's .lcp/.llv/.suf, the callbacks on
+# this thread) drives the same visitor restatement (orc_spmitv) and must
+# print the golden byte for byte; on the other fixtures the GPU-driven
+# output must equal the oracle-driven one.
+
+def _gpu_spmitv(ix, sep_text):
+    ev = _gpu_events_tables(ix.lcptab, ix.llvtab, ix.suftab, ix.totallength, ix.nonspecials)
+    return O.spmitv_lines(ev, sep_text, ix.nonspecials)
+
+
+def _gpu_events_tables(lcptab, llvtab, suftab, n, N):
+    ev = []
+    G.esa_bottomup(np.asarray(lcptab), np.asarray(llvtab), np.asarray(suftab), n, N,
+                   leaf_edge=lambda f, fd, flb, leaf: ev.append((0, f, fd, flb, leaf, 0, 0)),
+                   branching_edge=lambda f, fd, flb, sd, slb, srb:
+                   ev.append((1, f, fd, flb, sd, slb, srb)),
+                   lcp_interval=lambda l, lb, rb: ev.append((2, 0, l, lb, rb, 0, 0)))
+    return np.array(ev, dtype=np.uint64).reshape(-1, 7)
+
+
+def test_spmitv_reads2_golden_from_gpu_traversal(tmp_path):
+    import os
+    from conftest import GOLDEN
+    idx = str(tmp_path / "Reads2.fna")
+    O.index_fasta(os.path.join(GOLDEN, "Reads2.fna"), idx)
+    ix = G.EsaIndex(idx)
+    sep_text = np.zeros(ix.totallength, np.uint8)
+    sep_text[ix.separators().astype(np.int64)] = 255
+    lines = _gpu_spmitv(ix, sep_text)
+    with open(os.path.join(GOLDEN, "Reads2-spmitv.txt")) as fh:
+        assert lines == fh.read().splitlines()
+
+
+@pytest.mark.parametrize("name", ["Atinsert.fna", "at1MB", "Random.fna", "TTT-small.fna"])
+def test_spmitv_gpu_equals_oracle(name):
+    e = oracle_esa(name)
+    want = O.spmitv_lines(O.bottomup_events(e), e.text, e.nonspecials)
+    ev = _gpu_events_tables(e.lcpbytes, e.llv, e.suftab, e.n, e.nonspecials)
+    assert O.spmitv_lines(ev, e.text, e.nonspecials) == want
+
+
+def test_spmitv_device_event_stream():
+    # the device-resident path: gt_lcpitv_plan_events into HBM (no host
+    # callbacks), downloaded and fed to the same visitor
+    import torch
+    e = oracle_esa("Reads2.fna")
+    lcp = torch.from_numpy(np.ascontiguousarray(e.lcpbytes)).cuda()
+    llv = torch.from_numpy(np.ascontiguousarray(
+        np.vstack([e.llv, np.zeros((1, 2), np.uint64)]).view(np.int64))).cuda()
+    suf = torch.from_numpy(e.suftab.view(np.int64)).cuda()
+    plan = G.LcpitvPlan(lcp.data_ptr(), llv.data_ptr(), len(e.llv), suf.data_ptr(), 8,
+                        e.nonspecials)
+    ne = plan.num_events()
+    out = torch.zeros(7 * ne, dtype=torch.int64, device="cuda")
+    plan.events(out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    plan.close()
+    ev = out.cpu().numpy().view(np.uint64).reshape(-1, 7)
+    from conftest import GOLDEN
+    import os
+    with open(os.path.join(GOLDEN, "Reads2-spmitv.txt")) as fh:
+        assert O.spmitv_lines(ev, e.text, e.nonspecials) == fh.read().splitlines()

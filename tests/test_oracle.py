@@ -380,3 +380,40 @@ def test_event_slots_random(seed):
     assert _leafcount_visit(ev, sl) == []
     if seed % 2:
         assert nslots > 32
+
+
+# ------------------------------------------------- spmitv (F3 visitor golden)
+# `gt dev sfxmap -spmitv` on an index of Reads2.fna (-suf -lcp) must print
+# testdata/Reads2-spmitv.txt (testsuite/gt_suffixerator_include.rb:587-592):
+# gt_esa_bottomup driving the spmitvs visitor (src/match/esa-spmitvs.c:25-69,
+# src/match/esa_spmitvs_visitor.c:59-226).  This pins the oracle's bottom-up
+# event stream -- leaf numbers, branching-edge depths and child bounds, every
+# lcp-interval -- to a reference-produced file.
+
+def _index_events(tmp_path, fasta):
+    import genometools_smax_amd as G   # the host-side index reader (pure Python)
+    idx = str(tmp_path / os.path.basename(fasta))
+    O.index_fasta(os.path.join(GOLDEN, fasta), idx)
+    ix = G.EsaIndex(idx)
+    n, N = ix.totallength, ix.nonspecials
+    lcp = np.asarray(ix.lcptab).astype(np.uint64)
+    if len(ix.llvtab):
+        lcp[np.asarray(ix.llvtab)[:, 0].astype(np.int64)] = np.asarray(ix.llvtab)[:, 1]
+
+    class _E:
+        pass
+    e = _E()
+    e.lcp, e.suftab, e.nonspecials = lcp, np.asarray(ix.suftab).astype(np.uint64), N
+    sep_text = np.zeros(n, np.uint8)
+    sep_text[ix.separators().astype(np.int64)] = 255      # the encseq's separators
+    return ix, e, sep_text
+
+
+def test_spmitv_reproduces_reads2_golden(tmp_path):
+    ix, e, sep_text = _index_events(tmp_path, "Reads2.fna")
+    lines = O.spmitv_lines(O.bottomup_events(e), sep_text, ix.nonspecials)
+    with open(os.path.join(GOLDEN, "Reads2-spmitv.txt")) as fh:
+        gold = fh.read().splitlines()
+    assert len(gold) == 51
+    assert lines == gold
+
