@@ -15,22 +15,25 @@
 //   * leaf idx hangs (when LCP[idx+1] <= LCP[idx]) below the interval of
 //     depth LCP[idx] whose lb is the nearest p < idx with LCP[p] < LCP[idx].
 //
-// Each search climbs a 64-ary min hierarchy over the exact LCP array (u32)
-// and descends again: at most 63 reads per level, 6 levels for 10^10 rows.
-// One thread per row; the intervals are compacted and radix-sorted into pop
-// order (rb ascending, depth descending).  The tree stays in HBM
-// (GtLcpitvPlan); the visitor's event stream is generated there too, every
-// event at its position in the reference's order, no stack and no replay
-// loop (li_events_*): per row idx (X = LCP[idx], Y = LCP[idx+1]) the
-// traversal emits exactly one leaf edge, then for every interval popped at
-// idx (pop order) its lcp-interval and branching-edge events, so with
-// P(idx) = #intervals with rb < idx the leaf of row idx sits at
-// idx + 2 P(idx) and popped interval r of row idx at idx + 2 P(idx) + 1 + 2r.
-// The host entry points download the events in chunks and call the
-// visitor.
+// All of it follows from one ANSV quantity, the strict previous-smaller
+// value PL(k), computed per tile of 2048 rows in LDS (per-thread pointer
+// jumping inside 8-row segments, a segment-minimum search across the tile,
+// the 64-ary min hierarchy over the exact LCP array (u32) only for the few
+// rows with no smaller value earlier in their tile): the stack of the
+// reference after row idx is the PL chain from idx, so the intervals popped
+// at a row are read off that chain (li_walk) -- no sort, no per-row global
+// searches.  The tree stays in HBM (GtLcpitvPlan: the pop-ordered interval
+// records and the intervals popped before each tile); the visitor's event
+// stream is generated there too, every event at its position in the
+// reference's order, no stack and no replay loop (li_tile_events_kernel):
+// per row idx (X = LCP[idx], Y = LCP[idx+1]) the traversal emits exactly
+// one leaf edge, then for every interval popped at idx (pop order) its
+// lcp-interval and branching-edge events, so with P(idx) = #intervals with
+// rb < idx the leaf of row idx sits at idx + 2 P(idx) and popped interval r
+// of row idx at idx + 2 P(idx) + 1 + 2r.  The host entry points download
+// the events in chunks and call the visitor.
 #include <hip/hip_runtime.h>
 #include <vector>
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <stdarg.h>
 #include <stdio.h>
@@ -158,29 +161,7 @@ __device__ static uint64_t li_prev(const LiLevels &L, uint64_t k, uint32_t v, bo
   return p;
 }
 
-// nearest q > k with X[q] < v (X[N] == 0 guarantees one for v > 0)
-__device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v) {
-  uint64_t i = k, p = 0;
-  int lev = 0;
-  for (;;) {
-    const uint64_t b = (i >> 6) << 6;
-    const uint64_t upto = i - b;    // entries (i, b + 64)
-    const uint64_t m = upto >= 63 ? 0ull
-                                  : li_block_mask(L.lv[lev], b, L.n[lev], v, true) & ~((2ull << upto) - 1ull);
-    if (m) { p = b + (uint64_t) __builtin_ctzll(m); break; }
-    if (lev + 1 >= L.nlev) return L.n[0] - 1;    // row N
-    i >>= 6;
-    lev++;
-  }
-  while (lev > 0) {                // first child of p whose subtree qualifies
-    lev--;
-    const uint64_t b = p << 6;
-    p = b + (uint64_t) __builtin_ctzll(li_block_mask(L.lv[lev], b, L.n[lev], v, true));
-  }
-  return p;
-}
-
-// workgroup-wide exclusive prefix; *total = sum
+// workgroup-wide exclusive prefix (256 threads); *total = sum
 __device__ __forceinline__ uint32_t li_block_excl(uint32_t v, uint32_t *total) {
   __shared__ uint32_t sW[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -195,235 +176,347 @@ __device__ __forceinline__ uint32_t li_block_excl(uint32_t v, uint32_t *total) {
   uint32_t wo = 0;
   for (int w = 0; w < wave; w++) wo += sW[w];
   *total = sW[0] + sW[1] + sW[2] + sW[3];
+  __syncthreads();                     // sW is reused by the next call
   return wo + incl - v;
 }
 
-// row k (1 <= k < N) opens an interval: leftmost l-index
-__device__ __forceinline__ bool li_leftmost(const LiLevels &L, uint64_t k, uint64_t N,
-                                            uint64_t *lb) {
-  if (k < 1 || k >= N) return false;
-  const uint32_t v = L.lv[0][k];
-  if (v == 0) return false;
-  const uint64_t p = li_prev(L, k, v, false);
-  *lb = p;
-  return L.lv[0][p] < v;
-}
+// ------------------------------------------------------------ tiles
+//
+// The tree from the strict previous-smaller value PL(k) = the nearest p < k
+// with X[p] < X[k] alone.  The reference's stack after row idx holds
+// exactly the chain c0 = idx, c1 = PL(c0), c2 = PL(c1), ... (depths X[cj]
+// strictly decreasing, the interval of depth X[cj] starting at c(j+1)), so
+// the lcp-intervals popped at row idx (Y = X[idx+1]) are, deepest first,
+// [c(j+1), idx] of depth X[cj] for every cj with X[cj] > Y; the father of
+// pop j has depth max(X[c(j+1)], Y) and lb PL(c(j+1)) when X[c(j+1)] >= Y,
+// else it is the new interval (Y, c(j+1)) pushed after the pops.  The leaf
+// of row idx hangs below (X[idx], PL(idx)) when Y <= X[idx], else it is the
+// first child of (Y, idx).  Every interval is popped once, so the walks
+// cost O(N) over the whole table.
+//
+// A workgroup owns LI_T consecutive rows (a tile): their X in LDS, PL by
+// per-thread pointer jumping inside 8-row segments, the rows left
+// unresolved by a segment-minimum search across the tile, and the tile's
+// prefix minima (no smaller value in the tile before them, a handful per
+// tile) by the global 64-ary hierarchy (li_prev).  Chains that leave the
+// tile (intervals open at its start) continue through li_prev as well.
+// Three passes walk the chains: a count per tile (plan), the pop-ordered
+// interval records (plan) and the visitor event stream (events); the last
+// two stage their output in LDS and store it as contiguous 16-byte pieces.
+#define LI_T 2048                       // rows per tile
+#define LI_TPB 256                      // threads per tile workgroup
+#define LI_RPT (LI_T / LI_TPB)          // rows per segment (one thread)
+#define LI_GSEG 16                      // segments per group
+#define LI_NGRP (LI_TPB / LI_GSEG)
+#define LI_ITV_CAP 384                  // interval records staged per 256-row chunk
+#define LI_EV_STAGE 16384               // event staging bytes per workgroup
 
-// groups of 256 rows, group-stride over a capped grid (every thread of a
-// workgroup runs the same number of groups: li_block_excl synchronises)
-__global__ void __launch_bounds__(256) li_count_kernel(LiLevels L, uint64_t N, uint64_t ngroups,
-                                                       uint32_t *wg_cnt) {
-  for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const uint64_t k = g * 256 + threadIdx.x;
-    uint64_t lb;
-    uint32_t tot;
-    (void) li_block_excl(li_leftmost(L, k, N, &lb) ? 1u : 0u, &tot);
-    if (threadIdx.x == 0) wg_cnt[g] = tot;
-    __syncthreads();                 // sW is reused by the next group
+template <typename RowT>
+struct LiDesc {                         // one staged event (16 B / 32 B)
+  RowT a, b, c, d;                      // a: kind | firstsucc << 2
+};
+
+template <typename RowT>
+struct LiTile {
+  uint32_t x[LI_T + 1];                 // X[t0 .. t0 + LI_T] (0 past row N)
+  RowT pl[LI_T];                        // PL of the tile's rows (~0: none / pending)
+  uint32_t segmin[LI_TPB];
+  uint32_t grpmin[LI_NGRP];
+  union {
+    LiDesc<RowT> ev[LI_EV_STAGE / sizeof (LiDesc<RowT>)];
+    uint64_t itv[5 * LI_ITV_CAP];
+  } st;
+};
+
+template <typename RowT>
+__device__ __forceinline__ RowT li_none() { return (RowT) ~(RowT) 0; }
+
+// PL of every row of the tile [t0, t0 + LI_T) into S.pl (rows with X = 0
+// have none).  Ends with a barrier.
+template <typename RowT>
+__device__ void li_tile_ansv(const LiLevels &L, uint64_t N, uint64_t t0, LiTile<RowT> &S) {
+  const int tid = threadIdx.x;
+  const RowT none = li_none<RowT>();
+  for (int k = tid; k <= LI_T; k += LI_TPB) {
+    const uint64_t g = t0 + (uint64_t) k;
+    S.x[k] = g <= N ? L.lv[0][g] : 0u;   // lv[0] holds rows 0..N, X[N] = 0
   }
-}
-
-__device__ __forceinline__ void li_write_one(const LiLevels &L, uint64_t k, uint64_t lb,
-                                             uint64_t pos, uint64_t *rec, uint64_t *key,
-                                             uint64_t *idx) {
-  const uint32_t v = L.lv[0][k];
-  const uint64_t q = li_next(L, k, v);
-  const uint32_t xl = L.lv[0][lb], xq = L.lv[0][q];
-  const uint32_t fl = xl > xq ? xl : xq;
-  uint64_t flb = lb;
-  if (fl == 0) flb = 0;
-  else if (xl >= xq) flb = li_prev(L, lb, xl, true);
-  uint64_t *r = rec + 5 * pos;
-  r[0] = v;
-  r[1] = lb;
-  r[2] = q - 1;
-  r[3] = fl;
-  r[4] = flb;
-  key[pos] = q - 1;   // rb (past 2^32 rows li_key_kernel rewrites the keys)
-  idx[pos] = pos;
-}
-
-// records (lcp, lb, rb, fatherlcp, fatherlb) in row order of their
-// leftmost l-index, and the pop-order sort key rb alone: within a run of
-// equal rb the records stay in row order (lcp ascending) through the stable
-// sort, and li_gather_rev_kernel reverses each run into pop order -- so this
-// kernel must keep writing in row order
-__global__ void __launch_bounds__(256) li_write_kernel(LiLevels L, uint64_t N, uint64_t ngroups,
-                                                       const uint64_t *wg_off, uint64_t *rec,
-                                                       uint64_t *key, uint64_t *idx) {
-  for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const uint64_t k = g * 256 + threadIdx.x;
-    uint64_t lb = 0;
-    const bool open = li_leftmost(L, k, N, &lb);
-    uint32_t tot;
-    const uint64_t pos = wg_off[g] + li_block_excl(open ? 1u : 0u, &tot);
-    __syncthreads();                 // sW is reused by the next group
-    if (open) li_write_one(L, k, lb, pos, rec, key, idx);
-  }
-}
-
-
-// keys of the two-pass sort (rb >= 2^32): pass 0 ~lcp, pass 1 rb, of the
-// records in the current permutation
-__global__ void __launch_bounds__(256) li_key_kernel(const uint64_t *rec, const uint64_t *perm,
-                                                     uint64_t n, int pass, uint64_t *key) {
-  LI_FOR(i, n) {
-    const uint64_t *r = rec + 5 * perm[i];
-    key[i] = pass == 0 ? (uint64_t) (0xffffffffu - (uint32_t) r[0]) : r[2];
-  }
-}
-
-// the records sorted by rb alone into pop order: each run of equal rb is in
-// row order of its intervals' first l-index, i.e. lcp ascending (an outer
-// interval's l-indices lie at or before an inner one's lb), and the pops
-// take the deepest first -- the run reversed
-__global__ void __launch_bounds__(256) li_gather_rev_kernel(const uint64_t *rec, const uint64_t *idx,
-                                                            const uint64_t *rb,
-                                                            const uint32_t *before, uint64_t n,
-                                                            uint64_t *out) {
-  LI_FOR(i, n) {
-    const uint64_t v = rb[i];
-    const uint64_t dst = (uint64_t) before[v] + before[v + 1] - 1 - i;
-    const uint64_t *r = rec + 5 * (uint64_t) idx[i];
-    uint64_t *w = out + 5 * dst;
-#pragma unroll
-    for (int f = 0; f < 5; f++) w[f] = r[f];
-  }
-}
-
-__global__ void __launch_bounds__(256) li_gather_kernel(const uint64_t *rec, const uint64_t *idx,
-                                                        uint64_t n, uint64_t *out) {
-  LI_FOR(i, n) {
-    const uint64_t *r = rec + 5 * (uint64_t) idx[i];
-    uint64_t *w = out + 5 * i;
-#pragma unroll
-    for (int f = 0; f < 5; f++) w[f] = r[f];
-  }
-}
-
-// ------------------------------------------------------------ events
-
-// rows [lo, hi) of the sorted intervals: first index whose rb >= v
-__device__ __forceinline__ uint64_t li_lower_rb(const uint64_t *itv, uint64_t n, uint64_t v) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (itv[5 * mid + 2] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// intervals with rb < v: the plan's prefix array (one load) when it has
-// one, else a binary search over the pop-ordered records (26 dependent
-// loads at C2, in four kernels: 16.5 ms of the events pass, profiles/s7/)
-__device__ __forceinline__ uint64_t li_before(const uint32_t *C, const uint64_t *itv, uint64_t n,
-                                              uint64_t v) {
-  return C != nullptr ? (uint64_t) C[v] : li_lower_rb(itv, n, v);
-}
-
-// the prefix array's input: at rb + 1 of the last interval of each run of
-// equal rb (rb sorted), the number of intervals up to it (a max-scan fills
-// the rest)
-__global__ void __launch_bounds__(256) li_rb_marks_kernel(const uint64_t *rb, uint64_t n,
-                                                          uint32_t *D) {
-  LI_FOR(j, n) {
-    if (j + 1 == n || rb[j + 1] != rb[j]) D[rb[j] + 1] = (uint32_t) (j + 1);
-  }
-}
-
-// event positions of root edges that consume the reference's
-// firstedgefromroot flag (leaf edges to the root attached in step 1 and
-// branching edges to the root of pops); the first one in stream order gets
-// firstsucc = 1 (src/match/esa-bottomup.c:134-141)
-__global__ void __launch_bounds__(256) li_rootfirst_leaf_kernel(LiLevels L, uint64_t N,
-                                                                const uint64_t *itv, uint64_t nitv,
-                                                                const uint32_t *C,
-                                                                unsigned long long *first) {
-  LI_FOR(idx, N) {
-    const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
-    if (X != 0 || Y > X) continue;
-    const uint64_t pos = idx + 2 * li_before(C, itv, nitv, idx);
-    atomicMin(first, (unsigned long long) pos);
-  }
-}
-
-__global__ void __launch_bounds__(256) li_rootfirst_itv_kernel(const uint64_t *itv, uint64_t nitv,
-                                                               const uint32_t *C,
-                                                               unsigned long long *first) {
-  LI_FOR(j, nitv) {
-    const uint64_t *r = itv + 5 * j;
-    if (r[3] != 0) continue;
-    const uint64_t g = li_before(C, itv, nitv, r[2]);
-    const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g) + 1;
-    atomicMin(first, (unsigned long long) pos);
-  }
-}
-
-// leaf edge of row idx: (0, firstsucc, fd, flb, leafnumber, 0, 0)
-template <typename SufT>
-__global__ void __launch_bounds__(256) li_events_leaf_kernel(LiLevels L, uint64_t N,
-                                                             const uint64_t *itv, uint64_t nitv,
-                                                             const uint32_t *C, const void *suf,
-                                                             const unsigned long long *first,
-                                                             uint64_t *ev) {
-  LI_FOR(idx, N) {
-    const uint32_t X = L.lv[0][idx], Y = L.lv[0][idx + 1];
-    const uint64_t pos = idx + 2 * li_before(C, itv, nitv, idx);
-    uint64_t e1, e2, e3;
-    if (Y <= X) {            // attached to the interval of depth X holding idx
-      e1 = (X == 0 && pos == *first) ? 1u : 0u;
-      e2 = X;
-      e3 = X == 0 ? 0 : li_prev(L, idx, X, true);
-    } else {                 // firstsucc leaf of the new interval (Y, idx)
-      e1 = 1;
-      e2 = Y;
-      e3 = idx;
+  __syncthreads();
+  // the thread's segment, left to right: p jumps along PL inside it
+  const int lo = tid * LI_RPT;
+  uint32_t m = 0xffffffffu;
+  for (int i = lo; i < lo + LI_RPT; i++) {
+    const uint32_t v = S.x[i];
+    m = v < m ? v : m;
+    int p = i - 1;
+    while (p >= lo && S.x[p] >= v) {
+      const RowT q = S.pl[p];
+      p = q == none ? lo - 1 : (int) (q - (RowT) t0);
     }
-    const uint64_t e4 = suf == nullptr ? 0 : (uint64_t) reinterpret_cast<const SufT *>(suf)[idx];
-    uint64_t *w = ev + 7 * pos;   // 16-byte pieces, as li_events_itv_kernel
-    if ((pos & 1) == 0) {
-      reinterpret_cast<ulonglong2 *>(w)[0] = make_ulonglong2(0, e1);
-      reinterpret_cast<ulonglong2 *>(w)[1] = make_ulonglong2(e2, e3);
-      reinterpret_cast<ulonglong2 *>(w)[2] = make_ulonglong2(e4, 0);
-      w[6] = 0;
+    S.pl[i] = p >= lo ? (RowT) (t0 + (uint64_t) p) : none;
+  }
+  S.segmin[tid] = m;
+  __syncthreads();
+  if (tid < LI_NGRP) {
+    uint32_t g = 0xffffffffu;
+    for (int s = tid * LI_GSEG; s < (tid + 1) * LI_GSEG; s++) g = S.segmin[s] < g ? S.segmin[s] : g;
+    S.grpmin[tid] = g;
+  }
+  __syncthreads();
+  // rows with no smaller value earlier in their segment: the nearest segment
+  // before with a smaller minimum (then the last row below v along that
+  // segment's own PL chain, which stays inside it), else the global search
+  for (int i = lo; i < lo + LI_RPT; i++) {
+    const uint32_t v = S.x[i];
+    if (v == 0 || S.pl[i] != none) continue;
+    int found = -1;
+    for (int s = tid - 1; s >= (tid / LI_GSEG) * LI_GSEG; s--)
+      if (S.segmin[s] < v) { found = s; break; }
+    if (found < 0)
+      for (int g = tid / LI_GSEG - 1; g >= 0 && found < 0; g--)
+        if (S.grpmin[g] < v)
+          for (int s = g * LI_GSEG + LI_GSEG - 1; s >= g * LI_GSEG; s--)
+            if (S.segmin[s] < v) { found = s; break; }
+    if (found >= 0) {
+      int p = found * LI_RPT + LI_RPT - 1;
+      while (S.x[p] >= v) p = (int) (S.pl[p] - (RowT) t0);
+      S.pl[i] = (RowT) (t0 + (uint64_t) p);
     } else {
-      w[0] = 0;
-      reinterpret_cast<ulonglong2 *>(w + 1)[0] = make_ulonglong2(e1, e2);
-      reinterpret_cast<ulonglong2 *>(w + 1)[1] = make_ulonglong2(e3, e4);
-      reinterpret_cast<ulonglong2 *>(w + 1)[2] = make_ulonglong2(0, 0);
+      S.pl[i] = t0 > 0 ? (RowT) li_prev(L, t0, v, true) : none;
     }
   }
+  __syncthreads();
 }
 
-// popped interval j: (2, 0, lcp, lb, rb, 0, 0) then its branching edge
-// (1, firstsucc, fd, flb, sd, slb, srb); a father that is new at rb (same
-// lb, pushed after the pops) gets the firstsucc edge with its own lb
-__global__ void __launch_bounds__(256) li_events_itv_kernel(const uint64_t *itv, uint64_t nitv,
-                                                            const uint32_t *C,
-                                                            const unsigned long long *first,
-                                                            uint64_t *ev) {
-  LI_FOR(j, nitv) {
-    const uint64_t *r = itv + 5 * j;
-    const uint64_t g = li_before(C, itv, nitv, r[2]);
-    const uint64_t pos = r[2] + 2 * g + 1 + 2 * (j - g);
-    const uint64_t r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
-    const bool newfather = r3 > 0 && r4 == r1;
-    // the pop record and its branching edge: 14 consecutive words, stored
-    // as 16-byte pieces (8-byte stores: 9.0 ms at C2, profiles/s7/)
-    const uint64_t e[14] = {2, 0, r0, r1, r2, 0, 0,
-                            1, newfather ? 1u : ((r3 == 0 && pos + 1 == *first) ? 1u : 0u), r3,
-                            newfather ? r1 : r4, r0, r1, r2};
-    uint64_t *w = ev + 7 * pos;
-    if ((pos & 1) == 0) {   // 56 * pos: 16-byte aligned
-#pragma unroll
-      for (int q = 0; q < 7; q++)
-        reinterpret_cast<ulonglong2 *>(w)[q] = make_ulonglong2(e[2 * q], e[2 * q + 1]);
-    } else {
-      w[0] = e[0];
-#pragma unroll
-      for (int q = 0; q < 6; q++)
-        reinterpret_cast<ulonglong2 *>(w + 1)[q] = make_ulonglong2(e[2 * q + 1], e[2 * q + 2]);
-      w[13] = e[13];
+// X and PL of any row at or before the tile's end: the tile's from LDS,
+// earlier ones from the hierarchy
+template <typename RowT>
+__device__ __forceinline__ uint32_t li_tx(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0,
+                                          uint64_t c) {
+  return c >= t0 ? S.x[c - t0] : L.lv[0][c];
+}
+
+template <typename RowT>
+__device__ __forceinline__ uint64_t li_tpl(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0,
+                                           uint64_t c, uint32_t xc) {
+  return c >= t0 ? (uint64_t) S.pl[c - t0] : li_prev(L, c, xc, true);
+}
+
+// intervals popped at row t0 + i
+template <typename RowT>
+__device__ __forceinline__ uint32_t li_pops(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0,
+                                            int i) {
+  const uint32_t Y = S.x[i + 1];
+  uint64_t c = t0 + (uint64_t) i;
+  uint32_t xc = S.x[i], n = 0;
+  while (xc > Y) {
+    n++;
+    c = li_tpl(L, S, t0, c, xc);
+    xc = li_tx(L, S, t0, c);
+  }
+  return n;
+}
+
+// the pops of row idx = t0 + i in order, deepest first: f(j, lcp, lb, fd, flb, newfather)
+template <typename RowT, typename F>
+__device__ __forceinline__ void li_walk(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0, int i,
+                                        F f) {
+  const uint32_t Y = S.x[i + 1];
+  uint32_t xc = S.x[i];
+  if (xc <= Y) return;
+  uint64_t nx = li_tpl(L, S, t0, t0 + (uint64_t) i, xc);
+  uint32_t xn = li_tx(L, S, t0, nx);
+  for (uint32_t j = 0;; j++) {
+    const uint32_t fd = xn > Y ? xn : Y;
+    uint64_t nn = 0, flb = 0;
+    if (xn >= Y && fd > 0) {
+      nn = li_tpl(L, S, t0, nx, xn);
+      flb = nn;
+    } else if (fd > 0) {
+      flb = nx;                          // the new father (Y, nx)
+    }
+    f(j, xc, nx, fd, flb, xn < Y);
+    if (xn <= Y) break;
+    xc = xn;
+    nx = nn;
+    xn = li_tx(L, S, t0, nx);
+  }
+}
+
+// pass 1 (plan): intervals popped in each tile
+template <typename RowT>
+__global__ void __launch_bounds__(LI_TPB) li_tile_count_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
+                                                               uint32_t *tile_cnt) {
+  __shared__ LiTile<RowT> S;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t t0 = t * LI_T;
+    li_tile_ansv(L, N, t0, S);
+    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
+    uint32_t n = 0;
+    for (int i = threadIdx.x; i < nrows; i += LI_TPB) n += li_pops(L, S, t0, i);
+    uint32_t tot;
+    (void) li_block_excl(n, &tot);
+    if (threadIdx.x == 0) tile_cnt[t] = tot;
+  }
+}
+
+// pass 2 (plan): the interval records (lcp, lb, rb, father lcp, father lb)
+// in pop order at tile_off[t] on (staged per 256-row chunk, stored as
+// contiguous 16-byte pieces), and the stream position of the first edge to
+// the root (the reference's firstedgefromroot, esa-bottomup.c:134-141)
+template <typename RowT>
+__global__ void __launch_bounds__(LI_TPB) li_tile_itv_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
+                                                             const uint64_t *tile_off, uint64_t *itv,
+                                                             unsigned long long *first) {
+  __shared__ LiTile<RowT> S;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t t0 = t * LI_T;
+    li_tile_ansv(L, N, t0, S);
+    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
+    uint64_t base = tile_off[t];         // intervals popped before this chunk
+    for (int c0 = 0; c0 < nrows; c0 += LI_TPB) {
+      const int i = c0 + (int) threadIdx.x;
+      const bool row = i < nrows;
+      const uint32_t n = row ? li_pops(L, S, t0, i) : 0u;
+      uint32_t tot;
+      const uint32_t off = li_block_excl(n, &tot);
+      if (row) {
+        const uint64_t idx = t0 + (uint64_t) i;
+        const uint64_t pos = idx + 2 * (base + off);       // the row's leaf event
+        if (S.x[i] == 0 && S.x[i + 1] == 0) atomicMin(first, (unsigned long long) pos);
+        li_walk(L, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t fd, uint64_t flb,
+                                 bool) {
+          const uint32_t k = off + j;
+          uint64_t *r = k < LI_ITV_CAP ? S.st.itv + 5 * k : itv + 5 * (base + k);
+          r[0] = lcp;
+          r[1] = lb;
+          r[2] = idx;
+          r[3] = fd;
+          r[4] = flb;
+          if (fd == 0) atomicMin(first, (unsigned long long) (pos + 2 + 2 * j));
+        });
+      }
+      __syncthreads();
+      const uint32_t staged = tot < LI_ITV_CAP ? tot : LI_ITV_CAP;
+      // words [5 base, 5 (base + staged)) as aligned 16-byte pairs
+      const uint64_t w0 = 5 * base, w1 = 5 * (base + staged);
+      for (uint64_t q = (w0 >> 1) + threadIdx.x; 2 * q < w1; q += LI_TPB) {
+        const uint64_t a = 2 * q;
+        const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
+        const uint64_t v0 = lo_ok ? S.st.itv[a - w0] : 0, v1 = hi_ok ? S.st.itv[a + 1 - w0] : 0;
+        if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(itv)[q] = make_ulonglong2(v0, v1);
+        else if (lo_ok) itv[a] = v0;
+        else itv[a + 1] = v1;
+      }
+      __syncthreads();
+      base += tot;
+    }
+  }
+}
+
+// pass 3 (events): the gt_esa_bottomup event stream of the tile's rows,
+// every event at its position in the reference's order: per row its leaf
+// edge, then per pop its lcp-interval and branching-edge events
+//   (0, firstsucc, fd, flb, leafnumber, 0, 0)   visit_leaf_edge
+//   (2, 0, lcp, lb, rb, 0, 0)                   visit_lcp_interval
+//   (1, firstsucc, fd, flb, sd, slb, srb)       visit_branching_edge
+// staged per 256-row chunk as 4-word descriptors (the branching edge takes
+// sd, slb, srb from the lcp-interval event before it) and stored as aligned
+// 16-byte pieces of the 7-word records; events past the stage go straight
+// to memory
+template <typename RowT, typename SufT>
+__device__ __forceinline__ uint64_t li_event_word(const LiTile<RowT> &S, uint32_t e, uint32_t f,
+                                                  const SufT *suf) {
+  const LiDesc<RowT> d = S.st.ev[e];
+  const uint32_t kind = (uint32_t) d.a & 3u;
+  if (f == 0) return kind;
+  if (f == 1) return kind == 2u ? 0u : (uint64_t) (d.a >> 2);
+  if (f == 2) return d.b;
+  if (f == 3) return d.c;
+  if (kind == 1u) {                      // sd, slb, srb: the lcp-interval event before
+    const LiDesc<RowT> p = S.st.ev[e - 1];
+    return f == 4 ? (uint64_t) p.b : f == 5 ? (uint64_t) p.c : (uint64_t) p.d;
+  }
+  if (f == 4) return kind == 2u ? (uint64_t) d.d : (suf != nullptr ? (uint64_t) suf[d.d] : 0u);
+  return 0;
+}
+
+template <typename RowT, typename SufT>
+__global__ void __launch_bounds__(LI_TPB) li_tile_events_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
+                                                                const uint64_t *tile_off,
+                                                                const SufT *suf,
+                                                                const unsigned long long *firstp,
+                                                                uint64_t *ev) {
+  __shared__ LiTile<RowT> S;
+  constexpr uint32_t cap = LI_EV_STAGE / sizeof (LiDesc<RowT>);
+  const uint64_t first = *firstp;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t t0 = t * LI_T;
+    li_tile_ansv(L, N, t0, S);
+    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
+    uint64_t ebase = t0 + 2 * tile_off[t];   // stream position of the chunk's first event
+    for (int c0 = 0; c0 < nrows; c0 += LI_TPB) {
+      const int i = c0 + (int) threadIdx.x;
+      const bool row = i < nrows;
+      const uint32_t n = row ? li_pops(L, S, t0, i) : 0u;
+      uint32_t tot;
+      const uint32_t off = li_block_excl(row ? 1u + 2u * n : 0u, &tot);
+      if (row) {
+        const uint64_t idx = t0 + (uint64_t) i;
+        const uint32_t X = S.x[i], Y = S.x[i + 1];
+        const uint64_t pos = ebase + off;
+        uint64_t fs, fd, flb;
+        if (Y <= X) {
+          fs = (X == 0 && pos == first) ? 1u : 0u;
+          fd = X;
+          flb = X == 0 ? 0 : (uint64_t) S.pl[i];
+        } else {
+          fs = 1;
+          fd = Y;
+          flb = idx;
+        }
+        if (off < cap) {
+          S.st.ev[off] = LiDesc<RowT>{(RowT) (fs << 2), (RowT) fd, (RowT) flb, (RowT) idx};
+        } else {
+          uint64_t *w = ev + 7 * pos;
+          w[0] = 0; w[1] = fs; w[2] = fd; w[3] = flb;
+          w[4] = suf != nullptr ? (uint64_t) suf[idx] : 0u; w[5] = 0; w[6] = 0;
+        }
+        li_walk(L, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t pfd, uint64_t pflb,
+                                 bool newfather) {
+          const uint32_t k = off + 1 + 2 * j;
+          const uint64_t bfs = newfather ? 1u : (pfd == 0 && pos + 2 + 2 * j == first) ? 1u : 0u;
+          if (k < cap) S.st.ev[k] = LiDesc<RowT>{(RowT) 2, (RowT) lcp, (RowT) lb, (RowT) idx};
+          if (k + 1 < cap) {
+            S.st.ev[k + 1] = LiDesc<RowT>{(RowT) (1u | (bfs << 2)), (RowT) pfd, (RowT) pflb, (RowT) 0};
+          } else {
+            uint64_t *w = ev + 7 * (ebase + k);
+            if (k >= cap) { w[0] = 2; w[1] = 0; w[2] = lcp; w[3] = lb; w[4] = idx; w[5] = 0; w[6] = 0; }
+            w[7] = 1; w[8] = bfs; w[9] = pfd; w[10] = pflb; w[11] = lcp; w[12] = lb; w[13] = idx;
+          }
+        });
+      }
+      __syncthreads();
+      const uint32_t staged = tot < cap ? tot : cap;
+      const uint64_t w0 = 7 * ebase, w1 = 7 * (ebase + staged);
+      for (uint64_t q = (w0 >> 1) + threadIdx.x; 2 * q < w1; q += LI_TPB) {
+        const uint64_t a = 2 * q;
+        const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
+        uint64_t v0 = 0, v1 = 0;
+        if (lo_ok) {
+          const uint32_t r = (uint32_t) (a - w0);
+          v0 = li_event_word<RowT, SufT>(S, r / 7, r % 7, suf);
+        }
+        if (hi_ok) {
+          const uint32_t r = (uint32_t) (a + 1 - w0);
+          v1 = li_event_word<RowT, SufT>(S, r / 7, r % 7, suf);
+        }
+        if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(ev)[q] = make_ulonglong2(v0, v1);
+        else if (lo_ok) ev[a] = v0;
+        else ev[a + 1] = v1;
+      }
+      __syncthreads();
+      ebase += tot;
     }
   }
 }
@@ -432,46 +525,54 @@ __global__ void __launch_bounds__(256) li_events_itv_kernel(const uint64_t *itv,
 
 // a dispatch holds fewer than 2^32 work-items and N + 1 rows exceed that past
 // 2^32 suffixes: per-row kernels are grid-stride loops (LI_FOR) over a
-// capped grid, the 256-row group kernels group-stride loops
+// capped grid, the tile kernels tile-stride loops
 #define LI_MAX_BLOCKS (1ull << 22)
 static unsigned li_blocks(uint64_t n) {
   const uint64_t b = (n + 255) / 256;
   return (unsigned) (b > LI_MAX_BLOCKS ? LI_MAX_BLOCKS : (b ? b : 1));
 }
 
+static unsigned li_tile_grid(uint64_t ntiles) {
+  return (unsigned) (ntiles > LI_MAX_BLOCKS ? LI_MAX_BLOCKS : (ntiles ? ntiles : 1));
+}
+
 struct GtLcpitvPlan {
   GtLcpitvDevInput in;
   uint32_t *lev[LI_MAXLEV];
   LiLevels L;
+  bool wide;                     // rows past 2^32: 64-bit row indices in the tiles
+  uint64_t ntiles;
   uint64_t nitv;
   uint64_t *itv;                 // 5 * nitv, pop order
-  uint32_t *before;              // N + 1: intervals with rb < v (NULL past 2^32 rows)
-  unsigned long long *first;     // position of the first root edge
+  uint64_t *tile_off;            // intervals popped before each tile
+  unsigned long long *first;     // stream position of the first root edge
+  SmaxStreamMarks marks;         // streams the plan's work ran on
 };
 
 extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
-  // the plan's buffers go back to the runtime's cache (smax_dev_alloc): the
-  // work still queued on them (an events pass on a caller's stream) first
-  (void) hipDeviceSynchronize();
-  for (int l = 0; l < LI_MAXLEV; l++)
-    if (p->lev[l]) smax_dev_free(p->lev[l]);
-  if (p->itv) smax_dev_free(p->itv);
-  if (p->before) smax_dev_free(p->before);
-  if (p->first) smax_dev_free(p->first);
+  // the buffers return to the runtime's cache behind the plan's own work
+  // (events recorded where it was enqueued): nothing here waits, and no
+  // other stream of the device is involved
+  SmaxFence *fence = smax_marks_fence(&p->marks);
+  for (int l = 0; l < LI_MAXLEV; l++) smax_dev_free_fenced(p->lev[l], fence);
+  smax_dev_free_fenced(p->itv, fence);
+  smax_dev_free_fenced(p->tile_off, fence);
+  smax_dev_free_fenced(p->first, fence);
+  smax_fence_release(fence);
   free(p);
 }
 
-extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInput *in,
-                                     char *errbuf, size_t errlen) {
+extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitvDevInput *in,
+                                            void *stream, char *errbuf, size_t errlen) {
   GtLcpitvPlan *p = NULL;
-  uint32_t *derr = NULL, herr = 0, *wg_cnt = NULL, *dmarks = NULL;
-  uint64_t *wg_off = NULL, *rec = NULL, *key_a = NULL, *key_b = NULL, *idx_a = NULL,
-           *idx_b = NULL;
+  hipStream_t s = (hipStream_t) stream;
+  uint32_t *derr = NULL, herr = 0, *tile_cnt = NULL;
   void *tmp = NULL;
   size_t tmp_bytes = 0;
-  uint64_t N, nwg;
+  uint64_t N;
+  const unsigned long long none = ~0ull;
   *planp = NULL;
   if (in == NULL || in->lcp_dev == NULL) {
     li_seterr(errbuf, errlen, "missing device lcptab");
@@ -490,20 +591,24 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
     li_seterr(errbuf, errlen, "out of memory");
     return -1;
   }
+  smax_marks_init(&p->marks);
   p->in = *in;
   N = in->nonspecials;
+  p->wide = N + 1 >= 0xffffffffull;
+  p->ntiles = (N + LI_T - 1) / LI_T;
   LICHK(hipSetDevice(in->device));
   LICHK(smax_dev_alloc((void **) &derr, sizeof (uint32_t)));
-  LICHK(hipMemset(derr, 0, sizeof (uint32_t)));
+  LICHK(hipMemsetAsync(derr, 0, sizeof (uint32_t), s));
   LICHK(smax_dev_alloc((void **) &p->first, sizeof (unsigned long long)));
+  LICHK(hipMemcpyAsync(p->first, &none, sizeof none, hipMemcpyHostToDevice, s));
   // level 0: exact LCP, then 64-ary mins until one entry remains
   p->L.n[0] = N + 1;
   LICHK(smax_dev_alloc((void **) &p->lev[0], sizeof (uint32_t) * (p->L.n[0] + LI_PAD)));
-  hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, 0, in->lcp_dev, N,
+  hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, s, in->lcp_dev, N,
                      p->lev[0]);
   LICHK(hipGetLastError());
   if (in->numllv > 0) {
-    hipLaunchKernelGGL(li_llv_kernel, dim3(li_blocks(in->numllv)), dim3(256), 0, 0, in->llv_dev,
+    hipLaunchKernelGGL(li_llv_kernel, dim3(li_blocks(in->numllv)), dim3(256), 0, s, in->llv_dev,
                        in->numllv, in->lcp_dev, N, p->lev[0], derr);
     LICHK(hipGetLastError());
   }
@@ -512,7 +617,7 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
     const int l = p->L.nlev;
     p->L.n[l] = (p->L.n[l - 1] + 63) / 64;
     LICHK(smax_dev_alloc((void **) &p->lev[l], sizeof (uint32_t) * (p->L.n[l] + LI_PAD)));
-    hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(p->L.n[l])), dim3(256), 0, 0, p->lev[l - 1],
+    hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(p->L.n[l])), dim3(256), 0, s, p->lev[l - 1],
                        p->L.n[l - 1], p->lev[l], p->L.n[l]);
     LICHK(hipGetLastError());
     p->L.nlev++;
@@ -522,110 +627,75 @@ extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInpu
     goto fail;
   }
   for (int l = 0; l < p->L.nlev; l++) p->L.lv[l] = p->lev[l];
-  LICHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
+  // pops per tile, their exclusive scan, the records
+  LICHK(smax_dev_alloc((void **) &tile_cnt, sizeof (uint32_t) * (p->ntiles + 1)));
+  LICHK(smax_dev_alloc((void **) &p->tile_off, sizeof (uint64_t) * (p->ntiles + 1)));
+  LICHK(hipMemsetAsync(tile_cnt + p->ntiles, 0, sizeof (uint32_t), s));
+  if (p->ntiles > 0) {
+    if (p->wide)
+      hipLaunchKernelGGL(li_tile_count_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0,
+                         s, p->L, N, p->ntiles, tile_cnt);
+    else
+      hipLaunchKernelGGL(li_tile_count_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0,
+                         s, p->L, N, p->ntiles, tile_cnt);
+    LICHK(hipGetLastError());
+  }
+  LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, tile_cnt, p->tile_off, (uint64_t) 0,
+                                (size_t) (p->ntiles + 1), rocprim::plus<uint64_t>(), s));
+  LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
+  LICHK(rocprim::exclusive_scan(tmp, tmp_bytes, tile_cnt, p->tile_off, (uint64_t) 0,
+                                (size_t) (p->ntiles + 1), rocprim::plus<uint64_t>(), s));
+  LICHK(hipMemcpyAsync(&p->nitv, p->tile_off + p->ntiles, sizeof (uint64_t), hipMemcpyDeviceToHost, s));
+  LICHK(hipMemcpyAsync(&herr, derr, sizeof herr, hipMemcpyDeviceToHost, s));
+  LICHK(hipStreamSynchronize(s));      // the interval count sizes the records
   if (herr & 1u) { li_seterr(errbuf, errlen, "lcp value >= 2^32-1 in .llv"); goto fail; }
   if (herr & 2u) { li_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
-  // intervals: count per workgroup, scan, write, sort into pop order
-  nwg = (N + 255) / 256;
-  if (nwg > 0x7fffffffull) { li_seterr(errbuf, errlen, "too many suffixes"); goto fail; }
-  LICHK(smax_dev_alloc((void **) &wg_cnt, sizeof (uint32_t) * (nwg + 1)));
-  LICHK(smax_dev_alloc((void **) &wg_off, sizeof (uint64_t) * (nwg + 1)));
-  if (nwg > 0) {
-    hipLaunchKernelGGL(li_count_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, p->L, N, nwg, wg_cnt);
-    LICHK(hipGetLastError());
-    LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
-                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
-    LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
-    LICHK(rocprim::exclusive_scan(tmp, tmp_bytes, wg_cnt, wg_off, (uint64_t) 0, (size_t) nwg,
-                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
-    uint64_t lo = 0;
-    uint32_t lc = 0;
-    LICHK(hipMemcpy(&lo, wg_off + nwg - 1, sizeof lo, hipMemcpyDeviceToHost));
-    LICHK(hipMemcpy(&lc, wg_cnt + nwg - 1, sizeof lc, hipMemcpyDeviceToHost));
-    p->nitv = lo + lc;
-  }
   LICHK(smax_dev_alloc((void **) &p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
-  if (p->nitv > 0) {
-    const uint64_t n = p->nitv;
-    LICHK(smax_dev_alloc((void **) &rec, sizeof (uint64_t) * 5 * n));
-    LICHK(smax_dev_alloc((void **) &key_a, sizeof (uint64_t) * n));
-    LICHK(smax_dev_alloc((void **) &key_b, sizeof (uint64_t) * n));
-    LICHK(smax_dev_alloc((void **) &idx_a, sizeof (uint64_t) * n));
-    LICHK(smax_dev_alloc((void **) &idx_b, sizeof (uint64_t) * n));
-    hipLaunchKernelGGL(li_write_kernel, dim3(li_blocks(N)), dim3(256), 0, 0, p->L, N, nwg, wg_off,
-                       rec, key_a, idx_a);
+  if (p->ntiles > 0) {
+    if (p->wide)
+      hipLaunchKernelGGL(li_tile_itv_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s,
+                         p->L, N, p->ntiles, p->tile_off, p->itv, p->first);
+    else
+      hipLaunchKernelGGL(li_tile_itv_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s,
+                         p->L, N, p->ntiles, p->tile_off, p->itv, p->first);
     LICHK(hipGetLastError());
-    smax_dev_free(tmp);   // the scan is done: the copies above waited for it
-    tmp = NULL;
-    tmp_bytes = 0;
-    LICHK(rocprim::radix_sort_pairs(nullptr, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0,
-                                    64, (hipStream_t) 0));
-    LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
-    if (N < 0xffffffffull) {
-      // by rb alone: bits(N) radix bits instead of 64 (rb << 32 | ~lcp, 8
-      // onesweep passes, 4.1 ms of the C2 step), then the run reversal
-      const int rbits = 64 - __builtin_clzll((unsigned long long) N);
-      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0,
-                                      rbits, (hipStream_t) 0));
-      // before[v] = intervals with rb < v (the events pass's positions, and
-      // the runs here): a max-scan over the run ends, staged in key_a's
-      // space (free after the sort) where it fits
-      uint32_t *D = (uint32_t *) key_a;
-      LICHK(smax_dev_alloc((void **) &p->before, sizeof (uint32_t) * (N + 1)));
-      if (sizeof (uint64_t) * n < sizeof (uint32_t) * (N + 1)) {
-        LICHK(smax_dev_alloc((void **) &dmarks, sizeof (uint32_t) * (N + 1)));
-        D = dmarks;
-      }
-      LICHK(hipMemsetAsync(D, 0, sizeof (uint32_t) * (N + 1), 0));
-      hipLaunchKernelGGL(li_rb_marks_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, key_b, n, D);
-      LICHK(hipGetLastError());
-      size_t sb = 0;
-      LICHK(rocprim::inclusive_scan(nullptr, sb, D, p->before, (size_t) (N + 1),
-                                    rocprim::maximum<uint32_t>(), (hipStream_t) 0));
-      if (sb > tmp_bytes) {
-        LICHK(hipDeviceSynchronize());   // the sort is done with tmp
-        smax_dev_free(tmp);
-        tmp = NULL;
-        LICHK(smax_dev_alloc((void **) &tmp, sb));
-        tmp_bytes = sb;
-      }
-      LICHK(rocprim::inclusive_scan(tmp, sb, D, p->before, (size_t) (N + 1),
-                                    rocprim::maximum<uint32_t>(), (hipStream_t) 0));
-      hipLaunchKernelGGL(li_gather_rev_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, key_b,
-                         p->before, n, p->itv);
-      LICHK(hipGetLastError());
-    } else {
-      // rb >= 2^32 possible: stable passes by ~lcp, then by rb (past 2^32
-      // rows the events pass finds positions by binary search)
-      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_a, n, 0, key_a);
-      LICHK(hipGetLastError());
-      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_a, idx_b, (size_t) n, 0, 32,
-                                      (hipStream_t) 0));
-      hipLaunchKernelGGL(li_key_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_b, n, 1, key_a);
-      LICHK(hipGetLastError());
-      LICHK(rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, idx_b, idx_a, (size_t) n, 0, 64,
-                                      (hipStream_t) 0));
-      hipLaunchKernelGGL(li_gather_kernel, dim3(li_blocks(n)), dim3(256), 0, 0, rec, idx_a, n, p->itv);
-      LICHK(hipGetLastError());
-    }
   }
-  LICHK(hipDeviceSynchronize());
+  smax_marks_record(&p->marks, s);
   {
-    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp, dmarks};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) smax_dev_free(bufs[i]);
+    // the scratch buffers go back behind the plan's work on s
+    SmaxStreamMarks m;
+    smax_marks_init(&m);
+    smax_marks_record(&m, s);
+    SmaxFence *f = smax_marks_fence(&m);
+    smax_dev_free_fenced(derr, f);
+    smax_dev_free_fenced(tile_cnt, f);
+    smax_dev_free_fenced(tmp, f);
+    smax_fence_release(f);
   }
   *planp = p;
   return 0;
 fail:
   {
-    (void) hipDeviceSynchronize();   // nothing queued may still use a cached block
-    void *bufs[] = {derr, wg_cnt, wg_off, rec, key_a, key_b, idx_a, idx_b, tmp, dmarks};
+    (void) hipStreamSynchronize(s);    // nothing queued may still use a cached block
+    void *bufs[] = {derr, tile_cnt, tmp};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
       if (bufs[i]) smax_dev_free(bufs[i]);
   }
+  smax_marks_record(&p->marks, s);
   gt_lcpitv_plan_delete(p);
   return -1;
+}
+
+extern "C" int gt_lcpitv_plan_create(GtLcpitvPlan **planp, const GtLcpitvDevInput *in, char *errbuf,
+                                     size_t errlen) {
+  if (gt_lcpitv_plan_create_stream(planp, in, NULL, errbuf, errlen) != 0) return -1;
+  if (smax_marks_sync(&(*planp)->marks) != hipSuccess) {   // synchronous, as documented
+    li_seterr(errbuf, errlen, "lcp-interval tree construction failed");
+    gt_lcpitv_plan_delete(*planp);
+    *planp = NULL;
+    return -1;
+  }
+  return 0;
 }
 
 extern "C" uint64_t gt_lcpitv_plan_intervals(const GtLcpitvPlan *p, const uint64_t **itv_dev) {
@@ -639,25 +709,32 @@ extern "C" uint64_t gt_lcpitv_plan_num_events(const GtLcpitvPlan *p) {
 
 extern "C" int gt_lcpitv_plan_events(GtLcpitvPlan *p, uint64_t *events_dev, void *stream) {
   hipStream_t s = (hipStream_t) stream;
-  const uint64_t N = p->in.nonspecials, n = p->nitv;
-  const unsigned long long none = ~0ull;
+  const uint64_t N = p->in.nonspecials;
+  if (((uintptr_t) events_dev & 15) != 0) return -1;   // 16-byte pieces
   if (hipSetDevice(p->in.device) != hipSuccess) return -1;
   if (N == 0) return 0;
-  if (hipMemcpyAsync(p->first, &none, sizeof none, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
-  hipLaunchKernelGGL(li_rootfirst_leaf_kernel, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N, p->itv,
-                     n, p->before, p->first);
-  if (n > 0)
-    hipLaunchKernelGGL(li_rootfirst_itv_kernel, dim3(li_blocks(n)), dim3(256), 0, s, p->itv, n,
-                       p->before, p->first);
-  if (p->in.suf_bytes == 4)
-    hipLaunchKernelGGL(li_events_leaf_kernel<uint32_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N,
-                       p->itv, n, p->before, p->in.suf_dev, p->first, events_dev);
-  else
-    hipLaunchKernelGGL(li_events_leaf_kernel<uint64_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->L, N,
-                       p->itv, n, p->before, p->in.suf_dev, p->first, events_dev);
-  if (n > 0)
-    hipLaunchKernelGGL(li_events_itv_kernel, dim3(li_blocks(n)), dim3(256), 0, s, p->itv, n,
-                       p->before, p->first, events_dev);
+  // the tree (plan create, maybe on another stream) before the events
+  if (smax_marks_wait(&p->marks, s) != hipSuccess) return -1;
+  const dim3 g(li_tile_grid(p->ntiles)), b(LI_TPB);
+  const bool s4 = p->in.suf_dev != nullptr && p->in.suf_bytes == 4;
+  const uint32_t *suf4 = s4 ? (const uint32_t *) p->in.suf_dev : nullptr;
+  const uint64_t *suf8 = !s4 ? (const uint64_t *) p->in.suf_dev : nullptr;
+  if (p->wide) {
+    if (s4)
+      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint32_t>), g, b, 0, s, p->L, N, p->ntiles,
+                         p->tile_off, suf4, p->first, events_dev);
+    else
+      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint64_t>), g, b, 0, s, p->L, N, p->ntiles,
+                         p->tile_off, suf8, p->first, events_dev);
+  } else {
+    if (s4)
+      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint32_t>), g, b, 0, s, p->L, N, p->ntiles,
+                         p->tile_off, suf4, p->first, events_dev);
+    else
+      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint64_t>), g, b, 0, s, p->L, N, p->ntiles,
+                         p->tile_off, suf8, p->first, events_dev);
+  }
+  smax_marks_record(&p->marks, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -783,7 +860,7 @@ static int li_replay(const GtSmaxInput *in, bool need_suf, Sink sink, char *errb
   if (li_host_plan(in, need_suf, &h, &plan, errbuf, errlen) != 0) return -1;
   E = gt_lcpitv_plan_num_events(plan);
   if (E > 0) {
-    LICHK(hipMalloc(&ev, sizeof (uint64_t) * 7 * E));
+    LICHK(smax_dev_alloc((void **) &ev, sizeof (uint64_t) * 7 * E));
     if (gt_lcpitv_plan_events(plan, ev, NULL) != 0) {
       li_seterr(errbuf, errlen, "event generation failed");
       goto fail;
@@ -796,7 +873,8 @@ static int li_replay(const GtSmaxInput *in, bool need_suf, Sink sink, char *errb
     LICHK(hipMemcpy(host, ev + 7 * e0, sizeof (uint64_t) * 7 * n, hipMemcpyDeviceToHost));
     for (uint64_t k = 0; k < n && rc == 0; k++) rc = sink(host + 7 * k);
   }
-  if (ev) (void) hipFree(ev);
+  (void) hipStreamSynchronize(nullptr);   // (the copies above were synchronous)
+  smax_dev_free(ev);
   if (host) (void) hipHostFree(host);
   gt_lcpitv_plan_delete(plan);
   li_host_free(&h);
@@ -806,7 +884,8 @@ static int li_replay(const GtSmaxInput *in, bool need_suf, Sink sink, char *errb
   }
   return 0;
 fail:
-  if (ev) (void) hipFree(ev);
+  (void) hipStreamSynchronize(nullptr);
+  smax_dev_free(ev);
   if (host) (void) hipHostFree(host);
   gt_lcpitv_plan_delete(plan);
   li_host_free(&h);

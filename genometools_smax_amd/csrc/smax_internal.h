@@ -39,6 +39,28 @@ SmaxFence *smax_fence_adopt(const hipEvent_t *events, int nevents, bool whole_de
 void smax_dev_free_fenced(void *ptr, SmaxFence *fence);  // NULL ptr ok
 void smax_fence_release(SmaxFence *fence);               // the creator's reference
 
+// The streams a device-resident plan (F2 / F3) enqueued work on, each with
+// an event recorded behind its last work there: waits and the delete-time
+// fence of the plan's buffers use the events only (never a caller's stream
+// handle, which may be destroyed first) and never the whole device unless
+// more than SMAX_MARK_STREAMS streams were used.
+#define SMAX_MARK_STREAMS 4
+struct SmaxStreamMarks {
+  hipStream_t s[SMAX_MARK_STREAMS];
+  hipEvent_t ev[SMAX_MARK_STREAMS];
+  int n;
+  bool overflow;
+};
+void smax_marks_init(SmaxStreamMarks *m);
+// after enqueueing on stream s (current device): the mark now stands behind it
+void smax_marks_record(SmaxStreamMarks *m, hipStream_t s);
+// waits for everything marked (host side)
+hipError_t smax_marks_sync(SmaxStreamMarks *m);
+// makes stream s wait for everything marked (device side)
+hipError_t smax_marks_wait(SmaxStreamMarks *m, hipStream_t s);
+// a fence over the marks (ownership of the events moves to it; m is reset)
+SmaxFence *smax_marks_fence(SmaxStreamMarks *m);
+
 // Device records of a plan -> host (lcp, lb, rb) triples through the
 // device's pinned ring (the plan's work must be complete).
 hipError_t smax_d2h_triples(uint64_t *dst, const GtSmaxRecord *dev, uint64_t cnt, void *stream);

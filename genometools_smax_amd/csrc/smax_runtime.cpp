@@ -1470,6 +1470,55 @@ SmaxFence *smax_fence_adopt(const hipEvent_t *events, int nevents, bool whole_de
 
 void smax_fence_release(SmaxFence *fence) { fence_unref(fence); }
 
+void smax_marks_init(SmaxStreamMarks *m) {
+  m->n = 0;
+  m->overflow = false;
+}
+
+void smax_marks_record(SmaxStreamMarks *m, hipStream_t s) {
+  int i = 0;
+  while (i < m->n && m->s[i] != s) i++;
+  if (i == m->n) {
+    if (m->n == SMAX_MARK_STREAMS ||
+        hipEventCreateWithFlags(&m->ev[i], hipEventDisableTiming) != hipSuccess) {
+      (void) hipGetLastError();
+      m->overflow = true;
+      return;
+    }
+    m->s[i] = s;
+    m->n++;
+  }
+  if (hipEventRecord(m->ev[i], s) != hipSuccess) {
+    (void) hipGetLastError();
+    m->overflow = true;
+  }
+}
+
+hipError_t smax_marks_sync(SmaxStreamMarks *m) {
+  if (m->overflow) return hipDeviceSynchronize();
+  for (int i = 0; i < m->n; i++) {
+    const hipError_t e = hipEventSynchronize(m->ev[i]);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t smax_marks_wait(SmaxStreamMarks *m, hipStream_t s) {
+  if (m->overflow) return hipDeviceSynchronize();
+  for (int i = 0; i < m->n; i++) {
+    if (m->s[i] == s) continue;          // stream order already
+    const hipError_t e = hipStreamWaitEvent(s, m->ev[i], 0);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+SmaxFence *smax_marks_fence(SmaxStreamMarks *m) {
+  SmaxFence *f = smax_fence_adopt(m->ev, m->n, m->overflow);
+  smax_marks_init(m);
+  return f;
+}
+
 double smax_phase_clock() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }

@@ -25,9 +25,11 @@
  *                                 its father, in bottom-up (pop) order:
  *                                 (lcp, lb, rb, father lcp, father lb).
  *
- * Device form: the tree comes from all-nearest-smaller-value searches over
- * the exact LCP array (a 64-ary min hierarchy), one thread per row; no
- * stack walk.  The device-resident API (gt_lcpitv_plan_*) keeps the tree in
+ * Device form: the tree comes from the strict previous-smaller values of
+ * the exact LCP array (ANSV per 2048-row tile in LDS, a 64-ary min
+ * hierarchy across tiles): the reference's stack after each row is the
+ * previous-smaller chain from it, so the intervals popped there are read
+ * off that chain; no stack walk, no sort.  The device-resident API (gt_lcpitv_plan_*) keeps the tree in
  * HBM and writes the whole visitor event stream there, every event at its
  * position in the reference's order; the host entry points above are built
  * on it (events downloaded in chunks, callbacks on the calling thread).
@@ -114,6 +116,16 @@ typedef struct GtLcpitvPlan GtLcpitvPlan;
 /* Builds the lcp-interval tree in HBM (synchronous). */
 int gt_lcpitv_plan_create(GtLcpitvPlan **plan, const GtLcpitvDevInput *in, char *errbuf,
                           size_t errlen);
+/* The same, enqueued on stream (a hipStream_t, NULL = default stream): it
+ * waits on that stream once, for the interval count that sizes the records,
+ * and returns with the records still being written there.  Reading them
+ * (gt_lcpitv_plan_intervals) on another stream needs that stream ordered
+ * after `stream`; gt_lcpitv_plan_events orders itself. */
+int gt_lcpitv_plan_create_stream(GtLcpitvPlan **plan, const GtLcpitvDevInput *in, void *stream,
+                                 char *errbuf, size_t errlen);
+/* Frees the plan; its device buffers return to the runtime's cache behind
+ * events recorded where its work was enqueued (nothing waits; the caller's
+ * streams may already be destroyed). */
 void gt_lcpitv_plan_delete(GtLcpitvPlan *plan);
 
 /* Number of lcp-intervals of depth > 0; *itv_dev = their device records,
@@ -125,7 +137,9 @@ uint64_t gt_lcpitv_plan_intervals(const GtLcpitvPlan *plan, const uint64_t **itv
 uint64_t gt_lcpitv_plan_num_events(const GtLcpitvPlan *plan);
 
 /* Enqueues the event stream of gt_esa_bottomup (7 uint64 per event, in the
- * reference's order) into events_dev (gt_lcpitv_plan_num_events entries):
+ * reference's order) into events_dev (gt_lcpitv_plan_num_events entries;
+ * 16-byte aligned, else -1: the records are stored as 16-byte pieces) on
+ * stream, after the plan's construction (on whatever stream it ran):
  *   (0, firstsucc, fd, flb, leafnumber, 0, 0)   visit_leaf_edge
  *   (1, firstsucc, fd, flb, sd, slb, srb)       visit_branching_edge
  *   (2, 0, lcp, lb, rb, 0, 0)                   visit_lcp_interval  */

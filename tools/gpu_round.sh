@@ -171,6 +171,20 @@ for S in "$@"; do
         > "$O/mpprof_bench_$T.json" 2> "$O/mpprof_bench_$T.err")
       python3 tools/rocpd_summary.py stats "$O/mpprof_$T/p_results.db" "$O/kernel_stats_maxpairs_$T.csv"
       rm -rf "$O/mpprof_$T" ;;
+    mppmc:*|f3pmc:*)
+      # mppmc:CONFIG[:BASES] / f3pmc:CONFIG[:BASES] -- HBM bytes per launch of
+      # every F2 (mp_*) / F3 (li_*) kernel: --pmc FETCH_SIZE, then WRITE_SIZE
+      IFS=: read -r K C BASES <<< "$S"
+      T=$C${BASES:+_$BASES}
+      if [ "$K" = mppmc ]; then PTH=maxpairs; RX='mp_|rocprim'; else PTH=lcpitv; RX='li_|rocprim'; fi
+      for X in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $X --kernel-include-regex "$RX" \
+          -d "$O/${K}_${T}_$X" -o p -- python3 "$R/bench.py" --path $PTH --config "$C" ${BASES:+--bases $BASES} \
+          --no-cpu-baseline --steps 2 --warmup 1 --prime-s 0 > "$O/${K}_${T}_$X.log" 2>&1)
+      done
+      python3 tools/rocpd_summary.py pmcall "$O/${K}_$T.json" "$T" "$O/${K}_${T}_FETCH_SIZE/p_results.db" \
+        "$O/${K}_${T}_WRITE_SIZE/p_results.db"
+      rm -rf "$O/${K}_${T}_FETCH_SIZE" "$O/${K}_${T}_WRITE_SIZE" ;;
     f3:*)
       # f3:CONFIG[:BASES] -- the F3 leg, bench.py --path lcpitv (intervals + visitor events)
       IFS=: read -r _ C BASES <<< "$S"

@@ -4,6 +4,7 @@ profiles/.
 
   rocpd_summary.py stats  DB OUT.csv                   kernel-trace --stats table
   rocpd_summary.py pmc    OUT.json KERNEL CONFIG DB... per-launch counters of KERNEL
+  rocpd_summary.py pmcall OUT.json CONFIG DB...        per-launch HBM bytes of every kernel
 
 `pmc` keeps every counter of the passes (per launch), the HBM bytes when
 FETCH_SIZE and WRITE_SIZE are among them, the bench config the passes ran
@@ -72,8 +73,49 @@ def pmc(out, kernel, config, dbs):
     print(json.dumps({k: v for k, v in res.items() if k != "passes"}, indent=1))
 
 
+def pmcall(out, config, dbs):
+    """FETCH_SIZE / WRITE_SIZE per launch of every kernel in the passes
+    (same corrections as pmc), keyed by the short kernel name."""
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import genometools_smax_amd as G
+    per = {}
+    for db in dbs:
+        con = sqlite3.connect(db)
+        rows = con.execute("select kernel_name, counter_name, dispatch_id, sum(value), max(duration) "
+                           "from counters_collection group by kernel_name, counter_name, dispatch_id"
+                           ).fetchall()
+        for name, cname, _d, value, dur in rows:
+            short = name.replace("(anonymous namespace)::", "").split("(")[0]
+            k = per.setdefault(short, {}).setdefault(cname, [])
+            k.append((float(value), float(dur or 0)))
+    res = {"config": config, "build_id": G.build_id(),
+           "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                      "read = 2 x 1024 x FETCH_SIZE (gfx950 half-count correction), "
+                      "write = 1024 x WRITE_SIZE; per launch = mean over the kernel's launches"),
+           "kernels": {}}
+    for short, cs in sorted(per.items()):
+        d = {}
+        if "FETCH_SIZE" in cs:
+            v = cs["FETCH_SIZE"]
+            d["launches"] = len(v)
+            d["read_bytes_per_launch"] = 2 * 1024 * sum(x for x, _ in v) / len(v)
+        if "WRITE_SIZE" in cs:
+            v = cs["WRITE_SIZE"]
+            d["write_bytes_per_launch"] = 1024 * sum(x for x, _ in v) / len(v)
+        if "read_bytes_per_launch" in d and "write_bytes_per_launch" in d:
+            d["hbm_bytes_per_launch"] = d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
+        res["kernels"][short] = d
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    for k, d in res["kernels"].items():
+        print("%-50s %s" % (k[:50], {x: round(y) for x, y in d.items()}))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "pmcall":
+        pmcall(sys.argv[2], sys.argv[3], sys.argv[4:])
     else:
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5:])
