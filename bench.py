@@ -162,16 +162,15 @@ def main_lcpitv(args):
     stream in the reference's order (/root/reference/src/match/
     esa-bottomup.c:116-273) -- over tables resident in HBM.  A step is one
     gt_lcpitv_plan_create (the interval tree: exact LCP, 64-ary minimum
-    hierarchy, per-row interval records, pop-order sort) + one
+    hierarchy, per-tile ANSV count and pop-ordered interval records) + one
     gt_lcpitv_plan_events pass into a resident buffer + gt_lcpitv_plan_delete.
     One GPU (--gpus N: replicas).
 
     Algorithmic bytes per step (the roofline's "achieved"): per row the LCP
-    byte, its exact u32 written and read by the two hierarchy searches
-    (1 + 4 + 2 x 4 B), per interval its 5-word record written, its sort key
-    and index through one radix pass (2 x 2 x 16 B) and the gather (2 x 40 B),
-    per event its 7-word record (56 B) plus the leaf's suffix and LCP reads
-    (8 B per row)."""
+    byte read, its exact u32 written and read by the two tree passes
+    (1 + 4 + 2 x 4 B), per interval its 5-word record written (40 B), per
+    event its 7-word record (56 B) plus the events pass's LCP u32 and 4-byte
+    suffix reads (8 B per row)."""
     import numpy as np
     import torch
     import genometools_smax_amd as G
@@ -250,7 +249,7 @@ def main_lcpitv(args):
         mx = torch.tensor([el, el_tree], dtype=torch.float64)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         el, el_tree = float(mx[0]), float(mx[1])
-    alg_tree = N * 13 + nitv * (40 + 64 + 80)
+    alg_tree = N * 13 + nitv * 40
     alg = alg_tree + n_ev * 56 + N * 8
     parity = None
     cpu = None

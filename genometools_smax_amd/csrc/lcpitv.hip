@@ -33,6 +33,7 @@
 // of row idx at idx + 2 P(idx) + 1 + 2r.  The host entry points download
 // the events in chunks and call the visitor.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <vector>
 #include <rocprim/device/device_scan.hpp>
 #include <stdarg.h>
@@ -194,47 +195,56 @@ __device__ __forceinline__ uint32_t li_block_excl(uint32_t v, uint32_t *total) {
 // first child of (Y, idx).  Every interval is popped once, so the walks
 // cost O(N) over the whole table.
 //
-// A workgroup owns LI_T consecutive rows (a tile): their X in LDS, PL by
-// per-thread pointer jumping inside 8-row segments, the rows left
-// unresolved by a segment-minimum search across the tile, and the tile's
-// prefix minima (no smaller value in the tile before them, a handful per
-// tile) by the global 64-ary hierarchy (li_prev).  Chains that leave the
-// tile (intervals open at its start) continue through li_prev as well.
-// Three passes walk the chains: a count per tile (plan), the pop-ordered
-// interval records (plan) and the visitor event stream (events); the last
-// two stage their output in LDS and store it as contiguous 16-byte pieces.
+// A workgroup owns LI_T consecutive rows (a tile).  Pass 0 computes PL of
+// its rows in LDS -- per-thread pointer jumping inside 8-row segments, the
+// rows left unresolved by a segment-minimum search across the tile, and
+// the tile's prefix minima (no smaller value in the tile before them, a
+// handful per tile) by the global 64-ary hierarchy (li_prev) -- and stores
+// it in HBM.  Chains that leave a tile (intervals open at its start)
+// continue along the chain from the row before the tile, t0-1, PL(t0-1),
+// ... (every PL out of the tile lies on it): its first LI_BD entries are
+// gathered once per tile (li_bchain_kernel, one thread per tile) and
+// loaded with the tile.  Three passes walk the chains: a count per tile
+// (plan), the pop-ordered interval records (plan) and the visitor event
+// stream (events); the last two stage their output in LDS per 64-row wave
+// step and store it as contiguous 16-byte pieces.
 #define LI_T 2048                       // rows per tile
 #define LI_TPB 256                      // threads per tile workgroup
 #define LI_RPT (LI_T / LI_TPB)          // rows per segment (one thread)
 #define LI_GSEG 16                      // segments per group
 #define LI_NGRP (LI_TPB / LI_GSEG)
-#define LI_ITV_CAP 384                  // interval records staged per 256-row chunk
+#define LI_BD 64                        // boundary-chain entries kept per tile
+#define LI_ITV_CAP 384                  // interval records staged per workgroup
 #define LI_EV_STAGE 16384               // event staging bytes per workgroup
-
-template <typename RowT>
-struct LiDesc {                         // one staged event (16 B / 32 B)
-  RowT a, b, c, d;                      // a: kind | firstsucc << 2
-};
-
-template <typename RowT>
-struct LiTile {
-  uint32_t x[LI_T + 1];                 // X[t0 .. t0 + LI_T] (0 past row N)
-  RowT pl[LI_T];                        // PL of the tile's rows (~0: none / pending)
-  uint32_t segmin[LI_TPB];
-  uint32_t grpmin[LI_NGRP];
-  union {
-    LiDesc<RowT> ev[LI_EV_STAGE / sizeof (LiDesc<RowT>)];
-    uint64_t itv[5 * LI_ITV_CAP];
-  } st;
-};
 
 template <typename RowT>
 __device__ __forceinline__ RowT li_none() { return (RowT) ~(RowT) 0; }
 
+// pass 0's LDS
+template <typename RowT>
+struct LiAnsvTile {
+  uint32_t x[LI_T + 1];                 // X[t0 .. t0 + LI_T] (0 past row N)
+  RowT pl[LI_T];                        // PL of the tile's rows (~0: none / pending)
+  uint32_t segmin[LI_TPB];
+  uint32_t grpmin[LI_NGRP];
+};
+
+// the walking passes' LDS: the tile, its boundary chain, the output stage
+template <typename RowT, int STAGE>
+struct LiWalkTile {
+  uint32_t x[LI_T + 1];
+  RowT pl[LI_T];
+  RowT brow[LI_BD];                     // t0-1, PL(t0-1), ... (rows strictly decreasing)
+  uint32_t bx[LI_BD];                   // their X (strictly decreasing)
+  int nb;                               // entries held; the chain goes on past them iff
+                                        // nb == LI_BD and bx[nb-1] > 0
+  alignas(16) unsigned char stage[STAGE];
+};
+
 // PL of every row of the tile [t0, t0 + LI_T) into S.pl (rows with X = 0
 // have none).  Ends with a barrier.
 template <typename RowT>
-__device__ void li_tile_ansv(const LiLevels &L, uint64_t N, uint64_t t0, LiTile<RowT> &S) {
+__device__ void li_tile_ansv(const LiLevels &L, uint64_t N, uint64_t t0, LiAnsvTile<RowT> &S) {
   const int tid = threadIdx.x;
   const RowT none = li_none<RowT>();
   for (int k = tid; k <= LI_T; k += LI_TPB) {
@@ -288,49 +298,146 @@ __device__ void li_tile_ansv(const LiLevels &L, uint64_t N, uint64_t t0, LiTile<
   __syncthreads();
 }
 
-// X and PL of any row at or before the tile's end: the tile's from LDS,
-// earlier ones from the hierarchy
+// pass 0 (plan): PL of every row into HBM (RowT each, ~0 where X = 0)
 template <typename RowT>
-__device__ __forceinline__ uint32_t li_tx(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0,
-                                          uint64_t c) {
-  return c >= t0 ? S.x[c - t0] : L.lv[0][c];
+__global__ void __launch_bounds__(LI_TPB) li_pl_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
+                                                       RowT *PL) {
+  __shared__ LiAnsvTile<RowT> S;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t t0 = t * LI_T;
+    li_tile_ansv(L, N, t0, S);
+    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
+    for (int i = threadIdx.x; i < nrows; i += LI_TPB) PL[t0 + i] = S.pl[i];
+    __syncthreads();                     // S is rewritten by the next tile
+  }
+}
+
+// each tile's boundary chain t0-1, PL(t0-1), ... down to the first X = 0
+// entry, at most LI_BD entries (one thread per tile: a latency chain of
+// dependent loads, thousands of them in flight)
+template <typename RowT>
+__global__ void __launch_bounds__(256) li_bchain_kernel(const uint32_t *X, const RowT *PL,
+                                                        uint64_t ntiles, RowT *brow, uint32_t *bx,
+                                                        uint32_t *bn) {
+  LI_FOR(t, ntiles) {
+    int k = 0;
+    if (t > 0) {
+      uint64_t s = t * LI_T - 1;
+      for (; k < LI_BD;) {
+        const uint32_t xs = X[s];
+        brow[t * LI_BD + k] = (RowT) s;
+        bx[t * LI_BD + k] = xs;
+        k++;
+        if (xs == 0) break;
+        s = PL[s];
+      }
+    }
+    bn[t] = (uint32_t) k;
+  }
+}
+
+// the tile's X (rows t0 .. t0 + LI_T, 0 past row N), PL and boundary chain
+// into LDS
+template <typename RowT, int STAGE>
+__device__ __forceinline__ void li_tile_load(const uint32_t *X, const RowT *PL, const RowT *brow,
+                                             const uint32_t *bx, const uint32_t *bn, uint64_t N,
+                                             uint64_t t, LiWalkTile<RowT, STAGE> &S) {
+  const uint64_t t0 = t * LI_T;
+  for (int k = threadIdx.x; k <= LI_T; k += LI_TPB) {
+    const uint64_t g = t0 + (uint64_t) k;
+    S.x[k] = g <= N ? X[g] : 0u;
+    if (k < LI_T) S.pl[k] = g < N ? PL[g] : li_none<RowT>();
+  }
+  const int nb = (int) bn[t];
+  if (threadIdx.x < (unsigned) nb) {
+    S.brow[threadIdx.x] = brow[t * LI_BD + threadIdx.x];
+    S.bx[threadIdx.x] = bx[t * LI_BD + threadIdx.x];
+  }
+  if (threadIdx.x == 0) S.nb = nb;
+  __syncthreads();
+}
+
+// a row before the tile: its index in the boundary chain, -1 past the
+// entries held (binary search, rows strictly decreasing)
+template <typename RowT, int STAGE>
+__device__ __forceinline__ int li_bfind(const LiWalkTile<RowT, STAGE> &S, uint64_t c) {
+  int lo = 0, hi = S.nb - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint64_t r = (uint64_t) S.brow[mid];
+    if (r == c) return mid;
+    if (r > c) lo = mid + 1; else hi = mid - 1;
+  }
+  return -1;
+}
+
+// Rows deeper down the boundary chain than the LDS copy holds (rare) are
+// read by calls: inlined, the compiler would wait for every memory
+// operation of the wave (vmcnt counts the stage's 16-byte stores too) at
+// each join after the branch, taken or not -- the walks would pay the
+// store latency on every step
+// (counted: how often the LDS copy of the chain falls short, a diagnostic
+// read by gt_lcpitv_far_reads)
+__device__ unsigned long long li_far_reads;
+
+__device__ __noinline__ uint32_t li_x_far(const uint32_t *X, uint64_t c) {
+  atomicAdd(&li_far_reads, 1ull);
+  return X[c];
 }
 
 template <typename RowT>
-__device__ __forceinline__ uint64_t li_tpl(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0,
-                                           uint64_t c, uint32_t xc) {
-  return c >= t0 ? (uint64_t) S.pl[c - t0] : li_prev(L, c, xc, true);
+__device__ __noinline__ uint64_t li_pl_far(const RowT *PL, uint64_t c) {
+  atomicAdd(&li_far_reads, 1ull);
+  return (uint64_t) PL[c];
+}
+
+// X and PL of any row at or before the tile's end: the tile's and the
+// boundary chain's from LDS, rows deeper down the chain from HBM
+template <typename RowT, int STAGE>
+__device__ __forceinline__ uint32_t li_tx(const uint32_t *X, const LiWalkTile<RowT, STAGE> &S,
+                                          uint64_t t0, uint64_t c) {
+  if (c >= t0) return S.x[c - t0];
+  const int k = li_bfind(S, c);
+  return k >= 0 ? S.bx[k] : li_x_far(X, c);
+}
+
+template <typename RowT, int STAGE>
+__device__ __forceinline__ uint64_t li_tpl(const RowT *PL, const LiWalkTile<RowT, STAGE> &S,
+                                           uint64_t t0, uint64_t c) {
+  if (c >= t0) return (uint64_t) S.pl[c - t0];
+  const int k = li_bfind(S, c);
+  return k >= 0 && k + 1 < S.nb ? (uint64_t) S.brow[k + 1] : li_pl_far(PL, c);
 }
 
 // intervals popped at row t0 + i
-template <typename RowT>
-__device__ __forceinline__ uint32_t li_pops(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0,
-                                            int i) {
+template <typename RowT, int STAGE>
+__device__ __forceinline__ uint32_t li_pops(const uint32_t *X, const RowT *PL,
+                                            const LiWalkTile<RowT, STAGE> &S, uint64_t t0, int i) {
   const uint32_t Y = S.x[i + 1];
   uint64_t c = t0 + (uint64_t) i;
   uint32_t xc = S.x[i], n = 0;
   while (xc > Y) {
     n++;
-    c = li_tpl(L, S, t0, c, xc);
-    xc = li_tx(L, S, t0, c);
+    c = li_tpl(PL, S, t0, c);
+    xc = li_tx(X, S, t0, c);
   }
   return n;
 }
 
 // the pops of row idx = t0 + i in order, deepest first: f(j, lcp, lb, fd, flb, newfather)
-template <typename RowT, typename F>
-__device__ __forceinline__ void li_walk(const LiLevels &L, const LiTile<RowT> &S, uint64_t t0, int i,
-                                        F f) {
+template <typename RowT, int STAGE, typename F>
+__device__ __forceinline__ void li_walk(const uint32_t *X, const RowT *PL,
+                                        const LiWalkTile<RowT, STAGE> &S, uint64_t t0, int i, F f) {
   const uint32_t Y = S.x[i + 1];
   uint32_t xc = S.x[i];
   if (xc <= Y) return;
-  uint64_t nx = li_tpl(L, S, t0, t0 + (uint64_t) i, xc);
-  uint32_t xn = li_tx(L, S, t0, nx);
+  uint64_t nx = S.pl[i];
+  uint32_t xn = li_tx(X, S, t0, nx);
   for (uint32_t j = 0;; j++) {
     const uint32_t fd = xn > Y ? xn : Y;
     uint64_t nn = 0, flb = 0;
     if (xn >= Y && fd > 0) {
-      nn = li_tpl(L, S, t0, nx, xn);
+      nn = li_tpl(PL, S, t0, nx);
       flb = nn;
     } else if (fd > 0) {
       flb = nx;                          // the new father (Y, nx)
@@ -339,78 +446,136 @@ __device__ __forceinline__ void li_walk(const LiLevels &L, const LiTile<RowT> &S
     if (xn <= Y) break;
     xc = xn;
     nx = nn;
-    xn = li_tx(L, S, t0, nx);
+    xn = li_tx(X, S, t0, nx);
   }
 }
 
 // pass 1 (plan): intervals popped in each tile
 template <typename RowT>
-__global__ void __launch_bounds__(LI_TPB) li_tile_count_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
-                                                               uint32_t *tile_cnt) {
-  __shared__ LiTile<RowT> S;
+__global__ void __launch_bounds__(LI_TPB) li_tile_count_kernel(const uint32_t *X, const RowT *PL,
+                                                               const RowT *brow, const uint32_t *bx,
+                                                               const uint32_t *bn, uint64_t N,
+                                                               uint64_t ntiles, uint32_t *tile_cnt) {
+  __shared__ LiWalkTile<RowT, 16> S;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t t0 = t * LI_T;
-    li_tile_ansv(L, N, t0, S);
+    li_tile_load(X, PL, brow, bx, bn, N, t, S);
     const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
     uint32_t n = 0;
-    for (int i = threadIdx.x; i < nrows; i += LI_TPB) n += li_pops(L, S, t0, i);
+    for (int i = threadIdx.x; i < nrows; i += LI_TPB) n += li_pops(X, PL, S, t0, i);
     uint32_t tot;
     (void) li_block_excl(n, &tot);
     if (threadIdx.x == 0) tile_cnt[t] = tot;
   }
 }
 
+// The writing passes split a tile into four 512-row quarters, one per
+// wave: the waves' interval totals are exchanged once per tile (the only
+// workgroup barriers besides the tile load), then each wave walks its
+// quarter in 64-row steps on its own -- wave-level scans for the offsets,
+// its own part of the stage, its own 16-byte stores.
+#define LI_WAVES (LI_TPB / 64)
+#define LI_QROWS (LI_T / LI_WAVES)
+
+__device__ __forceinline__ uint32_t li_wave_excl(uint32_t v, uint32_t *total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  *total = __shfl(incl, 63, 64);
+  return incl - v;
+}
+
+// the wave's LDS stores before its loads (and its loads before the next
+// stores): LDS operations of one wave complete in order once waited for
+__device__ __forceinline__ void li_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// intervals popped before each wave's quarter, from tile_off[t]; ends with
+// a barrier
+template <typename RowT, int STAGE, typename Weight>
+__device__ __forceinline__ uint64_t li_wave_base(const uint32_t *X, const RowT *PL,
+                                                 const LiWalkTile<RowT, STAGE> &S, uint64_t t0,
+                                                 int nrows, uint64_t tile_base, uint32_t *sWT) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t n = 0;
+  for (int r = 0; r < LI_QROWS / 64; r++) {
+    const int i = wave * LI_QROWS + r * 64 + lane;
+    if (i < nrows) n += li_pops(X, PL, S, t0, i);
+  }
+  uint32_t tot;
+  (void) li_wave_excl(n, &tot);
+  if (lane == 0) sWT[wave] = tot;
+  __syncthreads();
+  uint64_t base = tile_base;
+  for (int w = 0; w < wave; w++) base += sWT[w];
+  return base;
+}
+
 // pass 2 (plan): the interval records (lcp, lb, rb, father lcp, father lb)
-// in pop order at tile_off[t] on (staged per 256-row chunk, stored as
+// in pop order at tile_off[t] on (staged per 64-row step, stored as
 // contiguous 16-byte pieces), and the stream position of the first edge to
 // the root (the reference's firstedgefromroot, esa-bottomup.c:134-141)
+#define LI_ITV_WCAP (LI_ITV_CAP / LI_WAVES)   // records staged per wave step
 template <typename RowT>
-__global__ void __launch_bounds__(LI_TPB) li_tile_itv_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
-                                                             const uint64_t *tile_off, uint64_t *itv,
-                                                             unsigned long long *first) {
-  __shared__ LiTile<RowT> S;
+__global__ void __launch_bounds__(LI_TPB) li_tile_itv_kernel(const uint32_t *X, const RowT *PL,
+                                                             const RowT *brow, const uint32_t *bx,
+                                                             const uint32_t *bn, uint64_t N,
+                                                             uint64_t ntiles, const uint64_t *tile_off,
+                                                             uint64_t *itv, unsigned long long *first) {
+  __shared__ LiWalkTile<RowT, 40 * LI_ITV_CAP> S;
+  __shared__ uint32_t sWT[LI_WAVES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t *stage = reinterpret_cast<uint64_t *>(S.stage) + 5 * LI_ITV_WCAP * wave;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t t0 = t * LI_T;
-    li_tile_ansv(L, N, t0, S);
+    li_tile_load(X, PL, brow, bx, bn, N, t, S);
     const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
-    uint64_t base = tile_off[t];         // intervals popped before this chunk
-    for (int c0 = 0; c0 < nrows; c0 += LI_TPB) {
-      const int i = c0 + (int) threadIdx.x;
+    uint64_t base = li_wave_base<RowT, 40 * LI_ITV_CAP, int>(X, PL, S, t0, nrows, tile_off[t], sWT);
+    for (int r = 0; r < LI_QROWS / 64; r++) {
+      const int i = wave * LI_QROWS + r * 64 + lane;
       const bool row = i < nrows;
-      const uint32_t n = row ? li_pops(L, S, t0, i) : 0u;
+      const uint32_t n = row ? li_pops(X, PL, S, t0, i) : 0u;
       uint32_t tot;
-      const uint32_t off = li_block_excl(n, &tot);
+      const uint32_t off = li_wave_excl(n, &tot);
       if (row) {
         const uint64_t idx = t0 + (uint64_t) i;
         const uint64_t pos = idx + 2 * (base + off);       // the row's leaf event
         if (S.x[i] == 0 && S.x[i + 1] == 0) atomicMin(first, (unsigned long long) pos);
-        li_walk(L, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t fd, uint64_t flb,
-                                 bool) {
+        li_walk(X, PL, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t fd, uint64_t flb,
+                                     bool) {
           const uint32_t k = off + j;
-          uint64_t *r = k < LI_ITV_CAP ? S.st.itv + 5 * k : itv + 5 * (base + k);
-          r[0] = lcp;
-          r[1] = lb;
-          r[2] = idx;
-          r[3] = fd;
-          r[4] = flb;
+          uint64_t *w = k < LI_ITV_WCAP ? stage + 5 * k : itv + 5 * (base + k);
+          w[0] = lcp;
+          w[1] = lb;
+          w[2] = idx;
+          w[3] = fd;
+          w[4] = flb;
           if (fd == 0) atomicMin(first, (unsigned long long) (pos + 2 + 2 * j));
         });
       }
-      __syncthreads();
-      const uint32_t staged = tot < LI_ITV_CAP ? tot : LI_ITV_CAP;
+      li_wave_sync();
+      const uint32_t staged = tot < LI_ITV_WCAP ? tot : LI_ITV_WCAP;
       // words [5 base, 5 (base + staged)) as aligned 16-byte pairs
       const uint64_t w0 = 5 * base, w1 = 5 * (base + staged);
-      for (uint64_t q = (w0 >> 1) + threadIdx.x; 2 * q < w1; q += LI_TPB) {
+      for (uint64_t q = (w0 >> 1) + lane; 2 * q < w1; q += 64) {
         const uint64_t a = 2 * q;
         const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
-        const uint64_t v0 = lo_ok ? S.st.itv[a - w0] : 0, v1 = hi_ok ? S.st.itv[a + 1 - w0] : 0;
+        const uint64_t v0 = lo_ok ? stage[a - w0] : 0, v1 = hi_ok ? stage[a + 1 - w0] : 0;
         if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(itv)[q] = make_ulonglong2(v0, v1);
         else if (lo_ok) itv[a] = v0;
-        else itv[a + 1] = v1;
+        else if (hi_ok) itv[a + 1] = v1;   // (neither: an empty step at an odd word)
       }
-      __syncthreads();
+      li_wave_sync();
       base += tot;
     }
+    __syncthreads();                     // S and sWT are rewritten by the next tile
   }
 }
 
@@ -420,75 +585,98 @@ __global__ void __launch_bounds__(LI_TPB) li_tile_itv_kernel(LiLevels L, uint64_
 //   (0, firstsucc, fd, flb, leafnumber, 0, 0)   visit_leaf_edge
 //   (2, 0, lcp, lb, rb, 0, 0)                   visit_lcp_interval
 //   (1, firstsucc, fd, flb, sd, slb, srb)       visit_branching_edge
-// staged per 256-row chunk as 4-word descriptors (the branching edge takes
-// sd, slb, srb from the lcp-interval event before it) and stored as aligned
-// 16-byte pieces of the 7-word records; events past the stage go straight
-// to memory
-template <typename RowT, typename SufT>
-__device__ __forceinline__ uint64_t li_event_word(const LiTile<RowT> &S, uint32_t e, uint32_t f,
-                                                  const SufT *suf) {
-  const LiDesc<RowT> d = S.st.ev[e];
+// staged per 64-row wave step as 4-word descriptors (a leaf's holds its
+// leaf number, read while walking; the branching edge takes sd, slb, srb
+// from the lcp-interval event before it) and stored as aligned 16-byte
+// pieces of the 7-word records; events past the stage go straight to memory
+template <typename DT>
+struct LiDesc {                         // one staged event
+  DT a, b, c, d;                        // a: kind | firstsucc << 2
+};
+
+template <typename DT>
+__device__ __forceinline__ uint64_t li_event_word(const LiDesc<DT> *st, uint32_t e, uint32_t f) {
+  const LiDesc<DT> d = st[e];
   const uint32_t kind = (uint32_t) d.a & 3u;
   if (f == 0) return kind;
   if (f == 1) return kind == 2u ? 0u : (uint64_t) (d.a >> 2);
   if (f == 2) return d.b;
   if (f == 3) return d.c;
   if (kind == 1u) {                      // sd, slb, srb: the lcp-interval event before
-    const LiDesc<RowT> p = S.st.ev[e - 1];
+    const LiDesc<DT> p = st[e - 1];
     return f == 4 ? (uint64_t) p.b : f == 5 ? (uint64_t) p.c : (uint64_t) p.d;
   }
-  if (f == 4) return kind == 2u ? (uint64_t) d.d : (suf != nullptr ? (uint64_t) suf[d.d] : 0u);
-  return 0;
+  return f == 4 ? (uint64_t) d.d : 0u;   // leaf number / rb
 }
 
 template <typename RowT, typename SufT>
-__global__ void __launch_bounds__(LI_TPB) li_tile_events_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
+__global__ void __launch_bounds__(LI_TPB) li_tile_events_kernel(const uint32_t *X, const RowT *PL,
+                                                                const RowT *brow, const uint32_t *bx,
+                                                                const uint32_t *bn, uint64_t N,
+                                                                uint64_t ntiles,
                                                                 const uint64_t *tile_off,
                                                                 const SufT *suf,
                                                                 const unsigned long long *firstp,
                                                                 uint64_t *ev) {
-  __shared__ LiTile<RowT> S;
-  constexpr uint32_t cap = LI_EV_STAGE / sizeof (LiDesc<RowT>);
+  // descriptor words wide enough for row indices and leaf numbers
+  using DT = typename std::conditional<(sizeof (RowT) >= sizeof (SufT)), RowT, SufT>::type;
+  __shared__ LiWalkTile<RowT, LI_EV_STAGE> S;
+  __shared__ uint32_t sWT[LI_WAVES];
+  constexpr uint32_t cap = LI_EV_STAGE / sizeof (LiDesc<DT>) / LI_WAVES;   // per wave step
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  LiDesc<DT> *stage = reinterpret_cast<LiDesc<DT> *>(S.stage) + cap * wave;
   const uint64_t first = *firstp;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t t0 = t * LI_T;
-    li_tile_ansv(L, N, t0, S);
+    li_tile_load(X, PL, brow, bx, bn, N, t, S);
     const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
-    uint64_t ebase = t0 + 2 * tile_off[t];   // stream position of the chunk's first event
-    for (int c0 = 0; c0 < nrows; c0 += LI_TPB) {
-      const int i = c0 + (int) threadIdx.x;
+    // stream position of the wave's next event: the rows before it and two
+    // events per interval popped before it
+    const uint64_t ib = li_wave_base<RowT, LI_EV_STAGE, int>(X, PL, S, t0, nrows, tile_off[t], sWT);
+    uint64_t ebase = t0 + (uint64_t) (wave * LI_QROWS) + 2 * ib;
+    // the leaf numbers of the wave's rows, loaded before its first store (a
+    // load inside the steps would wait for the stores before it)
+    uint64_t leaves[LI_QROWS / 64];
+#pragma unroll
+    for (int r = 0; r < LI_QROWS / 64; r++) {
+      const int i = wave * LI_QROWS + r * 64 + lane;
+      leaves[r] = i < nrows && suf != nullptr ? (uint64_t) suf[t0 + (uint64_t) i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < LI_QROWS / 64; r++) {
+      const int i = wave * LI_QROWS + r * 64 + lane;
       const bool row = i < nrows;
-      const uint32_t n = row ? li_pops(L, S, t0, i) : 0u;
+      const uint64_t idx = t0 + (uint64_t) i;
+      const uint64_t leaf = leaves[r];
+      const uint32_t n = row ? li_pops(X, PL, S, t0, i) : 0u;
       uint32_t tot;
-      const uint32_t off = li_block_excl(row ? 1u + 2u * n : 0u, &tot);
+      const uint32_t off = li_wave_excl(row ? 1u + 2u * n : 0u, &tot);
       if (row) {
-        const uint64_t idx = t0 + (uint64_t) i;
-        const uint32_t X = S.x[i], Y = S.x[i + 1];
+        const uint32_t xi = S.x[i], Y = S.x[i + 1];
         const uint64_t pos = ebase + off;
         uint64_t fs, fd, flb;
-        if (Y <= X) {
-          fs = (X == 0 && pos == first) ? 1u : 0u;
-          fd = X;
-          flb = X == 0 ? 0 : (uint64_t) S.pl[i];
+        if (Y <= xi) {
+          fs = (xi == 0 && pos == first) ? 1u : 0u;
+          fd = xi;
+          flb = xi == 0 ? 0 : (uint64_t) S.pl[i];
         } else {
           fs = 1;
           fd = Y;
           flb = idx;
         }
         if (off < cap) {
-          S.st.ev[off] = LiDesc<RowT>{(RowT) (fs << 2), (RowT) fd, (RowT) flb, (RowT) idx};
+          stage[off] = LiDesc<DT>{(DT) (fs << 2), (DT) fd, (DT) flb, (DT) leaf};
         } else {
           uint64_t *w = ev + 7 * pos;
-          w[0] = 0; w[1] = fs; w[2] = fd; w[3] = flb;
-          w[4] = suf != nullptr ? (uint64_t) suf[idx] : 0u; w[5] = 0; w[6] = 0;
+          w[0] = 0; w[1] = fs; w[2] = fd; w[3] = flb; w[4] = leaf; w[5] = 0; w[6] = 0;
         }
-        li_walk(L, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t pfd, uint64_t pflb,
-                                 bool newfather) {
+        li_walk(X, PL, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t pfd,
+                                     uint64_t pflb, bool newfather) {
           const uint32_t k = off + 1 + 2 * j;
           const uint64_t bfs = newfather ? 1u : (pfd == 0 && pos + 2 + 2 * j == first) ? 1u : 0u;
-          if (k < cap) S.st.ev[k] = LiDesc<RowT>{(RowT) 2, (RowT) lcp, (RowT) lb, (RowT) idx};
+          if (k < cap) stage[k] = LiDesc<DT>{(DT) 2, (DT) lcp, (DT) lb, (DT) idx};
           if (k + 1 < cap) {
-            S.st.ev[k + 1] = LiDesc<RowT>{(RowT) (1u | (bfs << 2)), (RowT) pfd, (RowT) pflb, (RowT) 0};
+            stage[k + 1] = LiDesc<DT>{(DT) (1u | (bfs << 2)), (DT) pfd, (DT) pflb, (DT) 0};
           } else {
             uint64_t *w = ev + 7 * (ebase + k);
             if (k >= cap) { w[0] = 2; w[1] = 0; w[2] = lcp; w[3] = lb; w[4] = idx; w[5] = 0; w[6] = 0; }
@@ -496,28 +684,29 @@ __global__ void __launch_bounds__(LI_TPB) li_tile_events_kernel(LiLevels L, uint
           }
         });
       }
-      __syncthreads();
+      li_wave_sync();
       const uint32_t staged = tot < cap ? tot : cap;
       const uint64_t w0 = 7 * ebase, w1 = 7 * (ebase + staged);
-      for (uint64_t q = (w0 >> 1) + threadIdx.x; 2 * q < w1; q += LI_TPB) {
+      for (uint64_t q = (w0 >> 1) + lane; 2 * q < w1; q += 64) {
         const uint64_t a = 2 * q;
         const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
         uint64_t v0 = 0, v1 = 0;
         if (lo_ok) {
-          const uint32_t r = (uint32_t) (a - w0);
-          v0 = li_event_word<RowT, SufT>(S, r / 7, r % 7, suf);
+          const uint32_t e = (uint32_t) (a - w0);
+          v0 = li_event_word(stage, e / 7, e % 7);
         }
         if (hi_ok) {
-          const uint32_t r = (uint32_t) (a + 1 - w0);
-          v1 = li_event_word<RowT, SufT>(S, r / 7, r % 7, suf);
+          const uint32_t e = (uint32_t) (a + 1 - w0);
+          v1 = li_event_word(stage, e / 7, e % 7);
         }
         if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(ev)[q] = make_ulonglong2(v0, v1);
         else if (lo_ok) ev[a] = v0;
-        else ev[a + 1] = v1;
+        else if (hi_ok) ev[a + 1] = v1;
       }
-      __syncthreads();
+      li_wave_sync();
       ebase += tot;
     }
+    __syncthreads();                     // S and sWT are rewritten by the next tile
   }
 }
 
@@ -545,6 +734,9 @@ struct GtLcpitvPlan {
   uint64_t nitv;
   uint64_t *itv;                 // 5 * nitv, pop order
   uint64_t *tile_off;            // intervals popped before each tile
+  void *pl;                      // PL of every row (RowT: u32, u64 when wide)
+  void *brow;                    // boundary chain of every tile (LI_BD RowT each)
+  uint32_t *bx, *bn;             // its X values, its length
   unsigned long long *first;     // stream position of the first root edge
   SmaxStreamMarks marks;         // streams the plan's work ran on
 };
@@ -559,6 +751,10 @@ extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
   for (int l = 0; l < LI_MAXLEV; l++) smax_dev_free_fenced(p->lev[l], fence);
   smax_dev_free_fenced(p->itv, fence);
   smax_dev_free_fenced(p->tile_off, fence);
+  smax_dev_free_fenced(p->pl, fence);
+  smax_dev_free_fenced(p->brow, fence);
+  smax_dev_free_fenced(p->bx, fence);
+  smax_dev_free_fenced(p->bn, fence);
   smax_dev_free_fenced(p->first, fence);
   smax_fence_release(fence);
   free(p);
@@ -627,17 +823,41 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     goto fail;
   }
   for (int l = 0; l < p->L.nlev; l++) p->L.lv[l] = p->lev[l];
-  // pops per tile, their exclusive scan, the records
+  // PL per row, pops per tile, their exclusive scan, the records
+  LICHK(smax_dev_alloc(&p->pl, (p->wide ? 8 : 4) * (N ? N : 1)));
+  if (p->ntiles > 0) {
+    if (p->wide)
+      hipLaunchKernelGGL(li_pl_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->L, N,
+                         p->ntiles, (uint64_t *) p->pl);
+    else
+      hipLaunchKernelGGL(li_pl_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->L, N,
+                         p->ntiles, (uint32_t *) p->pl);
+    LICHK(hipGetLastError());
+  }
+  LICHK(smax_dev_alloc(&p->brow, (p->wide ? 8 : 4) * LI_BD * (p->ntiles ? p->ntiles : 1)));
+  LICHK(smax_dev_alloc((void **) &p->bx, 4 * LI_BD * (p->ntiles ? p->ntiles : 1)));
+  LICHK(smax_dev_alloc((void **) &p->bn, 4 * (p->ntiles ? p->ntiles : 1)));
+  if (p->ntiles > 0) {
+    if (p->wide)
+      hipLaunchKernelGGL(li_bchain_kernel<uint64_t>, dim3(li_blocks(p->ntiles)), dim3(256), 0, s,
+                         p->lev[0], (const uint64_t *) p->pl, p->ntiles, (uint64_t *) p->brow, p->bx,
+                         p->bn);
+    else
+      hipLaunchKernelGGL(li_bchain_kernel<uint32_t>, dim3(li_blocks(p->ntiles)), dim3(256), 0, s,
+                         p->lev[0], (const uint32_t *) p->pl, p->ntiles, (uint32_t *) p->brow, p->bx,
+                         p->bn);
+    LICHK(hipGetLastError());
+  }
   LICHK(smax_dev_alloc((void **) &tile_cnt, sizeof (uint32_t) * (p->ntiles + 1)));
   LICHK(smax_dev_alloc((void **) &p->tile_off, sizeof (uint64_t) * (p->ntiles + 1)));
   LICHK(hipMemsetAsync(tile_cnt + p->ntiles, 0, sizeof (uint32_t), s));
   if (p->ntiles > 0) {
     if (p->wide)
       hipLaunchKernelGGL(li_tile_count_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0,
-                         s, p->L, N, p->ntiles, tile_cnt);
+                         s, p->lev[0], (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, tile_cnt);
     else
       hipLaunchKernelGGL(li_tile_count_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0,
-                         s, p->L, N, p->ntiles, tile_cnt);
+                         s, p->lev[0], (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, tile_cnt);
     LICHK(hipGetLastError());
   }
   LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, tile_cnt, p->tile_off, (uint64_t) 0,
@@ -654,10 +874,10 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   if (p->ntiles > 0) {
     if (p->wide)
       hipLaunchKernelGGL(li_tile_itv_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s,
-                         p->L, N, p->ntiles, p->tile_off, p->itv, p->first);
+                         p->lev[0], (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, p->itv, p->first);
     else
       hipLaunchKernelGGL(li_tile_itv_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s,
-                         p->L, N, p->ntiles, p->tile_off, p->itv, p->first);
+                         p->lev[0], (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, p->itv, p->first);
     LICHK(hipGetLastError());
   }
   smax_marks_record(&p->marks, s);
@@ -721,21 +941,29 @@ extern "C" int gt_lcpitv_plan_events(GtLcpitvPlan *p, uint64_t *events_dev, void
   const uint64_t *suf8 = !s4 ? (const uint64_t *) p->in.suf_dev : nullptr;
   if (p->wide) {
     if (s4)
-      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint32_t>), g, b, 0, s, p->L, N, p->ntiles,
-                         p->tile_off, suf4, p->first, events_dev);
+      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint32_t>), g, b, 0, s, p->lev[0],
+                         (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf4, p->first, events_dev);
     else
-      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint64_t>), g, b, 0, s, p->L, N, p->ntiles,
-                         p->tile_off, suf8, p->first, events_dev);
+      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint64_t>), g, b, 0, s, p->lev[0],
+                         (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf8, p->first, events_dev);
   } else {
     if (s4)
-      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint32_t>), g, b, 0, s, p->L, N, p->ntiles,
-                         p->tile_off, suf4, p->first, events_dev);
+      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint32_t>), g, b, 0, s, p->lev[0],
+                         (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf4, p->first, events_dev);
     else
-      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint64_t>), g, b, 0, s, p->L, N, p->ntiles,
-                         p->tile_off, suf8, p->first, events_dev);
+      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint64_t>), g, b, 0, s, p->lev[0],
+                         (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf8, p->first, events_dev);
   }
   smax_marks_record(&p->marks, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// diagnostic: far reads since the last call (current device), -1 on error
+extern "C" long long gt_lcpitv_far_reads(void) {
+  unsigned long long v = 0, z = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(li_far_reads), sizeof v) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(li_far_reads), &z, sizeof z) != hipSuccess) return -1;
+  return (long long) v;
 }
 
 // ------------------------------------------------------------ host boundary

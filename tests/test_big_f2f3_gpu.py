@@ -98,7 +98,11 @@ def test_lcpitv_intervals_past_2_32(tables):
     got = _u64_view(ptr, 5 * n).cpu().numpy().view(np.uint64).reshape(-1, 5)
     plan.close()
     del lcp_t, llv_t
-    assert np.array_equal(got, want)
+    if not np.array_equal(got, want):
+        k = int(np.flatnonzero((got != want).any(axis=1))[0])
+        raise AssertionError("first differing record %d: got %s want %s (rows %s)"
+                             % (k, got[k].tolist(), want[k].tolist(),
+                                lcp[int(want[k][1]):int(want[k][2]) + 2].tolist()))
 
 
 def test_maxpairs_past_2_32(tables):

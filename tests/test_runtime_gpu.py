@@ -364,6 +364,31 @@ def test_close_in_flight_then_reuse(human10):
         small.release()
 
 
+def test_stream_destroyed_before_plan_delete(human10):
+    """The caller's stream may be gone before gt_smax_plan_delete: the plan
+    waits and fences by the events it recorded when it enqueued the work,
+    never by the stream handle (gt_smax_hip.h, gt_smax_plan_delete)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    esa, host = human10
+    want = O.linsmax(host["lcptab"], host["llvtab"], host["bwttab"], esa.nonspecials, 20)
+    for _ in range(2):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        p = esa.plan(20)
+        for _ in range(3):
+            p.run(s.value)
+        got = p.fetch_triples()          # waits on the plan's events
+        p.run(s.value)
+        assert hip.hipStreamDestroy(s) == 0
+        p.close()                        # fence from the recorded events
+        assert np.array_equal(got, want)
+        q = esa.plan(20)
+        q.run()
+        assert np.array_equal(q.fetch_triples(), want)
+        q.close()
+
+
 @pytest.mark.skipif(G.device_count() < 2, reason="needs >= 2 visible GPUs")
 @pytest.mark.parametrize("shards", [2, 3, 8])
 def test_host_entry_across_devices(human10, shards):

@@ -185,6 +185,21 @@ for S in "$@"; do
       python3 tools/rocpd_summary.py pmcall "$O/${K}_$T.json" "$T" "$O/${K}_${T}_FETCH_SIZE/p_results.db" \
         "$O/${K}_${T}_WRITE_SIZE/p_results.db"
       rm -rf "$O/${K}_${T}_FETCH_SIZE" "$O/${K}_${T}_WRITE_SIZE" ;;
+    f3sq:*)
+      # f3sq:CONFIG[:BASES] -- SQ instruction / wait / LDS counters of every F3 kernel (two passes)
+      IFS=: read -r _ C BASES <<< "$S"
+      T=$C${BASES:+_$BASES}
+      SQA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
+      SQB="SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
+      for X in A B; do
+        if [ $X = A ]; then CS=$SQA; else CS=$SQB; fi
+        (cd /tmp && TMPDIR=/tmp timeout -s KILL 300 rocprofv3 --pmc $CS --kernel-include-regex 'li_' \
+          -d "$O/f3sq_${T}_$X" -o p -- python3 "$R/bench.py" --path lcpitv --config "$C" ${BASES:+--bases $BASES} \
+          --no-cpu-baseline --steps 2 --warmup 1 --prime-s 0 > "$O/f3sq_${T}_$X.log" 2>&1)
+      done
+      python3 tools/rocpd_summary.py pmcall "$O/f3sq_$T.json" "$T" "$O/f3sq_${T}_A/p_results.db" \
+        "$O/f3sq_${T}_B/p_results.db"
+      rm -rf "$O/f3sq_${T}_A" "$O/f3sq_${T}_B" ;;
     f3:*)
       # f3:CONFIG[:BASES] -- the F3 leg, bench.py --path lcpitv (intervals + visitor events)
       IFS=: read -r _ C BASES <<< "$S"

@@ -105,6 +105,9 @@ def pmcall(out, config, dbs):
             d["write_bytes_per_launch"] = 1024 * sum(x for x, _ in v) / len(v)
         if "read_bytes_per_launch" in d and "write_bytes_per_launch" in d:
             d["hbm_bytes_per_launch"] = d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
+        for cname, v in cs.items():            # every other counter, per launch
+            if cname not in ("FETCH_SIZE", "WRITE_SIZE"):
+                d[cname] = sum(x for x, _ in v) / len(v)
         res["kernels"][short] = d
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
