@@ -222,6 +222,8 @@ def lib():
                                                           ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
         L.gt_maxpairs_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtMaxpairsDevInput),
                                               u32, cs, sz]
+        L.gt_maxpairs_plan_create_stream.argtypes = [ctypes.POINTER(vp),
+                                                     ctypes.POINTER(GtMaxpairsDevInput), u32, vp, cs, sz]
         L.gt_maxpairs_plan_delete.argtypes = [vp]
         L.gt_maxpairs_plan_count.argtypes = [vp, vp]
         L.gt_maxpairs_plan_total.argtypes = [vp, ctypes.POINTER(u64)]
@@ -237,6 +239,8 @@ def lib():
         L.gt_lcpitv_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput),
                                                         ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
         L.gt_lcpitv_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtLcpitvDevInput), cs, sz]
+        L.gt_lcpitv_plan_create_stream.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtLcpitvDevInput),
+                                                   vp, cs, sz]
         L.gt_lcpitv_plan_delete.argtypes = [vp]
         L.gt_lcpitv_plan_intervals.argtypes = [vp, ctypes.POINTER(vp)]
         L.gt_lcpitv_plan_intervals.restype = u64
@@ -499,14 +503,22 @@ class LcpitvPlan:
     """Device-resident lcp-interval tree and visitor event stream
     (gt_lcpitv_plan_*)."""
 
-    def __init__(self, lcp_ptr, llv_ptr, numllv, suf_ptr, suf_bytes, nonspecials, device=0):
+    def __init__(self, lcp_ptr, llv_ptr, numllv, suf_ptr, suf_bytes, nonspecials, device=0,
+                 stream=None):
+        """stream=None: gt_lcpitv_plan_create (synchronous); else the tree is
+        built on that stream (gt_lcpitv_plan_create_stream)."""
         inp = GtLcpitvDevInput()
         inp.lcp_dev, inp.llv_dev, inp.numllv = lcp_ptr, llv_ptr, numllv
         inp.suf_dev, inp.suf_bytes = suf_ptr, suf_bytes
         inp.nonspecials, inp.device = nonspecials, device
         self._p = ctypes.c_void_p()
         eb = _errbuf()
-        _check(lib().gt_lcpitv_plan_create(ctypes.byref(self._p), ctypes.byref(inp), eb, len(eb)), eb)
+        if stream is None:
+            rc = lib().gt_lcpitv_plan_create(ctypes.byref(self._p), ctypes.byref(inp), eb, len(eb))
+        else:
+            rc = lib().gt_lcpitv_plan_create_stream(ctypes.byref(self._p), ctypes.byref(inp), stream,
+                                                    eb, len(eb))
+        _check(rc, eb)
         self.device = device
 
     def intervals(self):
@@ -538,15 +550,21 @@ class MaxpairsPlan:
     """Device-resident maximal pairs over HBM tables (gt_maxpairs_plan_*)."""
 
     def __init__(self, lcp_ptr, bwt_ptr, llv_ptr, numllv, suf_ptr, suf_bytes, nonspecials, minlen,
-                 device=0):
+                 device=0, stream=None):
+        """stream: build on that stream (gt_maxpairs_plan_create_stream)."""
         inp = GtMaxpairsDevInput()
         inp.lcp_dev, inp.bwt_dev, inp.llv_dev = lcp_ptr, bwt_ptr, llv_ptr
         inp.numllv, inp.suf_dev, inp.suf_bytes = numllv, suf_ptr, suf_bytes
         inp.nonspecials, inp.device = nonspecials, device
         self._p = ctypes.c_void_p()
         eb = _errbuf()
-        _check(lib().gt_maxpairs_plan_create(ctypes.byref(self._p), ctypes.byref(inp), int(minlen),
-                                             eb, len(eb)), eb)
+        if stream is None:
+            rc = lib().gt_maxpairs_plan_create(ctypes.byref(self._p), ctypes.byref(inp), int(minlen),
+                                               eb, len(eb))
+        else:
+            rc = lib().gt_maxpairs_plan_create_stream(ctypes.byref(self._p), ctypes.byref(inp),
+                                                      int(minlen), stream, eb, len(eb))
+        _check(rc, eb)
         self.device = device
 
     def count(self, stream=0):
@@ -1024,17 +1042,17 @@ class DeviceEsa:
                                                       eb, len(eb)), eb)
         return out
 
-    def maxpairs_plan(self, minlen):
+    def maxpairs_plan(self, minlen, stream=None):
         """Maximal pairs over the device tables (needs keep_suftab=True)."""
         if not self.esa.suftab_dev:
             raise SmaxError("maxpairs needs the suffix array: build with keep_suftab=True")
         return MaxpairsPlan(self.esa.lcptab_dev, self.esa.bwttab_dev, self.esa.llvtab_dev, self.numllv,
-                            self.esa.suftab_dev, 4, self.nonspecials, minlen, self.device)
+                            self.esa.suftab_dev, 4, self.nonspecials, minlen, self.device, stream)
 
-    def lcpitv_plan(self):
+    def lcpitv_plan(self, stream=None):
         """lcp-interval tree + visitor events over the device tables."""
         return LcpitvPlan(self.esa.lcptab_dev, self.esa.llvtab_dev, self.numllv,
-                          self.esa.suftab_dev or None, 4, self.nonspecials, self.device)
+                          self.esa.suftab_dev or None, 4, self.nonspecials, self.device, stream)
 
     def release(self):
         if self.esa.lcptab_dev:

@@ -673,6 +673,8 @@ struct GtMaxpairsPlan {
   uint32_t *hier;                // levels >= 1 of the minimum hierarchy (ordered emission)
   MpHier h;
   uint32_t xmax;                 // largest exact LCP value
+  SmaxStreamMarks marks;         // streams the plan's work ran on (waits and the
+                                 // delete-time fence use their events only)
 };
 
 // per-element kernels are grid-stride loops (MP_FOR) over a capped grid: a
@@ -702,16 +704,26 @@ static bool mp_lookback_on() {
 extern "C" void gt_maxpairs_plan_delete(GtMaxpairsPlan *p) {
   if (p == NULL) return;
   (void) hipSetDevice(p->in.device);
+  // the buffers return to the runtime's cache behind the plan's own work
+  // (events recorded where it was enqueued): nothing here waits
   void *bufs[] = {p->X, p->RM, p->RO, p->wg_cand, p->wg_cand_off, p->list, p->cnt, p->off,
                   p->total, p->scan_tmp, p->hier, p->masks, p->st_cnt};
-  for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-    if (bufs[i]) (void) hipFree(bufs[i]);
+  SmaxFence *fence = smax_marks_fence(&p->marks);
+  for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], fence);
+  smax_fence_release(fence);
   free(p);
 }
 
 extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsDevInput *in,
                                        unsigned int minlen, char *errbuf, size_t errlen) {
+  return gt_maxpairs_plan_create_stream(planp, in, minlen, NULL, errbuf, errlen);
+}
+
+extern "C" int gt_maxpairs_plan_create_stream(GtMaxpairsPlan **planp, const GtMaxpairsDevInput *in,
+                                              unsigned int minlen, void *stream, char *errbuf,
+                                              size_t errlen) {
   GtMaxpairsPlan *p = NULL;
+  hipStream_t s = (hipStream_t) stream;
   uint32_t *derr = NULL, herr = 0;
   const uint64_t N = in != NULL ? in->nonspecials : 0;
   *planp = NULL;
@@ -742,59 +754,70 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
   }
   p->in = *in;
   p->minlen = minlen;
+  smax_marks_init(&p->marks);
+  // every buffer from the runtime's caching allocator, every step on s
   MPCHK(hipSetDevice(in->device));
-  MPCHK(hipMalloc(&p->X, sizeof (uint32_t) * (N + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->X, sizeof (uint32_t) * (N + 1)));
   p->nwg = (N + MP_WG_ROWS - 1) / MP_WG_ROWS;
-  MPCHK(hipMalloc(&p->wg_cand, sizeof (uint64_t) * (p->nwg + 1)));
-  MPCHK(hipMalloc(&p->wg_cand_off, sizeof (uint64_t) * (p->nwg + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->wg_cand, sizeof (uint64_t) * (p->nwg + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->wg_cand_off, sizeof (uint64_t) * (p->nwg + 1)));
   // whole groups of MP_WR_GROUP pass-A workgroups; the masks past the last
   // one stay zero
-  MPCHK(hipMalloc(&p->masks, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
-  MPCHK(hipMemset(p->masks, 0, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
-  MPCHK(hipMalloc(&p->total, sizeof (uint64_t)));
-  MPCHK(hipMemset(p->total, 0, sizeof (uint64_t)));
-  MPCHK(hipMalloc(&derr, sizeof (uint32_t)));
-  MPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
-  hipLaunchKernelGGL(mp_expand_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, 0, in->lcp_dev, N,
+  MPCHK(smax_dev_alloc((void **) &p->masks, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
+  MPCHK(hipMemsetAsync(p->masks, 0, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP), s));
+  MPCHK(smax_dev_alloc((void **) &p->total, sizeof (uint64_t)));
+  MPCHK(hipMemsetAsync(p->total, 0, sizeof (uint64_t), s));
+  MPCHK(smax_dev_alloc((void **) &derr, sizeof (uint32_t)));
+  MPCHK(hipMemsetAsync(derr, 0, sizeof (uint32_t), s));
+  hipLaunchKernelGGL(mp_expand_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, s, in->lcp_dev, N,
                      p->X);
   MPCHK(hipGetLastError());
   if (in->numllv > 0) {
-    hipLaunchKernelGGL(mp_llv_kernel, dim3(mp_blocks(in->numllv)), dim3(256), 0, 0, in->llv_dev,
+    hipLaunchKernelGGL(mp_llv_kernel, dim3(mp_blocks(in->numllv)), dim3(256), 0, s, in->llv_dev,
                        in->numllv, in->lcp_dev, N, p->X, derr);
     MPCHK(hipGetLastError());
   }
-  hipLaunchKernelGGL(mp_llv_check_kernel, dim3(mp_blocks(N)), dim3(256), 0, 0, p->X, N, derr);
+  hipLaunchKernelGGL(mp_llv_check_kernel, dim3(mp_blocks(N)), dim3(256), 0, s, p->X, N, derr);
   MPCHK(hipGetLastError());
   // runs of equal BWT symbols: start offsets and running LCP minima
   {
     uint64_t *hv = NULL, *rs = NULL;
     void *tmp = NULL;
     size_t b1 = 0, b2 = 0;
-    hipError_t e = hipMalloc(&p->RM, sizeof (uint32_t) * (N + 1));
-    if (e == hipSuccess) e = hipMalloc(&p->RO, sizeof (uint32_t) * (N + 1));
-    if (e == hipSuccess) e = hipMalloc(&hv, sizeof (uint64_t) * (N + 1));
-    if (e == hipSuccess) e = hipMalloc(&rs, sizeof (uint64_t) * (N + 1));
+    hipError_t e = smax_dev_alloc((void **) &p->RM, sizeof (uint32_t) * (N + 1));
+    if (e == hipSuccess) e = smax_dev_alloc((void **) &p->RO, sizeof (uint32_t) * (N + 1));
+    if (e == hipSuccess) e = smax_dev_alloc((void **) &hv, sizeof (uint64_t) * (N + 1));
+    if (e == hipSuccess) e = smax_dev_alloc((void **) &rs, sizeof (uint64_t) * (N + 1));
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(mp_run_heads_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, 0,
+      hipLaunchKernelGGL(mp_run_heads_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, s,
                          in->bwt_dev, N, hv);
-      e = rocprim::inclusive_scan(nullptr, b1, hv, rs, (size_t) (N + 1), rocprim::maximum<uint64_t>());
+      e = rocprim::inclusive_scan(nullptr, b1, hv, rs, (size_t) (N + 1), rocprim::maximum<uint64_t>(),
+                                  s);
     }
     if (e == hipSuccess)
       e = rocprim::inclusive_scan_by_key(nullptr, b2, rs, p->X, p->RM, (size_t) (N + 1),
-                                         rocprim::minimum<uint32_t>());
-    if (e == hipSuccess) e = hipMalloc(&tmp, b1 > b2 ? b1 : b2);
+                                         rocprim::minimum<uint32_t>(), rocprim::equal_to<uint64_t>(), s);
+    if (e == hipSuccess) e = smax_dev_alloc(&tmp, b1 > b2 ? b1 : b2);
     if (e == hipSuccess)
-      e = rocprim::inclusive_scan(tmp, b1, hv, rs, (size_t) (N + 1), rocprim::maximum<uint64_t>());
+      e = rocprim::inclusive_scan(tmp, b1, hv, rs, (size_t) (N + 1), rocprim::maximum<uint64_t>(), s);
     if (e == hipSuccess)
       e = rocprim::inclusive_scan_by_key(tmp, b2, rs, p->X, p->RM, (size_t) (N + 1),
-                                         rocprim::minimum<uint32_t>());
+                                         rocprim::minimum<uint32_t>(), rocprim::equal_to<uint64_t>(), s);
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(mp_run_off_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, 0, rs, N, p->RO);
-      e = hipDeviceSynchronize();
+      hipLaunchKernelGGL(mp_run_off_kernel, dim3(mp_blocks(N + 1)), dim3(256), 0, s, rs, N, p->RO);
+      e = hipGetLastError();
     }
-    if (hv) (void) hipFree(hv);
-    if (rs) (void) hipFree(rs);
-    if (tmp) (void) hipFree(tmp);
+    {
+      // the temporaries go back behind the work on s, nothing waits here
+      SmaxStreamMarks m;
+      smax_marks_init(&m);
+      smax_marks_record(&m, s);
+      SmaxFence *f = smax_marks_fence(&m);
+      smax_dev_free_fenced(hv, f);
+      smax_dev_free_fenced(rs, f);
+      smax_dev_free_fenced(tmp, f);
+      smax_fence_release(f);
+    }
     MPCHK(e);
   }
   // candidate rows: their number sizes the per-candidate buffers (the tables
@@ -802,45 +825,52 @@ extern "C" int gt_maxpairs_plan_create(GtMaxpairsPlan **planp, const GtMaxpairsD
   if (N > 0) {
     size_t b1 = 0;
     MPCHK(rocprim::exclusive_scan(nullptr, b1, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
-                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), (hipStream_t) 0));
+                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), s));
     p->scan_tmp_bytes = b1;
-    hipLaunchKernelGGL(mp_cand_count_kernel, dim3((unsigned) p->nwg), dim3(256), 0, 0, in->lcp_dev,
+    hipLaunchKernelGGL(mp_cand_count_kernel, dim3((unsigned) p->nwg), dim3(256), 0, s, in->lcp_dev,
                        N, minlen < 255u ? minlen : 255u, p->wg_cand, p->masks);
     MPCHK(hipGetLastError());
-    MPCHK(hipMalloc(&p->scan_tmp, b1 ? b1 : 16));
+    MPCHK(smax_dev_alloc(&p->scan_tmp, b1 ? b1 : 16));
     MPCHK(rocprim::exclusive_scan(p->scan_tmp, b1, p->wg_cand, p->wg_cand_off, (uint64_t) 0,
-                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), (hipStream_t) 0));
+                                  (size_t) p->nwg, rocprim::plus<uint64_t>(), s));
     uint64_t last[2];
-    MPCHK(hipMemcpy(&last[0], p->wg_cand + p->nwg - 1, sizeof (uint64_t), hipMemcpyDeviceToHost));
-    MPCHK(hipMemcpy(&last[1], p->wg_cand_off + p->nwg - 1, sizeof (uint64_t), hipMemcpyDeviceToHost));
+    MPCHK(hipMemcpyAsync(&last[0], p->wg_cand + p->nwg - 1, sizeof (uint64_t), hipMemcpyDeviceToHost, s));
+    MPCHK(hipMemcpyAsync(&last[1], p->wg_cand_off + p->nwg - 1, sizeof (uint64_t), hipMemcpyDeviceToHost,
+                         s));
+    MPCHK(hipStreamSynchronize(s));    // the candidate count sizes the lists
     p->ncand = last[0] + last[1];
   }
-  MPCHK(hipMalloc(&p->list, sizeof (uint64_t) * (p->ncand + 1)));
-  MPCHK(hipMalloc(&p->cnt, sizeof (uint32_t) * (p->ncand + 1)));
-  MPCHK(hipMalloc(&p->off, sizeof (uint64_t) * (p->ncand + 1)));
-  MPCHK(hipMalloc(&p->st_cnt, sizeof (uint64_t) * (MP_LB_MAX_WG + 1)));
-  MPCHK(hipMemset(p->st_cnt, 0, sizeof (uint64_t) * (MP_LB_MAX_WG + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->list, sizeof (uint64_t) * (p->ncand + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->cnt, sizeof (uint32_t) * (p->ncand + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->off, sizeof (uint64_t) * (p->ncand + 1)));
+  MPCHK(smax_dev_alloc((void **) &p->st_cnt, sizeof (uint64_t) * (MP_LB_MAX_WG + 1)));
+  MPCHK(hipMemsetAsync(p->st_cnt, 0, sizeof (uint64_t) * (MP_LB_MAX_WG + 1), s));
   if (p->ncand > 0) {
     size_t b2 = 0;
     MPCHK(rocprim::exclusive_scan(nullptr, b2, p->cnt, p->off, (uint64_t) 0, (size_t) p->ncand,
-                                  rocprim::plus<uint64_t>(), (hipStream_t) 0));
+                                  rocprim::plus<uint64_t>(), s));
     if (b2 > p->scan_tmp_bytes) {
-      MPCHK(hipFree(p->scan_tmp));
+      MPCHK(hipStreamSynchronize(s));   // the candidate scan is done with it
+      smax_dev_free(p->scan_tmp);
       p->scan_tmp = NULL;
-      MPCHK(hipMalloc(&p->scan_tmp, b2));
+      MPCHK(smax_dev_alloc(&p->scan_tmp, b2));
       p->scan_tmp_bytes = b2;
     }
   }
-  if (p->scan_tmp == NULL) MPCHK(hipMalloc(&p->scan_tmp, 16));
-  MPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
+  if (p->scan_tmp == NULL) MPCHK(smax_dev_alloc(&p->scan_tmp, 16));
+  MPCHK(hipMemcpyAsync(&herr, derr, sizeof herr, hipMemcpyDeviceToHost, s));
+  MPCHK(hipStreamSynchronize(s));
   if (herr & 1u) { mp_seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
   if (herr & 2u) { mp_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
   if (herr & 4u) { mp_seterr(errbuf, errlen, "inconsistent index: a .lcp byte 255 without its .llv entry"); goto fail; }
-  (void) hipFree(derr);
+  smax_dev_free(derr);
+  smax_marks_record(&p->marks, s);
   *planp = p;
   return 0;
 fail:
-  if (derr) (void) hipFree(derr);
+  (void) hipStreamSynchronize(s);
+  smax_dev_free(derr);
+  smax_marks_record(&p->marks, s);
   gt_maxpairs_plan_delete(p);
   return -1;
 }
@@ -852,6 +882,7 @@ extern "C" int gt_maxpairs_plan_count(GtMaxpairsPlan *p, void *stream) {
   const uint64_t N = p->in.nonspecials, nc = p->ncand;
   const uint32_t mf = p->minlen < 255u ? p->minlen : 255u;
   MPCHK(hipSetDevice(p->in.device));
+  MPCHK(smax_marks_wait(&p->marks, s));   // the plan's earlier work on other streams
   if (nc == 0) {
     MPCHK(hipMemsetAsync(p->total, 0, sizeof (uint64_t), s));
   } else {
@@ -885,9 +916,11 @@ extern "C" int gt_maxpairs_plan_count(GtMaxpairsPlan *p, void *stream) {
       MPCHK(hipGetLastError());
     }
   }
+  smax_marks_record(&p->marks, s);
   p->counted = true;
   return 0;
 fail:
+  smax_marks_record(&p->marks, s);
   return -1;
 }
 
@@ -895,7 +928,7 @@ extern "C" int gt_maxpairs_plan_total(GtMaxpairsPlan *p, uint64_t *total) {
   char *errbuf = NULL;
   size_t errlen = 0;
   MPCHK(hipSetDevice(p->in.device));
-  MPCHK(hipDeviceSynchronize());
+  MPCHK(smax_marks_sync(&p->marks));     // the plan's own work, not the device
   MPCHK(hipMemcpy(total, p->total, sizeof (uint64_t), hipMemcpyDeviceToHost));
   return 0;
 fail:
@@ -913,6 +946,7 @@ extern "C" int gt_maxpairs_plan_emit(GtMaxpairsPlan *p, uint64_t *out_dev, uint6
   if (!p->counted) return -1;
   MPCHK(hipSetDevice(p->in.device));
   if (nc == 0 || capacity == 0) return 0;
+  MPCHK(smax_marks_wait(&p->marks, s));
   if (p->in.suf_bytes == 8)
     hipLaunchKernelGGL((mp_emit_kernel<uint64_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
                        p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
@@ -921,6 +955,7 @@ extern "C" int gt_maxpairs_plan_emit(GtMaxpairsPlan *p, uint64_t *out_dev, uint6
     hipLaunchKernelGGL((mp_emit_kernel<uint32_t>), dim3(mp_blocks(nc)), dim3(256), 0, s,
                        p->in.lcp_dev, p->X, p->in.bwt_dev, p->RM, p->RO, p->in.suf_dev, p->list, nc,
                        p->minlen, p->cnt, p->off, out_dev, capacity);
+  smax_marks_record(&p->marks, s);
   MPCHK(hipGetLastError());
   return 0;
 fail:
@@ -928,6 +963,23 @@ fail:
 }
 
 static int mp_bits(uint64_t v) { return v == 0 ? 1 : 64 - __builtin_clzll(v); }
+
+// an ordered pass's temporaries back to the cache behind its work on s;
+// the plan's mark on s stands behind the pass too
+static hipError_t mp_free_behind(GtMaxpairsPlan *p, hipStream_t s, void *a, void *b, void *c, void *d,
+                                 void *e, void *f) {
+  SmaxStreamMarks m;
+  smax_marks_init(&m);
+  smax_marks_record(&m, s);
+  SmaxFence *fence = smax_marks_fence(&m);
+  void *bufs[] = {a, b, c, d, e, f};
+  for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], fence);
+  smax_fence_release(fence);
+  smax_marks_record(&p->marks, s);
+  // the pass is complete when the call returns, as documented (its caller's
+  // stream only, never the device)
+  return hipStreamSynchronize(s);
+}
 
 // the minimum hierarchy and the largest LCP value, once per plan
 static int mp_build_hier(GtMaxpairsPlan *p, hipStream_t s, char *errbuf, size_t errlen) {
@@ -946,7 +998,7 @@ static int mp_build_hier(GtMaxpairsPlan *p, hipStream_t s, char *errbuf, size_t 
     tot += n[L];
     L++;
   }
-  if (tot > 0) MPCHK(hipMalloc(&p->hier, sizeof (uint32_t) * tot));
+  if (tot > 0) MPCHK(smax_dev_alloc((void **) &p->hier, sizeof (uint32_t) * tot));
   p->h.lv[0] = p->X;
   p->h.n[0] = n[0];
   for (int l = 1; l < L; l++) {
@@ -957,18 +1009,19 @@ static int mp_build_hier(GtMaxpairsPlan *p, hipStream_t s, char *errbuf, size_t 
     MPCHK(hipGetLastError());
   }
   p->h.levels = L;
-  MPCHK(hipMalloc(&dmax, sizeof (uint32_t)));
+  MPCHK(smax_dev_alloc((void **) &dmax, sizeof (uint32_t)));
   MPCHK(rocprim::reduce(nullptr, tb, p->X, dmax, 0u, (size_t) (N + 1), rocprim::maximum<uint32_t>(), s));
-  MPCHK(hipMalloc(&tmp, tb ? tb : 16));
+  MPCHK(smax_dev_alloc(&tmp, tb ? tb : 16));
   MPCHK(rocprim::reduce(tmp, tb, p->X, dmax, 0u, (size_t) (N + 1), rocprim::maximum<uint32_t>(), s));
   MPCHK(hipMemcpyAsync(&p->xmax, dmax, sizeof (uint32_t), hipMemcpyDeviceToHost, s));
-  MPCHK(hipStreamSynchronize(s));
-  (void) hipFree(dmax);
-  (void) hipFree(tmp);
+  MPCHK(hipStreamSynchronize(s));       // once per plan: the key widths need xmax
+  smax_dev_free(dmax);
+  smax_dev_free(tmp);
   return 0;
 fail:
-  if (dmax) (void) hipFree(dmax);
-  if (tmp) (void) hipFree(tmp);
+  (void) hipStreamSynchronize(s);
+  smax_dev_free(dmax);
+  smax_dev_free(tmp);
   return -1;
 }
 
@@ -986,8 +1039,9 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   bool by_rank = false;
   if (!p->counted) return -1;
   MPCHK(hipSetDevice(p->in.device));
-  MPCHK(hipStreamSynchronize(s));
-  MPCHK(hipMemcpy(&T, p->total, sizeof (uint64_t), hipMemcpyDeviceToHost));
+  MPCHK(smax_marks_wait(&p->marks, s));
+  MPCHK(hipMemcpyAsync(&T, p->total, sizeof (uint64_t), hipMemcpyDeviceToHost, s));
+  MPCHK(hipStreamSynchronize(s));        // the pair count sizes the pass
   if (T == 0) return 0;
   if (capacity < T) return -1;
   if (mp_build_hier(p, s, errbuf, errlen) != 0) return -1;
@@ -1028,9 +1082,7 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
     hipLaunchKernelGGL(mp_rank_scatter_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, tri, rank, T,
                        out_dev);
     MPCHK(hipGetLastError());
-    MPCHK(hipStreamSynchronize(s));
-    void *bufs[] = {tri, keys, ktmp};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
+    MPCHK(mp_free_behind(p, s, tri, keys, ktmp, NULL, NULL, NULL));
     return 0;
   }
   MPCHK(smax_dev_alloc((void **) &pa, sizeof (uint64_t) * T));
@@ -1062,11 +1114,7 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   hipLaunchKernelGGL((mp_gather_kernel<3>), dim3(mp_blocks(T)), dim3(256), 0, s, tri, pa, T,
                      out_dev);
   MPCHK(hipGetLastError());
-  MPCHK(hipStreamSynchronize(s));
-  {
-    void *bufs[] = {tri, keys, ktmp, pa, pb, st};   // the pass is complete: back to the cache
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
-  }
+  MPCHK(mp_free_behind(p, s, tri, keys, ktmp, pa, pb, st));
   return 0;
 fail:
   {

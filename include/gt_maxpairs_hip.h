@@ -84,12 +84,23 @@ typedef struct GtMaxpairsPlan GtMaxpairsPlan;
 /* Expands the exact LCP values (u32 per row, .llv applied) once. */
 int gt_maxpairs_plan_create(GtMaxpairsPlan **plan, const GtMaxpairsDevInput *in,
                             unsigned int minlen, char *errbuf, size_t errlen);
+/* The same on stream (a hipStream_t, NULL = default stream): waits on that
+ * stream only, for the candidate count that sizes the lists.  Every plan
+ * call orders itself after the plan's earlier work on other streams (events
+ * recorded at enqueue time); none synchronises the device. */
+int gt_maxpairs_plan_create_stream(GtMaxpairsPlan **plan, const GtMaxpairsDevInput *in,
+                                   unsigned int minlen, void *stream, char *errbuf,
+                                   size_t errlen);
+/* Frees the plan; its device buffers return to the runtime's cache behind
+ * the plan's enqueued work (nothing waits; the caller's streams may already
+ * be destroyed). */
 void gt_maxpairs_plan_delete(GtMaxpairsPlan *plan);
 
 /* Enqueue the counting pass (pairs per row + exclusive scan) on stream. */
 int gt_maxpairs_plan_count(GtMaxpairsPlan *plan, void *stream);
 
-/* Synchronises and returns the number of pairs of the last count pass. */
+/* Waits for the plan's own work (not the device) and returns the number of
+ * pairs of the last count pass. */
 int gt_maxpairs_plan_total(GtMaxpairsPlan *plan, uint64_t *total);
 
 /* Candidate rows of the plan (rows j >= 1 with LCP[j] >= minlen: the rows

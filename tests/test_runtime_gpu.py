@@ -528,3 +528,26 @@ def test_guided_schedule_against_static_grids():
         p.close()
         q.close()
     esa.release()
+
+
+def test_f2_f3_plans_do_not_wait_for_other_streams():
+    """The F2 and F3 device entry points are stream-ordered: an F3 plan built
+    and its events enqueued on one stream, an F2 plan counted and its total
+    read on another, all while a long smax pass runs on a third, return --
+    results final -- before that pass does (none of them synchronises the
+    device), and their results are bit-exact.  Run in a fresh process
+    (tests/stream_order_scenario.py): HIP multiplexes streams onto four
+    hardware queues round-robin, and after the other tests' streams the three
+    could share one, which serialises them in hardware whatever the library
+    does."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "stream_order_scenario.py")],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["waited"] == [], out
+    assert out["t_all"] > out["t_calls"]
+    assert out["intervals_equal"] and out["events_count_ok"] and out["pairs_equal"], out
