@@ -161,16 +161,17 @@ def main_lcpitv(args):
     lcp-interval with its father in pop order and the GtESAVisitor event
     stream in the reference's order (/root/reference/src/match/
     esa-bottomup.c:116-273) -- over tables resident in HBM.  A step is one
-    gt_lcpitv_plan_create (the interval tree: exact LCP, 64-ary minimum
-    hierarchy, per-tile ANSV count and pop-ordered interval records) + one
-    gt_lcpitv_plan_events pass into a resident buffer + gt_lcpitv_plan_delete.
-    One GPU (--gpus N: replicas).
+    gt_lcpitv_plan_create (the interval tree: exact LCP, per-tile ANSV of
+    PL / NSE / e, chain depths, the pops' exclusive scan, the pop-ordered
+    interval records) + one gt_lcpitv_plan_events pass into a resident
+    buffer + gt_lcpitv_plan_delete.  One GPU (--gpus N: replicas).
 
-    Algorithmic bytes per step (the roofline's "achieved"): per row the LCP
-    byte read, its exact u32 written and read by the two tree passes
-    (1 + 4 + 2 x 4 B), per interval its 5-word record written (40 B), per
-    event its 7-word record (56 B) plus the events pass's LCP u32 and 4-byte
-    suffix reads (8 B per row)."""
+    Algorithmic bytes per step (the roofline's "achieved", a fixed model, not
+    the kernels' traffic -- that is in profiles/r6/pmc_lcpitv_c2.json): per
+    row the LCP byte read, its exact u32 written and read twice (1 + 4 + 2 x
+    4 B), per interval its 5-word record written (40 B), per event its
+    7-word record (56 B) plus the events pass's LCP u32 and 4-byte suffix
+    reads (8 B per row)."""
     import numpy as np
     import torch
     import genometools_smax_amd as G

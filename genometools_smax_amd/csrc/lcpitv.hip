@@ -5,37 +5,27 @@
 // (gt_esa_bottomup, src/match/esa-bottomup.c:116-273), popping every
 // lcp-interval [lb..rb] of depth l > 0 at rb and calling the visitor's
 // leaf-edge / branching-edge / lcp-interval callbacks.  Here the tree is
-// computed data-parallel from all-nearest-smaller-value (ANSV) searches:
-//
-//   * row k with v = LCP[k] > 0 is the leftmost l-index of an interval iff
-//     the nearest p < k with LCP[p] <= v has LCP[p] < v; then lb = p and
-//     rb = q - 1 for the nearest q > k with LCP[q] < v (LCP[0] = LCP[N] = 0);
-//   * its father has depth max(LCP[lb], LCP[rb+1]) and lb = the nearest
-//     p' < lb with LCP[p'] < LCP[lb] when LCP[lb] is the larger (else lb);
-//   * leaf idx hangs (when LCP[idx+1] <= LCP[idx]) below the interval of
-//     depth LCP[idx] whose lb is the nearest p < idx with LCP[p] < LCP[idx].
-//
-// All of it follows from one ANSV quantity, the strict previous-smaller
-// value PL(k), computed per tile of 2048 rows in LDS (per-thread pointer
-// jumping inside 8-row segments, a segment-minimum search across the tile,
-// the 64-ary min hierarchy over the exact LCP array (u32) only for the few
-// rows with no smaller value earlier in their tile): the stack of the
-// reference after row idx is the PL chain from idx, so the intervals popped
-// at a row are read off that chain (li_walk) -- no sort, no per-row global
-// searches.  The tree stays in HBM (GtLcpitvPlan: the pop-ordered interval
-// records and the intervals popped before each tile); the visitor's event
-// stream is generated there too, every event at its position in the
-// reference's order, no stack and no replay loop (li_tile_events_kernel):
-// per row idx (X = LCP[idx], Y = LCP[idx+1]) the traversal emits exactly
-// one leaf edge, then for every interval popped at idx (pop order) its
-// lcp-interval and branching-edge events, so with P(idx) = #intervals with
-// rb < idx the leaf of row idx sits at idx + 2 P(idx) and popped interval r
-// of row idx at idx + 2 P(idx) + 1 + 2r.  The host entry points download
-// the events in chunks and call the visitor.
+// data-parallel, O(1) per row and per interval: three nearest-smaller-value
+// quantities of the exact LCP array (strict previous-smaller PL, next
+// smaller-or-equal NSE, and whether a row opens an interval) computed per
+// 2048-row tile in LDS, the depth of each row's previous-smaller chain (the
+// reference's stack depth), and one exclusive scan of the pops per row
+// (see "the tree" below).  Each interval is then written by its rightmost
+// l-index straight to its pop-order position; the tree stays in HBM
+// (GtLcpitvPlan), and the visitor's event stream is generated there too,
+// every event at its position in the reference's order: per row idx the
+// traversal emits exactly one leaf edge, then for every interval popped at
+// idx (pop order) its lcp-interval and branching-edge events, so with
+// P(idx) = #intervals with rb < idx the leaf of row idx sits at
+// idx + 2 P(idx) and popped interval r of row idx at idx + 2 P(idx) + 1 + 2r.
+// The host entry points download the events in chunks and call the
+// visitor.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <vector>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -109,29 +99,39 @@ __device__ __forceinline__ bool li_ok(uint32_t x, uint32_t v, bool strict) {
   return strict ? x < v : x <= v;
 }
 
-// The searches read a level's whole 64-entry block at once (16 independent
-// 16-byte loads, then a bit mask of the entries that qualify) instead of one
-// dependent load per entry: a search that climbs the hierarchy paid up to
-// 64 round trips per level, and a wave waits for its slowest lane
-// (li_write_kernel 14.7 -> 9.2 ms, li_count_kernel 5.2 -> 3.4 ms at C2,
-// profiles/s7/kernel_stats_lcpitv_c2*.csv; checking the 16 bytes next to
-// the row first changed nothing: the slowest lane of a wave, on a long
-// search, sets its time).  Levels are allocated LI_PAD
-// entries long past their end; bits past it are masked off.
+// A search reads a level's whole 64-entry block (16-byte pieces, then a bit
+// mask of the entries that qualify) instead of one dependent load per
+// entry.  Levels are allocated LI_PAD entries long past their end; bits
+// past it are masked off.
 #define LI_PAD 64
+// FAST: all 16 pieces in flight at once (one round trip per level, 64
+// VGPRs: pass B, which holds nothing else); else four at a time, for the
+// escape paths of the kernels that keep their occupancy
+template <bool FAST>
 __device__ __forceinline__ uint64_t li_block_mask(const uint32_t *lv, uint64_t b, uint64_t n,
                                                   uint32_t v, bool strict) {
   const uint4 *p = reinterpret_cast<const uint4 *>(lv + b);
-  uint4 t[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) t[j] = p[j];
   uint64_t m = 0;
+  if constexpr (FAST) {
+    uint4 t[16];
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    m |= (uint64_t) (li_ok(t[j].x, v, strict) ? 1u : 0u) << (4 * j);
-    m |= (uint64_t) (li_ok(t[j].y, v, strict) ? 1u : 0u) << (4 * j + 1);
-    m |= (uint64_t) (li_ok(t[j].z, v, strict) ? 1u : 0u) << (4 * j + 2);
-    m |= (uint64_t) (li_ok(t[j].w, v, strict) ? 1u : 0u) << (4 * j + 3);
+    for (int j = 0; j < 16; j++) t[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      m |= (uint64_t) (li_ok(t[j].x, v, strict) ? 1u : 0u) << (4 * j);
+      m |= (uint64_t) (li_ok(t[j].y, v, strict) ? 1u : 0u) << (4 * j + 1);
+      m |= (uint64_t) (li_ok(t[j].z, v, strict) ? 1u : 0u) << (4 * j + 2);
+      m |= (uint64_t) (li_ok(t[j].w, v, strict) ? 1u : 0u) << (4 * j + 3);
+    }
+  } else {
+#pragma unroll 4
+    for (int j = 0; j < 16; j++) {
+      const uint4 t = p[j];
+      m |= (uint64_t) (li_ok(t.x, v, strict) ? 1u : 0u) << (4 * j);
+      m |= (uint64_t) (li_ok(t.y, v, strict) ? 1u : 0u) << (4 * j + 1);
+      m |= (uint64_t) (li_ok(t.z, v, strict) ? 1u : 0u) << (4 * j + 2);
+      m |= (uint64_t) (li_ok(t.w, v, strict) ? 1u : 0u) << (4 * j + 3);
+    }
   }
   if (n - b < 64) m &= (1ull << (n - b)) - 1;
   return m;
@@ -139,13 +139,14 @@ __device__ __forceinline__ uint64_t li_block_mask(const uint32_t *lv, uint64_t b
 
 // nearest p < k with X[p] < v (strict) / <= v; X[0] == 0 guarantees one
 // for v > 0 (strict) and any v (<=)
+template <bool FAST>
 __device__ static uint64_t li_prev(const LiLevels &L, uint64_t k, uint32_t v, bool strict) {
   uint64_t i = k, p = 0;
   int lev = 0;
   for (;;) {
     const uint64_t b = (i >> 6) << 6;
     const uint64_t below = i - b;   // entries [b, i)
-    const uint64_t m = below ? li_block_mask(L.lv[lev], b, L.n[lev], v, strict) &
+    const uint64_t m = below ? li_block_mask<FAST>(L.lv[lev], b, L.n[lev], v, strict) &
                                    ((below >= 64 ? 0ull : (1ull << below)) - 1ull)
                              : 0ull;
     if (m) { p = b + 63 - (uint64_t) __builtin_clzll(m); break; }
@@ -156,439 +157,680 @@ __device__ static uint64_t li_prev(const LiLevels &L, uint64_t k, uint32_t v, bo
   while (lev > 0) {                // last child of p whose subtree qualifies
     lev--;
     const uint64_t b = p << 6;
-    const uint64_t m = li_block_mask(L.lv[lev], b, L.n[lev], v, strict);
+    const uint64_t m = li_block_mask<FAST>(L.lv[lev], b, L.n[lev], v, strict);
     p = b + 63 - (uint64_t) __builtin_clzll(m);
   }
   return p;
 }
 
-// workgroup-wide exclusive prefix (256 threads); *total = sum
-__device__ __forceinline__ uint32_t li_block_excl(uint32_t v, uint32_t *total) {
-  __shared__ uint32_t sW[4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
+// nearest q > k with X[q] < v (strict) / <= v; X[n-1] == 0 (row N, or the
+// last tile's minimum 0) guarantees one for any v when !strict, v > 0 when
+// strict
+template <bool FAST>
+__device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v, bool strict) {
+  uint64_t i = k, p = 0;
+  int lev = 0;
+  for (;;) {
+    const uint64_t b = (i >> 6) << 6;
+    const uint64_t upto = i - b;    // entries (i, b + 64)
+    const uint64_t m = upto >= 63 ? 0ull
+                                  : li_block_mask<FAST>(L.lv[lev], b, L.n[lev], v, strict) & ~((2ull << upto) - 1ull);
+    if (m) { p = b + (uint64_t) __builtin_ctzll(m); break; }
+    if (lev + 1 >= L.nlev) return L.n[0] - 1;
+    i >>= 6;
+    lev++;
   }
-  if (lane == 63) sW[wave] = incl;
-  __syncthreads();
-  uint32_t wo = 0;
-  for (int w = 0; w < wave; w++) wo += sW[w];
-  *total = sW[0] + sW[1] + sW[2] + sW[3];
-  __syncthreads();                     // sW is reused by the next call
-  return wo + incl - v;
+  while (lev > 0) {                // first child of p whose subtree qualifies
+    lev--;
+    const uint64_t b = p << 6;
+    p = b + (uint64_t) __builtin_ctzll(li_block_mask<FAST>(L.lv[lev], b, L.n[lev], v, strict));
+  }
+  return p;
 }
 
-// ------------------------------------------------------------ tiles
+// ------------------------------------------------------------ the tree
 //
-// The tree from the strict previous-smaller value PL(k) = the nearest p < k
-// with X[p] < X[k] alone.  The reference's stack after row idx holds
-// exactly the chain c0 = idx, c1 = PL(c0), c2 = PL(c1), ... (depths X[cj]
-// strictly decreasing, the interval of depth X[cj] starting at c(j+1)), so
-// the lcp-intervals popped at row idx (Y = X[idx+1]) are, deepest first,
-// [c(j+1), idx] of depth X[cj] for every cj with X[cj] > Y; the father of
-// pop j has depth max(X[c(j+1)], Y) and lb PL(c(j+1)) when X[c(j+1)] >= Y,
-// else it is the new interval (Y, c(j+1)) pushed after the pops.  The leaf
-// of row idx hangs below (X[idx], PL(idx)) when Y <= X[idx], else it is the
-// first child of (Y, idx).  Every interval is popped once, so the walks
-// cost O(N) over the whole table.
+// Every lcp-interval of depth v > 0 has one "rightmost l-index" c: X[c] = v,
+// and the nearest q > c with X[q] <= v has X[q] < v (NSE(c) = q, no equal
+// value after c inside the interval).  With PL(c) = the nearest p < c with
+// X[p] < X[c] (strict previous-smaller value), the interval is
+//   [lb, rb] = [PL(c), NSE(c) - 1],  father depth max(X[lb], X[rb + 1]),
+//   father lb = PL(lb) when X[lb] >= X[rb + 1], else lb (a new father).
+// The reference pops it at row rb (src/match/esa-bottomup.c:154-196): its
+// stack after row r holds exactly the PL chain r, PL(r), PL(PL(r)), ...
+// (depths strictly decreasing), so with d(k) = the chain's length from k
+// (d = 0 where X = 0, d(k) = 1 + d(PL(k))) the interval is the
+// (d(rb) - d(c))-th pop of row rb, deepest first, and the number of pops of
+// row r is
+//   cnt(r) = d(r)                              when X[r+1] = 0,
+//   cnt(r) = d(r) - d(r+1) + e(r+1)            else,
+// e(k) = 1 when the nearest p < k with X[p] <= X[k] has X[p] < X[k] (k
+// opens an interval).  P(r) = the pops of rows < r (an exclusive scan of
+// cnt) places every interval: record P(rb) + d(rb) - d(c), events from
+// r + 2 P(r) on.  So the tree is three nearest-smaller-value quantities
+// (PL, NSE, e) and one depth per row, each O(1) from its neighbours --
+// no stack walk, no per-row search, no sort.
 //
-// A workgroup owns LI_T consecutive rows (a tile).  Pass 0 computes PL of
-// its rows in LDS -- per-thread pointer jumping inside 8-row segments, the
-// rows left unresolved by a segment-minimum search across the tile, and
-// the tile's prefix minima (no smaller value in the tile before them, a
-// handful per tile) by the global 64-ary hierarchy (li_prev) -- and stores
-// it in HBM.  Chains that leave a tile (intervals open at its start)
-// continue along the chain from the row before the tile, t0-1, PL(t0-1),
-// ... (every PL out of the tile lies on it): its first LI_BD entries are
-// gathered once per tile (li_bchain_kernel, one thread per tile) and
-// loaded with the tile.  Three passes walk the chains: a count per tile
-// (plan), the pop-ordered interval records (plan) and the visitor event
-// stream (events); the last two stage their output in LDS per 64-row wave
-// step and store it as contiguous 16-byte pieces.
+// Pass A, per tile of LI_T rows in LDS: PL, e and NSE by per-thread
+// pointer jumping inside 8-row segments, then the nearest segment with a
+// small enough minimum (its own chain from the near end stays inside it);
+// rows without an answer in their tile (the tile's prefix or suffix
+// minima, a handful) are resolved by pass B over the tile minima (a 64-ary
+// hierarchy) and the found tile's resolved chain.  PL and NSE are stored
+// as u32 distances (ESC: the rare distance >= 2^32 - 1, found again by
+// search where it is read).  Depth: each tile's chain leaves the tile
+// through the chain of the row before it (t0-1, PL(t0-1), ...: the
+// boundary chain, its first LI_BD entries gathered per tile), so
+// d(k) = (steps inside the tile) + D_t - m with D_t = d(t0-1) and m the
+// exit's index on that chain; D(t+1) = a_t + b_t D_t is an inclusive scan
+// of affine maps over the tiles, then one LDS pointer-jumping pass per
+// tile gives every row's d.
 #define LI_T 2048                       // rows per tile
 #define LI_TPB 256                      // threads per tile workgroup
 #define LI_RPT (LI_T / LI_TPB)          // rows per segment (one thread)
 #define LI_GSEG 16                      // segments per group
 #define LI_NGRP (LI_TPB / LI_GSEG)
 #define LI_BD 64                        // boundary-chain entries kept per tile
-#define LI_ITV_CAP 384                  // interval records staged per workgroup
-#define LI_EV_STAGE 16384               // event staging bytes per workgroup
+#define LI_UNRES 0xfffffffeu            // distance not found inside the tile (pass A)
+#define LI_ESC 0xffffffffu              // distance >= 2^32 - 1: search again where read
+#define LI_EUNRES 2u
 
-template <typename RowT>
-__device__ __forceinline__ RowT li_none() { return (RowT) ~(RowT) 0; }
-
-// pass 0's LDS
-template <typename RowT>
-struct LiAnsvTile {
-  uint32_t x[LI_T + 1];                 // X[t0 .. t0 + LI_T] (0 past row N)
-  RowT pl[LI_T];                        // PL of the tile's rows (~0: none / pending)
-  uint32_t segmin[LI_TPB];
-  uint32_t grpmin[LI_NGRP];
-};
-
-// the walking passes' LDS: the tile, its boundary chain, the output stage
-template <typename RowT, int STAGE>
-struct LiWalkTile {
-  uint32_t x[LI_T + 1];
-  RowT pl[LI_T];
-  RowT brow[LI_BD];                     // t0-1, PL(t0-1), ... (rows strictly decreasing)
-  uint32_t bx[LI_BD];                   // their X (strictly decreasing)
-  int nb;                               // entries held; the chain goes on past them iff
-                                        // nb == LI_BD and bx[nb-1] > 0
-  alignas(16) unsigned char stage[STAGE];
-};
-
-// PL of every row of the tile [t0, t0 + LI_T) into S.pl (rows with X = 0
-// have none).  Ends with a barrier.
-template <typename RowT>
-__device__ void li_tile_ansv(const LiLevels &L, uint64_t N, uint64_t t0, LiAnsvTile<RowT> &S) {
-  const int tid = threadIdx.x;
-  const RowT none = li_none<RowT>();
-  for (int k = tid; k <= LI_T; k += LI_TPB) {
-    const uint64_t g = t0 + (uint64_t) k;
-    S.x[k] = g <= N ? L.lv[0][g] : 0u;   // lv[0] holds rows 0..N, X[N] = 0
-  }
-  __syncthreads();
-  // the thread's segment, left to right: p jumps along PL inside it
-  const int lo = tid * LI_RPT;
-  uint32_t m = 0xffffffffu;
-  for (int i = lo; i < lo + LI_RPT; i++) {
-    const uint32_t v = S.x[i];
-    m = v < m ? v : m;
-    int p = i - 1;
-    while (p >= lo && S.x[p] >= v) {
-      const RowT q = S.pl[p];
-      p = q == none ? lo - 1 : (int) (q - (RowT) t0);
-    }
-    S.pl[i] = p >= lo ? (RowT) (t0 + (uint64_t) p) : none;
-  }
-  S.segmin[tid] = m;
-  __syncthreads();
-  if (tid < LI_NGRP) {
-    uint32_t g = 0xffffffffu;
-    for (int s = tid * LI_GSEG; s < (tid + 1) * LI_GSEG; s++) g = S.segmin[s] < g ? S.segmin[s] : g;
-    S.grpmin[tid] = g;
-  }
-  __syncthreads();
-  // rows with no smaller value earlier in their segment: the nearest segment
-  // before with a smaller minimum (then the last row below v along that
-  // segment's own PL chain, which stays inside it), else the global search
-  for (int i = lo; i < lo + LI_RPT; i++) {
-    const uint32_t v = S.x[i];
-    if (v == 0 || S.pl[i] != none) continue;
-    int found = -1;
-    for (int s = tid - 1; s >= (tid / LI_GSEG) * LI_GSEG; s--)
-      if (S.segmin[s] < v) { found = s; break; }
-    if (found < 0)
-      for (int g = tid / LI_GSEG - 1; g >= 0 && found < 0; g--)
-        if (S.grpmin[g] < v)
-          for (int s = g * LI_GSEG + LI_GSEG - 1; s >= g * LI_GSEG; s--)
-            if (S.segmin[s] < v) { found = s; break; }
-    if (found >= 0) {
-      int p = found * LI_RPT + LI_RPT - 1;
-      while (S.x[p] >= v) p = (int) (S.pl[p] - (RowT) t0);
-      S.pl[i] = (RowT) (t0 + (uint64_t) p);
-    } else {
-      S.pl[i] = t0 > 0 ? (RowT) li_prev(L, t0, v, true) : none;
-    }
-  }
-  __syncthreads();
+__device__ __forceinline__ uint32_t li_dist32(uint64_t dist) {
+  return dist >= (uint64_t) LI_UNRES ? LI_ESC : (uint32_t) dist;
 }
 
-// pass 0 (plan): PL of every row into HBM (RowT each, ~0 where X = 0)
-template <typename RowT>
-__global__ void __launch_bounds__(LI_TPB) li_pl_kernel(LiLevels L, uint64_t N, uint64_t ntiles,
-                                                       RowT *PL) {
-  __shared__ LiAnsvTile<RowT> S;
+// LDS rows padded by one word per 8 (row i at i + i/8): a thread's 8-row
+// segment is contiguous, and without the pad the 64 lanes' rows 8 apart
+// fall on 8 banks
+#define LI_PADI(i) ((i) + ((i) >> 3))
+#define LI_TPAD (LI_T + LI_T / 8)
+#define LI_CH 64                        // chain entries kept per tile (suffix / prefix minima)
+// a chain's words: [0] length (| 0x80000000 when cut at LI_CH), [4, 4+LI_CH)
+// the values, [4+LI_CH, 4+2 LI_CH) the tile-local rows (16-byte aligned
+// value block: one round of 16-byte loads reads it whole)
+#define LI_CHW (4 + 2 * LI_CH)
+
+struct LiAnsvLds {
+  uint32_t x[LI_TPAD];
+  int16_t pl[LI_TPAD], ple[LI_TPAD], nse[LI_TPAD];   // tile-local rows, -1: none found
+  uint8_t e[LI_TPAD];
+  uint32_t wsum[2][LI_TPB / 64];
+  uint32_t segmin[LI_TPB];
+  uint32_t grpmin[LI_NGRP];
+  uint32_t tmin[LI_TPB / 64];
+};
+
+// nearest segment before tid (after, when !left) whose minimum is < v
+// (<= v when !strict); -1 if none in the tile
+__device__ __forceinline__ int li_seg_find(const LiAnsvLds &S, int tid, uint32_t v, bool strict,
+                                           bool left) {
+  auto ok = [&](uint32_t m) { return strict ? m < v : m <= v; };
+  const int g = tid / LI_GSEG;
+  if (left) {
+    for (int s = tid - 1; s >= g * LI_GSEG; s--)
+      if (ok(S.segmin[s])) return s;
+    for (int h = g - 1; h >= 0; h--)
+      if (ok(S.grpmin[h]))
+        for (int s = h * LI_GSEG + LI_GSEG - 1; s >= h * LI_GSEG; s--)
+          if (ok(S.segmin[s])) return s;
+  } else {
+    for (int s = tid + 1; s < (g + 1) * LI_GSEG; s++)
+      if (ok(S.segmin[s])) return s;
+    for (int h = g + 1; h < LI_NGRP; h++)
+      if (ok(S.grpmin[h]))
+        for (int s = h * LI_GSEG; s < (h + 1) * LI_GSEG; s++)
+          if (ok(S.segmin[s])) return s;
+  }
+  return -1;
+}
+
+// pass A: rows [t0, t0 + LI_T) of the N + 1 rows 0..N.  Besides PL, e and
+// NSE per row it stores the tile's two minimum chains for pass B: its
+// strict suffix minima from the last row (the PL chain from there, X
+// strictly decreasing) and its weak prefix minima from the first row (the
+// NSE chain, X non-increasing), LI_CH of each -- the nearest row below v on
+// either side of a tile is on them, found by one masked read.  The rows
+// left unresolved go to a list for pass B: entries (row << 2 | kind), kind
+// 0 PL, 1 PLE (e), 2 NSE; *ucnt counts them all, at most ucap are stored
+// (past it pass B scans every row).
+__global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, uint64_t N, uint64_t ntiles,
+                                                         uint32_t *pld, uint32_t *nsed, uint8_t *eb,
+                                                         uint32_t *tmin, uint32_t *sch, uint32_t *pch,
+                                                         uint64_t *ulist, unsigned long long *ucnt,
+                                                         uint64_t ucap) {
+  __shared__ LiAnsvLds S;
+  const int tid = threadIdx.x, lo = tid * LI_RPT, hi = lo + LI_RPT;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t t0 = t * LI_T;
-    li_tile_ansv(L, N, t0, S);
-    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
-    for (int i = threadIdx.x; i < nrows; i += LI_TPB) PL[t0 + i] = S.pl[i];
+    for (int k = tid; k < LI_T; k += LI_TPB) {
+      const uint64_t g = t0 + (uint64_t) k;
+      S.x[LI_PADI(k)] = g <= N ? X[g] : 0xffffffffu;   // past row N: never an answer
+    }
+    __syncthreads();
+    // the thread's segment: PLE / PL left to right, NSE right to left
+    uint32_t m = 0xffffffffu;
+    for (int i = lo; i < hi; i++) {
+      const uint32_t v = S.x[LI_PADI(i)];
+      m = v < m ? v : m;
+      int p = i - 1;
+      while (p >= lo && S.x[LI_PADI(p)] > v) p = S.ple[LI_PADI(p)];
+      int q = -1;
+      if (p >= lo) q = S.x[LI_PADI(p)] < v ? p : S.pl[LI_PADI(p)];
+      S.ple[LI_PADI(i)] = (int16_t) (p >= lo ? p : -1);
+      S.pl[LI_PADI(i)] = (int16_t) q;
+    }
+    for (int i = hi - 1; i >= lo; i--) {
+      const uint32_t v = S.x[LI_PADI(i)];
+      int q = i + 1;
+      while (q < hi && S.x[LI_PADI(q)] > v) q = S.nse[LI_PADI(q)] < 0 ? hi : S.nse[LI_PADI(q)];
+      S.nse[LI_PADI(i)] = (int16_t) (q < hi ? q : -1);
+    }
+    S.segmin[tid] = m;
+    uint32_t wm = m;                     // the wave's minimum, for the tile's
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t y = __shfl_xor(wm, o, 64);
+      wm = y < wm ? y : wm;
+    }
+    if ((tid & 63) == 0) S.tmin[tid >> 6] = wm;
+    __syncthreads();
+    if (tid < LI_NGRP) {
+      uint32_t g = 0xffffffffu;
+      for (int s = tid * LI_GSEG; s < (tid + 1) * LI_GSEG; s++) g = S.segmin[s] < g ? S.segmin[s] : g;
+      S.grpmin[tid] = g;
+    }
+    if (tid == 0) {
+      uint32_t g = S.tmin[0];
+      for (int w = 1; w < LI_TPB / 64; w++) g = S.tmin[w] < g ? S.tmin[w] : g;
+      tmin[t] = g;
+    }
+    __syncthreads();
+    // rows unresolved in their segment: the nearest segment with a small
+    // enough minimum; its chain from the near end stays inside it (every row
+    // it visits has a smaller one beyond it in that segment: resolved above).
+    // The answers go back into the LDS arrays (entries no walk here reads:
+    // the walks only visit rows resolved inside their segment)
+    for (int i = lo; i < hi; i++) {
+      const uint32_t v = S.x[LI_PADI(i)];
+      uint8_t e = 0;
+      if (v > 0 && v != 0xffffffffu) {
+        int p = S.pl[LI_PADI(i)];
+        if (p < 0) {
+          const int s = li_seg_find(S, tid, v, true, true);
+          if (s >= 0) {
+            p = s * LI_RPT + LI_RPT - 1;
+            while (S.x[LI_PADI(p)] >= v) p = S.pl[LI_PADI(p)];
+            S.pl[LI_PADI(i)] = (int16_t) p;
+          }
+        }
+        int pe = S.ple[LI_PADI(i)];
+        if (pe < 0) {
+          const int s = li_seg_find(S, tid, v, false, true);
+          if (s >= 0) {
+            pe = s * LI_RPT + LI_RPT - 1;
+            while (S.x[LI_PADI(pe)] > v) pe = S.pl[LI_PADI(pe)];   // the strict chain skips only values > v
+          }
+        }
+        e = pe >= 0 ? (S.x[LI_PADI(pe)] < v ? 1u : 0u) : LI_EUNRES;
+        int q = S.nse[LI_PADI(i)];
+        if (q < 0) {
+          const int s = li_seg_find(S, tid, v, false, false);
+          if (s >= 0) {
+            q = s * LI_RPT;
+            while (S.x[LI_PADI(q)] > v) q = S.nse[LI_PADI(q)];
+            S.nse[LI_PADI(i)] = (int16_t) q;
+          }
+        }
+      }
+      S.e[LI_PADI(i)] = e;
+    }
+    // the minimum chains' members: strict suffix minima (x below every row
+    // after them) and weak prefix minima (x at most every row before them),
+    // from the minima of the other segments (rows past N: x = 2^32-1, never
+    // members) and a pass over the thread's own rows
+    uint32_t after = 0xffffffffu, before = 0xffffffffu;
+    {
+      const int g = tid / LI_GSEG;
+      for (int s2 = tid + 1; s2 < (g + 1) * LI_GSEG; s2++) after = S.segmin[s2] < after ? S.segmin[s2] : after;
+      for (int h = g + 1; h < LI_NGRP; h++) after = S.grpmin[h] < after ? S.grpmin[h] : after;
+      for (int s2 = g * LI_GSEG; s2 < tid; s2++) before = S.segmin[s2] < before ? S.segmin[s2] : before;
+      for (int h = 0; h < g; h++) before = S.grpmin[h] < before ? S.grpmin[h] : before;
+    }
+    uint32_t sflag = 0, pflag = 0;
+    {
+      uint32_t run = after;
+      for (int i = hi - 1; i >= lo; i--) {
+        const uint32_t xi = S.x[LI_PADI(i)];
+        if (xi < run) sflag |= 1u << (i - lo);
+        run = xi < run ? xi : run;
+      }
+      run = before;
+      for (int i = lo; i < hi; i++) {
+        const uint32_t xi = S.x[LI_PADI(i)];
+        if (xi <= run && xi != 0xffffffffu) pflag |= 1u << (i - lo);
+        run = xi < run ? xi : run;
+      }
+    }
+    __syncthreads();
+    // ranks: suffix members counted from the right, prefix members from the left
+    {
+      const uint32_t cs = (uint32_t) __builtin_popcount(sflag), cp = (uint32_t) __builtin_popcount(pflag);
+      const int lane = tid & 63, wave = tid >> 6;
+      uint32_t is = cs, ip = cp;         // inclusive prefix sums over the workgroup's threads
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t os = __shfl_up(is, d, 64), op = __shfl_up(ip, d, 64);
+        if (lane >= d) { is += os; ip += op; }
+      }
+      if (lane == 63) { S.wsum[0][wave] = is; S.wsum[1][wave] = ip; }
+      __syncthreads();
+      uint32_t ws = 0, wp = 0, ts = 0, tp = 0;
+      for (int w = 0; w < LI_TPB / 64; w++) {
+        if (w < wave) { ws += S.wsum[0][w]; wp += S.wsum[1][w]; }
+        ts += S.wsum[0][w];
+        tp += S.wsum[1][w];
+      }
+      uint32_t *so = sch + t * LI_CHW, *po = pch + t * LI_CHW;
+      // suffix members after this thread's: ts - (ws + is)
+      uint32_t rs = ts - (ws + is);
+      for (int i = hi - 1; i >= lo; i--)
+        if (sflag >> (i - lo) & 1u) {
+          if (rs < LI_CH) { so[4 + rs] = S.x[LI_PADI(i)]; so[4 + LI_CH + rs] = (uint32_t) i; }
+          rs++;
+        }
+      uint32_t rp = wp + ip - cp;
+      for (int i = lo; i < hi; i++)
+        if (pflag >> (i - lo) & 1u) {
+          if (rp < LI_CH) { po[4 + rp] = S.x[LI_PADI(i)]; po[4 + LI_CH + rp] = (uint32_t) i; }
+          rp++;
+        }
+      if (tid == 0) {
+        so[0] = (ts < LI_CH ? ts : LI_CH) | (ts > LI_CH ? 0x80000000u : 0u);
+        po[0] = (tp < LI_CH ? tp : LI_CH) | (tp > LI_CH ? 0x80000000u : 0u);
+      }
+      if (tid < LI_CH) {                 // (unused value slots: never below, masked by the length)
+        if ((uint32_t) tid >= ts) so[4 + tid] = 0;
+        if ((uint32_t) tid >= tp) po[4 + tid] = 0;
+      }
+    }
+    // the rows' words, coalesced (row tid + 256 j), and the unresolved list
+    uint32_t umask = 0;
+    for (int j = 0; j < LI_RPT; j++) {
+      const int i = tid + LI_TPB * j;
+      const uint64_t k = t0 + (uint64_t) i;
+      if (k > N) break;
+      const uint32_t v = S.x[LI_PADI(i)];
+      uint32_t dpl = 0, dns = 0;
+      uint8_t e = 0;
+      if (v > 0) {
+        const int p = S.pl[LI_PADI(i)], q = S.nse[LI_PADI(i)];
+        dpl = p >= 0 ? (uint32_t) (i - p) : LI_UNRES;
+        dns = q >= 0 ? (uint32_t) (q - i) : LI_UNRES;
+        e = S.e[LI_PADI(i)];
+      }
+      pld[k] = dpl;
+      nsed[k] = dns;
+      eb[k] = e;
+      umask |= ((dpl == LI_UNRES ? 1u : 0u) | (e == LI_EUNRES ? 2u : 0u) | (dns == LI_UNRES ? 4u : 0u))
+               << (3 * j);
+    }
+    {
+      // append: a wave-level prefix of the counts, one atomic per wave
+      const uint32_t c = (uint32_t) __builtin_popcount(umask);
+      const int lane = tid & 63;
+      uint32_t incl = c;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+      }
+      const uint32_t tot = __shfl(incl, 63, 64);
+      unsigned long long base = 0;
+      if (lane == 63 && tot) base = atomicAdd(ucnt, (unsigned long long) tot);
+      base = __shfl(base, 63, 64);
+      uint64_t at = base + (incl - c);
+      while (umask) {
+        const int b = __builtin_ctz(umask);
+        umask &= umask - 1;
+        if (at < ucap) ulist[at] = ((t0 + (uint64_t) (tid + LI_TPB * (b / 3))) << 2) | (uint64_t) (b % 3);
+        at++;
+      }
+    }
     __syncthreads();                     // S is rewritten by the next tile
   }
 }
 
+// PL / PLE (strict / !strict) and NSE of row k with value v > 0 by search:
+// the nearest tile before (after) with a small enough minimum, then the
+// first entry of that tile's suffix (prefix) minimum chain with a small
+// enough value, by binary search; a chain cut at LI_CH entries is followed
+// on in HBM (pass A resolved every row on it inside the tile)
+struct LiTree {                         // what the searches need
+  LiLevels TL;                          // tile minima and their hierarchy
+  const uint32_t *sch, *pch;            // the tiles' minimum chains
+};
+
+template <bool FAST>
+__device__ uint64_t li_search_prev(const LiTree &T, const uint32_t *X, const uint32_t *pld,
+                                   uint64_t k, uint32_t v, bool strict) {
+  const uint64_t t = k / LI_T;
+  if (t == 0) return 0;                  // (never: X[0] = 0 lies in tile 0)
+  const uint64_t s = li_prev<FAST>(T.TL, t, v, strict);
+  const uint32_t *ch = T.sch + s * LI_CHW;
+  const int n = (int) (ch[0] & 0xffffu);
+  // the first entry with X < v (<= v) -- X strictly decreasing along the
+  // chain -- from one read of the value block
+  const uint64_t m = li_block_mask<FAST>(ch + 4, 0, (uint64_t) n, v, strict);
+  if (m) return s * LI_T + ch[4 + LI_CH + __builtin_ctzll(m)];
+  uint64_t p = s * LI_T + ch[4 + LI_CH + n - 1];   // past the entries held
+  while (strict ? X[p] >= v : X[p] > v) p -= pld[p];
+  return p;
+}
+
+template <bool FAST>
+__device__ uint64_t li_search_next(const LiTree &T, const uint32_t *X, const uint32_t *nsed,
+                                   uint64_t k, uint32_t v) {
+  const uint64_t t = k / LI_T;
+  const uint64_t s = li_next<FAST>(T.TL, t, v, false);
+  const uint32_t *ch = T.pch + s * LI_CHW;
+  const int n = (int) (ch[0] & 0xffffu);
+  const uint64_t m = li_block_mask<FAST>(ch + 4, 0, (uint64_t) n, v, false);   // X non-increasing
+  if (m) return s * LI_T + ch[4 + LI_CH + __builtin_ctzll(m)];
+  uint64_t q = s * LI_T + ch[4 + LI_CH + n - 1];
+  while (X[q] > v) q += nsed[q];
+  return q;
+}
+
+// pass B: the rows pass A left unresolved, about 20 per tile.  Four rows
+// per thread per step, their words read as 16-byte pieces; the searches
+// (one 16-byte piece of a level's block per load, all in flight) run only
+// on the rare lanes that found an unresolved row.
+__global__ void __launch_bounds__(256) li_resolve_kernel(LiTree T, const uint32_t *X, uint64_t N,
+                                                         uint32_t *pld, uint32_t *nsed, uint8_t *eb) {
+  const uint64_t nq = (N + 1 + 3) / 4;
+  for (uint64_t qd = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; qd < nq;
+       qd += (uint64_t) gridDim.x * blockDim.x) {
+    const uint64_t k0 = 4 * qd;
+    uint32_t xv[4], pv[4], nv[4], ev;
+    if (k0 + 4 <= N + 1) {
+      const uint4 a = reinterpret_cast<const uint4 *>(X)[qd];
+      const uint4 b = reinterpret_cast<const uint4 *>(pld)[qd];
+      const uint4 c = reinterpret_cast<const uint4 *>(nsed)[qd];
+      ev = reinterpret_cast<const uint32_t *>(eb)[qd];
+      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
+      pv[0] = b.x; pv[1] = b.y; pv[2] = b.z; pv[3] = b.w;
+      nv[0] = c.x; nv[1] = c.y; nv[2] = c.z; nv[3] = c.w;
+    } else {
+      ev = 0;
+      for (int j = 0; j < 4; j++) {
+        const bool in = k0 + j <= N;
+        xv[j] = in ? X[k0 + j] : 0u;
+        pv[j] = in ? pld[k0 + j] : 0u;
+        nv[j] = in ? nsed[k0 + j] : 0u;
+        ev |= (in ? (uint32_t) eb[k0 + j] : 0u) << (8 * j);
+      }
+    }
+    const bool any = pv[0] == LI_UNRES || pv[1] == LI_UNRES || pv[2] == LI_UNRES ||
+                     pv[3] == LI_UNRES || nv[0] == LI_UNRES || nv[1] == LI_UNRES ||
+                     nv[2] == LI_UNRES || nv[3] == LI_UNRES ||
+                     ((ev & 0x02020202u) != 0);
+    if (!any) continue;
+    for (int j = 0; j < 4; j++) {
+      const uint64_t k = k0 + j;
+      const uint32_t v = xv[j];
+      if (k > N || v == 0) continue;
+      if (pv[j] == LI_UNRES) pld[k] = li_dist32(k - li_search_prev<true>(T, X, pld, k, v, true));
+      if (((ev >> (8 * j)) & 0xffu) == LI_EUNRES)
+        eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
+      if (nv[j] == LI_UNRES) nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
+    }
+  }
+}
+
+// pass B over the list: one search per entry
+__global__ void __launch_bounds__(256) li_resolve_list_kernel(LiTree T, const uint32_t *X,
+                                                              const uint64_t *ulist,
+                                                              const unsigned long long *ucnt,
+                                                              uint64_t ucap, uint32_t *pld,
+                                                              uint32_t *nsed, uint8_t *eb) {
+  const uint64_t n = *ucnt < ucap ? *ucnt : ucap;
+  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t) gridDim.x * blockDim.x) {
+    const uint64_t w = ulist[i], k = w >> 2;
+    const uint32_t kind = (uint32_t) (w & 3u), v = X[k];
+    if (kind == 0) pld[k] = li_dist32(k - li_search_prev<true>(T, X, pld, k, v, true));
+    else if (kind == 1) eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
+    else nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
+  }
+}
+
+// PL / NSE of row k (X[k] = v > 0) from the distances, searching on escape
+__device__ __forceinline__ uint64_t li_pl(const LiTree &T, const uint32_t *X, const uint32_t *pld,
+                                          uint64_t k, uint32_t v) {
+  const uint32_t d = pld[k];
+  return d != LI_ESC ? k - d : li_search_prev<false>(T, X, pld, k, v, true);
+}
+
+__device__ __forceinline__ uint64_t li_nse(const LiTree &T, const uint32_t *X, const uint32_t *nsed,
+                                           uint64_t k, uint32_t v) {
+  const uint32_t d = nsed[k];
+  return d != LI_ESC ? k + d : li_search_next<false>(T, X, nsed, k, v);
+}
+
 // each tile's boundary chain t0-1, PL(t0-1), ... down to the first X = 0
-// entry, at most LI_BD entries (one thread per tile: a latency chain of
-// dependent loads, thousands of them in flight)
-template <typename RowT>
-__global__ void __launch_bounds__(256) li_bchain_kernel(const uint32_t *X, const RowT *PL,
-                                                        uint64_t ntiles, RowT *brow, uint32_t *bx,
-                                                        uint32_t *bn) {
+// entry, at most LI_BD entries (one thread per tile: a chain of dependent
+// loads, thousands in flight)
+__global__ void __launch_bounds__(256) li_bchain_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
+                                                        uint64_t N, uint64_t ntiles, uint64_t *brow,
+                                                        uint32_t *bx, uint32_t *bn) {
   LI_FOR(t, ntiles) {
     int k = 0;
     if (t > 0) {
       uint64_t s = t * LI_T - 1;
-      for (; k < LI_BD;) {
+      while (k < LI_BD) {
         const uint32_t xs = X[s];
-        brow[t * LI_BD + k] = (RowT) s;
+        brow[t * LI_BD + k] = s;
         bx[t * LI_BD + k] = xs;
         k++;
         if (xs == 0) break;
-        s = PL[s];
+        s = li_pl(T, X, pld, s, xs);
       }
     }
     bn[t] = (uint32_t) k;
   }
 }
 
-// the tile's X (rows t0 .. t0 + LI_T, 0 past row N), PL and boundary chain
-// into LDS
-template <typename RowT, int STAGE>
-__device__ __forceinline__ void li_tile_load(const uint32_t *X, const RowT *PL, const RowT *brow,
-                                             const uint32_t *bx, const uint32_t *bn, uint64_t N,
-                                             uint64_t t, LiWalkTile<RowT, STAGE> &S) {
-  const uint64_t t0 = t * LI_T;
-  for (int k = threadIdx.x; k <= LI_T; k += LI_TPB) {
-    const uint64_t g = t0 + (uint64_t) k;
-    S.x[k] = g <= N ? X[g] : 0u;
-    if (k < LI_T) S.pl[k] = g < N ? PL[g] : li_none<RowT>();
+// the index of row o on tile t's boundary chain (o lies on it, X[o] > 0):
+// binary search over the entries held (rows strictly decreasing), else the
+// chain followed on past them
+__device__ int64_t li_bindex_far(const LiTree &T, const uint32_t *X, const uint32_t *pld,
+                                              const uint64_t *brow, uint64_t t, uint64_t o) {
+  int64_t m = LI_BD - 1;
+  uint64_t s = brow[t * LI_BD + LI_BD - 1];
+  while (s != o && X[s] > 0) {       // (o is on the chain: the guard only bounds the loop)
+    s = li_pl(T, X, pld, s, X[s]);
+    m++;
   }
-  const int nb = (int) bn[t];
-  if (threadIdx.x < (unsigned) nb) {
-    S.brow[threadIdx.x] = brow[t * LI_BD + threadIdx.x];
-    S.bx[threadIdx.x] = bx[t * LI_BD + threadIdx.x];
-  }
-  if (threadIdx.x == 0) S.nb = nb;
-  __syncthreads();
+  return m;
 }
 
-// a row before the tile: its index in the boundary chain, -1 past the
-// entries held (binary search, rows strictly decreasing)
-template <typename RowT, int STAGE>
-__device__ __forceinline__ int li_bfind(const LiWalkTile<RowT, STAGE> &S, uint64_t c) {
-  int lo = 0, hi = S.nb - 1;
+__device__ __forceinline__ int64_t li_bindex(const LiTree &T, const uint32_t *X, const uint32_t *pld,
+                                             const uint64_t *brow, uint32_t nb, uint64_t t,
+                                             uint64_t o) {
+  int lo = 0, hi = (int) nb - 1;
   while (lo <= hi) {
     const int mid = (lo + hi) >> 1;
-    const uint64_t r = (uint64_t) S.brow[mid];
-    if (r == c) return mid;
-    if (r > c) lo = mid + 1; else hi = mid - 1;
+    const uint64_t r = brow[t * LI_BD + mid];
+    if (r == o) return mid;
+    if (r > o) lo = mid + 1; else hi = mid - 1;
   }
-  return -1;
+  return li_bindex_far(T, X, pld, brow, t, o);
 }
 
-// Rows deeper down the boundary chain than the LDS copy holds (rare) are
-// read by calls: inlined, the compiler would wait for every memory
-// operation of the wave (vmcnt counts the stage's 16-byte stores too) at
-// each join after the branch, taken or not -- the walks would pay the
-// store latency on every step
-// (counted: how often the LDS copy of the chain falls short, a diagnostic
-// read by gt_lcpitv_far_reads)
-__device__ unsigned long long li_far_reads;
+// the affine map D(t+1) = a_t + b_t D_t of tile t: its last row's chain
+// inside the tile, then where it leaves (one thread per tile)
+struct LiAffine {
+  int64_t a;
+  int64_t b;
+};
 
-__device__ __noinline__ uint32_t li_x_far(const uint32_t *X, uint64_t c) {
-  atomicAdd(&li_far_reads, 1ull);
-  return X[c];
-}
-
-template <typename RowT>
-__device__ __noinline__ uint64_t li_pl_far(const RowT *PL, uint64_t c) {
-  atomicAdd(&li_far_reads, 1ull);
-  return (uint64_t) PL[c];
-}
-
-// X and PL of any row at or before the tile's end: the tile's and the
-// boundary chain's from LDS, rows deeper down the chain from HBM
-template <typename RowT, int STAGE>
-__device__ __forceinline__ uint32_t li_tx(const uint32_t *X, const LiWalkTile<RowT, STAGE> &S,
-                                          uint64_t t0, uint64_t c) {
-  if (c >= t0) return S.x[c - t0];
-  const int k = li_bfind(S, c);
-  return k >= 0 ? S.bx[k] : li_x_far(X, c);
-}
-
-template <typename RowT, int STAGE>
-__device__ __forceinline__ uint64_t li_tpl(const RowT *PL, const LiWalkTile<RowT, STAGE> &S,
-                                           uint64_t t0, uint64_t c) {
-  if (c >= t0) return (uint64_t) S.pl[c - t0];
-  const int k = li_bfind(S, c);
-  return k >= 0 && k + 1 < S.nb ? (uint64_t) S.brow[k + 1] : li_pl_far(PL, c);
-}
-
-// intervals popped at row t0 + i
-template <typename RowT, int STAGE>
-__device__ __forceinline__ uint32_t li_pops(const uint32_t *X, const RowT *PL,
-                                            const LiWalkTile<RowT, STAGE> &S, uint64_t t0, int i) {
-  const uint32_t Y = S.x[i + 1];
-  uint64_t c = t0 + (uint64_t) i;
-  uint32_t xc = S.x[i], n = 0;
-  while (xc > Y) {
-    n++;
-    c = li_tpl(PL, S, t0, c);
-    xc = li_tx(X, S, t0, c);
+struct LiAffineCompose {
+  __device__ __host__ LiAffine operator()(const LiAffine &f, const LiAffine &g) const {
+    return LiAffine{g.a + g.b * f.a, g.b * f.b};   // g after f
   }
-  return n;
-}
+};
 
-// the pops of row idx = t0 + i in order, deepest first: f(j, lcp, lb, fd, flb, newfather)
-template <typename RowT, int STAGE, typename F>
-__device__ __forceinline__ void li_walk(const uint32_t *X, const RowT *PL,
-                                        const LiWalkTile<RowT, STAGE> &S, uint64_t t0, int i, F f) {
-  const uint32_t Y = S.x[i + 1];
-  uint32_t xc = S.x[i];
-  if (xc <= Y) return;
-  uint64_t nx = S.pl[i];
-  uint32_t xn = li_tx(X, S, t0, nx);
-  for (uint32_t j = 0;; j++) {
-    const uint32_t fd = xn > Y ? xn : Y;
-    uint64_t nn = 0, flb = 0;
-    if (xn >= Y && fd > 0) {
-      nn = li_tpl(PL, S, t0, nx);
-      flb = nn;
-    } else if (fd > 0) {
-      flb = nx;                          // the new father (Y, nx)
+__global__ void __launch_bounds__(256) li_tail_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
+                                                      uint64_t N, uint64_t ntiles, const uint64_t *brow,
+                                                      const uint32_t *bn, LiAffine *aff) {
+  LI_FOR(t, ntiles) {
+    const uint64_t t0 = t * LI_T;
+    const uint64_t last = (t0 + LI_T <= N + 1 ? t0 + LI_T : N + 1) - 1;
+    int64_t steps = 0;
+    uint64_t c = last;
+    uint32_t xc = X[c];
+    LiAffine f{0, 0};
+    while (xc > 0) {
+      steps++;
+      const uint64_t p = li_pl(T, X, pld, c, xc);
+      const uint32_t xp = X[p];
+      if (p < t0 && xp > 0) {
+        f.a = steps - li_bindex(T, X, pld, brow, bn[t], t, p);
+        f.b = 1;
+        break;
+      }
+      c = p;
+      xc = xp;
     }
-    f(j, xc, nx, fd, flb, xn < Y);
-    if (xn <= Y) break;
-    xc = xn;
-    nx = nn;
-    xn = li_tx(X, S, t0, nx);
+    if (f.b == 0) f.a = steps;
+    aff[t] = f;
   }
 }
 
-// pass 1 (plan): intervals popped in each tile
-template <typename RowT>
-__global__ void __launch_bounds__(LI_TPB) li_tile_count_kernel(const uint32_t *X, const RowT *PL,
-                                                               const RowT *brow, const uint32_t *bx,
-                                                               const uint32_t *bn, uint64_t N,
-                                                               uint64_t ntiles, uint32_t *tile_cnt) {
-  __shared__ LiWalkTile<RowT, 16> S;
+// d of every row: per tile, pointer jumping in LDS over PL inside the tile;
+// a chain leaving it ends on the boundary chain at index m, d = steps +
+// D_t - m (Dt[t] = D_t from the scan of the affine maps)
+struct LiDepthLds {
+  int32_t anc[2][LI_T];                  // >= 0: tile row; -1: d known; -2 - m: exit at chain index m
+  uint32_t dist[2][LI_T];
+};
+
+__global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
+                                                          uint64_t N, uint64_t ntiles, const uint64_t *brow,
+                                                          const uint32_t *bn, const LiAffine *scan,
+                                                          uint32_t *dep) {
+  __shared__ LiDepthLds S;
+  const int tid = threadIdx.x;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t t0 = t * LI_T;
-    li_tile_load(X, PL, brow, bx, bn, N, t, S);
-    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
-    uint32_t n = 0;
-    for (int i = threadIdx.x; i < nrows; i += LI_TPB) n += li_pops(X, PL, S, t0, i);
-    uint32_t tot;
-    (void) li_block_excl(n, &tot);
-    if (threadIdx.x == 0) tile_cnt[t] = tot;
+    const int nrows = N + 1 - t0 < LI_T ? (int) (N + 1 - t0) : LI_T;
+    const int64_t Dt = t == 0 ? 0 : scan[t - 1].a;
+    for (int i = tid; i < LI_T; i += LI_TPB) {
+      const uint64_t k = t0 + (uint64_t) i;
+      int32_t anc = -1;
+      uint32_t dist = 0;
+      if (i < nrows) {
+        const uint32_t v = X[k];
+        if (v > 0) {
+          const uint64_t p = li_pl(T, X, pld, k, v);
+          dist = 1;
+          if (p >= t0) {
+            anc = (int32_t) (p - t0);
+          } else if (X[p] > 0) {
+            anc = (int32_t) (-2 - li_bindex(T, X, pld, brow, bn[t], t, p));
+          }
+        }
+      }
+      S.anc[0][i] = anc;
+      S.dist[0][i] = dist;
+    }
+    __syncthreads();
+    // (at most 11 rounds: 2^11 = LI_T; a tile's chains are short, so the
+    // rounds stop once no row points inside the tile any more)
+    int cur = 0;
+    for (int round = 0; round < 12; round++) {
+      int open = 0;
+      for (int i = tid; i < LI_T; i += LI_TPB) {
+        int32_t a = S.anc[cur][i];
+        uint32_t d = S.dist[cur][i];
+        if (a >= 0) {
+          d += S.dist[cur][a];
+          a = S.anc[cur][a];
+        }
+        open |= a >= 0;
+        S.anc[cur ^ 1][i] = a;
+        S.dist[cur ^ 1][i] = d;
+      }
+      cur ^= 1;
+      if (!__syncthreads_or(open)) break;
+    }
+    for (int i = tid; i < nrows; i += LI_TPB) {
+      const int32_t a = S.anc[cur][i];
+      int64_t d = S.dist[cur][i];
+      if (a <= -2) d += Dt - (int64_t) (-2 - a);
+      dep[t0 + i] = (uint32_t) d;
+    }
+    __syncthreads();
   }
 }
 
-// The writing passes split a tile into four 512-row quarters, one per
-// wave: the waves' interval totals are exchanged once per tile (the only
-// workgroup barriers besides the tile load), then each wave walks its
-// quarter in 64-row steps on its own -- wave-level scans for the offsets,
-// its own part of the stage, its own 16-byte stores.
-#define LI_WAVES (LI_TPB / 64)
-#define LI_QROWS (LI_T / LI_WAVES)
-
-__device__ __forceinline__ uint32_t li_wave_excl(uint32_t v, uint32_t *total) {
-  const int lane = threadIdx.x & 63;
-  uint32_t incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
+// pops of row r (r < N): cnt(r) above; the exclusive scan's input
+struct LiCnt {
+  const uint32_t *X, *dep;
+  const uint8_t *eb;
+  uint64_t N;
+  __device__ __host__ uint64_t operator()(uint64_t r) const {
+    if (r >= N) return 0;
+    const uint32_t dr = dep[r];
+    if (X[r + 1] == 0) return dr;
+    return (uint64_t) ((int64_t) dr - (int64_t) dep[r + 1] + (int64_t) eb[r + 1]);
   }
-  *total = __shfl(incl, 63, 64);
-  return incl - v;
-}
+};
 
-// the wave's LDS stores before its loads (and its loads before the next
-// stores): LDS operations of one wave complete in order once waited for
-__device__ __forceinline__ void li_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// intervals popped before each wave's quarter, from tile_off[t]; ends with
-// a barrier
-template <typename RowT, int STAGE, typename Weight>
-__device__ __forceinline__ uint64_t li_wave_base(const uint32_t *X, const RowT *PL,
-                                                 const LiWalkTile<RowT, STAGE> &S, uint64_t t0,
-                                                 int nrows, uint64_t tile_base, uint32_t *sWT) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t n = 0;
-  for (int r = 0; r < LI_QROWS / 64; r++) {
-    const int i = wave * LI_QROWS + r * 64 + lane;
-    if (i < nrows) n += li_pops(X, PL, S, t0, i);
-  }
-  uint32_t tot;
-  (void) li_wave_excl(n, &tot);
-  if (lane == 0) sWT[wave] = tot;
-  __syncthreads();
-  uint64_t base = tile_base;
-  for (int w = 0; w < wave; w++) base += sWT[w];
-  return base;
-}
-
-// pass 2 (plan): the interval records (lcp, lb, rb, father lcp, father lb)
-// in pop order at tile_off[t] on (staged per 64-row step, stored as
-// contiguous 16-byte pieces), and the stream position of the first edge to
+// the interval records (lcp, lb, rb, father lcp, father lb) in pop order,
+// one per rightmost l-index; and the stream position of the first edge to
 // the root (the reference's firstedgefromroot, esa-bottomup.c:134-141)
-#define LI_ITV_WCAP (LI_ITV_CAP / LI_WAVES)   // records staged per wave step
-template <typename RowT>
-__global__ void __launch_bounds__(LI_TPB) li_tile_itv_kernel(const uint32_t *X, const RowT *PL,
-                                                             const RowT *brow, const uint32_t *bx,
-                                                             const uint32_t *bn, uint64_t N,
-                                                             uint64_t ntiles, const uint64_t *tile_off,
-                                                             uint64_t *itv, unsigned long long *first) {
-  __shared__ LiWalkTile<RowT, 40 * LI_ITV_CAP> S;
-  __shared__ uint32_t sWT[LI_WAVES];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint64_t *stage = reinterpret_cast<uint64_t *>(S.stage) + 5 * LI_ITV_WCAP * wave;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t t0 = t * LI_T;
-    li_tile_load(X, PL, brow, bx, bn, N, t, S);
-    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
-    uint64_t base = li_wave_base<RowT, 40 * LI_ITV_CAP, int>(X, PL, S, t0, nrows, tile_off[t], sWT);
-    for (int r = 0; r < LI_QROWS / 64; r++) {
-      const int i = wave * LI_QROWS + r * 64 + lane;
-      const bool row = i < nrows;
-      const uint32_t n = row ? li_pops(X, PL, S, t0, i) : 0u;
-      uint32_t tot;
-      const uint32_t off = li_wave_excl(n, &tot);
-      if (row) {
-        const uint64_t idx = t0 + (uint64_t) i;
-        const uint64_t pos = idx + 2 * (base + off);       // the row's leaf event
-        if (S.x[i] == 0 && S.x[i + 1] == 0) atomicMin(first, (unsigned long long) pos);
-        li_walk(X, PL, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t fd, uint64_t flb,
-                                     bool) {
-          const uint32_t k = off + j;
-          uint64_t *w = k < LI_ITV_WCAP ? stage + 5 * k : itv + 5 * (base + k);
-          w[0] = lcp;
-          w[1] = lb;
-          w[2] = idx;
-          w[3] = fd;
-          w[4] = flb;
-          if (fd == 0) atomicMin(first, (unsigned long long) (pos + 2 + 2 * j));
-        });
-      }
-      li_wave_sync();
-      const uint32_t staged = tot < LI_ITV_WCAP ? tot : LI_ITV_WCAP;
-      // words [5 base, 5 (base + staged)) as aligned 16-byte pairs
-      const uint64_t w0 = 5 * base, w1 = 5 * (base + staged);
-      for (uint64_t q = (w0 >> 1) + lane; 2 * q < w1; q += 64) {
-        const uint64_t a = 2 * q;
-        const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
-        const uint64_t v0 = lo_ok ? stage[a - w0] : 0, v1 = hi_ok ? stage[a + 1 - w0] : 0;
-        if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(itv)[q] = make_ulonglong2(v0, v1);
-        else if (lo_ok) itv[a] = v0;
-        else if (hi_ok) itv[a + 1] = v1;   // (neither: an empty step at an odd word)
-      }
-      li_wave_sync();
-      base += tot;
+template <typename PT>
+__global__ void __launch_bounds__(256) li_itv_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
+                                                     const uint32_t *nsed, const uint32_t *dep,
+                                                     const PT *P, uint64_t N, uint64_t *itv,
+                                                     unsigned long long *first) {
+  LI_FOR(c, N) {
+    const uint32_t v = X[c];
+    if (v == 0) {
+      if (X[c + 1] == 0) atomicMin(first, (unsigned long long) (c + 2 * (uint64_t) P[c]));
+      continue;
     }
-    __syncthreads();                     // S and sWT are rewritten by the next tile
+    const uint64_t q = li_nse(T, X, nsed, c, v);
+    const uint32_t xq = X[q];
+    if (xq == v) continue;               // not the interval's rightmost l-index
+    const uint64_t rb = q - 1, lb = li_pl(T, X, pld, c, v);
+    const uint64_t j = (uint64_t) (dep[rb] - dep[c]);
+    const uint64_t pos = (uint64_t) P[rb] + j;
+    const uint32_t xl = X[lb];
+    const uint32_t fd = xl > xq ? xl : xq;
+    const uint64_t flb = fd == 0 ? 0 : (xl >= xq ? li_pl(T, X, pld, lb, xl) : lb);
+    uint64_t *w = itv + 5 * pos;
+    w[0] = v;
+    w[1] = lb;
+    w[2] = rb;
+    w[3] = fd;
+    w[4] = flb;
+    if (fd == 0) atomicMin(first, (unsigned long long) (rb + 2 * (uint64_t) P[rb] + 2 + 2 * j));
   }
 }
 
-// pass 3 (events): the gt_esa_bottomup event stream of the tile's rows,
-// every event at its position in the reference's order: per row its leaf
-// edge, then per pop its lcp-interval and branching-edge events
+// the gt_esa_bottomup event stream, every event at its position in the
+// reference's order: per row its leaf edge, then per pop its lcp-interval
+// and branching-edge events
 //   (0, firstsucc, fd, flb, leafnumber, 0, 0)   visit_leaf_edge
 //   (2, 0, lcp, lb, rb, 0, 0)                   visit_lcp_interval
 //   (1, firstsucc, fd, flb, sd, slb, srb)       visit_branching_edge
-// staged per 64-row wave step as 4-word descriptors (a leaf's holds its
-// leaf number, read while walking; the branching edge takes sd, slb, srb
-// from the lcp-interval event before it) and stored as aligned 16-byte
-// pieces of the 7-word records; events past the stage go straight to memory
+// A workgroup takes 256 rows at a time: the rows' leaf data and the
+// chunk's interval records (P(r0) .. P(r0 + 256), consecutive) are read
+// coalesced and staged as one 4-word descriptor per event (the branching
+// edge takes sd, slb, srb from the lcp-interval event before it), then the
+// chunk's 7-word records are stored as aligned 16-byte pieces; events past
+// the stage go straight to memory.
+#define LI_EV_STAGE 16384               // event staging bytes per workgroup
+
 template <typename DT>
 struct LiDesc {                         // one staged event
   DT a, b, c, d;                        // a: kind | firstsucc << 2
@@ -609,104 +851,94 @@ __device__ __forceinline__ uint64_t li_event_word(const LiDesc<DT> *st, uint32_t
   return f == 4 ? (uint64_t) d.d : 0u;   // leaf number / rb
 }
 
-template <typename RowT, typename SufT>
-__global__ void __launch_bounds__(LI_TPB) li_tile_events_kernel(const uint32_t *X, const RowT *PL,
-                                                                const RowT *brow, const uint32_t *bx,
-                                                                const uint32_t *bn, uint64_t N,
-                                                                uint64_t ntiles,
-                                                                const uint64_t *tile_off,
-                                                                const SufT *suf,
-                                                                const unsigned long long *firstp,
-                                                                uint64_t *ev) {
-  // descriptor words wide enough for row indices and leaf numbers
-  using DT = typename std::conditional<(sizeof (RowT) >= sizeof (SufT)), RowT, SufT>::type;
-  __shared__ LiWalkTile<RowT, LI_EV_STAGE> S;
-  __shared__ uint32_t sWT[LI_WAVES];
-  constexpr uint32_t cap = LI_EV_STAGE / sizeof (LiDesc<DT>) / LI_WAVES;   // per wave step
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  LiDesc<DT> *stage = reinterpret_cast<LiDesc<DT> *>(S.stage) + cap * wave;
+template <typename PT, typename SufT, typename DT>
+__global__ void __launch_bounds__(256, 8) li_events_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
+                                                        const PT *P, const uint64_t *itv, uint64_t N,
+                                                        const SufT *suf, const unsigned long long *firstp,
+                                                        uint64_t *ev) {
+  __shared__ __attribute__((aligned(16))) unsigned char stage_bytes[LI_EV_STAGE];
+  __shared__ uint64_t sP[2];
+  LiDesc<DT> *stage = reinterpret_cast<LiDesc<DT> *>(stage_bytes);
+  constexpr uint32_t cap = LI_EV_STAGE / sizeof (LiDesc<DT>);
   const uint64_t first = *firstp;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t t0 = t * LI_T;
-    li_tile_load(X, PL, brow, bx, bn, N, t, S);
-    const int nrows = N - t0 < LI_T ? (int) (N - t0) : LI_T;
-    // stream position of the wave's next event: the rows before it and two
-    // events per interval popped before it
-    const uint64_t ib = li_wave_base<RowT, LI_EV_STAGE, int>(X, PL, S, t0, nrows, tile_off[t], sWT);
-    uint64_t ebase = t0 + (uint64_t) (wave * LI_QROWS) + 2 * ib;
-    // the leaf numbers of the wave's rows, loaded before its first store (a
-    // load inside the steps would wait for the stores before it)
-    uint64_t leaves[LI_QROWS / 64];
-#pragma unroll
-    for (int r = 0; r < LI_QROWS / 64; r++) {
-      const int i = wave * LI_QROWS + r * 64 + lane;
-      leaves[r] = i < nrows && suf != nullptr ? (uint64_t) suf[t0 + (uint64_t) i] : 0u;
+  const uint64_t nchunks = (N + 255) / 256;
+  for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const uint64_t r0 = ch * 256;
+    const uint64_t r = r0 + threadIdx.x;
+    const bool row = r < N;
+    // the row's data and the chunk's record range
+    uint64_t Pr = 0, leaf = 0, flb = 0;
+    uint32_t xr = 0, y = 0;
+    if (row) {
+      Pr = P[r];
+      xr = X[r];
+      y = X[r + 1];
+      leaf = suf != nullptr ? (uint64_t) suf[r] : 0u;
+      if (y <= xr && xr > 0) flb = li_pl(T, X, pld, r, xr);
     }
-#pragma unroll
-    for (int r = 0; r < LI_QROWS / 64; r++) {
-      const int i = wave * LI_QROWS + r * 64 + lane;
-      const bool row = i < nrows;
-      const uint64_t idx = t0 + (uint64_t) i;
-      const uint64_t leaf = leaves[r];
-      const uint32_t n = row ? li_pops(X, PL, S, t0, i) : 0u;
-      uint32_t tot;
-      const uint32_t off = li_wave_excl(row ? 1u + 2u * n : 0u, &tot);
-      if (row) {
-        const uint32_t xi = S.x[i], Y = S.x[i + 1];
-        const uint64_t pos = ebase + off;
-        uint64_t fs, fd, flb;
-        if (Y <= xi) {
-          fs = (xi == 0 && pos == first) ? 1u : 0u;
-          fd = xi;
-          flb = xi == 0 ? 0 : (uint64_t) S.pl[i];
-        } else {
-          fs = 1;
-          fd = Y;
-          flb = idx;
-        }
-        if (off < cap) {
-          stage[off] = LiDesc<DT>{(DT) (fs << 2), (DT) fd, (DT) flb, (DT) leaf};
-        } else {
-          uint64_t *w = ev + 7 * pos;
-          w[0] = 0; w[1] = fs; w[2] = fd; w[3] = flb; w[4] = leaf; w[5] = 0; w[6] = 0;
-        }
-        li_walk(X, PL, S, t0, i, [&](uint32_t j, uint32_t lcp, uint64_t lb, uint32_t pfd,
-                                     uint64_t pflb, bool newfather) {
-          const uint32_t k = off + 1 + 2 * j;
-          const uint64_t bfs = newfather ? 1u : (pfd == 0 && pos + 2 + 2 * j == first) ? 1u : 0u;
-          if (k < cap) stage[k] = LiDesc<DT>{(DT) 2, (DT) lcp, (DT) lb, (DT) idx};
-          if (k + 1 < cap) {
-            stage[k + 1] = LiDesc<DT>{(DT) (1u | (bfs << 2)), (DT) pfd, (DT) pflb, (DT) 0};
-          } else {
-            uint64_t *w = ev + 7 * (ebase + k);
-            if (k >= cap) { w[0] = 2; w[1] = 0; w[2] = lcp; w[3] = lb; w[4] = idx; w[5] = 0; w[6] = 0; }
-            w[7] = 1; w[8] = bfs; w[9] = pfd; w[10] = pflb; w[11] = lcp; w[12] = lb; w[13] = idx;
-          }
-        });
-      }
-      li_wave_sync();
-      const uint32_t staged = tot < cap ? tot : cap;
-      const uint64_t w0 = 7 * ebase, w1 = 7 * (ebase + staged);
-      for (uint64_t q = (w0 >> 1) + lane; 2 * q < w1; q += 64) {
-        const uint64_t a = 2 * q;
-        const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
-        uint64_t v0 = 0, v1 = 0;
-        if (lo_ok) {
-          const uint32_t e = (uint32_t) (a - w0);
-          v0 = li_event_word(stage, e / 7, e % 7);
-        }
-        if (hi_ok) {
-          const uint32_t e = (uint32_t) (a + 1 - w0);
-          v1 = li_event_word(stage, e / 7, e % 7);
-        }
-        if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(ev)[q] = make_ulonglong2(v0, v1);
-        else if (lo_ok) ev[a] = v0;
-        else if (hi_ok) ev[a + 1] = v1;
-      }
-      li_wave_sync();
-      ebase += tot;
+    if (threadIdx.x == 0) {
+      sP[0] = P[r0];
+      sP[1] = P[r0 + 256 <= N ? r0 + 256 : N];
     }
-    __syncthreads();                     // S and sWT are rewritten by the next tile
+    __syncthreads();
+    const uint64_t k0 = sP[0], k1 = sP[1];
+    const uint64_t nrows = N - r0 < 256 ? N - r0 : 256;
+    const uint64_t E = nrows + 2 * (k1 - k0);     // the chunk's events
+    const uint64_t ebase = r0 + 2 * k0;           // stream position of its first
+    if (row) {
+      const uint64_t off = (r - r0) + 2 * (Pr - k0);
+      uint64_t fs, fd, fl;
+      if (y <= xr) {
+        fs = (xr == 0 && ebase + off == first) ? 1u : 0u;
+        fd = xr;
+        fl = flb;
+      } else {
+        fs = 1;
+        fd = y;
+        fl = r;
+      }
+      if (off < cap) {
+        stage[off] = LiDesc<DT>{(DT) (fs << 2), (DT) fd, (DT) fl, (DT) leaf};
+      } else {
+        uint64_t *w = ev + 7 * (ebase + off);
+        w[0] = 0; w[1] = fs; w[2] = fd; w[3] = fl; w[4] = leaf; w[5] = 0; w[6] = 0;
+      }
+    }
+    for (uint64_t k = k0 + threadIdx.x; k < k1; k += 256) {
+      const uint64_t *rec = itv + 5 * k;
+      const uint64_t lcp = rec[0], lb = rec[1], rb = rec[2], fd = rec[3], fl = rec[4];
+      const uint64_t slot = (rb - r0) + 2 * (k - k0) + 1;
+      const bool newfather = fd > 0 && fl == lb;
+      const uint64_t bfs = newfather ? 1u : (fd == 0 && ebase + slot + 1 == first) ? 1u : 0u;
+      if (slot < cap) stage[slot] = LiDesc<DT>{(DT) 2, (DT) lcp, (DT) lb, (DT) rb};
+      if (slot + 1 < cap) {
+        stage[slot + 1] = LiDesc<DT>{(DT) (1u | (bfs << 2)), (DT) fd, (DT) fl, (DT) 0};
+      } else {
+        uint64_t *w = ev + 7 * (ebase + slot);
+        if (slot >= cap) { w[0] = 2; w[1] = 0; w[2] = lcp; w[3] = lb; w[4] = rb; w[5] = 0; w[6] = 0; }
+        w[7] = 1; w[8] = bfs; w[9] = fd; w[10] = fl; w[11] = lcp; w[12] = lb; w[13] = rb;
+      }
+    }
+    __syncthreads();
+    const uint64_t staged = E < cap ? E : cap;
+    const uint64_t w0 = 7 * ebase, w1 = 7 * (ebase + staged);
+    for (uint64_t q = (w0 >> 1) + threadIdx.x; 2 * q < w1; q += 256) {
+      const uint64_t a = 2 * q;
+      const bool lo_ok = a >= w0, hi_ok = a + 1 < w1;
+      uint64_t v0 = 0, v1 = 0;
+      if (lo_ok) {
+        const uint32_t e = (uint32_t) (a - w0);
+        v0 = li_event_word(stage, e / 7, e % 7);
+      }
+      if (hi_ok) {
+        const uint32_t e = (uint32_t) (a + 1 - w0);
+        v1 = li_event_word(stage, e / 7, e % 7);
+      }
+      if (lo_ok && hi_ok) reinterpret_cast<ulonglong2 *>(ev)[q] = make_ulonglong2(v0, v1);
+      else if (lo_ok) ev[a] = v0;
+      else if (hi_ok) ev[a + 1] = v1;
+    }
+    __syncthreads();
   }
 }
 
@@ -727,16 +959,17 @@ static unsigned li_tile_grid(uint64_t ntiles) {
 
 struct GtLcpitvPlan {
   GtLcpitvDevInput in;
-  uint32_t *lev[LI_MAXLEV];
-  LiLevels L;
-  bool wide;                     // rows past 2^32: 64-bit row indices in the tiles
+  bool wide;                     // rows past 2^32: 64-bit P
   uint64_t ntiles;
+  uint32_t *X;                   // exact LCP, rows 0..N
+  uint32_t *pld, *nsed, *dep;    // PL / NSE distances, chain depths
+  uint8_t *eb;                   // e (row opens an interval)
+  uint32_t *tlev[LI_MAXLEV];     // tile minima and their 64-ary hierarchy
+  uint32_t *sch, *pch;           // the tiles' suffix / prefix minimum chains
+  LiTree T;                      // the searches' view of them
+  void *P;                       // pops before each row (u32, u64 when wide), N + 1
   uint64_t nitv;
   uint64_t *itv;                 // 5 * nitv, pop order
-  uint64_t *tile_off;            // intervals popped before each tile
-  void *pl;                      // PL of every row (RowT: u32, u64 when wide)
-  void *brow;                    // boundary chain of every tile (LI_BD RowT each)
-  uint32_t *bx, *bn;             // its X values, its length
   unsigned long long *first;     // stream position of the first root edge
   SmaxStreamMarks marks;         // streams the plan's work ran on
 };
@@ -748,23 +981,46 @@ extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
   // (events recorded where it was enqueued): nothing here waits, and no
   // other stream of the device is involved
   SmaxFence *fence = smax_marks_fence(&p->marks);
-  for (int l = 0; l < LI_MAXLEV; l++) smax_dev_free_fenced(p->lev[l], fence);
-  smax_dev_free_fenced(p->itv, fence);
-  smax_dev_free_fenced(p->tile_off, fence);
-  smax_dev_free_fenced(p->pl, fence);
-  smax_dev_free_fenced(p->brow, fence);
-  smax_dev_free_fenced(p->bx, fence);
-  smax_dev_free_fenced(p->bn, fence);
-  smax_dev_free_fenced(p->first, fence);
+  void *bufs[] = {p->X, p->pld, p->nsed, p->dep, p->eb, p->P, p->itv, p->first, p->sch, p->pch};
+  for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], fence);
+  for (int l = 0; l < LI_MAXLEV; l++) smax_dev_free_fenced(p->tlev[l], fence);
   smax_fence_release(fence);
   free(p);
+}
+
+template <typename PT>
+static hipError_t li_scan_pops(GtLcpitvPlan *p, hipStream_t s, void **tmp, size_t *tmp_bytes) {
+  const uint64_t N = p->in.nonspecials;
+  auto cnt = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
+                                              LiCnt{p->X, p->dep, p->eb, N});
+  size_t b = 0;
+  hipError_t e = rocprim::exclusive_scan(nullptr, b, cnt, (PT *) p->P, (PT) 0, (size_t) (N + 1),
+                                         rocprim::plus<PT>(), s);
+  if (e != hipSuccess) return e;
+  if (b > *tmp_bytes) {
+    if (*tmp) {
+      e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return e;
+      smax_dev_free(*tmp);
+      *tmp = NULL;
+    }
+    e = smax_dev_alloc(tmp, b);
+    if (e != hipSuccess) return e;
+    *tmp_bytes = b;
+  }
+  return rocprim::exclusive_scan(*tmp, b, cnt, (PT *) p->P, (PT) 0, (size_t) (N + 1),
+                                 rocprim::plus<PT>(), s);
 }
 
 extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitvDevInput *in,
                                             void *stream, char *errbuf, size_t errlen) {
   GtLcpitvPlan *p = NULL;
   hipStream_t s = (hipStream_t) stream;
-  uint32_t *derr = NULL, herr = 0, *tile_cnt = NULL;
+  uint32_t *derr = NULL, herr = 0, *bx = NULL, *bn = NULL, nitv32 = 0;
+  uint64_t *ulist = NULL, ucap = 0;
+  unsigned long long *ucnt = NULL, nunres = 0;
+  uint64_t *brow = NULL;
+  LiAffine *aff = NULL, *affs = NULL;
   void *tmp = NULL;
   size_t tmp_bytes = 0;
   uint64_t N;
@@ -791,115 +1047,131 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   p->in = *in;
   N = in->nonspecials;
   p->wide = N + 1 >= 0xffffffffull;
-  p->ntiles = (N + LI_T - 1) / LI_T;
+  p->ntiles = (N + 1 + LI_T - 1) / LI_T;     // rows 0..N
   LICHK(hipSetDevice(in->device));
   LICHK(smax_dev_alloc((void **) &derr, sizeof (uint32_t)));
   LICHK(hipMemsetAsync(derr, 0, sizeof (uint32_t), s));
   LICHK(smax_dev_alloc((void **) &p->first, sizeof (unsigned long long)));
   LICHK(hipMemcpyAsync(p->first, &none, sizeof none, hipMemcpyHostToDevice, s));
-  // level 0: exact LCP, then 64-ary mins until one entry remains
-  p->L.n[0] = N + 1;
-  LICHK(smax_dev_alloc((void **) &p->lev[0], sizeof (uint32_t) * (p->L.n[0] + LI_PAD)));
-  hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, s, in->lcp_dev, N,
-                     p->lev[0]);
+  // exact LCP
+  LICHK(smax_dev_alloc((void **) &p->X, sizeof (uint32_t) * (N + 1 + LI_PAD)));
+  hipLaunchKernelGGL(li_expand_kernel, dim3(li_blocks(N + 1)), dim3(256), 0, s, in->lcp_dev, N, p->X);
   LICHK(hipGetLastError());
   if (in->numllv > 0) {
     hipLaunchKernelGGL(li_llv_kernel, dim3(li_blocks(in->numllv)), dim3(256), 0, s, in->llv_dev,
-                       in->numllv, in->lcp_dev, N, p->lev[0], derr);
+                       in->numllv, in->lcp_dev, N, p->X, derr);
     LICHK(hipGetLastError());
   }
-  p->L.nlev = 1;
-  while (p->L.n[p->L.nlev - 1] > 1 && p->L.nlev < LI_MAXLEV) {
-    const int l = p->L.nlev;
-    p->L.n[l] = (p->L.n[l - 1] + 63) / 64;
-    LICHK(smax_dev_alloc((void **) &p->lev[l], sizeof (uint32_t) * (p->L.n[l] + LI_PAD)));
-    hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(p->L.n[l])), dim3(256), 0, s, p->lev[l - 1],
-                       p->L.n[l - 1], p->lev[l], p->L.n[l]);
+  // pass A: PL, e, NSE inside the tiles; the tile minima and their hierarchy
+  LICHK(smax_dev_alloc((void **) &p->pld, sizeof (uint32_t) * (N + 1)));
+  LICHK(smax_dev_alloc((void **) &p->nsed, sizeof (uint32_t) * (N + 1)));
+  LICHK(smax_dev_alloc((void **) &p->eb, N + 1));
+  p->T.TL.n[0] = p->ntiles;
+  LICHK(smax_dev_alloc((void **) &p->tlev[0], sizeof (uint32_t) * (p->ntiles + LI_PAD)));
+  LICHK(smax_dev_alloc((void **) &p->sch, sizeof (uint32_t) * LI_CHW * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &p->pch, sizeof (uint32_t) * LI_CHW * p->ntiles));
+  ucap = 3 * (N + 1) < (1ull << 22) ? 3 * (N + 1) : ((N + 1) / 4 > (1ull << 22) ? (N + 1) / 4 : (1ull << 22));
+  LICHK(smax_dev_alloc((void **) &ulist, sizeof (uint64_t) * ucap));
+  LICHK(smax_dev_alloc((void **) &ucnt, sizeof (unsigned long long)));
+  LICHK(hipMemsetAsync(ucnt, 0, sizeof (unsigned long long), s));
+  hipLaunchKernelGGL(li_ansv_kernel, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->X, N,
+                     p->ntiles, p->pld, p->nsed, p->eb, p->tlev[0], p->sch, p->pch, ulist, ucnt, ucap);
+  LICHK(hipGetLastError());
+  p->T.TL.nlev = 1;
+  while (p->T.TL.n[p->T.TL.nlev - 1] > 1 && p->T.TL.nlev < LI_MAXLEV) {
+    const int l = p->T.TL.nlev;
+    p->T.TL.n[l] = (p->T.TL.n[l - 1] + 63) / 64;
+    LICHK(smax_dev_alloc((void **) &p->tlev[l], sizeof (uint32_t) * (p->T.TL.n[l] + LI_PAD)));
+    hipLaunchKernelGGL(li_min64_kernel, dim3(li_blocks(p->T.TL.n[l])), dim3(256), 0, s, p->tlev[l - 1],
+                       p->T.TL.n[l - 1], p->tlev[l], p->T.TL.n[l]);
     LICHK(hipGetLastError());
-    p->L.nlev++;
+    p->T.TL.nlev++;
   }
-  if (p->L.n[p->L.nlev - 1] > 1) {
+  if (p->T.TL.n[p->T.TL.nlev - 1] > 1) {
     li_seterr(errbuf, errlen, "too many suffixes for the minimum hierarchy");
     goto fail;
   }
-  for (int l = 0; l < p->L.nlev; l++) p->L.lv[l] = p->lev[l];
-  // PL per row, pops per tile, their exclusive scan, the records
-  LICHK(smax_dev_alloc(&p->pl, (p->wide ? 8 : 4) * (N ? N : 1)));
-  if (p->ntiles > 0) {
-    if (p->wide)
-      hipLaunchKernelGGL(li_pl_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->L, N,
-                         p->ntiles, (uint64_t *) p->pl);
-    else
-      hipLaunchKernelGGL(li_pl_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->L, N,
-                         p->ntiles, (uint32_t *) p->pl);
-    LICHK(hipGetLastError());
+  for (int l = 0; l < p->T.TL.nlev; l++) p->T.TL.lv[l] = p->tlev[l];
+  p->T.sch = p->sch;
+  p->T.pch = p->pch;
+  // pass B
+  LICHK(hipMemcpyAsync(&nunres, ucnt, sizeof nunres, hipMemcpyDeviceToHost, s));
+  LICHK(hipStreamSynchronize(s));      // the list's length picks pass B's form
+  if (nunres <= ucap)
+    hipLaunchKernelGGL(li_resolve_list_kernel, dim3(li_blocks(nunres)), dim3(256), 0, s, p->T, p->X,
+                       ulist, ucnt, ucap, p->pld, p->nsed, p->eb);
+  else
+    hipLaunchKernelGGL(li_resolve_kernel, dim3(li_blocks((N + 4) / 4 < 4096 * 256 ? (N + 4) / 4 : 4096 * 256)),
+                     dim3(256), 0, s, p->T, p->X, N, p->pld,
+                     p->nsed, p->eb);
+  LICHK(hipGetLastError());
+  // depths: boundary chains, the tiles' affine maps and their scan, d
+  LICHK(smax_dev_alloc((void **) &brow, sizeof (uint64_t) * LI_BD * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &bx, sizeof (uint32_t) * LI_BD * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &bn, sizeof (uint32_t) * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &aff, sizeof (LiAffine) * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &affs, sizeof (LiAffine) * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &p->dep, sizeof (uint32_t) * (N + 1)));
+  hipLaunchKernelGGL(li_bchain_kernel, dim3(li_blocks(p->ntiles)), dim3(256), 0, s, p->T, p->X, p->pld, N,
+                     p->ntiles, brow, bx, bn);
+  LICHK(hipGetLastError());
+  hipLaunchKernelGGL(li_tail_kernel, dim3(li_blocks(p->ntiles)), dim3(256), 0, s, p->T, p->X, p->pld, N,
+                     p->ntiles, brow, bn, aff);
+  LICHK(hipGetLastError());
+  {
+    size_t b = 0;
+    LICHK(rocprim::inclusive_scan(nullptr, b, aff, affs, (size_t) p->ntiles, LiAffineCompose(), s));
+    LICHK(smax_dev_alloc(&tmp, b ? b : 16));
+    tmp_bytes = b ? b : 16;
+    LICHK(rocprim::inclusive_scan(tmp, b, aff, affs, (size_t) p->ntiles, LiAffineCompose(), s));
   }
-  LICHK(smax_dev_alloc(&p->brow, (p->wide ? 8 : 4) * LI_BD * (p->ntiles ? p->ntiles : 1)));
-  LICHK(smax_dev_alloc((void **) &p->bx, 4 * LI_BD * (p->ntiles ? p->ntiles : 1)));
-  LICHK(smax_dev_alloc((void **) &p->bn, 4 * (p->ntiles ? p->ntiles : 1)));
-  if (p->ntiles > 0) {
-    if (p->wide)
-      hipLaunchKernelGGL(li_bchain_kernel<uint64_t>, dim3(li_blocks(p->ntiles)), dim3(256), 0, s,
-                         p->lev[0], (const uint64_t *) p->pl, p->ntiles, (uint64_t *) p->brow, p->bx,
-                         p->bn);
-    else
-      hipLaunchKernelGGL(li_bchain_kernel<uint32_t>, dim3(li_blocks(p->ntiles)), dim3(256), 0, s,
-                         p->lev[0], (const uint32_t *) p->pl, p->ntiles, (uint32_t *) p->brow, p->bx,
-                         p->bn);
-    LICHK(hipGetLastError());
-  }
-  LICHK(smax_dev_alloc((void **) &tile_cnt, sizeof (uint32_t) * (p->ntiles + 1)));
-  LICHK(smax_dev_alloc((void **) &p->tile_off, sizeof (uint64_t) * (p->ntiles + 1)));
-  LICHK(hipMemsetAsync(tile_cnt + p->ntiles, 0, sizeof (uint32_t), s));
-  if (p->ntiles > 0) {
-    if (p->wide)
-      hipLaunchKernelGGL(li_tile_count_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0,
-                         s, p->lev[0], (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, tile_cnt);
-    else
-      hipLaunchKernelGGL(li_tile_count_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0,
-                         s, p->lev[0], (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, tile_cnt);
-    LICHK(hipGetLastError());
-  }
-  LICHK(rocprim::exclusive_scan(nullptr, tmp_bytes, tile_cnt, p->tile_off, (uint64_t) 0,
-                                (size_t) (p->ntiles + 1), rocprim::plus<uint64_t>(), s));
-  LICHK(smax_dev_alloc((void **) &tmp, tmp_bytes ? tmp_bytes : 16));
-  LICHK(rocprim::exclusive_scan(tmp, tmp_bytes, tile_cnt, p->tile_off, (uint64_t) 0,
-                                (size_t) (p->ntiles + 1), rocprim::plus<uint64_t>(), s));
-  LICHK(hipMemcpyAsync(&p->nitv, p->tile_off + p->ntiles, sizeof (uint64_t), hipMemcpyDeviceToHost, s));
+  hipLaunchKernelGGL(li_depth_kernel, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->T, p->X, p->pld,
+                     N, p->ntiles, brow, bn, affs, p->dep);
+  LICHK(hipGetLastError());
+  // pops per row, their exclusive scan P (P[N] = intervals), the records
+  LICHK(smax_dev_alloc(&p->P, (p->wide ? 8 : 4) * (N + 1)));
+  LICHK(p->wide ? li_scan_pops<uint64_t>(p, s, &tmp, &tmp_bytes) : li_scan_pops<uint32_t>(p, s, &tmp, &tmp_bytes));
+  if (p->wide)
+    LICHK(hipMemcpyAsync(&p->nitv, (uint64_t *) p->P + N, sizeof (uint64_t), hipMemcpyDeviceToHost, s));
+  else
+    LICHK(hipMemcpyAsync(&nitv32, (uint32_t *) p->P + N, sizeof (uint32_t), hipMemcpyDeviceToHost, s));
   LICHK(hipMemcpyAsync(&herr, derr, sizeof herr, hipMemcpyDeviceToHost, s));
   LICHK(hipStreamSynchronize(s));      // the interval count sizes the records
+  if (!p->wide) p->nitv = nitv32;
   if (herr & 1u) { li_seterr(errbuf, errlen, "lcp value >= 2^32-1 in .llv"); goto fail; }
   if (herr & 2u) { li_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
   LICHK(smax_dev_alloc((void **) &p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
-  if (p->ntiles > 0) {
+  if (N > 0) {
     if (p->wide)
-      hipLaunchKernelGGL(li_tile_itv_kernel<uint64_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s,
-                         p->lev[0], (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, p->itv, p->first);
+      hipLaunchKernelGGL(li_itv_kernel<uint64_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->T, p->X, p->pld,
+                         p->nsed, p->dep, (const uint64_t *) p->P, N, p->itv, p->first);
     else
-      hipLaunchKernelGGL(li_tile_itv_kernel<uint32_t>, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s,
-                         p->lev[0], (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, p->itv, p->first);
+      hipLaunchKernelGGL(li_itv_kernel<uint32_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->T, p->X, p->pld,
+                         p->nsed, p->dep, (const uint32_t *) p->P, N, p->itv, p->first);
     LICHK(hipGetLastError());
   }
   smax_marks_record(&p->marks, s);
   {
-    // the scratch buffers go back behind the plan's work on s
+    // the scratch buffers go back behind the plan's work on s (the tree
+    // keeps X, PL, P and the records for the events pass)
     SmaxStreamMarks m;
     smax_marks_init(&m);
     smax_marks_record(&m, s);
     SmaxFence *f = smax_marks_fence(&m);
-    smax_dev_free_fenced(derr, f);
-    smax_dev_free_fenced(tile_cnt, f);
-    smax_dev_free_fenced(tmp, f);
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucnt, p->nsed, p->dep, p->eb};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], f);
     smax_fence_release(f);
+    p->nsed = NULL;
+    p->dep = NULL;
+    p->eb = NULL;
   }
   *planp = p;
   return 0;
 fail:
   {
     (void) hipStreamSynchronize(s);    // nothing queued may still use a cached block
-    void *bufs[] = {derr, tile_cnt, tmp};
-    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
-      if (bufs[i]) smax_dev_free(bufs[i]);
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucnt};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   smax_marks_record(&p->marks, s);
   gt_lcpitv_plan_delete(p);
@@ -927,6 +1199,14 @@ extern "C" uint64_t gt_lcpitv_plan_num_events(const GtLcpitvPlan *p) {
   return p->in.nonspecials + 2 * p->nitv;
 }
 
+template <typename PT, typename SufT>
+static void li_launch_events(GtLcpitvPlan *p, hipStream_t s, const SufT *suf, uint64_t *ev) {
+  using DT = typename std::conditional<(sizeof (PT) >= sizeof (SufT)), PT, SufT>::type;
+  const uint64_t N = p->in.nonspecials;
+  hipLaunchKernelGGL((li_events_kernel<PT, SufT, DT>), dim3(li_blocks(N)), dim3(256), 0, s, p->T, p->X,
+                     p->pld, (const PT *) p->P, p->itv, N, suf, p->first, ev);
+}
+
 extern "C" int gt_lcpitv_plan_events(GtLcpitvPlan *p, uint64_t *events_dev, void *stream) {
   hipStream_t s = (hipStream_t) stream;
   const uint64_t N = p->in.nonspecials;
@@ -935,35 +1215,18 @@ extern "C" int gt_lcpitv_plan_events(GtLcpitvPlan *p, uint64_t *events_dev, void
   if (N == 0) return 0;
   // the tree (plan create, maybe on another stream) before the events
   if (smax_marks_wait(&p->marks, s) != hipSuccess) return -1;
-  const dim3 g(li_tile_grid(p->ntiles)), b(LI_TPB);
   const bool s4 = p->in.suf_dev != nullptr && p->in.suf_bytes == 4;
   const uint32_t *suf4 = s4 ? (const uint32_t *) p->in.suf_dev : nullptr;
   const uint64_t *suf8 = !s4 ? (const uint64_t *) p->in.suf_dev : nullptr;
   if (p->wide) {
-    if (s4)
-      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint32_t>), g, b, 0, s, p->lev[0],
-                         (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf4, p->first, events_dev);
-    else
-      hipLaunchKernelGGL((li_tile_events_kernel<uint64_t, uint64_t>), g, b, 0, s, p->lev[0],
-                         (const uint64_t *) p->pl, (const uint64_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf8, p->first, events_dev);
+    if (s4) li_launch_events<uint64_t, uint32_t>(p, s, suf4, events_dev);
+    else li_launch_events<uint64_t, uint64_t>(p, s, suf8, events_dev);
   } else {
-    if (s4)
-      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint32_t>), g, b, 0, s, p->lev[0],
-                         (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf4, p->first, events_dev);
-    else
-      hipLaunchKernelGGL((li_tile_events_kernel<uint32_t, uint64_t>), g, b, 0, s, p->lev[0],
-                         (const uint32_t *) p->pl, (const uint32_t *) p->brow, p->bx, p->bn, N, p->ntiles, p->tile_off, suf8, p->first, events_dev);
+    if (s4) li_launch_events<uint32_t, uint32_t>(p, s, suf4, events_dev);
+    else li_launch_events<uint32_t, uint64_t>(p, s, suf8, events_dev);
   }
   smax_marks_record(&p->marks, s);
   return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// diagnostic: far reads since the last call (current device), -1 on error
-extern "C" long long gt_lcpitv_far_reads(void) {
-  unsigned long long v = 0, z = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(li_far_reads), sizeof v) != hipSuccess) return -1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(li_far_reads), &z, sizeof z) != hipSuccess) return -1;
-  return (long long) v;
 }
 
 // ------------------------------------------------------------ host boundary
