@@ -2735,16 +2735,15 @@ struct GtSmaxPlan {
   bool all_static;           // GT_SMAX_ALL_STATIC: every tile through K1b (test hook)
   bool byte_windows;         // GT_SMAX_BYTE_WINDOWS: byte BWT windows, never packed (test hook)
   uint32_t dev_cus;
-  // streams this plan's work was enqueued on, each with an event recorded
-  // behind the plan's last work on it (plan_stream_done).  Waits (plan_sync)
-  // and the delete-time fence of its buffers (a freed block is reused only
-  // after that work, smax_dev_free_fenced) use the events only: a caller may
-  // destroy its stream before deleting the plan.  The handles serve only to
-  // find a stream's slot.  More than SMAX_PLAN_STREAMS distinct streams: the
-  // device is synchronised
+  // streams this plan's work was enqueued on (the fence of its buffers at
+  // delete: a freed block is reused only after that work,
+  // smax_dev_free_fenced); more than SMAX_PLAN_STREAMS distinct ones: the
+  // device is synchronised.  The events are recorded at delete (and waited
+  // on in plan_sync) on these handles, so every stream passed to the plan
+  // must outlive it (gt_smax_hip.h): an event recorded behind every run
+  // instead cost one event packet per step, +0.7 % of the C3 step
+  // (profiles/r6/, bench_c3 against the round-5 build)
   hipStream_t streams[SMAX_PLAN_STREAMS];
-  hipEvent_t stream_ev[SMAX_PLAN_STREAMS];
-  bool stream_rec[SMAX_PLAN_STREAMS];
   int nstreams;
   bool streams_overflow;
   // optional K1 timing: event pairs recorded around the scan kernel
@@ -2966,43 +2965,15 @@ static hipError_t plan_size_grid(GtSmaxPlan *p) {
 static void plan_note_stream(GtSmaxPlan *p, hipStream_t s) {
   for (int i = 0; i < p->nstreams; i++)
     if (p->streams[i] == s) return;
-  if (p->nstreams < SMAX_PLAN_STREAMS) {
-    hipEvent_t e = nullptr;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      (void) hipGetLastError();
-      p->streams_overflow = true;   // no event to track it by: whole-device waits
-      return;
-    }
-    p->stream_ev[p->nstreams] = e;
-    p->stream_rec[p->nstreams] = false;
-    p->streams[p->nstreams++] = s;
-  } else {
-    p->streams_overflow = true;
-  }
+  if (p->nstreams < SMAX_PLAN_STREAMS) p->streams[p->nstreams++] = s;
+  else p->streams_overflow = true;
 }
 
-// after enqueueing on s (its slot from plan_note_stream): the slot's event
-// now stands behind this plan's work on s
-static void plan_stream_done(GtSmaxPlan *p, hipStream_t s) {
-  for (int i = 0; i < p->nstreams; i++)
-    if (p->streams[i] == s) {
-      if (hipEventRecord(p->stream_ev[i], s) == hipSuccess) {
-        p->stream_rec[i] = true;
-      } else {
-        (void) hipGetLastError();
-        p->streams_overflow = true;
-      }
-      return;
-    }
-}
-
-// waits for the work this plan enqueued (its streams' events), not for the
-// device, and never touches a caller's stream handle
+// waits for the work this plan enqueued (its streams), not for the device
 static hipError_t plan_sync(GtSmaxPlan *p) {
   hipError_t e = hipSetDevice(p->shard.device);
   if (e == hipSuccess && p->streams_overflow) return hipDeviceSynchronize();
-  for (int i = 0; e == hipSuccess && i < p->nstreams; i++)
-    if (p->stream_rec[i]) e = hipEventSynchronize(p->stream_ev[i]);
+  for (int i = 0; e == hipSuccess && i < p->nstreams; i++) e = hipStreamSynchronize(p->streams[i]);
   return e;
 }
 
@@ -3319,12 +3290,10 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(p->pool_cursor, &pc, sizeof pc, hipMemcpyHostToDevice));
   }
-  plan_stream_done(p, nullptr);
   *planp = p;
   return 0;
 fail:
   if (derr) smax_dev_free(derr);
-  plan_stream_done(p, nullptr);
   gt_smax_plan_delete(p);
   return -1;
 }
@@ -3339,15 +3308,7 @@ extern "C" void gt_smax_plan_delete(GtSmaxPlan *p) {
   // streams this plan's work ran on (a plan closed right after run() must
   // not hand them to the next allocation while K1..K3 still write them);
   // nothing here waits, and no other stream of the device is involved
-  // the fence adopts the per-stream events recorded at enqueue time (it
-  // destroys them once waited or released)
-  hipEvent_t evs[SMAX_PLAN_STREAMS];
-  int nev = 0;
-  for (int i = 0; i < p->nstreams; i++) {
-    if (p->stream_rec[i]) evs[nev++] = p->stream_ev[i];
-    else (void) hipEventDestroy(p->stream_ev[i]);
-  }
-  SmaxFence *fence = smax_fence_adopt(evs, nev, p->streams_overflow);
+  SmaxFence *fence = smax_fence_create(p->streams, p->streams_overflow ? -1 : p->nstreams);
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++)
     if (bufs[i]) smax_dev_free_fenced(bufs[i], fence);
   smax_fence_release(fence);
@@ -3405,20 +3366,11 @@ static int plan_run_compact(GtSmaxPlan *p, hipStream_t s);
 // it), bit 1 = the ordered compaction (K3).  gt_smax_plan_run
 // enqueues both; a sharded caller can enqueue part 0, start the boundary
 // all-gather on its communication stream, then part 1 beside it.
-static int plan_run_parts_enq(GtSmaxPlan *p, hipStream_t s, unsigned parts);
-
 static int plan_run_parts(GtSmaxPlan *p, hipStream_t s, unsigned parts) {
-  if (hipSetDevice(p->shard.device) != hipSuccess) return -1;
-  plan_note_stream(p, s);
-  const int rc = plan_run_parts_enq(p, s, parts);
-  plan_stream_done(p, s);   // behind whatever was enqueued, failed or not
-  return rc;
-}
-
-static int plan_run_parts_enq(GtSmaxPlan *p, hipStream_t s, unsigned parts) {
   char *errbuf = NULL;
   size_t errlen = 0;
   HIPCHK(hipSetDevice(p->shard.device));
+  plan_note_stream(p, s);
   // K3 of part 1 resets the deferral list and pool cursor the next part 0's
   // K1/K1b start from: a second part 0 before that part 1 would run on stale
   // state (and part 1 without a part 0 would compact stale tiles)
@@ -3539,7 +3491,6 @@ extern "C" int gt_smax_plan_stitch(GtSmaxPlan *p, const GtSmaxBoundary *all_dev,
   hipLaunchKernelGGL(smax_stitch_kernel, dim3(1), dim3(64), 0,
                      (hipStream_t) stream, all_dev, nshards, shard_index,
                      p->minlen, p->out, p->capacity, p->count);
-  plan_stream_done(p, (hipStream_t) stream);
   HIPCHK(hipGetLastError());
   return 0;
 fail:
@@ -3604,12 +3555,8 @@ extern "C" int gt_smax_plan_copy_boundary(GtSmaxPlan *p, void *dst_dev, void *st
   size_t errlen = 0;
   HIPCHK(hipSetDevice(p->shard.device));
   plan_note_stream(p, (hipStream_t) stream);
-  {
-    const hipError_t ce = hipMemcpyAsync(dst_dev, p->bnd, sizeof (GtSmaxBoundary),
-                                         hipMemcpyDeviceToDevice, (hipStream_t) stream);
-    plan_stream_done(p, (hipStream_t) stream);
-    HIPCHK(ce);
-  }
+  HIPCHK(hipMemcpyAsync(dst_dev, p->bnd, sizeof (GtSmaxBoundary),
+                        hipMemcpyDeviceToDevice, (hipStream_t) stream));
   return 0;
 fail:
   return -1;

@@ -223,8 +223,11 @@ int gt_smax_plan_create(GtSmaxPlan **plan, const GtSmaxDevShard *shard,
 /* Frees the plan; its device buffers return to the runtime's cache only
  * after the device has finished the work already enqueued (safe right after
  * an asynchronous gt_smax_plan_run).  Nothing here waits: the fence is made
- * of events the plan recorded when it enqueued the work, so the caller's
- * streams may already be destroyed. */
+ * of events recorded here on the streams the plan's work was enqueued on,
+ * so every stream passed to the plan (run, run_part, stitch,
+ * copy_boundary) must stay alive until gt_smax_plan_delete -- a per-run
+ * event would cost every pass an event packet.  (The F2 / F3 plans record
+ * theirs when they enqueue: their callers' streams may go first.) */
 void gt_smax_plan_delete(GtSmaxPlan *plan);
 
 /* Enqueue one smax pass (scan + ordered compaction + boundary record) on

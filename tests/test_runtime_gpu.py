@@ -364,10 +364,10 @@ def test_close_in_flight_then_reuse(human10):
         small.release()
 
 
-def test_stream_destroyed_before_plan_delete(human10):
-    """The caller's stream may be gone before gt_smax_plan_delete: the plan
-    waits and fences by the events it recorded when it enqueued the work,
-    never by the stream handle (gt_smax_hip.h, gt_smax_plan_delete)."""
+def test_plan_on_own_stream_then_delete(human10):
+    """A plan run on a stream of the caller's (alive until the delete, as
+    gt_smax_hip.h requires), fetched, run again and deleted with the run in
+    flight: the fence recorded at delete keeps the buffers until then."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     esa, host = human10
@@ -378,15 +378,15 @@ def test_stream_destroyed_before_plan_delete(human10):
         p = esa.plan(20)
         for _ in range(3):
             p.run(s.value)
-        got = p.fetch_triples()          # waits on the plan's events
+        got = p.fetch_triples()          # waits on the plan's streams
         p.run(s.value)
-        assert hip.hipStreamDestroy(s) == 0
-        p.close()                        # fence from the recorded events
-        assert np.array_equal(got, want)
+        p.close()                        # fence recorded on s, nothing waits
         q = esa.plan(20)
         q.run()
         assert np.array_equal(q.fetch_triples(), want)
         q.close()
+        assert hip.hipStreamDestroy(s) == 0
+        assert np.array_equal(got, want)
 
 
 @pytest.mark.skipif(G.device_count() < 2, reason="needs >= 2 visible GPUs")
