@@ -218,6 +218,7 @@ def lib():
         L.gt_smax_plan_deferred_tiles.argtypes = [vp]
         L.gt_smax_plan_deferred_tiles.restype = ctypes.c_uint32
         L.gt_smax_plan_debug_tiles.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_uint32)]
+        L.gt_smax_plan_debug_windows.argtypes = [vp, vp]
         L.gt_maxpairs_hip_enumerate_to_buffer.argtypes = [ctypes.POINTER(GtSmaxInput), u32,
                                                           ctypes.POINTER(vp), ctypes.POINTER(u64), cs, sz]
         L.gt_maxpairs_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(GtMaxpairsDevInput),
@@ -876,6 +877,15 @@ class SmaxPlan:
                                           ctypes.byref(n)) != 0:
             raise SmaxError("gt_smax_plan_debug_tiles failed")
         return counts, deferred[: n.value].copy()
+
+    def debug_windows(self):
+        """Diagnostic: the plan's per-tile .llv window words, (num_tiles, 2)
+        uint32 (gt_smax_plan_debug_windows)."""
+        import numpy as np
+        w = np.zeros((self.num_tiles, 2), dtype=np.uint32)
+        if lib().gt_smax_plan_debug_windows(self.plan, w.ctypes.data) != 0:
+            raise SmaxError("gt_smax_plan_debug_windows failed")
+        return w
 
     def fetch_count(self):
         c = ctypes.c_uint64()

@@ -2539,89 +2539,261 @@ hipError_t smax_groups_from_planes(uint64_t *groups, const uint32_t *planes, uin
 
 // ------------------------------------------------------------ llv index
 
-// Packed groups [g_lo, g_hi) holding a special BWT row (the plan's choice of
-// K1's window stream): one atomic per wave
+// K1's 2-plane window stream from the packed BWT, one pass over the groups:
+// bwt2[g] = the code planes of group g, and the groups of [g_lo, g_hi) (the
+// plan's windows) holding a special row counted in *nspec and listed in
+// spec[] (the first spec_cap of them; one atomic per wave).  The plan picks
+// the 2-plane stream from the count and then flags the listed groups'
+// windows (smax_spec_mark_kernel).  Replaced a counting pass plus a
+// conversion pass over the 1.5 GB of groups (268 + 437 us at C3).
 __global__ void __launch_bounds__(256)
-smax_special_groups_kernel(const uint64_t *pk, uint64_t g_lo, uint64_t g_hi, uint32_t *count) {
+smax_bwt2_kernel(const uint64_t *pk, uint64_t ngroups, uint32_t *bwt2, uint64_t g_lo,
+                 uint64_t g_hi, uint32_t *nspec, uint64_t *spec, uint32_t spec_cap) {
   const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-  uint32_t c = 0;
-  for (uint64_t g = g_lo + blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; g < g_hi; g += stride)
-    c += ((pk[g] >> 32) & 0xffffull) != 0 ? 1u : 0u;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-  if ((threadIdx.x & 63) == 0 && c != 0) atomicAdd(count, c);
-}
-
-// K1's 2-plane window stream from the packed BWT: bwt2[g] = the code planes
-// of group g; a group with a special row flags every K1 window that reads it
-// (tile i's window: groups L/16 .. L/16 + 129, L = (tile_first + i) * TILE)
-// for the static K1b list
-__global__ void __launch_bounds__(256)
-smax_bwt2_kernel(const uint64_t *pk, uint64_t ngroups, uint32_t *bwt2, uint2 *llv_win,
-                 uint64_t tile_first, uint64_t num_tiles) {
-  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-  for (uint64_t g = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; g < ngroups; g += stride) {
-    const uint64_t w = pk[g];
-    bwt2[g] = (uint32_t) w;
-    if ((w >> 32) & 0xffffull) {
-      constexpr uint64_t GPT = SMAX_TILE / 16;                      // groups per tile
-      const uint64_t t_hi = g / GPT;                                 // L/16 <= g
-      const uint64_t t_lo = g >= 129 ? (g - 129 + GPT - 1) / GPT : 0; // g <= L/16 + 129
-      for (uint64_t t = t_lo; t <= t_hi; t++)
-        if (t >= tile_first && t - tile_first < num_tiles)
-          atomicOr(&llv_win[t - tile_first].y, SMAX_WIN_STATIC);
+  const uint32_t lane = threadIdx.x & 63u;
+  // wave-uniform trip count (the ballot below needs the whole wave)
+  for (uint64_t g0 = blockIdx.x * (uint64_t) blockDim.x; g0 < ngroups; g0 += stride) {
+    const uint64_t g = g0 + threadIdx.x;
+    bool sp = false;
+    if (g < ngroups) {
+      const uint64_t w = pk[g];
+      bwt2[g] = (uint32_t) w;
+      sp = g >= g_lo && g < g_hi && ((w >> 32) & 0xffffull) != 0;
+    }
+    const uint64_t m = __ballot(sp);
+    if (m == 0) continue;
+    uint32_t base = 0;
+    if (lane == (uint32_t) __builtin_ctzll(m)) base = atomicAdd(nspec, (uint32_t) __popcll(m));
+    base = __shfl(base, __builtin_ctzll(m), 64);
+    if (sp) {
+      const uint32_t k = base + (uint32_t) __popcll(m & ((1ull << lane) - 1ull));
+      if (k < spec_cap) spec[k] = g;
     }
   }
 }
 
+// Flags for the static K1b list every K1 window reading a group with a
+// special row (tile i's window: groups L/16 .. L/16 + 129, L = (tile_first +
+// i) * TILE): the listed groups, or (list == NULL: more special groups than
+// the list holds, the 2-plane stream forced by GT_SMAX_BW2 or the diagnostic
+// kernel) every group of [0, n) read again
+__device__ __forceinline__ void smax_spec_mark(uint64_t g, uint2 *llv_win, uint64_t tile_first,
+                                               uint64_t num_tiles) {
+  constexpr uint64_t GPT = SMAX_TILE / 16;                      // groups per tile
+  const uint64_t t_hi = g / GPT;                                 // L/16 <= g
+  const uint64_t t_lo = g >= 129 ? (g - 129 + GPT - 1) / GPT : 0; // g <= L/16 + 129
+  for (uint64_t t = t_lo; t <= t_hi; t++)
+    if (t >= tile_first && t - tile_first < num_tiles)
+      atomicOr(&llv_win[t - tile_first].y, SMAX_WIN_STATIC);
+}
+
+__global__ void __launch_bounds__(256)
+smax_spec_mark_kernel(const uint64_t *list, const uint64_t *pk, uint64_t n, uint2 *llv_win,
+                      uint64_t tile_first, uint64_t num_tiles) {
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (list != NULL) smax_spec_mark(list[i], llv_win, tile_first, num_tiles);
+    else if ((pk[i] >> 32) & 0xffffull) smax_spec_mark(i, llv_win, tile_first, num_tiles);
+  }
+}
+
 // u16 copies of the .llv values (larger values are flagged per tile by the
-// index kernel; those windows never read this array)
+// index kernels; those windows never read this array)
 __global__ void __launch_bounds__(256)
 smax_llv16_kernel(const GtSmaxLlv *llv, uint64_t numllv, uint16_t *out) {
   const uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
   if (i < numllv) out[i] = (uint16_t) llv[i].value;
 }
 
-__global__ void smax_llv_index_kernel(const GtSmaxLlv *llv, uint64_t numllv,
-                                      uint64_t base, uint64_t tile_first, uint64_t begin,
-                                      uint64_t end, uint32_t num_tiles, uint2 *win_out,
-                                      uint32_t *err, uint32_t all_static) {
-  const uint64_t t = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
-  if (t < numllv) {
-    if (llv[t].value > 0xffffffffull) atomicOr(err, 1u);
-    if (t > 0 && llv[t].position <= llv[t - 1].position) atomicOr(err, 2u);
+// .llv window index (plan time).  Tile t's window stages the entries with
+// positions in [K_lo(t), K_hi(t)) -- K_lo = g0 - LH (0 below), K_hi = g0 +
+// TILE + RH, g0 = base + (tile_first + t) * TILE -- and counts those below
+// g0 (its left halo).  Each bound is a lower_bound over the sorted
+// positions, found without a search: the keys of consecutive tiles are
+// TILE apart, so for an entry at position p the number of tiles whose key
+// is <= p is arithmetic, c(p); the entry lies below key(t) exactly for
+// t >= c(p), so lower_bound(key(t)) = #{entries : c <= t} = the first entry
+// with c > t: a max-scan over the tiles of where each run of equal c
+// starts (smax_llv_hist_kernel, then the three scan launches below).  One
+// pass over the entries instead of two dependent binary searches per tile
+// (815 us at C3: 1.45 M tiles, 11.7 M entries, 24 dependent loads a
+// search).
+struct SmaxLlvKeys {
+  int64_t a_lo, a_hi, a_g0;   // key(t) = a + t * TILE (K_lo clamped at 0)
+  uint32_t num_tiles;
+};
+
+// #{t in [0, nt) : max(a + t * TILE, 0) <= p}
+__device__ __forceinline__ uint32_t smax_tiles_le(int64_t a, uint64_t p, uint32_t nt) {
+  const int64_t d = (int64_t) p - a;
+  if (d < 0) return 0u;
+  const uint64_t c = (uint64_t) d / SMAX_TILE + 1;
+  return c < nt ? (uint32_t) c : nt;
+}
+
+// Pass 1, one thread per entry e (and one past the last): c is
+// nondecreasing in e, so the tiles whose lower bound is e are [c(e-1), c(e))
+// and A[c(e-1)] = e marks where that run starts -- one plain store, and no
+// other entry writes that word; lower_bound(key(t)) = max of A over [0, t],
+// a max-scan.  A[t].w: the tile's window holds a value >= 2^16 (K1 stages
+// u16).  err bit 1: a value >= 2^32, bit 2: positions not strictly
+// increasing.  (A histogram of c with one atomic per run of equal c cost
+// 434 us at C3: 7 M atomics on neighbouring words.)
+__global__ void __launch_bounds__(256)
+smax_llv_hist_kernel(const GtSmaxLlv *llv, uint64_t numllv, SmaxLlvKeys k, uint4 *A,
+                     uint32_t *err) {
+  const uint64_t e = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x;
+  if (e > numllv) return;
+  uint32_t c[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, cp[3] = {0u, 0u, 0u}, bad = 0;
+  uint64_t pos = 0, v = 0;
+  if (e < numllv) {
+    pos = llv[e].position;
+    v = llv[e].value;
+    c[0] = smax_tiles_le(k.a_lo, pos, k.num_tiles);
+    c[1] = smax_tiles_le(k.a_hi, pos, k.num_tiles);
+    c[2] = smax_tiles_le(k.a_g0, pos, k.num_tiles);
+    if (v > 0xffffffffull) bad |= 1u;
   }
-  if (t >= num_tiles) return;
-  const uint64_t g0 = base + (tile_first + t) * (uint64_t) SMAX_TILE;
-  const uint64_t key = g0 >= SMAX_LH ? g0 - SMAX_LH : 0;
-  const uint64_t key2 = g0 + SMAX_TILE + SMAX_RH;
-  uint64_t lo = 0, hi = numllv;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (llv[mid].position < key) lo = mid + 1; else hi = mid;
+  if (e > 0) {
+    const uint64_t pp = llv[e - 1].position;
+    cp[0] = smax_tiles_le(k.a_lo, pp, k.num_tiles);
+    cp[1] = smax_tiles_le(k.a_hi, pp, k.num_tiles);
+    cp[2] = smax_tiles_le(k.a_g0, pp, k.num_tiles);
+    if (e < numllv && pos <= pp) bad |= 2u;
   }
-  uint64_t lo2 = lo, hi2 = numllv;
-  while (lo2 < hi2) {
-    const uint64_t mid = (lo2 + hi2) >> 1;
-    if (llv[mid].position < key2) lo2 = mid + 1; else hi2 = mid;
+#pragma unroll
+  for (int q = 0; q < 3; q++)
+    if (c[q] > cp[q] && cp[q] < k.num_tiles)
+      reinterpret_cast<uint32_t *>(A)[4 * (uint64_t) cp[q] + q] = (uint32_t) e;
+  // the windows holding p: K_lo(t) <= p < K_hi(t), i.e. c_hi <= t < c_lo
+  if (e < numllv && v > 0xffffull)
+    for (uint32_t t = c[1]; t < c[0]; t++)
+      atomicOr(reinterpret_cast<uint32_t *>(A) + 4 * (uint64_t) t + 3, 1u);
+  if (bad) atomicOr(err, bad);
+}
+
+// The max-scan of A over the tiles, in three launches of this module (a
+// library scan's first call cost ~3 ms of one-time setup in a fresh
+// process): per-block maxima of 1024 tiles, one workgroup scanning them,
+// then each block's scan from its prefix, which also assembles the tiles'
+// llv_win words.
+#define SMAX_IDX_PER 4
+#define SMAX_IDX_BLK (256 * SMAX_IDX_PER)
+
+__device__ __forceinline__ uint3 smax_u3max(uint3 a, uint3 b) {
+  return make_uint3(a.x > b.x ? a.x : b.x, a.y > b.y ? a.y : b.y, a.z > b.z ? a.z : b.z);
+}
+
+// exclusive prefix maximum over the 256 threads of one uint3 each (0 for
+// thread 0); *total = the maximum
+__device__ __forceinline__ uint3 smax_block_excl3(uint3 v, uint3 *total) {
+  __shared__ uint3 sW[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint3 inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint3 o = make_uint3(__shfl_up(inc.x, d, 64), __shfl_up(inc.y, d, 64), __shfl_up(inc.z, d, 64));
+    if (lane >= d) inc = smax_u3max(inc, o);
   }
-  bool wide = false;                       // K1 stages values as u16
-  uint32_t halo = 0;                       // entries in the left halo [g0 - LH, g0)
-  for (uint64_t k = lo; k < lo2; k++) {
-    if (llv[k].value > 0xffffull) wide = true;
-    if (llv[k].position < g0) halo++;
+  if (lane == 63) sW[wave] = inc;
+  __syncthreads();
+  uint3 wo = make_uint3(0u, 0u, 0u);
+  for (int w = 0; w < wave; w++) wo = smax_u3max(wo, sW[w]);
+  // the thread's exclusive value: its lane predecessor's inclusive one
+  uint3 ex = make_uint3(__shfl_up(inc.x, 1, 64), __shfl_up(inc.y, 1, 64), __shfl_up(inc.z, 1, 64));
+  if (lane == 0) ex = make_uint3(0u, 0u, 0u);
+  *total = smax_u3max(smax_u3max(sW[0], sW[1]), smax_u3max(sW[2], sW[3]));
+  __syncthreads();   // sW before a next use
+  return smax_u3max(wo, ex);
+}
+
+__global__ void __launch_bounds__(256)
+smax_llv_bsum_kernel(const uint4 *hist, uint32_t nt, uint3 *bsum) {
+  const uint64_t t0 = blockIdx.x * (uint64_t) SMAX_IDX_BLK + threadIdx.x * (uint64_t) SMAX_IDX_PER;
+  uint3 s = make_uint3(0u, 0u, 0u);
+#pragma unroll
+  for (int q = 0; q < SMAX_IDX_PER; q++)
+    if (t0 + q < nt) {
+      const uint4 h = hist[t0 + q];
+      s = smax_u3max(s, make_uint3(h.x, h.y, h.z));
+    }
+  uint3 tot;
+  (void) smax_block_excl3(s, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// one workgroup: bsum[0..nb) -> exclusive prefixes, in place
+__global__ void __launch_bounds__(256) smax_llv_btop_kernel(uint3 *bsum, uint32_t nb) {
+  uint3 run = make_uint3(0u, 0u, 0u);
+  for (uint64_t c0 = 0; c0 < nb; c0 += SMAX_IDX_BLK) {
+    const uint64_t b0 = c0 + threadIdx.x * (uint64_t) SMAX_IDX_PER;
+    uint3 v[SMAX_IDX_PER], s = make_uint3(0u, 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < SMAX_IDX_PER; q++) {
+      v[q] = b0 + q < nb ? bsum[b0 + q] : make_uint3(0u, 0u, 0u);
+      s = smax_u3max(s, v[q]);
+    }
+    uint3 tot;
+    uint3 o = smax_u3max(run, smax_block_excl3(s, &tot));
+#pragma unroll
+    for (int q = 0; q < SMAX_IDX_PER; q++)
+      if (b0 + q < nb) {
+        bsum[b0 + q] = o;
+        o = smax_u3max(o, v[q]);
+      }
+    run = smax_u3max(run, tot);
   }
-  const uint32_t wn = (uint32_t) (lo2 - lo);   // <= SMAX_LDSB rows
-  // g0 < begin: the shard's first tile when begin is not tile-aligned (K1
-  // assumes every row of its tiles is owned)
-  // all_static (GT_SMAX_ALL_STATIC, a test hook): every tile through K1b's
-  // exact path
-  const bool stat = g0 < SMAX_LH || g0 < begin || g0 + SMAX_TILE + SMAX_RH > end || wide ||
-                    wn + ((uint32_t) lo & 7u) > SMAX_LLV_CAP || all_static;
-  const uint32_t nl8 = wn == 0 ? 0u : (wn + ((uint32_t) lo & 7u) + 7u) / 8u;
-  const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;
-  static_assert(SMAX_LLV_CAP / 8 < 64, "lane count fits SMAX_WIN_LANES");
-  win_out[t] = make_uint2((uint32_t) lo, wn | (halo << 12) | (nl << 17) | (stat ? SMAX_WIN_STATIC : 0u));
+}
+
+// each tile's three lower bounds (the inclusive scan at the tile) and its
+// llv_win word
+__global__ void __launch_bounds__(256)
+smax_llv_win_kernel(const uint4 *hist, const uint3 *bsum, uint32_t nt, uint64_t g0_first,
+                    uint64_t begin, uint64_t end, uint2 *win_out, uint32_t all_static) {
+  const uint64_t t0 = blockIdx.x * (uint64_t) SMAX_IDX_BLK + threadIdx.x * (uint64_t) SMAX_IDX_PER;
+  uint4 h[SMAX_IDX_PER];
+  uint3 s = make_uint3(0u, 0u, 0u);
+#pragma unroll
+  for (int q = 0; q < SMAX_IDX_PER; q++) {
+    h[q] = t0 + q < nt ? hist[t0 + q] : make_uint4(0u, 0u, 0u, 0u);
+    s = smax_u3max(s, make_uint3(h[q].x, h[q].y, h[q].z));
+  }
+  uint3 tot;
+  uint3 run = smax_u3max(bsum[blockIdx.x], smax_block_excl3(s, &tot));
+#pragma unroll
+  for (int q = 0; q < SMAX_IDX_PER; q++) {
+    const uint64_t t = t0 + q;
+    run = smax_u3max(run, make_uint3(h[q].x, h[q].y, h[q].z));
+    if (t >= nt) continue;
+    const uint64_t g0 = g0_first + t * (uint64_t) SMAX_TILE;
+    const uint32_t lo = run.x, wn = run.y - run.x;   // <= SMAX_LDSB rows
+    const uint32_t halo = run.z - run.x;             // entries in the left halo [g0 - LH, g0)
+    const bool wide = h[q].w != 0;                   // K1 stages values as u16
+    // g0 < begin: the shard's first tile when begin is not tile-aligned (K1
+    // assumes every row of its tiles is owned)
+    // all_static (GT_SMAX_ALL_STATIC, a test hook): every tile through K1b's
+    // exact path
+    const bool stat = g0 < SMAX_LH || g0 < begin || g0 + SMAX_TILE + SMAX_RH > end || wide ||
+                      wn + (lo & 7u) > SMAX_LLV_CAP || all_static;
+    const uint32_t nl8 = wn == 0 ? 0u : (wn + (lo & 7u) + 7u) / 8u;
+    const uint32_t nl = nl8 < SMAX_LLV_CAP / 8 ? nl8 : SMAX_LLV_CAP / 8;
+    static_assert(SMAX_LLV_CAP / 8 < 64, "lane count fits SMAX_WIN_LANES");
+    win_out[t] = make_uint2(lo, wn | (halo << 12) | (nl << 17) | (stat ? SMAX_WIN_STATIC : 0u));
+  }
+}
+
+// the plan's host-side scalars in one copy: the static list's length and
+// the first and last tiles' llv_win words
+__global__ void smax_plan_probe_kernel(const uint32_t *static_count, const uint2 *llv_win,
+                                       uint32_t num_tiles, uint32_t *out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  out[0] = *static_count;
+  const uint2 w0 = num_tiles ? llv_win[0] : make_uint2(0u, 0u);
+  const uint2 w1 = num_tiles ? llv_win[num_tiles - 1] : make_uint2(0u, 0u);
+  out[1] = w0.x;
+  out[2] = w0.y;
+  out[3] = w1.x;
+  out[4] = w1.y;
 }
 
 // ------------------------------------------------------------ stitch
@@ -2828,8 +3000,10 @@ hipError_t smax_plan_reserve(const GtSmaxDevShard *shard, uint64_t capacity) {
       sizeof (unsigned long long), sizeof (uint64_t) * nt, sizeof (uint32_t) * nt,
       sizeof (uint32_t) * (2 * smax_bs_stride(cg) + 1), sizeof (uint64_t), sizeof (GtSmaxBoundary),
       sizeof (uint2) * (nt + 2), sizeof (uint32_t), sizeof (uint32_t) * (2 * nt + 1),
-      sizeof (uint2) * (2 * nt + 1), sizeof (uint32_t), sizeof (uint32_t), sizeof (uint32_t),
-      sizeof (uint16_t) * (shard->numllv + 16), sizeof (uint32_t), sizeof (uint32_t) * (ngroups + 4),
+      sizeof (uint2) * (2 * nt + 1), sizeof (uint32_t), sizeof (uint32_t), sizeof (uint32_t) * 8,
+      sizeof (uint16_t) * (shard->numllv + 16), sizeof (uint4) * nt,
+      sizeof (uint3) * ((nt + SMAX_IDX_BLK - 1) / SMAX_IDX_BLK + 1), sizeof (uint32_t) * ngroups,
+      sizeof (uint64_t) * (std::max<uint64_t>(nt / 256u, 64u) / 2u + 1u),
       64 * nt, sizeof (uint32_t) * (nt + 1), sizeof (uint32_t)};
   // (not K1b's record pool: its size depends on the static list, an
   // estimate parked a block of up to ~2x the plan's need in the cache)
@@ -2983,7 +3157,11 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
                                    char *errbuf, size_t errlen) {
   GtSmaxPlan *p = (GtSmaxPlan *) calloc(1, sizeof *p);
   uint32_t *derr = NULL;
-  uint32_t herr = 0;
+  uint32_t probe[5] = {0u, 0u, 0u, 0u, 0u};
+  // plan-time scratch, returned once a blocking copy has passed its users
+  uint4 *ihist = NULL;
+  uint3 *ibsum = NULL;
+  uint64_t *spec = NULL;
   *planp = NULL;
   if (p == NULL) { seterr(errbuf, errlen, "out of memory"); return -1; }
   if (minlen == 0) { seterr(errbuf, errlen, "minlen must be >= 1"); free(p); return -1; }
@@ -3124,30 +3302,51 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   HIPCHK(hipMemset(p->defer_count, 0, sizeof (uint32_t)));
   HIPCHK(dalloc(&p->defer_last, sizeof (uint32_t)));
   HIPCHK(hipMemset(p->defer_last, 0, sizeof (uint32_t)));
-  HIPCHK(dalloc(&derr, sizeof (uint32_t)));
-  HIPCHK(hipMemset(derr, 0, sizeof (uint32_t)));
+  // plan-time scalars read back by the host: [0] the .llv errors, [1] the
+  // special groups in the windows' range, [2..6] smax_plan_probe_kernel's
+  HIPCHK(dalloc(&derr, sizeof (uint32_t) * 8));
+  HIPCHK(hipMemset(derr, 0, sizeof (uint32_t) * 8));
   if (shard->numllv > 0xffffffffull) {
     seterr(errbuf, errlen, "more than 2^32 .llv entries in one shard");
     goto fail;
   }
   {
-    const uint64_t work = shard->numllv > p->num_tiles ? shard->numllv : p->num_tiles;
-    const unsigned blocks = (unsigned) ((work + 255) / 256);
+    // the .llv window index: run starts of the entries over the tiles' keys,
+    // max-scanned (smax_llv_hist_kernel)
     HIPCHK(dalloc(&p->llv16, sizeof (uint16_t) * (shard->numllv + 16)));
-    HIPCHK(hipMemset(p->llv16, 0, sizeof (uint16_t) * (shard->numllv + 16)));
+    HIPCHK(hipMemset(p->llv16 + shard->numllv, 0, sizeof (uint16_t) * 16));
     if (shard->numllv)
       hipLaunchKernelGGL(smax_llv16_kernel, dim3((unsigned) ((shard->numllv + 255) / 256)),
                          dim3(256), 0, 0, shard->llv_dev, shard->numllv, p->llv16);
-    hipLaunchKernelGGL(smax_llv_index_kernel, dim3(blocks), dim3(256), 0, 0,
-                       shard->llv_dev, shard->numllv, shard->base, p->tile_first, shard->begin,
-                       shard->end, p->num_tiles, p->llv_win, derr, p->all_static ? 1u : 0u);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(&herr, derr, sizeof herr, hipMemcpyDeviceToHost));
+    if (p->num_tiles > 0) {
+      const uint64_t nt = p->num_tiles;
+      const int64_t g0f = (int64_t) (shard->base + p->tile_first * (uint64_t) SMAX_TILE);
+      SmaxLlvKeys k;
+      k.a_lo = g0f - SMAX_LH;
+      k.a_hi = g0f + SMAX_TILE + SMAX_RH;
+      k.a_g0 = g0f;
+      k.num_tiles = p->num_tiles;
+      const uint32_t nb = (uint32_t) ((nt + SMAX_IDX_BLK - 1) / SMAX_IDX_BLK);
+      HIPCHK(dalloc(&ihist, sizeof (uint4) * nt));
+      HIPCHK(dalloc(&ibsum, sizeof (uint3) * nb));
+      HIPCHK(hipMemset(ihist, 0, sizeof (uint4) * nt));
+      hipLaunchKernelGGL(smax_llv_hist_kernel, dim3((unsigned) ((shard->numllv + 1 + 255) / 256)),
+                         dim3(256), 0, 0, shard->llv_dev, shard->numllv, k, ihist, derr);
+      hipLaunchKernelGGL(smax_llv_bsum_kernel, dim3(nb), dim3(256), 0, 0, ihist, p->num_tiles, ibsum);
+      hipLaunchKernelGGL(smax_llv_btop_kernel, dim3(1), dim3(256), 0, 0, ibsum, nb);
+      hipLaunchKernelGGL(smax_llv_win_kernel, dim3(nb), dim3(256), 0, 0, ihist, ibsum, p->num_tiles,
+                         (uint64_t) g0f, shard->begin, shard->end, p->llv_win,
+                         p->all_static ? 1u : 0u);
+      HIPCHK(hipGetLastError());
+    } else if (shard->numllv) {
+      // no tiles: only the entries' checks
+      const SmaxLlvKeys k = {0, 0, 0, 0u};
+      hipLaunchKernelGGL(smax_llv_hist_kernel, dim3((unsigned) ((shard->numllv + 1 + 255) / 256)),
+                         dim3(256), 0, 0, shard->llv_dev, shard->numllv, k, (uint4 *) NULL, derr);
+      HIPCHK(hipGetLastError());
+    }
   }
-  if (herr & 1u) { seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
-  if (herr & 2u) { seterr(errbuf, errlen, ".llv positions not strictly increasing"); goto fail; }
-  smax_dev_free(derr);
-  derr = NULL;
   smax_phase_mark(" llv_index", &tpc);
   // K1's 2-plane window stream: the packed BWT without its special plane
   // (0.25 B per row instead of 0.5); a window that holds a special BWT row
@@ -3156,33 +3355,54 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   // (read sets: a separator every few hundred rows puts a special BWT row in
   // most windows, and a K1b tile costs ~14 K1 tiles; K1 then streams the u64
   // groups, specials and all).  GT_SMAX_BW2=0/1 overrides; the diagnostic
-  // kernel is a 2-plane one.
-  if (p->pk) {
-    const char *b2 = getenv("GT_SMAX_BW2");
-    const uint64_t g_lo = p->tile_first * (SMAX_TILE / 16);     // groups the windows read
-    const uint64_t g_hi = g_lo + (uint64_t) p->num_tiles * (SMAX_TILE / 16) + 2;
-    uint32_t *cnt = NULL, nsp = 0;
-    HIPCHK(dalloc(&cnt, sizeof (uint32_t)));
-    HIPCHK(hipMemset(cnt, 0, sizeof (uint32_t)));
-    hipLaunchKernelGGL(smax_special_groups_kernel,
-                       dim3((unsigned) std::min<uint64_t>((g_hi - g_lo + 255) / 256, 1u << 16)), dim3(256), 0, 0,
-                       p->bwtpk, g_lo, std::min<uint64_t>(g_hi, GT_SMAX_PK_GROUPS(shard->local_len)), cnt);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(&nsp, cnt, sizeof nsp, hipMemcpyDeviceToHost));
-    smax_dev_free(cnt);
-    // a special group flags at most two windows
-    // (the diagnostic kernel streams the 2-plane form: bw2 whatever
-    // GT_SMAX_BW2 says while GT_SMAX_DEBUG/STAMPS select it)
-    p->bw2 = p->dbg != 0 ? true
-           : b2 ? strtol(b2, NULL, 0) != 0
-                : 2ull * nsp <= std::max<uint32_t>(p->num_tiles / 256u, 64u);
-    if (p->bw2) {
+  // kernel is a 2-plane one.  The planes are written in the same pass that
+  // counts the special groups, and dropped when the plan does not take them.
+  {
+    uint32_t h[2] = {0u, 0u};
+    uint32_t spec_cap = 0;
+    if (p->pk) {
       const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
+      const uint64_t g_lo = p->tile_first * (SMAX_TILE / 16);     // groups the windows read
+      const uint64_t g_hi = std::min<uint64_t>(g_lo + (uint64_t) p->num_tiles * (SMAX_TILE / 16) + 2,
+                                               ngroups);
+      spec_cap = std::max<uint32_t>(p->num_tiles / 256u, 64u) / 2u + 1u;
       HIPCHK(dalloc(&p->bwt2, sizeof (uint32_t) * ngroups));
+      HIPCHK(dalloc(&spec, sizeof (uint64_t) * spec_cap));
       hipLaunchKernelGGL(smax_bwt2_kernel, dim3((unsigned) std::min<uint64_t>((ngroups + 255) / 256, 1u << 20)),
-                         dim3(256), 0, 0, p->bwtpk, ngroups, p->bwt2, p->llv_win, p->tile_first,
-                         (uint64_t) p->num_tiles);
+                         dim3(256), 0, 0, p->bwtpk, ngroups, p->bwt2, g_lo, g_hi, derr + 1, spec,
+                         spec_cap);
       HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipMemcpy(h, derr, sizeof h, hipMemcpyDeviceToHost));   // the index kernels are done
+    smax_phase_mark(" index+bwt2", &tpc);
+    smax_dev_free(ibsum);
+    smax_dev_free(ihist);
+    ibsum = NULL;
+    ihist = NULL;
+    if (h[0] & 1u) { seterr(errbuf, errlen, "lcp value >= 2^32 in .llv"); goto fail; }
+    if (h[0] & 2u) { seterr(errbuf, errlen, ".llv positions not strictly increasing"); goto fail; }
+    if (p->pk) {
+      const char *b2 = getenv("GT_SMAX_BW2");
+      const uint32_t nsp = h[1];
+      // a special group flags at most two windows
+      // (the diagnostic kernel streams the 2-plane form: bw2 whatever
+      // GT_SMAX_BW2 says while GT_SMAX_DEBUG/STAMPS select it)
+      p->bw2 = p->dbg != 0 ? true
+             : b2 ? strtol(b2, NULL, 0) != 0
+                  : 2ull * nsp <= std::max<uint32_t>(p->num_tiles / 256u, 64u);
+      if (p->bw2 && nsp > 0) {
+        const uint64_t ngroups = GT_SMAX_PK_GROUPS(shard->local_len);
+        const bool listed = nsp <= spec_cap;
+        const uint64_t n = listed ? nsp : ngroups;
+        hipLaunchKernelGGL(smax_spec_mark_kernel, dim3((unsigned) std::min<uint64_t>((n + 255) / 256, 1u << 20)),
+                           dim3(256), 0, 0, listed ? spec : (const uint64_t *) NULL, p->bwtpk, n,
+                           p->llv_win, p->tile_first, (uint64_t) p->num_tiles);
+        HIPCHK(hipGetLastError());
+      }
+      if (!p->bw2) {
+        smax_dev_free(p->bwt2);
+        p->bwt2 = NULL;
+      }
     }
   }
   // static K1b list (needs llv_win), copied to the front of K1b's list: one
@@ -3197,8 +3417,14 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     if (p->num_tiles > 0)
       hipLaunchKernelGGL(smax_static_defer_kernel, dim3((p->num_tiles + 255) / 256), dim3(256), 0, 0,
                        a, p->static_list, p->static_count);
+    hipLaunchKernelGGL(smax_plan_probe_kernel, dim3(1), dim3(64), 0, 0, p->static_count,
+                       (const uint2 *) p->llv_win, p->num_tiles, derr + 2);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(&p->n_static, p->static_count, sizeof (uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(probe, derr + 2, sizeof probe, hipMemcpyDeviceToHost));
+    p->n_static = probe[0];
+    smax_phase_mark(" static_list", &tpc);
+    smax_dev_free(spec);   // the marking kernel is done
+    spec = NULL;
     p->wide_cap = p->n_static + std::max<uint32_t>(256u, p->num_tiles / 256u);
     HIPCHK(dalloc(&p->pool, sizeof (GtSmaxRecord) *
                                 ((uint64_t) p->wide_cap * (SMAX_TILE / 2) + capacity)));
@@ -3216,11 +3442,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     // sees every .llv entry): first entry of the first window to the end
     // of the last one
     const char *dv = getenv("GT_SMAX_DENSE");   // diagnostic override: 0 / 1
-    uint2 w0 = make_uint2(0, 0), w1 = make_uint2(0, 0);
-    if (p->num_tiles > 0) {
-      HIPCHK(hipMemcpy(&w0, p->llv_win, sizeof w0, hipMemcpyDeviceToHost));
-      HIPCHK(hipMemcpy(&w1, p->llv_win + (p->num_tiles - 1), sizeof w1, hipMemcpyDeviceToHost));
-    }
+    const uint2 w0 = make_uint2(probe[1], probe[2]), w1 = make_uint2(probe[3], probe[4]);
     const uint64_t inrange = (uint64_t) w1.x + SMAX_WIN_N(w1.y) - w0.x;
     const uint64_t rows = (uint64_t) p->num_tiles * SMAX_TILE;
     p->dense = dv ? strtol(dv, NULL, 0) != 0
@@ -3239,6 +3461,7 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
   }
   // K1's grid, from the occupancy of the variant this plan launches (the
   // u64-group kernels hold 5 waves per SIMD, the 2-plane ones 6)
+  smax_phase_mark(" pool", &tpc);
   HIPCHK(plan_size_grid(p));
   if (p->sched_n > 1) {
     // the schedule's per-workgroup entries: {first tile, stride, end, 0},
@@ -3290,10 +3513,16 @@ extern "C" int gt_smax_plan_create(GtSmaxPlan **planp,
     HIPCHK(hipMemcpy(p->defer_count, &p->n_static, sizeof (uint32_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(p->pool_cursor, &pc, sizeof pc, hipMemcpyHostToDevice));
   }
+  smax_phase_mark(" schedule", &tpc);
+  smax_dev_free(derr);   // past the blocking copies above
   *planp = p;
   return 0;
 fail:
-  if (derr) smax_dev_free(derr);
+  (void) hipStreamSynchronize(nullptr);   // plan-time kernels (null stream) may still use the scratch
+  smax_dev_free(derr);
+  smax_dev_free(ibsum);
+  smax_dev_free(ihist);
+  smax_dev_free(spec);
   gt_smax_plan_delete(p);
   return -1;
 }
@@ -3618,6 +3847,14 @@ extern "C" int gt_smax_plan_debug_tiles(GtSmaxPlan *p, uint32_t *counts, uint32_
   if (ndeferred) *ndeferred = n;
   if (deferred && n && hipMemcpy(deferred, p->defer_list + base, sizeof (uint32_t) * n,
                                  hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 0;
+}
+
+extern "C" int gt_smax_plan_debug_windows(GtSmaxPlan *p, uint32_t *words) {
+  if (plan_sync(p) != hipSuccess) return -1;
+  if (p->num_tiles && hipMemcpy(words, p->llv_win, sizeof (uint2) * (uint64_t) p->num_tiles,
+                                hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return 0;
 }

@@ -323,6 +323,12 @@ uint32_t gt_smax_plan_deferred_tiles(GtSmaxPlan *plan);
 int gt_smax_plan_debug_tiles(GtSmaxPlan *plan, uint32_t *counts, uint32_t *deferred,
                              uint32_t *ndeferred);
 
+/* Diagnostic: copies the plan's per-tile .llv window words -- the plan-time
+ * index K1 reads, num_tiles pairs {first entry of the window, entries |
+ * left-halo entries << 12 | DMA lanes << 17 | static-K1b flag << 31} -- to a
+ * host buffer of 2 * num_tiles words.  0 on success, -1 on a HIP error. */
+int gt_smax_plan_debug_windows(GtSmaxPlan *plan, uint32_t *words);
+
 #ifdef __cplusplus
 }
 #endif
