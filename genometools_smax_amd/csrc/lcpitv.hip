@@ -63,6 +63,7 @@ struct LiLevels {
 // ------------------------------------------------------------ kernels
 
 // grid-stride loop over [0, n) of a 1-D launch (li_blocks caps the grid)
+#define LI_ITV_ROWS 4                   // rows per thread of li_itv_kernel, in step
 #define LI_FOR(i, n)                                                          \
   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x,         \
                 i##_stride = (uint64_t) gridDim.x * blockDim.x;               \
@@ -211,9 +212,9 @@ __device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v, bo
 // (PL, NSE, e) and one depth per row, each O(1) from its neighbours --
 // no stack walk, no per-row search, no sort.
 //
-// Pass A, per tile of LI_T rows in LDS: PL, e and NSE by per-thread
-// pointer jumping inside 8-row segments, then the nearest segment with a
-// small enough minimum (its own chain from the near end stays inside it);
+// Pass A, per tile of LI_T rows in LDS: PL, e and NSE by comparisons
+// inside each thread's 8-row segment (in registers), then the nearest
+// segment with a small enough minimum and the nearest qualifying row in it;
 // rows without an answer in their tile (the tile's prefix or suffix
 // minima, a handful) are resolved by pass B over the tile minima (a 64-ary
 // hierarchy) and the found tile's resolved chain.  PL and NSE are stored
@@ -234,6 +235,8 @@ __device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v, bo
 #define LI_UNRES 0xfffffffeu            // distance not found inside the tile (pass A)
 #define LI_ESC 0xffffffffu              // distance >= 2^32 - 1: search again where read
 #define LI_EUNRES 2u
+#define LI_UCAP 128                     // unresolved entries kept per tile (more: pass B scans the tile)
+static_assert(LI_T * 4 <= 65536, "a slot entry (tile row << 2 | kind) fits 16 bits");
 
 __device__ __forceinline__ uint32_t li_dist32(uint64_t dist) {
   return dist >= (uint64_t) LI_UNRES ? LI_ESC : (uint32_t) dist;
@@ -252,36 +255,72 @@ __device__ __forceinline__ uint32_t li_dist32(uint64_t dist) {
 
 struct LiAnsvLds {
   uint32_t x[LI_TPAD];
-  int16_t pl[LI_TPAD], ple[LI_TPAD], nse[LI_TPAD];   // tile-local rows, -1: none found
+  int16_t pl[LI_TPAD], nse[LI_TPAD];   // tile-local rows, -1: none found
   uint8_t e[LI_TPAD];
   uint32_t wsum[2][LI_TPB / 64];
-  uint32_t segmin[LI_TPB];
-  uint32_t grpmin[LI_NGRP];
+  alignas(16) uint32_t segmin[LI_TPB];   // (16-byte reads of a group's 16)
+  alignas(16) uint32_t grpmin[LI_NGRP];
+  uint32_t gpre[LI_NGRP], gsuf[LI_NGRP];   // minima of the groups before / after
+  uint32_t uw[LI_TPB / 64];                 // unresolved entries per wave
   uint32_t tmin[LI_TPB / 64];
 };
 
-// nearest segment before tid (after, when !left) whose minimum is < v
-// (<= v when !strict); -1 if none in the tile
-__device__ __forceinline__ int li_seg_find(const LiAnsvLds &S, int tid, uint32_t v, bool strict,
-                                           bool left) {
-  auto ok = [&](uint32_t m) { return strict ? m < v : m <= v; };
-  const int g = tid / LI_GSEG;
-  if (left) {
-    for (int s = tid - 1; s >= g * LI_GSEG; s--)
-      if (ok(S.segmin[s])) return s;
-    for (int h = g - 1; h >= 0; h--)
-      if (ok(S.grpmin[h]))
-        for (int s = h * LI_GSEG + LI_GSEG - 1; s >= h * LI_GSEG; s--)
-          if (ok(S.segmin[s])) return s;
-  } else {
-    for (int s = tid + 1; s < (g + 1) * LI_GSEG; s++)
-      if (ok(S.segmin[s])) return s;
-    for (int h = g + 1; h < LI_NGRP; h++)
-      if (ok(S.grpmin[h]))
-        for (int s = h * LI_GSEG; s < (h + 1) * LI_GSEG; s++)
-          if (ok(S.segmin[s])) return s;
+// 16 words of LDS (16-byte aligned) into registers
+__device__ __forceinline__ void li_load16(const uint32_t *src, uint32_t (&d)[16]) {
+  const uint4 *a = reinterpret_cast<const uint4 *>(src);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint4 u = a[k];
+    d[4 * k] = u.x;
+    d[4 * k + 1] = u.y;
+    d[4 * k + 2] = u.z;
+    d[4 * k + 3] = u.w;
   }
-  return -1;
+}
+
+// bit s: m[s] <= vt
+template <int W>
+__device__ __forceinline__ uint32_t li_lemask(const uint32_t (&m)[W], uint32_t vt) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int s = 0; s < W; s++) b |= m[s] <= vt ? (1u << s) : 0u;
+  return b;
+}
+
+// the highest (left: the nearest before) or lowest set bit of b != 0
+__device__ __forceinline__ int li_near(uint32_t b, bool left) {
+  return left ? 31 - __builtin_clz(b) : __builtin_ctz(b);
+}
+
+// nearest segment before tid (after it when !left) whose minimum is <= vt
+// (a strict query for v asks vt = v - 1); -1 if none in the tile: the
+// minima of the thread's own group of segments, past it the group minima,
+// then the hit group's 16 minima (four 16-byte LDS reads each) -- bit masks
+// over registers, no dependent LDS chain
+__device__ __forceinline__ int li_seg_find(const LiAnsvLds &S, int tid, uint32_t vt, bool left) {
+  static_assert(LI_GSEG == 16 && LI_NGRP == 16, "16-bit masks");
+  const int g = tid / LI_GSEG, o = tid % LI_GSEG;
+  uint32_t smo[LI_GSEG];
+  li_load16(S.segmin + g * LI_GSEG, smo);
+  uint32_t b = li_lemask(smo, vt) & (left ? (1u << o) - 1u : 0xfffeu << o);
+  if (b) return g * LI_GSEG + li_near(b, left);
+  uint32_t gm[LI_NGRP];
+  li_load16(S.grpmin, gm);
+  b = li_lemask(gm, vt) & (left ? (1u << g) - 1u : 0xfffeu << g) & 0xffffu;
+  if (!b) return -1;
+  const int h = li_near(b, left);
+  uint32_t sm[LI_GSEG];
+  li_load16(S.segmin + h * LI_GSEG, sm);
+  return h * LI_GSEG + li_near(li_lemask(sm, vt), left);
+}
+
+// the row of segment s (whose minimum qualifies) nearest its right end
+// (from_right) or its left end with X <= vt: eight independent LDS reads
+__device__ __forceinline__ int li_seg_row(const LiAnsvLds &S, int s, uint32_t vt, bool from_right) {
+  uint32_t xs[LI_RPT];
+#pragma unroll
+  for (int q = 0; q < LI_RPT; q++) xs[q] = S.x[LI_PADI(s * LI_RPT + q)];
+  return s * LI_RPT + li_near(li_lemask(xs, vt), from_right);
 }
 
 // pass A: rows [t0, t0 + LI_T) of the N + 1 rows 0..N.  Besides PL, e and
@@ -290,40 +329,70 @@ __device__ __forceinline__ int li_seg_find(const LiAnsvLds &S, int tid, uint32_t
 // strictly decreasing) and its weak prefix minima from the first row (the
 // NSE chain, X non-increasing), LI_CH of each -- the nearest row below v on
 // either side of a tile is on them, found by one masked read.  The rows
-// left unresolved go to a list for pass B: entries (row << 2 | kind), kind
-// 0 PL, 1 PLE (e), 2 NSE; *ucnt counts them all, at most ucap are stored
-// (past it pass B scans every row).
-__global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, uint64_t N, uint64_t ntiles,
+// left unresolved go to the tile's slots for pass B: entries (tile row << 2
+// | kind), kind 0 PL, 1 PLE (e), 2 NSE; ucount[t] counts them all, at most
+// LI_UCAP are kept (past it pass B scans the tile's rows).
+// One tile per workgroup, tile t_base + blockIdx.x (the host launches the
+// tiles past the grid cap in further launches): a tile loop made the
+// compiler hoist its per-thread LDS and shuffle addresses out of it, spill
+// them (1.4 GB of scratch traffic each way at C2) and reload them per tile.
+__global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, uint64_t N, uint64_t t_base,
                                                          uint32_t *pld, uint32_t *nsed, uint8_t *eb,
                                                          uint32_t *tmin, uint32_t *sch, uint32_t *pch,
-                                                         uint64_t *ulist, unsigned long long *ucnt,
-                                                         uint64_t ucap) {
+                                                         uint16_t *ulist, uint32_t *ucount) {
   __shared__ LiAnsvLds S;
   const int tid = threadIdx.x, lo = tid * LI_RPT, hi = lo + LI_RPT;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  {
+    const uint64_t t = t_base + blockIdx.x;
     const uint64_t t0 = t * LI_T;
-    for (int k = tid; k < LI_T; k += LI_TPB) {
-      const uint64_t g = t0 + (uint64_t) k;
-      S.x[LI_PADI(k)] = g <= N ? X[g] : 0xffffffffu;   // past row N: never an answer
+    {
+      // every load issued before the first wait (a load under the row
+      // test had made each of the eight wait for the one before)
+      uint32_t xv[LI_RPT];
+#pragma unroll
+      for (int j = 0; j < LI_RPT; j++) {
+        const uint64_t g = t0 + (uint64_t) (tid + LI_TPB * j);
+        xv[j] = X[g <= N ? g : N];
+      }
+#pragma unroll
+      for (int j = 0; j < LI_RPT; j++) {
+        const int k = tid + LI_TPB * j;
+        S.x[LI_PADI(k)] = t0 + (uint64_t) k <= N ? xv[j] : 0xffffffffu;   // past row N: never an answer
+      }
     }
     __syncthreads();
-    // the thread's segment: PLE / PL left to right, NSE right to left
+    // the thread's segment in registers: PLE / PL / NSE by comparisons
+    // (no data-dependent loop; the pointer-jumping walks over LDS these
+    // replace were the kernel's dependent-latency chains)
+    uint32_t xr[LI_RPT];
+#pragma unroll
+    for (int q = 0; q < LI_RPT; q++) xr[q] = S.x[LI_PADI(lo + q)];
     uint32_t m = 0xffffffffu;
-    for (int i = lo; i < hi; i++) {
-      const uint32_t v = S.x[LI_PADI(i)];
-      m = v < m ? v : m;
-      int p = i - 1;
-      while (p >= lo && S.x[LI_PADI(p)] > v) p = S.ple[LI_PADI(p)];
-      int q = -1;
-      if (p >= lo) q = S.x[LI_PADI(p)] < v ? p : S.pl[LI_PADI(p)];
-      S.ple[LI_PADI(i)] = (int16_t) (p >= lo ? p : -1);
-      S.pl[LI_PADI(i)] = (int16_t) q;
-    }
-    for (int i = hi - 1; i >= lo; i--) {
-      const uint32_t v = S.x[LI_PADI(i)];
-      int q = i + 1;
-      while (q < hi && S.x[LI_PADI(q)] > v) q = S.nse[LI_PADI(q)] < 0 ? hi : S.nse[LI_PADI(q)];
-      S.nse[LI_PADI(i)] = (int16_t) (q < hi ? q : -1);
+#pragma unroll
+    for (int q = 0; q < LI_RPT; q++) m = xr[q] < m ? xr[q] : m;
+    // queries left for outside the segment: bit 3 r + k, row lo + r, kind k
+    // (0: PL, 1: PLE for e, 2: NSE); e where the segment decides it (the
+    // nearest row before with X <= v has X < v: it is also the nearest with
+    // X < v), LI_EUNRES until a query does
+    uint32_t qm = 0;
+#pragma unroll
+    for (int i = 0; i < LI_RPT; i++) {
+      int pe = -1, ps = -1, ns = -1;
+#pragma unroll
+      for (int j = 0; j < i; j++) {
+        pe = xr[j] <= xr[i] ? j : pe;      // nearest before with X <= v
+        ps = xr[j] < xr[i] ? j : ps;       // nearest before with X < v
+      }
+#pragma unroll
+      for (int j = LI_RPT - 1; j > i; j--) ns = xr[j] <= xr[i] ? j : ns;   // nearest after, X <= v
+      S.pl[LI_PADI(lo + i)] = (int16_t) (ps >= 0 ? lo + ps : -1);
+      S.nse[LI_PADI(lo + i)] = (int16_t) (ns >= 0 ? lo + ns : -1);
+      uint8_t e = 0;
+      if (xr[i] > 0 && xr[i] != 0xffffffffu) {
+        qm |= ((ps < 0 ? 1u : 0u) | (pe < 0 ? 2u : 0u) | (ns < 0 ? 4u : 0u)) << (3 * i);
+        e = pe < 0 ? LI_EUNRES : ps == pe ? 1u : 0u;
+      }
+      S.e[LI_PADI(lo + i)] = e;
     }
     S.segmin[tid] = m;
     uint32_t wm = m;                     // the wave's minimum, for the tile's
@@ -333,10 +402,20 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
     }
     if ((tid & 63) == 0) S.tmin[tid >> 6] = wm;
     __syncthreads();
-    if (tid < LI_NGRP) {
+    if (tid < LI_NGRP) {                 // wave 0, lanes 0..15
       uint32_t g = 0xffffffffu;
       for (int s = tid * LI_GSEG; s < (tid + 1) * LI_GSEG; s++) g = S.segmin[s] < g ? S.segmin[s] : g;
       S.grpmin[tid] = g;
+      uint32_t pre = g, suf = g;         // inclusive prefix / suffix minima over the groups
+#pragma unroll
+      for (int d = 1; d < LI_NGRP; d <<= 1) {
+        const uint32_t a = __shfl_up(pre, d, LI_NGRP), c = __shfl_down(suf, d, LI_NGRP);
+        if (tid >= d) pre = a < pre ? a : pre;
+        if (tid + d < LI_NGRP) suf = c < suf ? c : suf;
+      }
+      const uint32_t ep = __shfl_up(pre, 1, LI_NGRP), es = __shfl_down(suf, 1, LI_NGRP);
+      S.gpre[tid] = tid > 0 ? ep : 0xffffffffu;
+      S.gsuf[tid] = tid + 1 < LI_NGRP ? es : 0xffffffffu;
     }
     if (tid == 0) {
       uint32_t g = S.tmin[0];
@@ -344,70 +423,65 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
       tmin[t] = g;
     }
     __syncthreads();
-    // rows unresolved in their segment: the nearest segment with a small
-    // enough minimum; its chain from the near end stays inside it (every row
-    // it visits has a smaller one beyond it in that segment: resolved above).
-    // The answers go back into the LDS arrays (entries no walk here reads:
-    // the walks only visit rows resolved inside their segment)
-    for (int i = lo; i < hi; i++) {
-      const uint32_t v = S.x[LI_PADI(i)];
-      uint8_t e = 0;
-      if (v > 0 && v != 0xffffffffu) {
-        int p = S.pl[LI_PADI(i)];
-        if (p < 0) {
-          const int s = li_seg_find(S, tid, v, true, true);
-          if (s >= 0) {
-            p = s * LI_RPT + LI_RPT - 1;
-            while (S.x[LI_PADI(p)] >= v) p = S.pl[LI_PADI(p)];
-            S.pl[LI_PADI(i)] = (int16_t) p;
-          }
-        }
-        int pe = S.ple[LI_PADI(i)];
-        if (pe < 0) {
-          const int s = li_seg_find(S, tid, v, false, true);
-          if (s >= 0) {
-            pe = s * LI_RPT + LI_RPT - 1;
-            while (S.x[LI_PADI(pe)] > v) pe = S.pl[LI_PADI(pe)];   // the strict chain skips only values > v
-          }
-        }
-        e = pe >= 0 ? (S.x[LI_PADI(pe)] < v ? 1u : 0u) : LI_EUNRES;
-        int q = S.nse[LI_PADI(i)];
-        if (q < 0) {
-          const int s = li_seg_find(S, tid, v, false, false);
-          if (s >= 0) {
-            q = s * LI_RPT;
-            while (S.x[LI_PADI(q)] > v) q = S.nse[LI_PADI(q)];
-            S.nse[LI_PADI(i)] = (int16_t) q;
-          }
+    // the queries, one per lane per round (a lane takes its next one; kinds
+    // mixed in one round): the nearest segment with a small enough minimum
+    // (li_seg_find), then the nearest qualifying row in it (li_seg_row).
+    // Only S.x of other segments is read, so the answers go straight back
+    // into the thread's own LDS entries
+    while (__ballot(qm != 0) != 0ull) {
+      if (qm != 0) {
+        const int b = __builtin_ctz(qm);
+        qm &= qm - 1u;
+        const int r = b / 3, k = b - 3 * r, i = lo + r;
+        const uint32_t v = S.x[LI_PADI(i)];
+        const uint32_t vt = k == 0 ? v - 1u : v;   // v > 0: X < v is X <= v - 1
+        const bool left = k != 2;
+        const int sg = li_seg_find(S, tid, vt, left);
+        if (sg >= 0) {
+          const int row = li_seg_row(S, sg, vt, left);
+          if (k == 0) S.pl[LI_PADI(i)] = (int16_t) row;
+          else if (k == 2) S.nse[LI_PADI(i)] = (int16_t) row;
+          else S.e[LI_PADI(i)] = S.x[LI_PADI(row)] < v ? 1u : 0u;
         }
       }
-      S.e[LI_PADI(i)] = e;
     }
     // the minimum chains' members: strict suffix minima (x below every row
     // after them) and weak prefix minima (x at most every row before them),
     // from the minima of the other segments (rows past N: x = 2^32-1, never
     // members) and a pass over the thread's own rows
-    uint32_t after = 0xffffffffu, before = 0xffffffffu;
+    uint32_t after, before;
     {
-      const int g = tid / LI_GSEG;
-      for (int s2 = tid + 1; s2 < (g + 1) * LI_GSEG; s2++) after = S.segmin[s2] < after ? S.segmin[s2] : after;
-      for (int h = g + 1; h < LI_NGRP; h++) after = S.grpmin[h] < after ? S.grpmin[h] : after;
-      for (int s2 = g * LI_GSEG; s2 < tid; s2++) before = S.segmin[s2] < before ? S.segmin[s2] : before;
-      for (int h = 0; h < g; h++) before = S.grpmin[h] < before ? S.grpmin[h] : before;
+      // the other segments of the group (16 consecutive lanes: shuffles
+      // of width 16), then the groups before / after
+      const int g = tid / LI_GSEG, o = tid % LI_GSEG;
+      uint32_t pre = m, suf = m;
+#pragma unroll
+      for (int d = 1; d < LI_GSEG; d <<= 1) {
+        const uint32_t a = __shfl_up(pre, d, LI_GSEG), c = __shfl_down(suf, d, LI_GSEG);
+        if (o >= d) pre = a < pre ? a : pre;
+        if (o + d < LI_GSEG) suf = c < suf ? c : suf;
+      }
+      before = __shfl_up(pre, 1, LI_GSEG);
+      after = __shfl_down(suf, 1, LI_GSEG);
+      if (o == 0) before = 0xffffffffu;
+      if (o == LI_GSEG - 1) after = 0xffffffffu;
+      const uint32_t gp = S.gpre[g], gs = S.gsuf[g];
+      before = gp < before ? gp : before;
+      after = gs < after ? gs : after;
     }
     uint32_t sflag = 0, pflag = 0;
     {
       uint32_t run = after;
-      for (int i = hi - 1; i >= lo; i--) {
-        const uint32_t xi = S.x[LI_PADI(i)];
-        if (xi < run) sflag |= 1u << (i - lo);
-        run = xi < run ? xi : run;
+#pragma unroll
+      for (int q = LI_RPT - 1; q >= 0; q--) {
+        if (xr[q] < run) sflag |= 1u << q;
+        run = xr[q] < run ? xr[q] : run;
       }
       run = before;
-      for (int i = lo; i < hi; i++) {
-        const uint32_t xi = S.x[LI_PADI(i)];
-        if (xi <= run && xi != 0xffffffffu) pflag |= 1u << (i - lo);
-        run = xi < run ? xi : run;
+#pragma unroll
+      for (int q = 0; q < LI_RPT; q++) {
+        if (xr[q] <= run && xr[q] != 0xffffffffu) pflag |= 1u << q;
+        run = xr[q] < run ? xr[q] : run;
       }
     }
     __syncthreads();
@@ -431,15 +505,17 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
       uint32_t *so = sch + t * LI_CHW, *po = pch + t * LI_CHW;
       // suffix members after this thread's: ts - (ws + is)
       uint32_t rs = ts - (ws + is);
-      for (int i = hi - 1; i >= lo; i--)
-        if (sflag >> (i - lo) & 1u) {
-          if (rs < LI_CH) { so[4 + rs] = S.x[LI_PADI(i)]; so[4 + LI_CH + rs] = (uint32_t) i; }
+#pragma unroll
+      for (int q = LI_RPT - 1; q >= 0; q--)
+        if (sflag >> q & 1u) {
+          if (rs < LI_CH) { so[4 + rs] = xr[q]; so[4 + LI_CH + rs] = (uint32_t) (lo + q); }
           rs++;
         }
       uint32_t rp = wp + ip - cp;
-      for (int i = lo; i < hi; i++)
-        if (pflag >> (i - lo) & 1u) {
-          if (rp < LI_CH) { po[4 + rp] = S.x[LI_PADI(i)]; po[4 + LI_CH + rp] = (uint32_t) i; }
+#pragma unroll
+      for (int q = 0; q < LI_RPT; q++)
+        if (pflag >> q & 1u) {
+          if (rp < LI_CH) { po[4 + rp] = xr[q]; po[4 + LI_CH + rp] = (uint32_t) (lo + q); }
           rp++;
         }
       if (tid == 0) {
@@ -473,27 +549,32 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
                << (3 * j);
     }
     {
-      // append: a wave-level prefix of the counts, one atomic per wave
+      // the tile's own slots (no device-wide counter: one returning atomic
+      // per wave on a single word had bounded the kernel at ~88 of them per
+      // microsecond, 2.2 ms at C2): the workgroup's prefix of the counts
       const uint32_t c = (uint32_t) __builtin_popcount(umask);
-      const int lane = tid & 63;
+      const int lane = tid & 63, wave = tid >> 6;
       uint32_t incl = c;
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t o = __shfl_up(incl, d, 64);
         if (lane >= d) incl += o;
       }
-      const uint32_t tot = __shfl(incl, 63, 64);
-      unsigned long long base = 0;
-      if (lane == 63 && tot) base = atomicAdd(ucnt, (unsigned long long) tot);
-      base = __shfl(base, 63, 64);
-      uint64_t at = base + (incl - c);
+      if (lane == 63) S.uw[wave] = incl;
+      __syncthreads();
+      uint32_t at = incl - c, tot = 0;
+      for (int w = 0; w < LI_TPB / 64; w++) {
+        if (w < wave) at += S.uw[w];
+        tot += S.uw[w];
+      }
+      uint16_t *ul = ulist + t * LI_UCAP;
       while (umask) {
         const int b = __builtin_ctz(umask);
         umask &= umask - 1;
-        if (at < ucap) ulist[at] = ((t0 + (uint64_t) (tid + LI_TPB * (b / 3))) << 2) | (uint64_t) (b % 3);
+        if (at < LI_UCAP) ul[at] = (uint16_t) (((tid + LI_TPB * (b / 3)) << 2) | (b % 3));
         at++;
       }
+      if (tid == 0) ucount[t] = tot;
     }
-    __syncthreads();                     // S is rewritten by the next tile
   }
 }
 
@@ -542,62 +623,39 @@ __device__ uint64_t li_search_next(const LiTree &T, const uint32_t *X, const uin
 // per thread per step, their words read as 16-byte pieces; the searches
 // (one 16-byte piece of a level's block per load, all in flight) run only
 // on the rare lanes that found an unresolved row.
-__global__ void __launch_bounds__(256) li_resolve_kernel(LiTree T, const uint32_t *X, uint64_t N,
-                                                         uint32_t *pld, uint32_t *nsed, uint8_t *eb) {
-  const uint64_t nq = (N + 1 + 3) / 4;
-  for (uint64_t qd = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; qd < nq;
-       qd += (uint64_t) gridDim.x * blockDim.x) {
-    const uint64_t k0 = 4 * qd;
-    uint32_t xv[4], pv[4], nv[4], ev;
-    if (k0 + 4 <= N + 1) {
-      const uint4 a = reinterpret_cast<const uint4 *>(X)[qd];
-      const uint4 b = reinterpret_cast<const uint4 *>(pld)[qd];
-      const uint4 c = reinterpret_cast<const uint4 *>(nsed)[qd];
-      ev = reinterpret_cast<const uint32_t *>(eb)[qd];
-      xv[0] = a.x; xv[1] = a.y; xv[2] = a.z; xv[3] = a.w;
-      pv[0] = b.x; pv[1] = b.y; pv[2] = b.z; pv[3] = b.w;
-      nv[0] = c.x; nv[1] = c.y; nv[2] = c.z; nv[3] = c.w;
-    } else {
-      ev = 0;
-      for (int j = 0; j < 4; j++) {
-        const bool in = k0 + j <= N;
-        xv[j] = in ? X[k0 + j] : 0u;
-        pv[j] = in ? pld[k0 + j] : 0u;
-        nv[j] = in ? nsed[k0 + j] : 0u;
-        ev |= (in ? (uint32_t) eb[k0 + j] : 0u) << (8 * j);
-      }
-    }
-    const bool any = pv[0] == LI_UNRES || pv[1] == LI_UNRES || pv[2] == LI_UNRES ||
-                     pv[3] == LI_UNRES || nv[0] == LI_UNRES || nv[1] == LI_UNRES ||
-                     nv[2] == LI_UNRES || nv[3] == LI_UNRES ||
-                     ((ev & 0x02020202u) != 0);
-    if (!any) continue;
-    for (int j = 0; j < 4; j++) {
-      const uint64_t k = k0 + j;
-      const uint32_t v = xv[j];
-      if (k > N || v == 0) continue;
-      if (pv[j] == LI_UNRES) pld[k] = li_dist32(k - li_search_prev<true>(T, X, pld, k, v, true));
-      if (((ev >> (8 * j)) & 0xffu) == LI_EUNRES)
-        eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
-      if (nv[j] == LI_UNRES) nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
-    }
-  }
+// pass B, a wave per tile (four per workgroup): one search per entry of the tile's slots, or
+// (more entries than the slots hold) every unresolved row of the tile
+__device__ __forceinline__ void li_resolve_one(const LiTree &T, const uint32_t *X, uint64_t k,
+                                               uint32_t kind, uint32_t *pld, uint32_t *nsed,
+                                               uint8_t *eb) {
+  const uint32_t v = X[k];
+  if (kind == 0) pld[k] = li_dist32(k - li_search_prev<true>(T, X, pld, k, v, true));
+  else if (kind == 1) eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
+  else nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
 }
 
-// pass B over the list: one search per entry
-__global__ void __launch_bounds__(256) li_resolve_list_kernel(LiTree T, const uint32_t *X,
-                                                              const uint64_t *ulist,
-                                                              const unsigned long long *ucnt,
-                                                              uint64_t ucap, uint32_t *pld,
-                                                              uint32_t *nsed, uint8_t *eb) {
-  const uint64_t n = *ucnt < ucap ? *ucnt : ucap;
-  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t) gridDim.x * blockDim.x) {
-    const uint64_t w = ulist[i], k = w >> 2;
-    const uint32_t kind = (uint32_t) (w & 3u), v = X[k];
-    if (kind == 0) pld[k] = li_dist32(k - li_search_prev<true>(T, X, pld, k, v, true));
-    else if (kind == 1) eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
-    else nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
+__global__ void __launch_bounds__(256) li_resolve_tiles_kernel(LiTree T, const uint32_t *X, uint64_t N,
+                                                               uint64_t ntiles, const uint16_t *ulist,
+                                                               const uint32_t *ucount, uint32_t *pld,
+                                                               uint32_t *nsed, uint8_t *eb) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t t = blockIdx.x * 4ull + (threadIdx.x >> 6); t < ntiles; t += 4ull * gridDim.x) {
+    const uint32_t n = ucount[t];
+    const uint64_t t0 = t * LI_T;
+    if (n <= LI_UCAP) {
+      for (uint32_t j = lane; j < n; j += 64) {
+        const uint32_t w = ulist[t * LI_UCAP + j];
+        li_resolve_one(T, X, t0 + (w >> 2), w & 3u, pld, nsed, eb);
+      }
+    } else {
+      for (int i = lane; i < LI_T; i += 64) {
+        const uint64_t k = t0 + (uint64_t) i;
+        if (k > N || X[k] == 0) continue;
+        if (pld[k] == LI_UNRES) li_resolve_one(T, X, k, 0u, pld, nsed, eb);
+        if (eb[k] == LI_EUNRES) li_resolve_one(T, X, k, 1u, pld, nsed, eb);
+        if (nsed[k] == LI_UNRES) li_resolve_one(T, X, k, 2u, pld, nsed, eb);
+      }
+    }
   }
 }
 
@@ -722,14 +780,34 @@ __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32
     const uint64_t t0 = t * LI_T;
     const int nrows = N + 1 - t0 < LI_T ? (int) (N + 1 - t0) : LI_T;
     const int64_t Dt = t == 0 ? 0 : scan[t - 1].a;
+    {
+      // the tile's X and PL distances staged in the second buffers (free
+      // until the first round), every load issued before the first wait
+      uint32_t xv[LI_RPT], dv[LI_RPT];
+#pragma unroll
+      for (int j = 0; j < LI_RPT; j++) {
+        const uint64_t k = t0 + (uint64_t) (tid + LI_TPB * j);
+        const uint64_t kc = k <= N ? k : N;
+        xv[j] = X[kc];
+        dv[j] = pld[kc];
+      }
+#pragma unroll
+      for (int j = 0; j < LI_RPT; j++) {
+        S.anc[1][tid + LI_TPB * j] = (int32_t) xv[j];
+        S.dist[1][tid + LI_TPB * j] = dv[j];
+      }
+    }
+    __syncthreads();
+    // a parent inside the tile is a row index; one before it (the tile's
+    // prefix minima, a few rows) its place on the boundary chain
     for (int i = tid; i < LI_T; i += LI_TPB) {
       const uint64_t k = t0 + (uint64_t) i;
       int32_t anc = -1;
       uint32_t dist = 0;
       if (i < nrows) {
-        const uint32_t v = X[k];
+        const uint32_t v = (uint32_t) S.anc[1][i], d = S.dist[1][i];
         if (v > 0) {
-          const uint64_t p = li_pl(T, X, pld, k, v);
+          const uint64_t p = d != LI_ESC ? k - d : li_search_prev<false>(T, X, pld, k, v, true);
           dist = 1;
           if (p >= t0) {
             anc = (int32_t) (p - t0);
@@ -792,28 +870,71 @@ __global__ void __launch_bounds__(256) li_itv_kernel(LiTree T, const uint32_t *X
                                                      const uint32_t *nsed, const uint32_t *dep,
                                                      const PT *P, uint64_t N, uint64_t *itv,
                                                      unsigned long long *first) {
-  LI_FOR(c, N) {
-    const uint32_t v = X[c];
-    if (v == 0) {
-      if (X[c + 1] == 0) atomicMin(first, (unsigned long long) (c + 2 * (uint64_t) P[c]));
-      continue;
+  // LI_ITV_ROWS rows per thread, a grid-stride apart, taken through each
+  // step together: every step's loads (X, NSE and PL, then X at NSE, then
+  // X and PL at PL, depths and P) are issued for all of them before the
+  // first wait -- one row per thread waited out a chain of five dependent
+  // loads per row (1.6 ms at C2).  (Walking each row's pops instead, so
+  // that consecutive rows write consecutive records: 1.85 ms, the waves
+  // waiting for their longest chain.)
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t c0 = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; c0 < N;
+       c0 += LI_ITV_ROWS * stride) {
+    uint64_t c[LI_ITV_ROWS], q[LI_ITV_ROWS], lb[LI_ITV_ROWS];
+    uint32_t v[LI_ITV_ROWS], nd[LI_ITV_ROWS], xq[LI_ITV_ROWS], pd[LI_ITV_ROWS];
+    bool ok[LI_ITV_ROWS];
+#pragma unroll
+    for (int j = 0; j < LI_ITV_ROWS; j++) {
+      c[j] = c0 + (uint64_t) j * stride;
+      ok[j] = c[j] < N;
+      const uint64_t cc = ok[j] ? c[j] : 0;
+      v[j] = X[cc];
+      nd[j] = nsed[cc];
+      pd[j] = pld[cc];
     }
-    const uint64_t q = li_nse(T, X, nsed, c, v);
-    const uint32_t xq = X[q];
-    if (xq == v) continue;               // not the interval's rightmost l-index
-    const uint64_t rb = q - 1, lb = li_pl(T, X, pld, c, v);
-    const uint64_t j = (uint64_t) (dep[rb] - dep[c]);
-    const uint64_t pos = (uint64_t) P[rb] + j;
-    const uint32_t xl = X[lb];
-    const uint32_t fd = xl > xq ? xl : xq;
-    const uint64_t flb = fd == 0 ? 0 : (xl >= xq ? li_pl(T, X, pld, lb, xl) : lb);
-    uint64_t *w = itv + 5 * pos;
-    w[0] = v;
-    w[1] = lb;
-    w[2] = rb;
-    w[3] = fd;
-    w[4] = flb;
-    if (fd == 0) atomicMin(first, (unsigned long long) (rb + 2 * (uint64_t) P[rb] + 2 + 2 * j));
+#pragma unroll
+    for (int j = 0; j < LI_ITV_ROWS; j++) {
+      if (ok[j] && v[j] == 0) {
+        if (X[c[j] + 1] == 0) atomicMin(first, (unsigned long long) (c[j] + 2 * (uint64_t) P[c[j]]));
+        ok[j] = false;
+      }
+      q[j] = !ok[j] ? 0 : nd[j] != LI_ESC ? c[j] + nd[j] : li_search_next<false>(T, X, nsed, c[j], v[j]);
+      xq[j] = X[q[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < LI_ITV_ROWS; j++) {
+      ok[j] = ok[j] && xq[j] != v[j];     // c is the interval's rightmost l-index
+      lb[j] = !ok[j] ? 0 : pd[j] != LI_ESC ? c[j] - pd[j] : li_search_prev<false>(T, X, pld, c[j], v[j], true);
+    }
+    uint32_t xl[LI_ITV_ROWS], dr[LI_ITV_ROWS], dc[LI_ITV_ROWS], pl2[LI_ITV_ROWS];
+    uint64_t prb[LI_ITV_ROWS];
+#pragma unroll
+    for (int j = 0; j < LI_ITV_ROWS; j++) {
+      const uint64_t rb = ok[j] ? q[j] - 1 : 0, cc = ok[j] ? c[j] : 0;
+      xl[j] = X[lb[j]];
+      pl2[j] = pld[lb[j]];
+      dr[j] = dep[rb];
+      dc[j] = dep[cc];
+      prb[j] = (uint64_t) P[rb];
+    }
+#pragma unroll
+    for (int j = 0; j < LI_ITV_ROWS; j++) {
+      if (!ok[j]) continue;
+      const uint64_t rb = q[j] - 1, jj = (uint64_t) (dr[j] - dc[j]);
+      const uint64_t pos = prb[j] + jj;
+      const uint32_t fd = xl[j] > xq[j] ? xl[j] : xq[j];
+      const uint64_t flb = fd == 0 ? 0
+                         : xl[j] >= xq[j] ? (pl2[j] != LI_ESC ? lb[j] - pl2[j]
+                                                             : li_search_prev<false>(T, X, pld, lb[j], xl[j], true))
+                                          : lb[j];
+      uint64_t *w = itv + 5 * pos;
+      w[0] = v[j];
+      w[1] = lb[j];
+      w[2] = rb;
+      w[3] = fd;
+      w[4] = flb;
+      if (fd == 0) atomicMin(first, (unsigned long long) (rb + 2 * prb[j] + 2 + 2 * jj));
+    }
   }
 }
 
@@ -1017,8 +1138,8 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   GtLcpitvPlan *p = NULL;
   hipStream_t s = (hipStream_t) stream;
   uint32_t *derr = NULL, herr = 0, *bx = NULL, *bn = NULL, nitv32 = 0;
-  uint64_t *ulist = NULL, ucap = 0;
-  unsigned long long *ucnt = NULL, nunres = 0;
+  uint16_t *ulist = NULL;
+  uint32_t *ucount = NULL;
   uint64_t *brow = NULL;
   LiAffine *aff = NULL, *affs = NULL;
   void *tmp = NULL;
@@ -1070,13 +1191,14 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   LICHK(smax_dev_alloc((void **) &p->tlev[0], sizeof (uint32_t) * (p->ntiles + LI_PAD)));
   LICHK(smax_dev_alloc((void **) &p->sch, sizeof (uint32_t) * LI_CHW * p->ntiles));
   LICHK(smax_dev_alloc((void **) &p->pch, sizeof (uint32_t) * LI_CHW * p->ntiles));
-  ucap = 3 * (N + 1) < (1ull << 22) ? 3 * (N + 1) : ((N + 1) / 4 > (1ull << 22) ? (N + 1) / 4 : (1ull << 22));
-  LICHK(smax_dev_alloc((void **) &ulist, sizeof (uint64_t) * ucap));
-  LICHK(smax_dev_alloc((void **) &ucnt, sizeof (unsigned long long)));
-  LICHK(hipMemsetAsync(ucnt, 0, sizeof (unsigned long long), s));
-  hipLaunchKernelGGL(li_ansv_kernel, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->X, N,
-                     p->ntiles, p->pld, p->nsed, p->eb, p->tlev[0], p->sch, p->pch, ulist, ucnt, ucap);
-  LICHK(hipGetLastError());
+  LICHK(smax_dev_alloc((void **) &ulist, sizeof (uint16_t) * LI_UCAP * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &ucount, sizeof (uint32_t) * p->ntiles));
+  for (uint64_t tb = 0; tb < p->ntiles; tb += LI_MAX_BLOCKS) {
+    const uint64_t nb = p->ntiles - tb < LI_MAX_BLOCKS ? p->ntiles - tb : LI_MAX_BLOCKS;
+    hipLaunchKernelGGL(li_ansv_kernel, dim3((unsigned) nb), dim3(LI_TPB), 0, s, p->X, N, tb, p->pld,
+                       p->nsed, p->eb, p->tlev[0], p->sch, p->pch, ulist, ucount);
+    LICHK(hipGetLastError());
+  }
   p->T.TL.nlev = 1;
   while (p->T.TL.n[p->T.TL.nlev - 1] > 1 && p->T.TL.nlev < LI_MAXLEV) {
     const int l = p->T.TL.nlev;
@@ -1095,15 +1217,8 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   p->T.sch = p->sch;
   p->T.pch = p->pch;
   // pass B
-  LICHK(hipMemcpyAsync(&nunres, ucnt, sizeof nunres, hipMemcpyDeviceToHost, s));
-  LICHK(hipStreamSynchronize(s));      // the list's length picks pass B's form
-  if (nunres <= ucap)
-    hipLaunchKernelGGL(li_resolve_list_kernel, dim3(li_blocks(nunres)), dim3(256), 0, s, p->T, p->X,
-                       ulist, ucnt, ucap, p->pld, p->nsed, p->eb);
-  else
-    hipLaunchKernelGGL(li_resolve_kernel, dim3(li_blocks((N + 4) / 4 < 4096 * 256 ? (N + 4) / 4 : 4096 * 256)),
-                     dim3(256), 0, s, p->T, p->X, N, p->pld,
-                     p->nsed, p->eb);
+  hipLaunchKernelGGL(li_resolve_tiles_kernel, dim3(li_tile_grid((p->ntiles + 3) / 4)), dim3(256), 0, s, p->T,
+                     p->X, N, p->ntiles, ulist, ucount, p->pld, p->nsed, p->eb);
   LICHK(hipGetLastError());
   // depths: boundary chains, the tiles' affine maps and their scan, d
   LICHK(smax_dev_alloc((void **) &brow, sizeof (uint64_t) * LI_BD * p->ntiles));
@@ -1143,11 +1258,11 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   LICHK(smax_dev_alloc((void **) &p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
   if (N > 0) {
     if (p->wide)
-      hipLaunchKernelGGL(li_itv_kernel<uint64_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->T, p->X, p->pld,
-                         p->nsed, p->dep, (const uint64_t *) p->P, N, p->itv, p->first);
+      hipLaunchKernelGGL(li_itv_kernel<uint64_t>, dim3(li_blocks((N + LI_ITV_ROWS - 1) / LI_ITV_ROWS)), dim3(256), 0, s,
+                         p->T, p->X, p->pld, p->nsed, p->dep, (const uint64_t *) p->P, N, p->itv, p->first);
     else
-      hipLaunchKernelGGL(li_itv_kernel<uint32_t>, dim3(li_blocks(N)), dim3(256), 0, s, p->T, p->X, p->pld,
-                         p->nsed, p->dep, (const uint32_t *) p->P, N, p->itv, p->first);
+      hipLaunchKernelGGL(li_itv_kernel<uint32_t>, dim3(li_blocks((N + LI_ITV_ROWS - 1) / LI_ITV_ROWS)), dim3(256), 0, s,
+                         p->T, p->X, p->pld, p->nsed, p->dep, (const uint32_t *) p->P, N, p->itv, p->first);
     LICHK(hipGetLastError());
   }
   smax_marks_record(&p->marks, s);
@@ -1158,7 +1273,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     smax_marks_init(&m);
     smax_marks_record(&m, s);
     SmaxFence *f = smax_marks_fence(&m);
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucnt, p->nsed, p->dep, p->eb};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, p->nsed, p->dep, p->eb};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], f);
     smax_fence_release(f);
     p->nsed = NULL;
@@ -1170,7 +1285,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
 fail:
   {
     (void) hipStreamSynchronize(s);    // nothing queued may still use a cached block
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucnt};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   smax_marks_record(&p->marks, s);

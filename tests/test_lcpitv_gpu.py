@@ -74,6 +74,23 @@ def test_random_texts(seed):
                           _want_intervals(want))
 
 
+def test_homopolymer_tiles_overflow_slots():
+    """Homopolymer runs give whole tiles of monotone LCP (a run followed by a
+    larger symbol: decreasing, every row's PL outside its tile; a run at the
+    end of a sequence: increasing, every row's NSE outside): more unresolved
+    rows per tile than pass A's slots hold, so pass B scans those tiles."""
+    rng = np.random.default_rng(71)
+    t = np.concatenate([rng.integers(0, 4, 3000, dtype=np.uint8), np.zeros(5000, np.uint8),
+                        np.ones(1, np.uint8), rng.integers(0, 4, 3000, dtype=np.uint8),
+                        np.full(4500, 2, np.uint8), np.array([254], np.uint8),
+                        rng.integers(0, 4, 2000, dtype=np.uint8), np.full(2500, 3, np.uint8)])
+    e = O.Esa(t)
+    want = O.bottomup_events(e)
+    assert np.array_equal(_gpu_events(e), want)
+    assert np.array_equal(G.enumerate_lcp_intervals(e.lcpbytes, e.llv, e.n, e.nonspecials),
+                          _want_intervals(want))
+
+
 def test_callback_stop_and_partial_visitor():
     e = oracle_esa("Atinsert.fna")
     seen = []
