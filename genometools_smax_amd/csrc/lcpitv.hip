@@ -771,25 +771,28 @@ struct LiDepthLds {
 };
 
 __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
-                                                          uint64_t N, uint64_t ntiles, const uint64_t *brow,
-                                                          const uint32_t *bn, const LiAffine *scan,
-                                                          uint32_t *dep) {
+                                                          const uint8_t *eb, uint64_t N, uint64_t ntiles,
+                                                          const uint64_t *brow, const uint32_t *bn,
+                                                          const LiAffine *scan, uint32_t *dep, uint32_t *cnt) {
   __shared__ LiDepthLds S;
   const int tid = threadIdx.x;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint64_t t0 = t * LI_T;
     const int nrows = N + 1 - t0 < LI_T ? (int) (N + 1 - t0) : LI_T;
     const int64_t Dt = t == 0 ? 0 : scan[t - 1].a;
+    // the tile's X and PL distances staged in the second buffers (free
+    // until the first round), every load issued before the first wait; X
+    // and e stay in registers for the pop counts at the end
+    uint32_t xv[LI_RPT], ev[LI_RPT];
     {
-      // the tile's X and PL distances staged in the second buffers (free
-      // until the first round), every load issued before the first wait
-      uint32_t xv[LI_RPT], dv[LI_RPT];
+      uint32_t dv[LI_RPT];
 #pragma unroll
       for (int j = 0; j < LI_RPT; j++) {
         const uint64_t k = t0 + (uint64_t) (tid + LI_TPB * j);
         const uint64_t kc = k <= N ? k : N;
         xv[j] = X[kc];
         dv[j] = pld[kc];
+        ev[j] = eb[kc];
       }
 #pragma unroll
       for (int j = 0; j < LI_RPT; j++) {
@@ -844,23 +847,26 @@ __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32
       int64_t d = S.dist[cur][i];
       if (a <= -2) d += Dt - (int64_t) (-2 - a);
       dep[t0 + i] = (uint32_t) d;
+      S.dist[cur ^ 1][i] = (uint32_t) d;   // (the other buffer is free)
+    }
+    __syncthreads();
+    // pops of row r = t0 + i - 1 (the row before the tile: its d is D_t):
+    // cnt(r) = d(r) when X[r+1] = 0, else d(r) - d(r+1) + e(r+1) -- the
+    // scan's input, so that it reads one word per row
+#pragma unroll
+    for (int j = 0; j < LI_RPT; j++) {
+      const int i = tid + LI_TPB * j;
+      const uint64_t r1 = t0 + (uint64_t) i;
+      if (i >= nrows) break;
+      if (r1 == N) cnt[N] = 0;
+      if (r1 == 0) continue;
+      const uint32_t d1 = S.dist[cur ^ 1][i];
+      const uint32_t d0 = i > 0 ? S.dist[cur ^ 1][i - 1] : (uint32_t) Dt;
+      cnt[r1 - 1] = xv[j] == 0 ? d0 : d0 - d1 + ev[j];
     }
     __syncthreads();
   }
 }
-
-// pops of row r (r < N): cnt(r) above; the exclusive scan's input
-struct LiCnt {
-  const uint32_t *X, *dep;
-  const uint8_t *eb;
-  uint64_t N;
-  __device__ __host__ uint64_t operator()(uint64_t r) const {
-    if (r >= N) return 0;
-    const uint32_t dr = dep[r];
-    if (X[r + 1] == 0) return dr;
-    return (uint64_t) ((int64_t) dr - (int64_t) dep[r + 1] + (int64_t) eb[r + 1]);
-  }
-};
 
 // the interval records (lcp, lb, rb, father lcp, father lb) in pop order,
 // one per rightmost l-index; and the stream position of the first edge to
@@ -1110,10 +1116,10 @@ extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
 }
 
 template <typename PT>
-static hipError_t li_scan_pops(GtLcpitvPlan *p, hipStream_t s, void **tmp, size_t *tmp_bytes) {
+static hipError_t li_scan_pops(GtLcpitvPlan *p, const uint32_t *cnt_in, hipStream_t s, void **tmp,
+                               size_t *tmp_bytes) {
   const uint64_t N = p->in.nonspecials;
-  auto cnt = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
-                                              LiCnt{p->X, p->dep, p->eb, N});
+  const uint32_t *cnt = cnt_in;         // pops per row (li_depth_kernel), cnt[N] = 0
   size_t b = 0;
   hipError_t e = rocprim::exclusive_scan(nullptr, b, cnt, (PT *) p->P, (PT) 0, (size_t) (N + 1),
                                          rocprim::plus<PT>(), s);
@@ -1139,7 +1145,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   hipStream_t s = (hipStream_t) stream;
   uint32_t *derr = NULL, herr = 0, *bx = NULL, *bn = NULL, nitv32 = 0;
   uint16_t *ulist = NULL;
-  uint32_t *ucount = NULL;
+  uint32_t *ucount = NULL, *cnt = NULL;
   uint64_t *brow = NULL;
   LiAffine *aff = NULL, *affs = NULL;
   void *tmp = NULL;
@@ -1240,12 +1246,14 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     tmp_bytes = b ? b : 16;
     LICHK(rocprim::inclusive_scan(tmp, b, aff, affs, (size_t) p->ntiles, LiAffineCompose(), s));
   }
+  LICHK(smax_dev_alloc((void **) &cnt, sizeof (uint32_t) * (N + 1)));
   hipLaunchKernelGGL(li_depth_kernel, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->T, p->X, p->pld,
-                     N, p->ntiles, brow, bn, affs, p->dep);
+                     p->eb, N, p->ntiles, brow, bn, affs, p->dep, cnt);
   LICHK(hipGetLastError());
   // pops per row, their exclusive scan P (P[N] = intervals), the records
   LICHK(smax_dev_alloc(&p->P, (p->wide ? 8 : 4) * (N + 1)));
-  LICHK(p->wide ? li_scan_pops<uint64_t>(p, s, &tmp, &tmp_bytes) : li_scan_pops<uint32_t>(p, s, &tmp, &tmp_bytes));
+  LICHK(p->wide ? li_scan_pops<uint64_t>(p, cnt, s, &tmp, &tmp_bytes)
+                : li_scan_pops<uint32_t>(p, cnt, s, &tmp, &tmp_bytes));
   if (p->wide)
     LICHK(hipMemcpyAsync(&p->nitv, (uint64_t *) p->P + N, sizeof (uint64_t), hipMemcpyDeviceToHost, s));
   else
@@ -1273,7 +1281,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     smax_marks_init(&m);
     smax_marks_record(&m, s);
     SmaxFence *f = smax_marks_fence(&m);
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, p->nsed, p->dep, p->eb};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt, p->nsed, p->dep, p->eb};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], f);
     smax_fence_release(f);
     p->nsed = NULL;
@@ -1285,7 +1293,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
 fail:
   {
     (void) hipStreamSynchronize(s);    // nothing queued may still use a cached block
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   smax_marks_record(&p->marks, s);
