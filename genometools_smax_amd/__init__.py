@@ -766,7 +766,10 @@ class SmaxPlan:
     """One shard's smax pass over device-resident tables (gt_smax_plan_*).
 
     lcp_ptr/bwt_ptr are device pointers laid out as GtSmaxDevShard requires
-    (DeviceTable, or torch tensors with PAD_FRONT/PAD_BACK slack)."""
+    (DeviceTable, or torch tensors with PAD_FRONT/PAD_BACK slack).  Every
+    stream handed to run / run_part / stitch / copy_boundary must stay alive
+    until close(): the delete fences the plan's buffers on those streams
+    (include/gt_smax_hip.h, gt_smax_plan_delete)."""
 
     def __init__(self, lcp_ptr, bwt_ptr, llv_ptr, numllv, base, local_len, begin, end,
                  nonspecials, minlen, device=0, capacity=0, bwtpk_ptr=None):
