@@ -312,14 +312,15 @@ __device__ __forceinline__ uint64_t mp_block_excl(uint64_t v, uint64_t *total) {
 }
 
 // Candidate rows (LCP[j] >= minlen, j >= 1: rows whose walk is not empty),
-// found per workgroup of MP_WG_ROWS rows: every thread tests 16 consecutive
-// rows with one 16-byte LCP load (byte >= min(minlen, 255), exact below
-// 255).  Pass A counts them per workgroup, pass B (after a scan of those
+// found per workgroup of MP_WG_ROWS rows: every thread tests MP_CPT groups
+// of 16 consecutive rows, one 16-byte LCP load each (byte >= min(minlen,
+// 255), exact below 255).  Pass A counts them per workgroup, pass B (after a scan of those
 // counts) writes them to one global list in row order.  The walks then run
 // one lane per candidate row (passes C and D), so neighbouring lanes walk
 // neighbouring rows (coalesced) and a long block spreads over the device.
 #define MP_ROWS 16
-#define MP_WG_ROWS (256 * MP_ROWS)
+#define MP_CPT 4                          // 16-row groups per pass-A thread
+#define MP_WG_ROWS (256 * MP_ROWS * MP_CPT)
 
 __device__ __forceinline__ uint32_t mp_candidates(const uint8_t *lcp, uint64_t j0, uint64_t N,
                                                   uint32_t mf) {
@@ -342,22 +343,27 @@ __device__ __forceinline__ uint32_t mp_candidates(const uint8_t *lcp, uint64_t j
 __global__ void __launch_bounds__(256)
 mp_cand_count_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, uint64_t *wg_cand,
                      uint16_t *masks) {
-  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) MP_ROWS;
-  const uint32_t m = mp_candidates(lcp, j0, N, mf);
-  masks[blockIdx.x * (uint64_t) 256 + threadIdx.x] = (uint16_t) m;
+  // MP_CPT groups of 16 rows per thread, their loads issued together (one
+  // 16-row group per thread streamed the LCP bytes at 4.4 TB/s); the
+  // thread's four 16-bit masks go out as one 8-byte word, in row order
+  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) (MP_ROWS * MP_CPT);
+  uint64_t m = 0;
+#pragma unroll
+  for (int c = 0; c < MP_CPT; c++) m |= (uint64_t) mp_candidates(lcp, j0 + MP_ROWS * c, N, mf) << (16 * c);
+  reinterpret_cast<uint64_t *>(masks)[blockIdx.x * (uint64_t) 256 + threadIdx.x] = m;
   uint64_t tot;
-  (void) mp_block_excl((uint64_t) __popc(m), &tot);
+  (void) mp_block_excl((uint64_t) __popcll(m), &tot);
   if (threadIdx.x == 0) wg_cand[blockIdx.x] = tot;
 }
 
 // pass B reads pass A's 16-row masks (2 B per 16 rows), not the LCP bytes;
-// one workgroup per MP_WR_GROUP of pass A's workgroups, 4 masks (64 rows)
-// per thread: one 8-byte load each (a workgroup per pass-A workgroup, one
-// mask per thread: 15.5 us for C2's 12.5 MB)
-#define MP_WR_GROUP 4
+// one workgroup per MP_WR_GROUP of pass A's workgroups, 4 masks (64 rows,
+// one pass-A thread's) per thread: one 8-byte load each (one mask per
+// thread: 15.5 us for C2's 12.5 MB)
+#define MP_WR_GROUP 1
 __global__ void __launch_bounds__(256)
 mp_cand_write_kernel(const uint16_t *masks, const uint64_t *wg_cand_off, uint64_t *list) {
-  const uint64_t k0 = (uint64_t) blockIdx.x * (256 * MP_WR_GROUP) + 4u * threadIdx.x;
+  const uint64_t k0 = (uint64_t) blockIdx.x * (256 * MP_CPT * MP_WR_GROUP) + 4u * threadIdx.x;
   uint64_t m = *reinterpret_cast<const uint64_t *>(masks + k0);
   uint64_t tot;
   uint64_t pos = wg_cand_off[(uint64_t) blockIdx.x * MP_WR_GROUP] +
@@ -763,8 +769,8 @@ extern "C" int gt_maxpairs_plan_create_stream(GtMaxpairsPlan **planp, const GtMa
   MPCHK(smax_dev_alloc((void **) &p->wg_cand_off, sizeof (uint64_t) * (p->nwg + 1)));
   // whole groups of MP_WR_GROUP pass-A workgroups; the masks past the last
   // one stay zero
-  MPCHK(smax_dev_alloc((void **) &p->masks, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
-  MPCHK(hipMemsetAsync(p->masks, 0, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP), s));
+  MPCHK(smax_dev_alloc((void **) &p->masks, sizeof (uint16_t) * 256 * MP_CPT * (p->nwg + MP_WR_GROUP)));
+  MPCHK(hipMemsetAsync(p->masks, 0, sizeof (uint16_t) * 256 * MP_CPT * (p->nwg + MP_WR_GROUP), s));
   MPCHK(smax_dev_alloc((void **) &p->total, sizeof (uint64_t)));
   MPCHK(hipMemsetAsync(p->total, 0, sizeof (uint64_t), s));
   MPCHK(smax_dev_alloc((void **) &derr, sizeof (uint32_t)));
