@@ -649,8 +649,8 @@ __device__ uint64_t li_search_next(const LiTree &T, const uint32_t *X, const uin
 // per thread per step, their words read as 16-byte pieces; the searches
 // (one 16-byte piece of a level's block per load, all in flight) run only
 // on the rare lanes that found an unresolved row.
-// pass B, a wave per tile (four per workgroup): one search per entry of the tile's slots, or
-// (more entries than the slots hold) every unresolved row of the tile
+// pass B: one search per open row, from the tiles' slots packed densely, or
+// (a tile with more open rows than its slots hold) every open row of it
 __device__ __forceinline__ void li_resolve_one(const LiTree &T, const uint32_t *X, uint64_t k,
                                                uint32_t kind, uint32_t *pld, uint32_t *nsed,
                                                uint8_t *eb) {
@@ -660,18 +660,32 @@ __device__ __forceinline__ void li_resolve_one(const LiTree &T, const uint32_t *
   else nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
 }
 
-__global__ void __launch_bounds__(256) li_resolve_tiles_kernel(LiTree T, const uint32_t *X, uint64_t N,
+// entries a tile's slots hold (a tile past them resolves its rows itself)
+struct LiSlotLen {
+  const uint32_t *ucount;
+  __device__ __host__ uint32_t operator()(uint64_t t) const {
+    const uint32_t n = ucount[t];
+    return n <= LI_UCAP ? n : 0u;
+  }
+};
+
+// the slots packed into one dense list at their scanned offsets (row << 2 |
+// kind), a wave per tile; a tile past its slots scans its own rows here.
+// *ntot = the list's length (written by the last tile)
+__global__ void __launch_bounds__(256) li_compact_slots_kernel(LiTree T, const uint32_t *X, uint64_t N,
                                                                uint64_t ntiles, const uint16_t *ulist,
-                                                               const uint32_t *ucount, uint32_t *pld,
-                                                               uint32_t *nsed, uint8_t *eb) {
+                                                               const uint32_t *ucount, const uint32_t *uoff,
+                                                               uint64_t *dense, uint32_t *ntot,
+                                                               uint32_t *pld, uint32_t *nsed, uint8_t *eb) {
   const int lane = threadIdx.x & 63;
   for (uint64_t t = blockIdx.x * 4ull + (threadIdx.x >> 6); t < ntiles; t += 4ull * gridDim.x) {
     const uint32_t n = ucount[t];
     const uint64_t t0 = t * LI_T;
     if (n <= LI_UCAP) {
+      const uint64_t base = uoff[t];
       for (uint32_t j = lane; j < n; j += 64) {
         const uint32_t w = ulist[t * LI_UCAP + j];
-        li_resolve_one(T, X, t0 + (w >> 2), w & 3u, pld, nsed, eb);
+        dense[base + j] = ((t0 + (w >> 2)) << 2) | (uint64_t) (w & 3u);
       }
     } else {
       for (int i = lane; i < LI_T; i += 64) {
@@ -682,6 +696,20 @@ __global__ void __launch_bounds__(256) li_resolve_tiles_kernel(LiTree T, const u
         if (nsed[k] == LI_UNRES) li_resolve_one(T, X, k, 2u, pld, nsed, eb);
       }
     }
+    if (t == ntiles - 1 && lane == 0) *ntot = uoff[t] + (n <= LI_UCAP ? n : 0u);
+  }
+}
+
+// the dense list, one search per entry, every lane busy (a wave per tile
+// woke 64 lanes for ~20 searches: 0.24 ms at C2)
+__global__ void __launch_bounds__(256) li_resolve_list_kernel(LiTree T, const uint32_t *X,
+                                                              const uint64_t *dense, const uint32_t *ntot,
+                                                              uint32_t *pld, uint32_t *nsed, uint8_t *eb) {
+  const uint64_t n = *ntot;
+  for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t) gridDim.x * blockDim.x) {
+    const uint64_t w = dense[i];
+    li_resolve_one(T, X, w >> 2, (uint32_t) (w & 3u), pld, nsed, eb);
   }
 }
 
@@ -1171,7 +1199,9 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   hipStream_t s = (hipStream_t) stream;
   uint32_t *derr = NULL, herr = 0, *bx = NULL, *bn = NULL, nitv32 = 0;
   uint16_t *ulist = NULL;
-  uint32_t *ucount = NULL, *cnt = NULL;
+  uint32_t *ucount = NULL, *cnt = NULL, *uoff = NULL, *ntot = NULL;
+  uint64_t *dense = NULL;
+  void *stmp = NULL;                   // the slot-count scan's temporary
   uint64_t *brow = NULL;
   LiAffine *aff = NULL, *affs = NULL;
   void *tmp = NULL;
@@ -1225,6 +1255,9 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   LICHK(smax_dev_alloc((void **) &p->pch, sizeof (uint32_t) * LI_CHW * p->ntiles));
   LICHK(smax_dev_alloc((void **) &ulist, sizeof (uint16_t) * LI_UCAP * p->ntiles));
   LICHK(smax_dev_alloc((void **) &ucount, sizeof (uint32_t) * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &uoff, sizeof (uint32_t) * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &dense, sizeof (uint64_t) * LI_UCAP * p->ntiles));
+  LICHK(smax_dev_alloc((void **) &ntot, sizeof (uint32_t)));
   for (uint64_t tb = 0; tb < p->ntiles; tb += LI_MAX_BLOCKS) {
     const uint64_t nb = p->ntiles - tb < LI_MAX_BLOCKS ? p->ntiles - tb : LI_MAX_BLOCKS;
     hipLaunchKernelGGL(li_ansv_kernel, dim3((unsigned) nb), dim3(LI_TPB), 0, s, p->X, N, tb, p->pld,
@@ -1249,8 +1282,20 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   p->T.sch = p->sch;
   p->T.pch = p->pch;
   // pass B
-  hipLaunchKernelGGL(li_resolve_tiles_kernel, dim3(li_tile_grid((p->ntiles + 3) / 4)), dim3(256), 0, s, p->T,
-                     p->X, N, p->ntiles, ulist, ucount, p->pld, p->nsed, p->eb);
+  {
+    auto lens = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
+                                                 LiSlotLen{ucount});
+    size_t b = 0;
+    LICHK(rocprim::exclusive_scan(nullptr, b, lens, uoff, 0u, (size_t) p->ntiles, rocprim::plus<uint32_t>(), s));
+    LICHK(smax_dev_alloc(&stmp, b ? b : 16));
+    LICHK(rocprim::exclusive_scan(stmp, b, lens, uoff, 0u, (size_t) p->ntiles, rocprim::plus<uint32_t>(), s));
+    hipLaunchKernelGGL(li_compact_slots_kernel, dim3(li_tile_grid((p->ntiles + 3) / 4)), dim3(256), 0, s,
+                       p->T, p->X, N, p->ntiles, ulist, ucount, uoff, dense, ntot, p->pld, p->nsed, p->eb);
+    LICHK(hipGetLastError());
+    hipLaunchKernelGGL(li_resolve_list_kernel, dim3(li_blocks(32 * p->ntiles)), dim3(256), 0, s, p->T, p->X,
+                       dense, ntot, p->pld, p->nsed, p->eb);
+    LICHK(hipGetLastError());
+  }
   LICHK(hipGetLastError());
   // depths: boundary chains, the tiles' affine maps and their scan, d
   LICHK(smax_dev_alloc((void **) &brow, sizeof (uint64_t) * LI_BD * p->ntiles));
@@ -1307,7 +1352,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     smax_marks_init(&m);
     smax_marks_record(&m, s);
     SmaxFence *f = smax_marks_fence(&m);
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt, p->nsed, p->dep, p->eb};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt, uoff, dense, ntot, stmp, p->nsed, p->dep, p->eb};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], f);
     smax_fence_release(f);
     p->nsed = NULL;
@@ -1319,7 +1364,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
 fail:
   {
     (void) hipStreamSynchronize(s);    // nothing queued may still use a cached block
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt, uoff, dense, ntot, stmp};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   smax_marks_record(&p->marks, s);
