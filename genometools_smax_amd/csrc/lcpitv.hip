@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
                                                          uint32_t *tmin, uint32_t *sch, uint32_t *pch,
                                                          uint16_t *ulist, uint32_t *ucount) {
   __shared__ LiAnsvLds S;
-  const int tid = threadIdx.x, lo = tid * LI_RPT, hi = lo + LI_RPT;
+  const int tid = threadIdx.x, lo = tid * LI_RPT;
   {
     const uint64_t t = t_base + blockIdx.x;
     const uint64_t t0 = t * LI_T;
@@ -822,12 +822,15 @@ __global__ void __launch_bounds__(256) li_tail_kernel(LiTree T, const uint32_t *
 struct LiDepthLds {
   int32_t anc[2][LI_T];                  // >= 0: tile row; -1: d known; -2 - m: exit at chain index m
   uint32_t dist[2][LI_T];
+  uint64_t brow[LI_BD];                  // the tile's boundary chain: rows, X
+  uint32_t bx[LI_BD];
 };
 
 __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
                                                           const uint8_t *eb, uint64_t N, uint64_t ntiles,
-                                                          const uint64_t *brow, const uint32_t *bn,
-                                                          const LiAffine *scan, uint32_t *dep, uint32_t *cnt) {
+                                                          const uint64_t *brow, const uint32_t *bx,
+                                                          const uint32_t *bn, const LiAffine *scan,
+                                                          uint32_t *dep, uint32_t *cnt) {
   __shared__ LiDepthLds S;
   const int tid = threadIdx.x;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -853,7 +856,12 @@ __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32
         S.anc[1][tid + LI_TPB * j] = (int32_t) xv[j];
         S.dist[1][tid + LI_TPB * j] = dv[j];
       }
+      if (tid < LI_BD) {                 // the boundary chain's held entries
+        S.brow[tid] = brow[t * LI_BD + tid];
+        S.bx[tid] = bx[t * LI_BD + tid];
+      }
     }
+    const int nb = (int) bn[t];
     __syncthreads();
     // a parent inside the tile is a row index; one before it (the tile's
     // prefix minima, a few rows) its place on the boundary chain
@@ -868,8 +876,22 @@ __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32
           dist = 1;
           if (p >= t0) {
             anc = (int32_t) (p - t0);
-          } else if (X[p] > 0) {
-            anc = (int32_t) (-2 - li_bindex(T, X, pld, brow, bn[t], t, p));
+          } else {
+            // p is on the boundary chain: its index by a binary search of
+            // the held entries in LDS (rows strictly decreasing), X beside
+            // it; past them the chain is followed in HBM (li_bindex_far)
+            int lo = 0, hi = nb - 1, m = -1;
+            while (lo <= hi) {
+              const int mid = (lo + hi) >> 1;
+              const uint64_t r = S.brow[mid];
+              if (r == p) { m = mid; break; }
+              if (r > p) lo = mid + 1; else hi = mid - 1;
+            }
+            if (m >= 0) {
+              if (S.bx[m] > 0) anc = (int32_t) (-2 - m);
+            } else if (X[p] > 0) {
+              anc = (int32_t) (-2 - li_bindex_far(T, X, pld, brow, t, p));
+            }
           }
         }
       }
@@ -1319,7 +1341,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   }
   LICHK(smax_dev_alloc((void **) &cnt, sizeof (uint32_t) * (N + 1)));
   hipLaunchKernelGGL(li_depth_kernel, dim3(li_tile_grid(p->ntiles)), dim3(LI_TPB), 0, s, p->T, p->X, p->pld,
-                     p->eb, N, p->ntiles, brow, bn, affs, p->dep, cnt);
+                     p->eb, N, p->ntiles, brow, bx, bn, affs, p->dep, cnt);
   LICHK(hipGetLastError());
   // pops per row, their exclusive scan P (P[N] = intervals), the records
   LICHK(smax_dev_alloc(&p->P, (p->wide ? 8 : 4) * (N + 1)));
