@@ -5,13 +5,13 @@
 // (gt_esa_bottomup, src/match/esa-bottomup.c:116-273), popping every
 // lcp-interval [lb..rb] of depth l > 0 at rb and calling the visitor's
 // leaf-edge / branching-edge / lcp-interval callbacks.  Here the tree is
-// data-parallel, O(1) per row and per interval: three nearest-smaller-value
-// quantities of the exact LCP array (strict previous-smaller PL, next
-// smaller-or-equal NSE, and whether a row opens an interval) computed per
-// 2048-row tile in LDS, the depth of each row's previous-smaller chain (the
-// reference's stack depth), and one exclusive scan of the pops per row
-// (see "the tree" below).  Each interval is then written by its rightmost
-// l-index straight to its pop-order position; the tree stays in HBM
+// data-parallel, O(1) per row and per interval: two nearest-smaller-value
+// quantities of the exact LCP array (strict previous-smaller PL and whether
+// a row opens an interval) computed per 2048-row tile in LDS, the depth of
+// each row's previous-smaller chain (the reference's stack depth), and one
+// exclusive scan of the pops per row (see "the tree" below).  Each row then
+// writes the intervals it pops, deepest first, at their pop-order
+// positions; the tree stays in HBM
 // (GtLcpitvPlan), and the visitor's event stream is generated there too,
 // every event at its position in the reference's order: per row idx the
 // traversal emits exactly one leaf edge, then for every interval popped at
@@ -63,7 +63,6 @@ struct LiLevels {
 // ------------------------------------------------------------ kernels
 
 // grid-stride loop over [0, n) of a 1-D launch (li_blocks caps the grid)
-#define LI_ITV_ROWS 4                   // rows per thread of li_itv_kernel, in step
 #define LI_FOR(i, n)                                                          \
   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x,         \
                 i##_stride = (uint64_t) gridDim.x * blockDim.x;               \
@@ -234,18 +233,20 @@ __device__ static uint64_t li_next(const LiLevels &L, uint64_t k, uint32_t v, bo
 // e(k) = 1 when the nearest p < k with X[p] <= X[k] has X[p] < X[k] (k
 // opens an interval).  P(r) = the pops of rows < r (an exclusive scan of
 // cnt) places every interval: record P(rb) + d(rb) - d(c), events from
-// r + 2 P(r) on.  So the tree is three nearest-smaller-value quantities
-// (PL, NSE, e) and one depth per row, each O(1) from its neighbours --
-// no stack walk, no per-row search, no sort.
+// r + 2 P(r) on.  Row r pops exactly the elements of its PL chain with X >
+// X[r+1] (every row between such an element c and r lies above X[c], so
+// NSE(c) = r + 1), so the records are written by walking those chains: the
+// tree is two nearest-smaller-value quantities (PL, e) and one depth per
+// row, each O(1) from its neighbours -- no stack walk, no sort.
 //
-// Pass A, per tile of LI_T rows in LDS: PL, e and NSE by comparisons
-// inside each thread's 8-row segment (in registers), then the nearest
-// segment with a small enough minimum and the nearest qualifying row in it;
-// rows without an answer in their tile (the tile's prefix or suffix
-// minima, a handful) are resolved by pass B over the tile minima (a 64-ary
-// hierarchy) and the found tile's resolved chain.  PL and NSE are stored
-// as u32 distances (ESC: the rare distance >= 2^32 - 1, found again by
-// search where it is read).  Depth: each tile's chain leaves the tile
+// Pass A, per tile of LI_T rows in LDS: PL and e by comparisons inside each
+// thread's 8-row segment (in registers), then the nearest segment with a
+// small enough minimum and the nearest qualifying row in it; rows without
+// an answer in their tile (the tile's prefix minima, a handful) are
+// resolved by pass B over the tile minima (a 64-ary hierarchy) and the
+// found tile's resolved suffix-minimum chain.  PL is stored as a u32
+// distance (ESC: the rare distance >= 2^32 - 1, found again by search where
+// it is read).  Depth: each tile's chain leaves the tile
 // through the chain of the row before it (t0-1, PL(t0-1), ...: the
 // boundary chain, its first LI_BD entries gathered per tile), so
 // d(k) = (steps inside the tile) + D_t - m with D_t = d(t0-1) and m the
@@ -273,7 +274,7 @@ __device__ __forceinline__ uint32_t li_dist32(uint64_t dist) {
 // fall on 8 banks
 #define LI_PADI(i) ((i) + ((i) >> 3))
 #define LI_TPAD (LI_T + LI_T / 8)
-#define LI_CH 64                        // chain entries kept per tile (suffix / prefix minima)
+#define LI_CH 64                        // chain entries kept per tile (suffix minima)
 // a chain's words: [0] length (| 0x80000000 when cut at LI_CH), [4, 4+LI_CH)
 // the values, [4+LI_CH, 4+2 LI_CH) the tile-local rows (16-byte aligned
 // value block: one round of 16-byte loads reads it whole)
@@ -281,12 +282,12 @@ __device__ __forceinline__ uint32_t li_dist32(uint64_t dist) {
 
 struct LiAnsvLds {
   uint32_t x[LI_TPAD];
-  int16_t pl[LI_TPAD], nse[LI_TPAD];   // tile-local rows, -1: none found
+  int16_t pl[LI_TPAD];                  // tile-local rows, -1: none found
   uint8_t e[LI_TPAD];
   uint32_t wsum[2][LI_TPB / 64];
   alignas(16) uint32_t segmin[LI_TPB];   // (16-byte reads of a group's 16)
   alignas(16) uint32_t grpmin[LI_NGRP];
-  uint32_t gpre[LI_NGRP], gsuf[LI_NGRP];   // minima of the groups before / after
+  uint32_t gsuf[LI_NGRP];                  // minima of the groups after
   uint32_t uw[LI_TPB / 64];                 // unresolved entries per wave
   uint32_t tmin[LI_TPB / 64];
 };
@@ -349,22 +350,22 @@ __device__ __forceinline__ int li_seg_row(const LiAnsvLds &S, int s, uint32_t vt
   return s * LI_RPT + li_near(li_lemask(xs, vt), from_right);
 }
 
-// pass A: rows [t0, t0 + LI_T) of the N + 1 rows 0..N.  Besides PL, e and
-// NSE per row it stores the tile's two minimum chains for pass B: its
-// strict suffix minima from the last row (the PL chain from there, X
-// strictly decreasing) and its weak prefix minima from the first row (the
-// NSE chain, X non-increasing), LI_CH of each -- the nearest row below v on
-// either side of a tile is on them, found by one masked read.  The rows
-// left unresolved go to the tile's slots for pass B: entries (tile row << 2
-// | kind), kind 0 PL, 1 PLE (e), 2 NSE; ucount[t] counts them all, at most
-// LI_UCAP are kept (past it pass B scans the tile's rows).
+// pass A: rows [t0, t0 + LI_T) of the N + 1 rows 0..N.  Besides PL and e
+// per row it stores the tile's strict suffix minima from the last row (the
+// PL chain from there, X strictly decreasing), LI_CH of them, for pass B:
+// the nearest row below v before a tile is on it, found by one masked read.
+// The rows left unresolved go to the tile's slots for pass B: entries (tile
+// row << 2 | kind), kind 0 PL, 1 PLE (e); ucount[t] counts them all, at
+// most LI_UCAP are kept (past it pass B scans the tile's rows).  (NSE, the
+// next smaller-or-equal value, was computed here too until the interval
+// records were written by pop row: 0.84 -> 0.70 ms at C2 without it.)
 // One tile per workgroup, tile t_base + blockIdx.x (the host launches the
 // tiles past the grid cap in further launches): a tile loop made the
 // compiler hoist its per-thread LDS and shuffle addresses out of it, spill
 // them (1.4 GB of scratch traffic each way at C2) and reload them per tile.
 __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, uint64_t N, uint64_t t_base,
-                                                         uint32_t *pld, uint32_t *nsed, uint8_t *eb,
-                                                         uint32_t *tmin, uint32_t *sch, uint32_t *pch,
+                                                         uint32_t *pld, uint8_t *eb,
+                                                         uint32_t *tmin, uint32_t *sch,
                                                          uint16_t *ulist, uint32_t *ucount) {
   __shared__ LiAnsvLds S;
   const int tid = threadIdx.x, lo = tid * LI_RPT;
@@ -387,7 +388,7 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
       }
     }
     __syncthreads();
-    // the thread's segment in registers: PLE / PL / NSE by comparisons
+    // the thread's segment in registers: PLE / PL by comparisons
     // (no data-dependent loop; the pointer-jumping walks over LDS these
     // replace were the kernel's dependent-latency chains)
     uint32_t xr[LI_RPT];
@@ -397,25 +398,22 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
 #pragma unroll
     for (int q = 0; q < LI_RPT; q++) m = xr[q] < m ? xr[q] : m;
     // queries left for outside the segment: bit 3 r + k, row lo + r, kind k
-    // (0: PL, 1: PLE for e, 2: NSE); e where the segment decides it (the
+    // (0: PL, 1: PLE for e); e where the segment decides it (the
     // nearest row before with X <= v has X < v: it is also the nearest with
     // X < v), LI_EUNRES until a query does
     uint32_t qm = 0;
 #pragma unroll
     for (int i = 0; i < LI_RPT; i++) {
-      int pe = -1, ps = -1, ns = -1;
+      int pe = -1, ps = -1;
 #pragma unroll
       for (int j = 0; j < i; j++) {
         pe = xr[j] <= xr[i] ? j : pe;      // nearest before with X <= v
         ps = xr[j] < xr[i] ? j : ps;       // nearest before with X < v
       }
-#pragma unroll
-      for (int j = LI_RPT - 1; j > i; j--) ns = xr[j] <= xr[i] ? j : ns;   // nearest after, X <= v
       S.pl[LI_PADI(lo + i)] = (int16_t) (ps >= 0 ? lo + ps : -1);
-      S.nse[LI_PADI(lo + i)] = (int16_t) (ns >= 0 ? lo + ns : -1);
       uint8_t e = 0;
       if (xr[i] > 0 && xr[i] != 0xffffffffu) {
-        qm |= ((ps < 0 ? 1u : 0u) | (pe < 0 ? 2u : 0u) | (ns < 0 ? 4u : 0u)) << (3 * i);
+        qm |= ((ps < 0 ? 1u : 0u) | (pe < 0 ? 2u : 0u)) << (3 * i);
         e = pe < 0 ? LI_EUNRES : ps == pe ? 1u : 0u;
       }
       S.e[LI_PADI(lo + i)] = e;
@@ -432,15 +430,13 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
       uint32_t g = 0xffffffffu;
       for (int s = tid * LI_GSEG; s < (tid + 1) * LI_GSEG; s++) g = S.segmin[s] < g ? S.segmin[s] : g;
       S.grpmin[tid] = g;
-      uint32_t pre = g, suf = g;         // inclusive prefix / suffix minima over the groups
+      uint32_t suf = g;                  // inclusive suffix minima over the groups
 #pragma unroll
       for (int d = 1; d < LI_NGRP; d <<= 1) {
-        const uint32_t a = __shfl_up(pre, d, LI_NGRP), c = __shfl_down(suf, d, LI_NGRP);
-        if (tid >= d) pre = a < pre ? a : pre;
+        const uint32_t c = __shfl_down(suf, d, LI_NGRP);
         if (tid + d < LI_NGRP) suf = c < suf ? c : suf;
       }
-      const uint32_t ep = __shfl_up(pre, 1, LI_NGRP), es = __shfl_down(suf, 1, LI_NGRP);
-      S.gpre[tid] = tid > 0 ? ep : 0xffffffffu;
+      const uint32_t es = __shfl_down(suf, 1, LI_NGRP);
       S.gsuf[tid] = tid + 1 < LI_NGRP ? es : 0xffffffffu;
     }
     if (tid == 0) {
@@ -466,36 +462,30 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
         if (sg >= 0) {
           const int row = li_seg_row(S, sg, vt, left);
           if (k == 0) S.pl[LI_PADI(i)] = (int16_t) row;
-          else if (k == 2) S.nse[LI_PADI(i)] = (int16_t) row;
           else S.e[LI_PADI(i)] = S.x[LI_PADI(row)] < v ? 1u : 0u;
         }
       }
     }
-    // the minimum chains' members: strict suffix minima (x below every row
-    // after them) and weak prefix minima (x at most every row before them),
-    // from the minima of the other segments (rows past N: x = 2^32-1, never
+    // the suffix-minimum chain's members (x below every row after them),
+    // from the minima of the later segments (rows past N: x = 2^32-1, never
     // members) and a pass over the thread's own rows
-    uint32_t after, before;
+    uint32_t after;
     {
       // the other segments of the group (16 consecutive lanes: shuffles
       // of width 16), then the groups before / after
       const int g = tid / LI_GSEG, o = tid % LI_GSEG;
-      uint32_t pre = m, suf = m;
+      uint32_t suf = m;
 #pragma unroll
       for (int d = 1; d < LI_GSEG; d <<= 1) {
-        const uint32_t a = __shfl_up(pre, d, LI_GSEG), c = __shfl_down(suf, d, LI_GSEG);
-        if (o >= d) pre = a < pre ? a : pre;
+        const uint32_t c = __shfl_down(suf, d, LI_GSEG);
         if (o + d < LI_GSEG) suf = c < suf ? c : suf;
       }
-      before = __shfl_up(pre, 1, LI_GSEG);
       after = __shfl_down(suf, 1, LI_GSEG);
-      if (o == 0) before = 0xffffffffu;
       if (o == LI_GSEG - 1) after = 0xffffffffu;
-      const uint32_t gp = S.gpre[g], gs = S.gsuf[g];
-      before = gp < before ? gp : before;
+      const uint32_t gs = S.gsuf[g];
       after = gs < after ? gs : after;
     }
-    uint32_t sflag = 0, pflag = 0;
+    uint32_t sflag = 0;
     {
       uint32_t run = after;
 #pragma unroll
@@ -503,32 +493,25 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
         if (xr[q] < run) sflag |= 1u << q;
         run = xr[q] < run ? xr[q] : run;
       }
-      run = before;
-#pragma unroll
-      for (int q = 0; q < LI_RPT; q++) {
-        if (xr[q] <= run && xr[q] != 0xffffffffu) pflag |= 1u << q;
-        run = xr[q] < run ? xr[q] : run;
-      }
     }
     __syncthreads();
-    // ranks: suffix members counted from the right, prefix members from the left
+    // ranks: suffix members counted from the right
     {
-      const uint32_t cs = (uint32_t) __builtin_popcount(sflag), cp = (uint32_t) __builtin_popcount(pflag);
+      const uint32_t cs = (uint32_t) __builtin_popcount(sflag);
       const int lane = tid & 63, wave = tid >> 6;
-      uint32_t is = cs, ip = cp;         // inclusive prefix sums over the workgroup's threads
+      uint32_t is = cs;                  // inclusive prefix sums over the workgroup's threads
       for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t os = __shfl_up(is, d, 64), op = __shfl_up(ip, d, 64);
-        if (lane >= d) { is += os; ip += op; }
+        const uint32_t os = __shfl_up(is, d, 64);
+        if (lane >= d) is += os;
       }
-      if (lane == 63) { S.wsum[0][wave] = is; S.wsum[1][wave] = ip; }
+      if (lane == 63) S.wsum[0][wave] = is;
       __syncthreads();
-      uint32_t ws = 0, wp = 0, ts = 0, tp = 0;
+      uint32_t ws = 0, ts = 0;
       for (int w = 0; w < LI_TPB / 64; w++) {
-        if (w < wave) { ws += S.wsum[0][w]; wp += S.wsum[1][w]; }
+        if (w < wave) ws += S.wsum[0][w];
         ts += S.wsum[0][w];
-        tp += S.wsum[1][w];
       }
-      uint32_t *so = sch + t * LI_CHW, *po = pch + t * LI_CHW;
+      uint32_t *so = sch + t * LI_CHW;
       // suffix members after this thread's: ts - (ws + is)
       uint32_t rs = ts - (ws + is);
 #pragma unroll
@@ -537,21 +520,8 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
           if (rs < LI_CH) { so[4 + rs] = xr[q]; so[4 + LI_CH + rs] = (uint32_t) (lo + q); }
           rs++;
         }
-      uint32_t rp = wp + ip - cp;
-#pragma unroll
-      for (int q = 0; q < LI_RPT; q++)
-        if (pflag >> q & 1u) {
-          if (rp < LI_CH) { po[4 + rp] = xr[q]; po[4 + LI_CH + rp] = (uint32_t) (lo + q); }
-          rp++;
-        }
-      if (tid == 0) {
-        so[0] = (ts < LI_CH ? ts : LI_CH) | (ts > LI_CH ? 0x80000000u : 0u);
-        po[0] = (tp < LI_CH ? tp : LI_CH) | (tp > LI_CH ? 0x80000000u : 0u);
-      }
-      if (tid < LI_CH) {                 // (unused value slots: never below, masked by the length)
-        if ((uint32_t) tid >= ts) so[4 + tid] = 0;
-        if ((uint32_t) tid >= tp) po[4 + tid] = 0;
-      }
+      if (tid == 0) so[0] = (ts < LI_CH ? ts : LI_CH) | (ts > LI_CH ? 0x80000000u : 0u);
+      if (tid < LI_CH && (uint32_t) tid >= ts) so[4 + tid] = 0;   // (unused value slots: masked by the length)
     }
     // the rows' words, coalesced (row tid + 256 j), and the unresolved list
     uint32_t umask = 0;
@@ -560,18 +530,16 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
       const uint64_t k = t0 + (uint64_t) i;
       if (k > N) break;
       const uint32_t v = S.x[LI_PADI(i)];
-      uint32_t dpl = 0, dns = 0;
+      uint32_t dpl = 0;
       uint8_t e = 0;
       if (v > 0) {
-        const int p = S.pl[LI_PADI(i)], q = S.nse[LI_PADI(i)];
+        const int p = S.pl[LI_PADI(i)];
         dpl = p >= 0 ? (uint32_t) (i - p) : LI_UNRES;
-        dns = q >= 0 ? (uint32_t) (q - i) : LI_UNRES;
         e = S.e[LI_PADI(i)];
       }
       pld[k] = dpl;
-      nsed[k] = dns;
       eb[k] = e;
-      umask |= ((dpl == LI_UNRES ? 1u : 0u) | (e == LI_EUNRES ? 2u : 0u) | (dns == LI_UNRES ? 4u : 0u))
+      umask |= ((dpl == LI_UNRES ? 1u : 0u) | (e == LI_EUNRES ? 2u : 0u))
                << (3 * j);
     }
     {
@@ -604,14 +572,14 @@ __global__ void __launch_bounds__(LI_TPB, 6) li_ansv_kernel(const uint32_t *X, u
   }
 }
 
-// PL / PLE (strict / !strict) and NSE of row k with value v > 0 by search:
-// the nearest tile before (after) with a small enough minimum, then the
-// first entry of that tile's suffix (prefix) minimum chain with a small
-// enough value, by binary search; a chain cut at LI_CH entries is followed
-// on in HBM (pass A resolved every row on it inside the tile)
+// PL / PLE (strict / !strict) of row k with value v > 0 by search: the
+// nearest tile before with a small enough minimum, then the first entry of
+// that tile's suffix-minimum chain with a small enough value, by binary
+// search; a chain cut at LI_CH entries is followed on in HBM (pass A
+// resolved every row on it inside the tile)
 struct LiTree {                         // what the searches need
   LiLevels TL;                          // tile minima and their hierarchy
-  const uint32_t *sch, *pch;            // the tiles' minimum chains
+  const uint32_t *sch;                  // the tiles' suffix-minimum chains
 };
 
 template <bool FAST>
@@ -631,19 +599,6 @@ __device__ uint64_t li_search_prev(const LiTree &T, const uint32_t *X, const uin
   return p;
 }
 
-template <bool FAST>
-__device__ uint64_t li_search_next(const LiTree &T, const uint32_t *X, const uint32_t *nsed,
-                                   uint64_t k, uint32_t v) {
-  const uint64_t t = k / LI_T;
-  const uint64_t s = li_next<FAST>(T.TL, t, v, false);
-  const uint32_t *ch = T.pch + s * LI_CHW;
-  const int n = (int) (ch[0] & 0xffffu);
-  const uint64_t m = li_block_mask<FAST>(ch + 4, 0, (uint64_t) n, v, false);   // X non-increasing
-  if (m) return s * LI_T + ch[4 + LI_CH + __builtin_ctzll(m)];
-  uint64_t q = s * LI_T + ch[4 + LI_CH + n - 1];
-  while (X[q] > v) q += nsed[q];
-  return q;
-}
 
 // pass B: the rows pass A left unresolved, about 20 per tile.  Four rows
 // per thread per step, their words read as 16-byte pieces; the searches
@@ -652,12 +607,10 @@ __device__ uint64_t li_search_next(const LiTree &T, const uint32_t *X, const uin
 // pass B: one search per open row, from the tiles' slots packed densely, or
 // (a tile with more open rows than its slots hold) every open row of it
 __device__ __forceinline__ void li_resolve_one(const LiTree &T, const uint32_t *X, uint64_t k,
-                                               uint32_t kind, uint32_t *pld, uint32_t *nsed,
-                                               uint8_t *eb) {
+                                               uint32_t kind, uint32_t *pld, uint8_t *eb) {
   const uint32_t v = X[k];
   if (kind == 0) pld[k] = li_dist32(k - li_search_prev<true>(T, X, pld, k, v, true));
-  else if (kind == 1) eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
-  else nsed[k] = li_dist32(li_search_next<true>(T, X, nsed, k, v) - k);
+  else eb[k] = X[li_search_prev<true>(T, X, pld, k, v, false)] < v ? 1u : 0u;
 }
 
 // entries a tile's slots hold (a tile past them resolves its rows itself)
@@ -676,7 +629,7 @@ __global__ void __launch_bounds__(256) li_compact_slots_kernel(LiTree T, const u
                                                                uint64_t ntiles, const uint16_t *ulist,
                                                                const uint32_t *ucount, const uint32_t *uoff,
                                                                uint64_t *dense, uint32_t *ntot,
-                                                               uint32_t *pld, uint32_t *nsed, uint8_t *eb) {
+                                                               uint32_t *pld, uint8_t *eb) {
   const int lane = threadIdx.x & 63;
   for (uint64_t t = blockIdx.x * 4ull + (threadIdx.x >> 6); t < ntiles; t += 4ull * gridDim.x) {
     const uint32_t n = ucount[t];
@@ -691,9 +644,8 @@ __global__ void __launch_bounds__(256) li_compact_slots_kernel(LiTree T, const u
       for (int i = lane; i < LI_T; i += 64) {
         const uint64_t k = t0 + (uint64_t) i;
         if (k > N || X[k] == 0) continue;
-        if (pld[k] == LI_UNRES) li_resolve_one(T, X, k, 0u, pld, nsed, eb);
-        if (eb[k] == LI_EUNRES) li_resolve_one(T, X, k, 1u, pld, nsed, eb);
-        if (nsed[k] == LI_UNRES) li_resolve_one(T, X, k, 2u, pld, nsed, eb);
+        if (pld[k] == LI_UNRES) li_resolve_one(T, X, k, 0u, pld, eb);
+        if (eb[k] == LI_EUNRES) li_resolve_one(T, X, k, 1u, pld, eb);
       }
     }
     if (t == ntiles - 1 && lane == 0) *ntot = uoff[t] + (n <= LI_UCAP ? n : 0u);
@@ -704,27 +656,22 @@ __global__ void __launch_bounds__(256) li_compact_slots_kernel(LiTree T, const u
 // woke 64 lanes for ~20 searches: 0.24 ms at C2)
 __global__ void __launch_bounds__(256) li_resolve_list_kernel(LiTree T, const uint32_t *X,
                                                               const uint64_t *dense, const uint32_t *ntot,
-                                                              uint32_t *pld, uint32_t *nsed, uint8_t *eb) {
+                                                              uint32_t *pld, uint8_t *eb) {
   const uint64_t n = *ntot;
   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n;
        i += (uint64_t) gridDim.x * blockDim.x) {
     const uint64_t w = dense[i];
-    li_resolve_one(T, X, w >> 2, (uint32_t) (w & 3u), pld, nsed, eb);
+    li_resolve_one(T, X, w >> 2, (uint32_t) (w & 3u), pld, eb);
   }
 }
 
-// PL / NSE of row k (X[k] = v > 0) from the distances, searching on escape
+// PL of row k (X[k] = v > 0) from the distances, searching on escape
 __device__ __forceinline__ uint64_t li_pl(const LiTree &T, const uint32_t *X, const uint32_t *pld,
                                           uint64_t k, uint32_t v) {
   const uint32_t d = pld[k];
   return d != LI_ESC ? k - d : li_search_prev<false>(T, X, pld, k, v, true);
 }
 
-__device__ __forceinline__ uint64_t li_nse(const LiTree &T, const uint32_t *X, const uint32_t *nsed,
-                                           uint64_t k, uint32_t v) {
-  const uint32_t d = nsed[k];
-  return d != LI_ESC ? k + d : li_search_next<false>(T, X, nsed, k, v);
-}
 
 // each tile's boundary chain t0-1, PL(t0-1), ... down to the first X = 0
 // entry, at most LI_BD entries (one thread per tile: a chain of dependent
@@ -947,75 +894,135 @@ __global__ void __launch_bounds__(LI_TPB) li_depth_kernel(LiTree T, const uint32
 // the interval records (lcp, lb, rb, father lcp, father lb) in pop order,
 // one per rightmost l-index; and the stream position of the first edge to
 // the root (the reference's firstedgefromroot, esa-bottomup.c:134-141)
+// a chain element of the tile's rows: its row, X, and where it lies -- in
+// the tile (m < 0, !far), on the boundary chain's held entries (m >= 0), or
+// past them (far: followed in HBM)
+struct LiElem {
+  uint64_t row;
+  uint32_t x;
+  int m;
+  bool far;
+};
+
+struct LiItvLds {
+  uint32_t x[LI_T + 1];                  // X of the tile's rows and the row after
+  uint32_t d[LI_T];                      // their PL distances
+  uint64_t brow[LI_BD];                  // the boundary chain's held entries
+  uint32_t bx[LI_BD];
+};
+
+// PL of chain element e (X > 0)
+__device__ __forceinline__ LiElem li_itv_next(const LiItvLds &S, const LiTree &T, const uint32_t *X,
+                                              const uint32_t *pld, uint64_t t0, int nb, const LiElem &e) {
+  LiElem n;
+  n.m = -1;
+  n.far = false;
+  if (!e.far && e.m < 0) {
+    const uint32_t d = S.d[e.row - t0];
+    n.row = d != LI_ESC ? e.row - d : li_search_prev<false>(T, X, pld, e.row, e.x, true);
+    if (n.row >= t0) {
+      n.x = S.x[n.row - t0];
+      return n;
+    }
+    int lo = 0, hi = nb - 1;             // rows strictly decreasing
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      const uint64_t r = S.brow[mid];
+      if (r == n.row) { n.m = mid; break; }
+      if (r > n.row) lo = mid + 1; else hi = mid - 1;
+    }
+    if (n.m >= 0) n.x = S.bx[n.m];
+    else { n.far = true; n.x = X[n.row]; }
+    return n;
+  }
+  if (!e.far && e.m + 1 < nb) {
+    n.m = e.m + 1;
+    n.row = S.brow[n.m];
+    n.x = S.bx[n.m];
+    return n;
+  }
+  n.far = true;
+  n.row = li_pl(T, X, pld, e.row, e.x);
+  n.x = X[n.row];
+  return n;
+}
+
+// The interval records by pop row, a tile per workgroup: row r pops the
+// first elements of its PL chain r, PL(r), ... -- exactly those with X >
+// X[r+1] (every row between a chain element c and r is above X[c], so
+// NSE(c) = r + 1) -- deepest first, records P(r), P(r) + 1, ...; the
+// interval of element c is [PL(c), r], PL(c) the chain's next element.  The
+// tile's X and PL distances and its boundary chain (the chain every row of
+// the tile continues on once it leaves the tile: t0 - 1, PL(t0 - 1), ...)
+// are in LDS, so a chain step is an LDS read, and neighbouring lanes write
+// neighbouring records.  (One thread per rightmost l-index, each record's
+// position from P and the depths: 1.3 ms at C2, its 40-byte records
+// scattered; the same pop-row walk over HBM: 1.85 ms.)
 template <typename PT>
-__global__ void __launch_bounds__(256) li_itv_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
-                                                     const uint32_t *nsed, const uint32_t *dep,
-                                                     const PT *P, uint64_t N, uint64_t *itv,
-                                                     unsigned long long *first) {
-  // LI_ITV_ROWS rows per thread, a grid-stride apart, taken through each
-  // step together: every step's loads (X, NSE and PL, then X at NSE, then
-  // X and PL at PL, depths and P) are issued for all of them before the
-  // first wait -- one row per thread waited out a chain of five dependent
-  // loads per row (1.6 ms at C2).  (Walking each row's pops instead, so
-  // that consecutive rows write consecutive records: 1.85 ms, the waves
-  // waiting for their longest chain.)
-  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-  for (uint64_t c0 = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; c0 < N;
-       c0 += LI_ITV_ROWS * stride) {
-    uint64_t c[LI_ITV_ROWS], q[LI_ITV_ROWS], lb[LI_ITV_ROWS];
-    uint32_t v[LI_ITV_ROWS], nd[LI_ITV_ROWS], xq[LI_ITV_ROWS], pd[LI_ITV_ROWS];
-    bool ok[LI_ITV_ROWS];
+__global__ void __launch_bounds__(LI_TPB) li_itv_kernel(LiTree T, const uint32_t *X, const uint32_t *pld,
+                                                        const PT *P, uint64_t N, uint64_t t_base,
+                                                        const uint64_t *brow, const uint32_t *bx,
+                                                        const uint32_t *bn, uint64_t *itv,
+                                                        unsigned long long *first) {
+  __shared__ LiItvLds S;
+  const int tid = threadIdx.x;
+  const uint64_t t = t_base + blockIdx.x, t0 = t * LI_T;
+  uint64_t pv[LI_RPT];                   // P of the thread's rows (loaded with X and PL)
+  {
+    uint32_t xv[LI_RPT], dv[LI_RPT];
 #pragma unroll
-    for (int j = 0; j < LI_ITV_ROWS; j++) {
-      c[j] = c0 + (uint64_t) j * stride;
-      ok[j] = c[j] < N;
-      const uint64_t cc = ok[j] ? c[j] : 0;
-      v[j] = X[cc];
-      nd[j] = nsed[cc];
-      pd[j] = pld[cc];
+    for (int j = 0; j < LI_RPT; j++) {
+      const uint64_t k = t0 + (uint64_t) (tid + LI_TPB * j);
+      const uint64_t kc = k <= N ? k : N;
+      xv[j] = X[kc];
+      dv[j] = pld[kc];
+      pv[j] = (uint64_t) P[kc];
     }
 #pragma unroll
-    for (int j = 0; j < LI_ITV_ROWS; j++) {
-      if (ok[j] && v[j] == 0) {
-        if (X[c[j] + 1] == 0) atomicMin(first, (unsigned long long) (c[j] + 2 * (uint64_t) P[c[j]]));
-        ok[j] = false;
-      }
-      q[j] = !ok[j] ? 0 : nd[j] != LI_ESC ? c[j] + nd[j] : li_search_next<false>(T, X, nsed, c[j], v[j]);
-      xq[j] = X[q[j]];
+    for (int j = 0; j < LI_RPT; j++) {
+      const int i = tid + LI_TPB * j;
+      S.x[i] = t0 + (uint64_t) i <= N ? xv[j] : 0u;
+      S.d[i] = dv[j];
     }
-#pragma unroll
-    for (int j = 0; j < LI_ITV_ROWS; j++) {
-      ok[j] = ok[j] && xq[j] != v[j];     // c is the interval's rightmost l-index
-      lb[j] = !ok[j] ? 0 : pd[j] != LI_ESC ? c[j] - pd[j] : li_search_prev<false>(T, X, pld, c[j], v[j], true);
+    if (tid == 0) S.x[LI_T] = t0 + LI_T <= N ? X[t0 + LI_T] : 0u;
+    if (tid < LI_BD) {
+      S.brow[tid] = brow[t * LI_BD + tid];
+      S.bx[tid] = bx[t * LI_BD + tid];
     }
-    uint32_t xl[LI_ITV_ROWS], dr[LI_ITV_ROWS], dc[LI_ITV_ROWS], pl2[LI_ITV_ROWS];
-    uint64_t prb[LI_ITV_ROWS];
+  }
+  const int nb = (int) bn[t];
+  __syncthreads();
 #pragma unroll
-    for (int j = 0; j < LI_ITV_ROWS; j++) {
-      const uint64_t rb = ok[j] ? q[j] - 1 : 0, cc = ok[j] ? c[j] : 0;
-      xl[j] = X[lb[j]];
-      pl2[j] = pld[lb[j]];
-      dr[j] = dep[rb];
-      dc[j] = dep[cc];
-      prb[j] = (uint64_t) P[rb];
+  for (int j = 0; j < LI_RPT; j++) {
+    const int i = tid + LI_TPB * j;
+    const uint64_t r = t0 + (uint64_t) i;
+    if (r >= N) break;
+    const uint32_t xr = S.x[i], x1 = S.x[i + 1];
+    const uint64_t pr = pv[j];
+    if (xr == 0) {
+      if (x1 == 0) atomicMin(first, (unsigned long long) (r + 2 * pr));
+      continue;
     }
-#pragma unroll
-    for (int j = 0; j < LI_ITV_ROWS; j++) {
-      if (!ok[j]) continue;
-      const uint64_t rb = q[j] - 1, jj = (uint64_t) (dr[j] - dc[j]);
-      const uint64_t pos = prb[j] + jj;
-      const uint32_t fd = xl[j] > xq[j] ? xl[j] : xq[j];
-      const uint64_t flb = fd == 0 ? 0
-                         : xl[j] >= xq[j] ? (pl2[j] != LI_ESC ? lb[j] - pl2[j]
-                                                             : li_search_prev<false>(T, X, pld, lb[j], xl[j], true))
-                                          : lb[j];
-      uint64_t *w = itv + 5 * pos;
-      w[0] = v[j];
-      w[1] = lb[j];
-      w[2] = rb;
+    LiElem c;
+    c.row = r;
+    c.x = xr;
+    c.m = -1;
+    c.far = false;
+    uint64_t *w = itv + 5 * pr;
+    for (uint64_t q = 0; c.x > x1; q++) {
+      const LiElem lb = li_itv_next(S, T, X, pld, t0, nb, c);
+      const uint32_t fd = lb.x > x1 ? lb.x : x1;
+      uint64_t flb = lb.row;
+      if (fd == 0) flb = 0;
+      else if (lb.x >= x1) flb = li_itv_next(S, T, X, pld, t0, nb, lb).row;
+      w[0] = c.x;
+      w[1] = lb.row;
+      w[2] = r;
       w[3] = fd;
       w[4] = flb;
-      if (fd == 0) atomicMin(first, (unsigned long long) (rb + 2 * prb[j] + 2 + 2 * jj));
+      w += 5;
+      if (fd == 0) atomicMin(first, (unsigned long long) (r + 2 * pr + 2 + 2 * q));
+      c = lb;
     }
   }
 }
@@ -1165,10 +1172,10 @@ struct GtLcpitvPlan {
   bool wide;                     // rows past 2^32: 64-bit P
   uint64_t ntiles;
   uint32_t *X;                   // exact LCP, rows 0..N
-  uint32_t *pld, *nsed, *dep;    // PL / NSE distances, chain depths
+  uint32_t *pld, *dep;           // PL distances, chain depths
   uint8_t *eb;                   // e (row opens an interval)
   uint32_t *tlev[LI_MAXLEV];     // tile minima and their 64-ary hierarchy
-  uint32_t *sch, *pch;           // the tiles' suffix / prefix minimum chains
+  uint32_t *sch;                 // the tiles' suffix-minimum chains
   LiTree T;                      // the searches' view of them
   void *P;                       // pops before each row (u32, u64 when wide), N + 1
   uint64_t nitv;
@@ -1184,7 +1191,7 @@ extern "C" void gt_lcpitv_plan_delete(GtLcpitvPlan *p) {
   // (events recorded where it was enqueued): nothing here waits, and no
   // other stream of the device is involved
   SmaxFence *fence = smax_marks_fence(&p->marks);
-  void *bufs[] = {p->X, p->pld, p->nsed, p->dep, p->eb, p->P, p->itv, p->first, p->sch, p->pch};
+  void *bufs[] = {p->X, p->pld, p->dep, p->eb, p->P, p->itv, p->first, p->sch};
   for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], fence);
   for (int l = 0; l < LI_MAXLEV; l++) smax_dev_free_fenced(p->tlev[l], fence);
   smax_fence_release(fence);
@@ -1267,14 +1274,12 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
                        in->numllv, in->lcp_dev, N, p->X, derr);
     LICHK(hipGetLastError());
   }
-  // pass A: PL, e, NSE inside the tiles; the tile minima and their hierarchy
+  // pass A: PL and e inside the tiles; the tile minima and their hierarchy
   LICHK(smax_dev_alloc((void **) &p->pld, sizeof (uint32_t) * (N + 1)));
-  LICHK(smax_dev_alloc((void **) &p->nsed, sizeof (uint32_t) * (N + 1)));
   LICHK(smax_dev_alloc((void **) &p->eb, N + 1));
   p->T.TL.n[0] = p->ntiles;
   LICHK(smax_dev_alloc((void **) &p->tlev[0], sizeof (uint32_t) * (p->ntiles + LI_PAD)));
   LICHK(smax_dev_alloc((void **) &p->sch, sizeof (uint32_t) * LI_CHW * p->ntiles));
-  LICHK(smax_dev_alloc((void **) &p->pch, sizeof (uint32_t) * LI_CHW * p->ntiles));
   LICHK(smax_dev_alloc((void **) &ulist, sizeof (uint16_t) * LI_UCAP * p->ntiles));
   LICHK(smax_dev_alloc((void **) &ucount, sizeof (uint32_t) * p->ntiles));
   LICHK(smax_dev_alloc((void **) &uoff, sizeof (uint32_t) * p->ntiles));
@@ -1283,7 +1288,7 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   for (uint64_t tb = 0; tb < p->ntiles; tb += LI_MAX_BLOCKS) {
     const uint64_t nb = p->ntiles - tb < LI_MAX_BLOCKS ? p->ntiles - tb : LI_MAX_BLOCKS;
     hipLaunchKernelGGL(li_ansv_kernel, dim3((unsigned) nb), dim3(LI_TPB), 0, s, p->X, N, tb, p->pld,
-                       p->nsed, p->eb, p->tlev[0], p->sch, p->pch, ulist, ucount);
+                       p->eb, p->tlev[0], p->sch, ulist, ucount);
     LICHK(hipGetLastError());
   }
   p->T.TL.nlev = 1;
@@ -1302,7 +1307,6 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   }
   for (int l = 0; l < p->T.TL.nlev; l++) p->T.TL.lv[l] = p->tlev[l];
   p->T.sch = p->sch;
-  p->T.pch = p->pch;
   // pass B
   {
     auto lens = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
@@ -1312,10 +1316,10 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     LICHK(smax_dev_alloc(&stmp, b ? b : 16));
     LICHK(rocprim::exclusive_scan(stmp, b, lens, uoff, 0u, (size_t) p->ntiles, rocprim::plus<uint32_t>(), s));
     hipLaunchKernelGGL(li_compact_slots_kernel, dim3(li_tile_grid((p->ntiles + 3) / 4)), dim3(256), 0, s,
-                       p->T, p->X, N, p->ntiles, ulist, ucount, uoff, dense, ntot, p->pld, p->nsed, p->eb);
+                       p->T, p->X, N, p->ntiles, ulist, ucount, uoff, dense, ntot, p->pld, p->eb);
     LICHK(hipGetLastError());
     hipLaunchKernelGGL(li_resolve_list_kernel, dim3(li_blocks(32 * p->ntiles)), dim3(256), 0, s, p->T, p->X,
-                       dense, ntot, p->pld, p->nsed, p->eb);
+                       dense, ntot, p->pld, p->eb);
     LICHK(hipGetLastError());
   }
   LICHK(hipGetLastError());
@@ -1358,13 +1362,16 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
   if (herr & 2u) { li_seterr(errbuf, errlen, "inconsistent .llv entry (lcp byte is not 255)"); goto fail; }
   LICHK(smax_dev_alloc((void **) &p->itv, sizeof (uint64_t) * 5 * (p->nitv ? p->nitv : 1)));
   if (N > 0) {
-    if (p->wide)
-      hipLaunchKernelGGL(li_itv_kernel<uint64_t>, dim3(li_blocks((N + LI_ITV_ROWS - 1) / LI_ITV_ROWS)), dim3(256), 0, s,
-                         p->T, p->X, p->pld, p->nsed, p->dep, (const uint64_t *) p->P, N, p->itv, p->first);
-    else
-      hipLaunchKernelGGL(li_itv_kernel<uint32_t>, dim3(li_blocks((N + LI_ITV_ROWS - 1) / LI_ITV_ROWS)), dim3(256), 0, s,
-                         p->T, p->X, p->pld, p->nsed, p->dep, (const uint32_t *) p->P, N, p->itv, p->first);
-    LICHK(hipGetLastError());
+    for (uint64_t tb = 0; tb < p->ntiles; tb += LI_MAX_BLOCKS) {
+      const uint64_t nb = p->ntiles - tb < LI_MAX_BLOCKS ? p->ntiles - tb : LI_MAX_BLOCKS;
+      if (p->wide)
+        hipLaunchKernelGGL(li_itv_kernel<uint64_t>, dim3((unsigned) nb), dim3(LI_TPB), 0, s, p->T, p->X,
+                           p->pld, (const uint64_t *) p->P, N, tb, brow, bx, bn, p->itv, p->first);
+      else
+        hipLaunchKernelGGL(li_itv_kernel<uint32_t>, dim3((unsigned) nb), dim3(LI_TPB), 0, s, p->T, p->X,
+                           p->pld, (const uint32_t *) p->P, N, tb, brow, bx, bn, p->itv, p->first);
+      LICHK(hipGetLastError());
+    }
   }
   smax_marks_record(&p->marks, s);
   {
@@ -1374,10 +1381,9 @@ extern "C" int gt_lcpitv_plan_create_stream(GtLcpitvPlan **planp, const GtLcpitv
     smax_marks_init(&m);
     smax_marks_record(&m, s);
     SmaxFence *f = smax_marks_fence(&m);
-    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt, uoff, dense, ntot, stmp, p->nsed, p->dep, p->eb};
+    void *bufs[] = {derr, brow, bx, bn, aff, affs, tmp, ulist, ucount, cnt, uoff, dense, ntot, stmp, p->dep, p->eb};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free_fenced(bufs[i], f);
     smax_fence_release(f);
-    p->nsed = NULL;
     p->dep = NULL;
     p->eb = NULL;
   }
