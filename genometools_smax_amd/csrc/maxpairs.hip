@@ -312,15 +312,14 @@ __device__ __forceinline__ uint64_t mp_block_excl(uint64_t v, uint64_t *total) {
 }
 
 // Candidate rows (LCP[j] >= minlen, j >= 1: rows whose walk is not empty),
-// found per workgroup of MP_WG_ROWS rows: every thread tests MP_CPT groups
-// of 16 consecutive rows, one 16-byte LCP load each (byte >= min(minlen,
-// 255), exact below 255).  Pass A counts them per workgroup, pass B (after a scan of those
+// found per workgroup of MP_WG_ROWS rows: every thread tests 16 consecutive
+// rows with one 16-byte LCP load (byte >= min(minlen, 255), exact below
+// 255).  Pass A counts them per workgroup, pass B (after a scan of those
 // counts) writes them to one global list in row order.  The walks then run
 // one lane per candidate row (passes C and D), so neighbouring lanes walk
 // neighbouring rows (coalesced) and a long block spreads over the device.
 #define MP_ROWS 16
-#define MP_CPT 4                          // 16-row groups per pass-A thread
-#define MP_WG_ROWS (256 * MP_ROWS * MP_CPT)
+#define MP_WG_ROWS (256 * MP_ROWS)
 
 __device__ __forceinline__ uint32_t mp_candidates(const uint8_t *lcp, uint64_t j0, uint64_t N,
                                                   uint32_t mf) {
@@ -343,27 +342,22 @@ __device__ __forceinline__ uint32_t mp_candidates(const uint8_t *lcp, uint64_t j
 __global__ void __launch_bounds__(256)
 mp_cand_count_kernel(const uint8_t *lcp, uint64_t N, uint32_t mf, uint64_t *wg_cand,
                      uint16_t *masks) {
-  // MP_CPT groups of 16 rows per thread, their loads issued together (one
-  // 16-row group per thread streamed the LCP bytes at 4.4 TB/s); the
-  // thread's four 16-bit masks go out as one 8-byte word, in row order
-  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) (MP_ROWS * MP_CPT);
-  uint64_t m = 0;
-#pragma unroll
-  for (int c = 0; c < MP_CPT; c++) m |= (uint64_t) mp_candidates(lcp, j0 + MP_ROWS * c, N, mf) << (16 * c);
-  reinterpret_cast<uint64_t *>(masks)[blockIdx.x * (uint64_t) 256 + threadIdx.x] = m;
+  const uint64_t j0 = blockIdx.x * (uint64_t) MP_WG_ROWS + threadIdx.x * (uint64_t) MP_ROWS;
+  const uint32_t m = mp_candidates(lcp, j0, N, mf);
+  masks[blockIdx.x * (uint64_t) 256 + threadIdx.x] = (uint16_t) m;
   uint64_t tot;
-  (void) mp_block_excl((uint64_t) __popcll(m), &tot);
+  (void) mp_block_excl((uint64_t) __popc(m), &tot);
   if (threadIdx.x == 0) wg_cand[blockIdx.x] = tot;
 }
 
 // pass B reads pass A's 16-row masks (2 B per 16 rows), not the LCP bytes;
-// one workgroup per MP_WR_GROUP of pass A's workgroups, 4 masks (64 rows,
-// one pass-A thread's) per thread: one 8-byte load each (one mask per
-// thread: 15.5 us for C2's 12.5 MB)
-#define MP_WR_GROUP 1
+// one workgroup per MP_WR_GROUP of pass A's workgroups, 4 masks (64 rows)
+// per thread: one 8-byte load each (a workgroup per pass-A workgroup, one
+// mask per thread: 15.5 us for C2's 12.5 MB)
+#define MP_WR_GROUP 4
 __global__ void __launch_bounds__(256)
 mp_cand_write_kernel(const uint16_t *masks, const uint64_t *wg_cand_off, uint64_t *list) {
-  const uint64_t k0 = (uint64_t) blockIdx.x * (256 * MP_CPT * MP_WR_GROUP) + 4u * threadIdx.x;
+  const uint64_t k0 = (uint64_t) blockIdx.x * (256 * MP_WR_GROUP) + 4u * threadIdx.x;
   uint64_t m = *reinterpret_cast<const uint64_t *>(masks + k0);
   uint64_t tot;
   uint64_t pos = wg_cand_off[(uint64_t) blockIdx.x * MP_WR_GROUP] +
@@ -569,6 +563,38 @@ __global__ void __launch_bounds__(256) mp_gather_kernel(const uint64_t *src, con
   }
 }
 
+// The order inside each event (equal k3, after a stable sort by k3 alone):
+// (k2, k1), by an insertion sort of the event's permutation entries run by
+// the thread of its first entry -- events hold a few pairs (a leaf's or two
+// children's cartesian product), so this replaces the two 40- and 48-bit
+// LSD sorts.  An event of more than MP_SEG_MAX pairs sets *big and the pass
+// sorts by all three keys instead.
+#define MP_SEG_MAX 64
+__global__ void __launch_bounds__(256) mp_segfix_kernel(const uint64_t *ks, const uint64_t *k1,
+                                                        const uint64_t *k2, uint64_t *pa, uint64_t n,
+                                                        uint32_t *big) {
+  MP_FOR(i, n) {
+    if (i > 0 && ks[i] == ks[i - 1]) continue;   // not an event's first entry
+    uint64_t e = i + 1;
+    while (e < n && e - i <= MP_SEG_MAX && ks[e] == ks[i]) e++;
+    if (e - i > MP_SEG_MAX) {
+      atomicOr(big, 1u);
+      continue;
+    }
+    for (uint64_t a = i + 1; a < e; a++) {       // stable: strict comparisons
+      const uint64_t v = pa[a], v2 = k2[v], v1 = k1[v];
+      uint64_t b = a;
+      while (b > i) {
+        const uint64_t u = pa[b - 1], u2 = k2[u];
+        if (u2 < v2 || (u2 == v2 && k1[u] <= v1)) break;
+        pa[b] = u;
+        b--;
+      }
+      pa[b] = v;
+    }
+  }
+}
+
 // Small ordered passes (T <= mp_rank_max()): the stable LSD passes below
 // are one rank count instead -- the final order is the composite key
 // (k_{NK-1}, ..., k_1, emission index) in lexicographic order, so an
@@ -769,8 +795,8 @@ extern "C" int gt_maxpairs_plan_create_stream(GtMaxpairsPlan **planp, const GtMa
   MPCHK(smax_dev_alloc((void **) &p->wg_cand_off, sizeof (uint64_t) * (p->nwg + 1)));
   // whole groups of MP_WR_GROUP pass-A workgroups; the masks past the last
   // one stay zero
-  MPCHK(smax_dev_alloc((void **) &p->masks, sizeof (uint16_t) * 256 * MP_CPT * (p->nwg + MP_WR_GROUP)));
-  MPCHK(hipMemsetAsync(p->masks, 0, sizeof (uint16_t) * 256 * MP_CPT * (p->nwg + MP_WR_GROUP), s));
+  MPCHK(smax_dev_alloc((void **) &p->masks, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP)));
+  MPCHK(hipMemsetAsync(p->masks, 0, sizeof (uint16_t) * 256 * (p->nwg + MP_WR_GROUP), s));
   MPCHK(smax_dev_alloc((void **) &p->total, sizeof (uint64_t)));
   MPCHK(hipMemsetAsync(p->total, 0, sizeof (uint64_t), s));
   MPCHK(smax_dev_alloc((void **) &derr, sizeof (uint32_t)));
@@ -1038,7 +1064,8 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   hipStream_t s = (hipStream_t) stream;
   const uint64_t nc = p->ncand;
   uint64_t T = 0;
-  uint64_t *tri = NULL, *keys = NULL, *ktmp = NULL, *pa = NULL, *pb = NULL;
+  uint64_t *tri = NULL, *keys = NULL, *ktmp = NULL, *pa = NULL, *pb = NULL, *ks = NULL;
+  uint32_t *big = NULL;
   void *st = NULL;
   size_t sb = 0;
   MpKeys K;
@@ -1097,6 +1124,40 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
   MPCHK(hipGetLastError());
   MPCHK(rocprim::radix_sort_pairs(nullptr, sb, ktmp, ktmp, pa, pb, (size_t) T, 0, 64, s));
   MPCHK(smax_dev_alloc(&st, sb ? sb : 16));
+  if (!K.split) {
+    // one stable sort by the event (k3), then each event's few pairs put in
+    // (k2, k1) order in place (mp_segfix_kernel): 5 radix passes instead of
+    // 16 at 3 Gbp
+    MPCHK(smax_dev_alloc((void **) &ks, sizeof (uint64_t) * T));
+    MPCHK(smax_dev_alloc((void **) &big, sizeof (uint32_t)));
+    MPCHK(hipMemsetAsync(big, 0, sizeof (uint32_t), s));
+    MPCHK(hipMemcpyAsync(ktmp, K.k3, sizeof (uint64_t) * T, hipMemcpyDeviceToDevice, s));
+    size_t b = sb;
+    MPCHK(rocprim::radix_sort_pairs(st, b, ktmp, ks, pa, pb, (size_t) T, 0, K.rowbits + K.lbits, s));
+    uint64_t *t = pa; pa = pb; pb = t;
+    hipLaunchKernelGGL(mp_segfix_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, ks, K.k1, K.k2, pa, T, big);
+    MPCHK(hipGetLastError());
+    uint32_t hbig = 0;
+    MPCHK(hipMemcpyAsync(&hbig, big, sizeof hbig, hipMemcpyDeviceToHost, s));
+    MPCHK(hipStreamSynchronize(s));      // an event past MP_SEG_MAX pairs: all three keys
+    if (hbig == 0) {
+      hipLaunchKernelGGL((mp_gather_kernel<3>), dim3(mp_blocks(T)), dim3(256), 0, s, tri, pa, T,
+                         out_dev);
+      MPCHK(hipGetLastError());
+      smax_dev_free(ks);                 // the sync above passed their users
+      smax_dev_free(big);
+      ks = NULL;
+      big = NULL;
+      MPCHK(mp_free_behind(p, s, tri, keys, ktmp, pa, pb, st));
+      return 0;
+    }
+    smax_dev_free(ks);
+    smax_dev_free(big);
+    ks = NULL;
+    big = NULL;
+    hipLaunchKernelGGL(mp_iota_kernel, dim3(mp_blocks(T)), dim3(256), 0, s, pa, T);
+    MPCHK(hipGetLastError());
+  }
   {
     // stable LSD passes: r2, then (classes, r1), then the event [depth, then t]
     const int nk = K.split ? 4 : 3;
@@ -1125,7 +1186,7 @@ extern "C" int gt_maxpairs_plan_emit_ordered(GtMaxpairsPlan *p, uint64_t *out_de
 fail:
   {
     (void) hipStreamSynchronize(s);
-    void *bufs[] = {tri, keys, ktmp, pa, pb, st};
+    void *bufs[] = {tri, keys, ktmp, pa, pb, st, ks, big};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; i++) smax_dev_free(bufs[i]);
   }
   return -1;
